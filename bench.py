@@ -1,0 +1,193 @@
+"""Headline benchmark: primary Mrays/s at 3840x2160 on a 1024^3 brick tree (BASELINE.json `metric`).
+
+One step = one frame: every pixel's primary ray traced with get_by_ray semantics (src/raytracing/cpu.rs:296-458)
+through the HIP kernel, shaded to RGBA8 + f32 depth in HBM. With N GPUs (torchrun, one process per GPU, RCCL) the
+frame is split into 64x64 screen tiles dealt round-robin over the ranks; each rank traces its tiles into a
+contiguous buffer, rank 0 gathers the RGBA tiles over RCCL and scatters them into the framebuffer (strong scaling:
+the frame is fixed, N GPUs share it).
+
+Workload: the reference's lattice+cube scene S (examples/gpu_render.rs:57-82) at 1024^3
+with brick_dim 4 (1024 is not a valid size for brick_dim 8, src/boxtree/mod.rs:188-202; the 1024^3 .vox model is not
+in the reference checkout), glass camera of benches/performance.rs on radius 2S at 40 rad aimed at the centre.
+
+Also printed: roofline (algorithmic bytes per launch, counted by the instrumented kernel, / measured kernel time vs
+8 TB/s), and cpu_baseline: the CPU restatement of the reference raytracer (oracle/) on the host cores over the
+same frame.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+BASELINE = json.load(open(os.path.join(ROOT, "BASELINE.json")))
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--size", type=int, default=1024)
+    p.add_argument("--brick-dim", type=int, default=4)
+    p.add_argument("--width", type=int, default=3840)
+    p.add_argument("--height", type=int, default=2160)
+    p.add_argument("--scene", type=int, default=1, help="VHX_SCENE_* (1 = lattice+cube scene S)")
+    p.add_argument("--tile", type=int, default=64)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-roofline", action="store_true")
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    import voxelhex_amd as vhx
+    from voxelhex_amd import _native as N
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    t0 = time.time()
+    flat = vhx.FlatTree.build_scene(args.scene, args.size, args.brick_dim, threads=min(16, os.cpu_count() or 1))
+    build_s = time.time() - t0
+    rt = vhx.Raytracer(local)
+    stream = torch.cuda.current_stream(dev)
+    rt.set_stream(stream.cuda_stream)  # kernels run on torch's stream: torch events and RCCL see them in order
+    t0 = time.time()
+    rt.upload(flat)
+    upload_s = time.time() - t0
+
+    W, H, T = args.width, args.height, args.tile
+    c = args.size / 2.0
+    cam = vhx.glass_camera(args.size, W, H, target=(c, c, c))
+    if world == 1:
+        n_out = W * H
+        trace_kw = dict(tile_size=0, tile_start=0, tile_stride=1, layout=N.VHX_LAYOUT_FRAMEBUFFER)
+        tiles_per_rank = 0
+    else:
+        ntiles = ((W + T - 1) // T) * ((H + T - 1) // T)
+        tiles_per_rank = (ntiles + world - 1) // world
+        n_out = tiles_per_rank * T * T
+        trace_kw = dict(tile_size=T, tile_start=rank, tile_stride=world, layout=N.VHX_LAYOUT_TILES)
+    rgba = torch.zeros(n_out, dtype=torch.int32, device=dev)
+    depth = torch.zeros(n_out, dtype=torch.float32, device=dev)
+    out = {"rgba": rgba, "depth": depth}
+    if world > 1 and rank == 0:
+        gathered = [torch.zeros(n_out, dtype=torch.int32, device=dev) for _ in range(world)]
+        framebuffer = torch.zeros(W * H, dtype=torch.int32, device=dev)
+
+    ev = []
+
+    def step(timed):
+        if timed:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+        rt.trace_primary(cam, out=out, **trace_kw)
+        if timed:
+            e1.record(stream)
+            ev.append((e0, e1))
+        if world > 1:
+            dist.gather(rgba, gathered if rank == 0 else None, dst=0)
+            if rank == 0:
+                flatg = torch.cat(gathered)
+                rt.untile_rgba(flatg.data_ptr(), world, tiles_per_rank, T, W, H, framebuffer.data_ptr())
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+
+    total_rays = W * H
+    mrays = total_rays * args.steps / elapsed / 1e6
+    ms_per_step = elapsed * 1e3 / args.steps
+
+    # ---- roofline: algorithmic bytes of this rank's launch (instrumented kernel, untimed) -------------------------
+    roof = None
+    if not args.no_roofline:
+        res = rt.trace_primary(cam, fields=(), count_bytes=True, **trace_kw)
+        tree_bytes = float(res["bytes"].astype(np.float64).sum())
+        if world == 1:
+            my_rays = W * H
+        else:
+            tx = (W + T - 1) // T
+            my_rays = sum(min(T, W - (k % tx) * T) * min(T, H - (k // tx) * T)
+                          for k in range(rank, ((W + T - 1) // T) * ((H + T - 1) // T), world))
+        out_bytes = 8.0 * my_rays  # rgba8 + f32 depth per ray
+        launch_bytes = tree_bytes + out_bytes
+        achieved = launch_bytes / (kernel_ms * 1e-3) / 1e9
+        roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                "kernel": "k_trace_primary<false>", "kernel_ms": round(kernel_ms, 4),
+                "algorithmic_bytes_per_launch": launch_bytes, "tree_bytes_per_ray": round(tree_bytes / max(1, my_rays), 2)}
+
+    # ---- CPU baseline: the oracle (reference semantics) on the host cores, rank 0 at N=1 only ----------------------
+    cpu = None
+    if world == 1 and rank == 0 and not args.no_cpu_baseline:
+        from tests._oracle import Oracle
+        orc = Oracle()
+        cores = max(1, min(16, len(os.sched_getaffinity(0))))
+        orc.trace_primary(flat, cam, 0, 0, W, 16, threads=cores, fields=("rgba",))  # warm
+        t0 = time.perf_counter()
+        orc.trace_primary(flat, cam, 0, 0, W, H, threads=cores, fields=("rgba", "depth"))
+        cpu_s = time.perf_counter() - t0
+        cpu = {"value": round(W * H / cpu_s / 1e6, 4), "unit": "Mrays/s", "cores": cores, "kind": "port",
+               "sample": f"full {W}x{H} frame, same tree and camera, OpenMP dynamic over pixels, {cpu_s:.2f} s"}
+
+    if rank == 0:
+        line = {
+            "metric": BASELINE["metric"], "value": round(mrays, 3), "unit": "Mrays/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic",
+            "config": {"workload": f"primary rays {W}x{H}, {args.size}^3 procedural scene S (lattice+cube), "
+                                   f"brick_dim {args.brick_dim}, glass camera",
+                       "tree_size": args.size, "brick_dim": args.brick_dim, "width": W, "height": H,
+                       "scene": args.scene, "tile": T if world > 1 else None,
+                       "parallelism": f"screen-tile split x{world} + RCCL gather" if world > 1 else "single GPU",
+                       "tree_nodes": int(flat.desc.node_count), "tree_bricks": int(flat.desc.brick_count),
+                       "tree_gb": round(flat.nbytes() / 1e9, 3), "build_s": round(build_s, 2),
+                       "upload_s": round(upload_s, 2)},
+            "roofline": roof, "cpu_baseline": cpu,
+        }
+        if cpu:
+            line["gpu_over_cpu"] = round(mrays / cpu["value"], 2)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    rt.close()
+
+
+if __name__ == "__main__":
+    main()

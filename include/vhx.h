@@ -1,0 +1,175 @@
+/*
+ * vhx.h — C ABI of the MI355X primary-ray voxel-brick raytracer (libvhx.so).
+ *
+ * This is the drop-in boundary for VoxelHex's `src/raytracing` module. Each entry point names the
+ * reference interface it replaces (paths relative to the VoxelHex repository root):
+ *
+ *   vhx_tree_desc        <- BoxTreeRenderData + BoxTreeMetaData, the flattened node/brick/palette buffers
+ *                           (src/raytracing/bevy/types.rs:27-57, 203-256) that the Bevy host builds in
+ *                           BoxTreeGPUDataHandler::add_node / add_brick (src/raytracing/bevy/streaming/cache.rs:226-455,
+ *                           608-716) and binds in create_tree_bind_group (src/raytracing/bevy/pipeline/bind_groups.rs:366-482)
+ *   vhx_create/destroy   <- BoxTreeGPUHost::new / create_new_view (src/raytracing/bevy/mod.rs:164-180,
+ *                           src/raytracing/bevy/view.rs:36-137): owns the device copy of the tree
+ *   vhx_upload_tree      <- prepare_bind_groups full-buffer writes (src/raytracing/bevy/pipeline/mod.rs:242-402)
+ *   vhx_update_range     <- write_range_to_buffer (src/raytracing/bevy/streaming/mod.rs:344-370)
+ *   vhx_trace_primary    <- VhxRenderNode::run main dispatch (src/raytracing/bevy/pipeline/mod.rs:96-155) running the
+ *                           per-pixel kernel, with the semantics of the reference CPU raytracer
+ *                           BoxTree::get_by_ray (src/raytracing/cpu.rs:296-458) and the CPU frame of
+ *                           examples/gpu_render.rs:196-257 / benches/performance.rs:29-66
+ *   vhx_trace_rays       <- BoxTree::get_by_ray (src/raytracing/cpu.rs:296) over an explicit batch of rays
+ *   vhx_last_error       <- the Result<_, ()> / expect() error paths of the plugin (src/raytracing/bevy/streaming/mod.rs:63-73)
+ *
+ * Conventions: every function returns 0 on success or a negative VHX_E_* code; a message is kept per context
+ * (vhx_last_error). Host pointers are only read during the call. A context is single-threaded and all work is
+ * ordered on its HIP stream. Nothing in this header uses HIP, torch or C++ types.
+ */
+#ifndef VHX_H
+#define VHX_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VHX_ABI_VERSION 1u
+
+/* ---- error codes ------------------------------------------------------------------------------------------ */
+#define VHX_OK 0
+#define VHX_E_INVALID_ARG (-1) /* bad pointer / size / layout                                                 */
+#define VHX_E_HIP (-2)         /* a HIP runtime call failed (message in vhx_last_error)                         */
+#define VHX_E_CAPACITY (-3)    /* update_range outside the uploaded capacity: grow and re-upload, mirroring
+                                  view.resize / re_evaluate_view_size (src/raytracing/bevy/streaming/mod.rs:292-340) */
+#define VHX_E_NO_DEVICE (-4)   /* no HIP device available                                                       */
+#define VHX_E_STATE (-5)       /* call order violated (e.g. trace before upload)                                */
+
+/* ---- node types (NodeContent, src/boxtree/types.rs:57-73) ------------------------------------------------- */
+#define VHX_NODE_NOTHING 0u
+#define VHX_NODE_INTERNAL 1u
+#define VHX_NODE_LEAF 2u
+#define VHX_NODE_UNIFORM_LEAF 3u
+
+/* ---- child / brick descriptors in node_children -----------------------------------------------------------
+ * Internal node : node_children[64*n + s] = child node index, or VHX_EMPTY (NodeChildren, types.rs:75-80)
+ * Leaf node     : node_children[64*n + s] = brick descriptor of sectant s (BrickData, types.rs:41-54)
+ * UniformLeaf   : node_children[64*n + 0] = brick descriptor of the whole node, slots 1..63 = VHX_EMPTY
+ * brick descriptor: VHX_EMPTY = BrickData::Empty;
+ *                   bit31 set  = BrickData::Solid, low 31 bits index solid_values[] (exact 32-bit voxel value);
+ *                   bit31 clear= BrickData::Parted, brick index into voxels[] (brick_dim^3 values per brick).
+ * (The WGSL host ORs the solid voxel into bit 31 directly, cache.rs:391; that loses the data-palette index of
+ *  PaletteIndexValues >= 0x80000000, so this ABI keeps solid values in their own table.)                        */
+#define VHX_EMPTY 0xFFFFFFFFu
+#define VHX_SOLID_BIT 0x80000000u
+
+/* Flattened BoxTree<u32> (full residency). Node 0 is the root (ROOT_NODE_KEY, src/boxtree/detail.rs:140).
+ * Voxel values are PaletteIndexValues (src/boxtree/types.rs:111): color index in bits 0-15, data index in
+ * bits 16-31, 0xFFFF = none in either half (src/boxtree/node.rs:260-309).                                    */
+typedef struct vhx_tree_desc {
+    uint32_t boxtree_size;   /* BoxTree::boxtree_size (edge length of the root cube)                          */
+    uint32_t brick_dim;      /* BoxTree::brick_dim                                                            */
+    uint32_t node_count;
+    uint32_t brick_count;    /* number of Parted bricks in voxels[]                                           */
+    uint32_t solid_count;    /* entries of solid_values[]                                                     */
+    uint32_t color_count;    /* entries of color_palette[]                                                    */
+    uint32_t data_count;     /* entries of data_palette[]                                                     */
+    uint32_t reserved0;
+    const uint32_t *node_type;     /* [node_count]      VHX_NODE_*                                            */
+    const uint64_t *node_ocbits;   /* [node_count]      NodeData::occupied_bits                               */
+    const uint32_t *node_children; /* [node_count*64]   see above                                             */
+    const uint32_t *voxels;        /* [brick_count*brick_dim^3] flat index x + y*bd + z*bd*bd                  */
+    const uint32_t *solid_values;  /* [solid_count]                                                           */
+    const uint32_t *color_palette; /* [color_count] Albedo packed r | g<<8 | b<<16 | a<<24                     */
+    const uint32_t *data_palette;  /* [data_count]  user data T=u32 (empty <=> 0, src/boxtree/detail.rs:18-24)  */
+} vhx_tree_desc;
+
+/* ---- ray generation ---------------------------------------------------------------------------------------- */
+#define VHX_RAY_INVERSE_VP 0u /* examples/gpu_render.rs:203-224: NDC -> world via inverse view-projection, glam op order */
+#define VHX_RAY_GLASS 1u      /* benches/performance.rs:32-61: pinhole "glass" plane, V3c op order                    */
+
+typedef struct vhx_camera {
+    uint32_t ray_model;      /* VHX_RAY_*                                                                    */
+    uint32_t width, height;  /* full frame resolution in pixels                                              */
+    uint32_t reserved0;
+    float origin[3];         /* ray origin for every pixel (Viewport::origin / viewport.origin)              */
+    /* VHX_RAY_GLASS: glass_point = bottom_left + right*x*pixel_width + up*y*pixel_height                    */
+    float glass_bottom_left[3];
+    float glass_right[3];
+    float glass_up[3];
+    float pixel_width, pixel_height;
+    /* VHX_RAY_INVERSE_VP: column-major 4x4 (glam Mat4 layout), Viewport::inverse_view_projection_matrix     */
+    float inv_view_proj[16];
+} vhx_camera;
+
+/* Output layout of vhx_trace_primary */
+#define VHX_LAYOUT_FRAMEBUFFER 0u /* ray (x,y) -> index y*width + x                                               */
+#define VHX_LAYOUT_TILES 1u       /* tile-major: k-th traced tile owns indices [k*T*T, (k+1)*T*T), row-major inside */
+
+/* Per-ray hit records, structure of arrays; any pointer may be NULL to skip that field.
+ * Device pointers when passed to vhx_trace_primary/vhx_trace_rays with on_device=1, host pointers otherwise.
+ *   value  : PaletteIndexValues of the hit voxel; VHX_EMPTY = no hit (get_by_ray returned None)
+ *   cell   : flat index of the hit cell inside its Parted brick (cpu.rs:136-144); VHX_EMPTY for Solid/miss
+ *   voxel  : 3 u32 per ray, integer min corner of the hit cube (the cell for Parted hits, the brick/node bounds
+ *            for Solid hits); VHX_EMPTY x3 on miss
+ *   impact : 3 f32 per ray, impact point (cpu.rs:257, 284);   miss: 0,0,0
+ *   normal : 3 f32 per ray, cube_impact_normal (spatial/raytracing/mod.rs:97-125); miss: 0,0,0
+ *   depth  : |impact - origin| (V3c::length);                   miss: +inf
+ *   rgba   : r | g<<8 | b<<16 | a<<24 shaded as examples/gpu_render.rs:236-249 (miss 128,128,128,255;
+ *            a hit without albedo - where the example would unwrap() None - is 0,0,0,255)
+ *   bytes  : algorithmic bytes touched by this ray (instrumentation; definition in DESIGN.md)            */
+typedef struct vhx_hits {
+    uint32_t *value;
+    uint32_t *cell;
+    uint32_t *voxel;
+    float *impact;
+    float *normal;
+    float *depth;
+    uint32_t *rgba;
+    uint32_t *bytes;
+} vhx_hits;
+
+typedef struct vhx_ctx vhx_ctx;
+
+/* Library / device ------------------------------------------------------------------------------------------ */
+uint32_t vhx_abi_version(void);
+int vhx_device_count(int *count);
+int vhx_create(int hip_device, vhx_ctx **out);
+void vhx_destroy(vhx_ctx *ctx);
+const char *vhx_last_error(const vhx_ctx *ctx);
+/* Use an external HIP stream (hipStream_t passed as void*; NULL = the context's own stream). */
+int vhx_set_stream(vhx_ctx *ctx, void *hip_stream);
+/* Wait for all work of the context; optionally return the device time of the last trace in milliseconds. */
+int vhx_sync(vhx_ctx *ctx, float *last_trace_ms);
+
+/* Tree upload ----------------------------------------------------------------------------------------------- */
+/* Copies the flattened tree to HBM (full residency) and builds the device-side layout. */
+int vhx_upload_tree(vhx_ctx *ctx, const vhx_tree_desc *tree);
+#define VHX_BUF_NODE_TYPE 0
+#define VHX_BUF_NODE_OCBITS 1
+#define VHX_BUF_NODE_CHILDREN 2
+#define VHX_BUF_VOXELS 3
+#define VHX_BUF_SOLID_VALUES 4
+#define VHX_BUF_COLOR_PALETTE 5
+#define VHX_BUF_DATA_PALETTE 6
+/* Overwrites elements [elem_offset, elem_offset+elem_count) of one uploaded buffer (element = one entry of the
+ * corresponding vhx_tree_desc array) and refreshes the derived device state. VHX_E_CAPACITY past the end. */
+int vhx_update_range(vhx_ctx *ctx, int buffer_id, uint64_t elem_offset, uint64_t elem_count, const void *src);
+/* Device bytes held by the uploaded tree. */
+int vhx_tree_device_bytes(const vhx_ctx *ctx, uint64_t *bytes);
+
+/* Tracing --------------------------------------------------------------------------------------------------- */
+/* Traces primary rays for every pixel of the square tiles k = tile_start, tile_start+tile_stride, ... (raster order
+ * of ceil(W/T) x ceil(H/T) tiles, T = tile_size). tile_size 0 with layout FRAMEBUFFER traces the whole frame. */
+int vhx_trace_primary(vhx_ctx *ctx, const vhx_camera *cam, uint32_t tile_size, uint32_t tile_start,
+                      uint32_t tile_stride, uint32_t layout, const vhx_hits *out, int on_device);
+/* Traces n explicit rays; rays = 6 f32 per ray (origin xyz, direction xyz), host or device per on_device. */
+int vhx_trace_rays(vhx_ctx *ctx, const float *rays, uint64_t n, const vhx_hits *out, int on_device);
+/* Scatters tile-major RGBA buffers gathered from `ranks` ranks (rank r traced tiles r, r+ranks, ...; each rank's
+ * buffer holds tiles_per_rank*T*T pixels, concatenated by rank) into a width x height framebuffer.       */
+int vhx_untile_rgba(vhx_ctx *ctx, const uint32_t *gathered, uint32_t ranks, uint32_t tiles_per_rank,
+                    uint32_t tile_size, uint32_t width, uint32_t height, uint32_t *framebuffer, int on_device);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VHX_H */

@@ -1,0 +1,82 @@
+/*
+ * vhx_boxtree.h — C ABI of the host-side BoxTree (libvhx.so, host code only, no GPU needed).
+ *
+ * The reference keeps the voxel tree in Rust (`BoxTree<T>`); its toolchain is not available to this build, so the
+ * host side of the raytracing drop-in is restated in C++ behind this ABI:
+ *
+ *   vhx_boxtree_new            <- BoxTree::new            (src/boxtree/mod.rs:188-219)
+ *   vhx_boxtree_insert         <- BoxTree::insert         (src/boxtree/update/insert.rs:21-30)
+ *   vhx_boxtree_insert_at_lod  <- BoxTree::insert_at_lod  (src/boxtree/update/insert.rs:37-47)
+ *   vhx_boxtree_update         <- BoxTree::update         (src/boxtree/update/insert.rs:53-62)
+ *   vhx_boxtree_get            <- BoxTree::get            (src/boxtree/mod.rs:223-233)
+ *   vhx_boxtree_simplify       <- BoxTree::simplify(ROOT, recursive) (src/boxtree/update/mod.rs:617-867)
+ *   vhx_boxtree_flatten        <- BoxTreeGPUDataHandler::add_node/add_brick with every node resident
+ *                                 (src/raytracing/bevy/streaming/cache.rs:226-455, 608-716)
+ *   vhx_scene_build            <- bulk builder producing exactly the flattened tree that inserting a procedural
+ *                                 scene voxel by voxel (x, then y, then z loops) would produce
+ *
+ * Tree type parameter: T = u32 (the reference default, BoxTree<T = u32>, src/boxtree/types.rs:219).
+ */
+#ifndef VHX_BOXTREE_H
+#define VHX_BOXTREE_H
+
+#include "vhx.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* OctreeError (src/boxtree/types.rs:9-21) */
+#define VHX_E_TREE_INVALID_SIZE (-10)
+#define VHX_E_TREE_INVALID_BRICK_DIMENSION (-11)
+#define VHX_E_TREE_INVALID_STRUCTURE (-12)
+#define VHX_E_TREE_INVALID_POSITION (-13)
+
+/* BoxTreeEntry kinds (src/boxtree/types.rs:25-37) */
+#define VHX_ENTRY_EMPTY 0u
+#define VHX_ENTRY_VISUAL 1u      /* albedo only  */
+#define VHX_ENTRY_INFORMATIVE 2u /* data only    */
+#define VHX_ENTRY_COMPLEX 3u     /* albedo+data  */
+
+/* Procedural scenes for vhx_scene_build / vhx_scene_insert */
+#define VHX_SCENE_LATTICE_CUBE 1u /* examples/gpu_render.rs:57-82: lattice where any coord < S/4 + cube >= S/2, axis-plane colours */
+#define VHX_SCENE_BENCH_REGION 2u /* benches/performance.rs:11-27: [0,100)^3 slab where x|y|z < S/4 or all >= S/2, 0x00ABCDEF */
+#define VHX_SCENE_LATTICE 3u      /* src/raytracing/tests.rs:777-789 (context_bleed): lattice only, colour 255*c/S            */
+#define VHX_SCENE_CUBE 4u         /* src/raytracing/tests.rs:736-748 (cube_flaps): cube >= S/2, colour 255*c/S                 */
+#define VHX_SCENE_BOUNDARY 5u     /* src/raytracing/tests.rs:692-703 (brick_boundary): lattice+cube, colour 255*(c%6)/6         */
+#define VHX_SCENE_HEIGHTFIELD 6u  /* seeded value-noise terrain (no reference equivalent; SURVEY.md 8d config 3 secondary)   */
+
+typedef struct vhx_boxtree vhx_boxtree;
+typedef struct vhx_flat vhx_flat;
+
+int vhx_boxtree_new(uint32_t size, uint32_t brick_dim, vhx_boxtree **out);
+void vhx_boxtree_free(vhx_boxtree *tree);
+int vhx_boxtree_set_auto_simplify(vhx_boxtree *tree, int enabled);
+/* albedo packed r | g<<8 | b<<16 | a<<24 */
+int vhx_boxtree_insert(vhx_boxtree *tree, uint32_t x, uint32_t y, uint32_t z, uint32_t kind, uint32_t albedo,
+                       uint32_t data);
+int vhx_boxtree_insert_at_lod(vhx_boxtree *tree, uint32_t x, uint32_t y, uint32_t z, uint32_t insert_size,
+                              uint32_t kind, uint32_t albedo, uint32_t data);
+int vhx_boxtree_update(vhx_boxtree *tree, uint32_t x, uint32_t y, uint32_t z, uint32_t kind, uint32_t albedo,
+                       uint32_t data);
+int vhx_boxtree_get(const vhx_boxtree *tree, uint32_t x, uint32_t y, uint32_t z, uint32_t *kind, uint32_t *albedo,
+                    uint32_t *data);
+int vhx_boxtree_simplify(vhx_boxtree *tree, int recursive);
+/* size, brick_dim, node count (pool length), color and data palette sizes */
+int vhx_boxtree_info(const vhx_boxtree *tree, uint32_t info[5]);
+/* Runs the reference insert loop (x outer, z inner) of a procedural scene on `tree` (for cross-checking the bulk
+ * builder at small sizes; O(size^3) inserts). */
+int vhx_scene_insert(vhx_boxtree *tree, uint32_t scene, uint64_t seed);
+
+/* Flattened trees ------------------------------------------------------------------------------------------- */
+/* Nodes are renumbered breadth-first from the root; bricks and solid values are numbered in that node order. */
+int vhx_boxtree_flatten(const vhx_boxtree *tree, vhx_flat **out);
+int vhx_scene_build(uint32_t scene, uint32_t size, uint32_t brick_dim, uint64_t seed, int threads, vhx_flat **out);
+/* Fills *desc with pointers into the flat object (valid until vhx_flat_free). */
+int vhx_flat_desc(const vhx_flat *flat, vhx_tree_desc *desc);
+void vhx_flat_free(vhx_flat *flat);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VHX_BOXTREE_H */

@@ -1,0 +1,213 @@
+"""GPU parity: libvhx HIP kernels vs the CPU restatement (oracle) on the same inputs.
+
+Bar (BASELINE.json north_star): integer fields (hit value, brick cell, hit voxel, rgba, byte counts) exact; depth,
+impact and normal within |d| <= 1e-5 * max(1, |ref|). The kernels are expected to be bit-exact, so the
+float comparison below checks bits first and reports the tolerance margin only if bits differ.
+"""
+import numpy as np
+import pytest
+
+import voxelhex_amd as vhx
+from tests import kat_cases
+from tests.test_oracle_kats import run_oracle
+from voxelhex_amd import _native as N
+
+pytestmark = pytest.mark.gpu
+
+INT_FIELDS = ("value", "cell", "voxel", "rgba", "bytes")
+FLOAT_FIELDS = ("impact", "normal", "depth")
+TOL = 1e-5
+
+
+def assert_same(got, ref, ctx=""):
+    for k in ref:
+        a, b = np.asarray(got[k]), np.asarray(ref[k])
+        assert a.shape == b.shape, (k, a.shape, b.shape)
+        if k in INT_FIELDS:
+            bad = np.flatnonzero((a != b).reshape(a.shape[0], -1).any(axis=1))
+            assert bad.size == 0, f"{ctx}: {k} differs at {bad.size} rays, first {bad[:5]}: {a[bad[:3]]} vs {b[bad[:3]]}"
+        else:
+            if np.array_equal(a.view(np.uint32), b.view(np.uint32)):
+                continue
+            fin = np.isfinite(b)
+            same_inf = ~fin & (a == b)
+            err = np.abs(a.astype(np.float64) - b.astype(np.float64))
+            lim = TOL * np.maximum(1.0, np.abs(b.astype(np.float64)))
+            ok = same_inf | (fin & (err <= lim)) | (np.isnan(a) & np.isnan(b))
+            assert ok.all(), f"{ctx}: {k} beyond tolerance at {np.count_nonzero(~ok)} entries"
+
+
+def rand_rays(rng, size, n, inside_frac=0.3):
+    S = float(size)
+    o = rng.uniform(-0.5 * S, 1.5 * S, (n, 3)).astype(np.float32)
+    inside = rng.random(n) < inside_frac
+    o[inside] = rng.uniform(0.0, S, (inside.sum(), 3)).astype(np.float32)
+    tgt = rng.uniform(0.0, S, (n, 3)).astype(np.float32)
+    d = tgt - o
+    l = np.sqrt((d[:, 0] * d[:, 0] + d[:, 1] * d[:, 1]) + d[:, 2] * d[:, 2]).astype(np.float32)
+    d = (d / l[:, None]).astype(np.float32)
+    # axis-aligned and signed-zero directions exercise the inf/NaN paths of get_dda_scale_factors
+    k = max(1, n // 50)
+    d[:k] = np.array([0.0, -1.0, 0.0], np.float32)
+    d[k:2 * k] = np.array([-0.0, 0.0, 1.0], np.float32)
+    d[2 * k:3 * k] = np.array([0.6, -0.8, 0.0], np.float32)
+    return o, d
+
+
+@pytest.mark.parametrize("case", kat_cases.cases(), ids=lambda c: c.name)
+def test_reference_kats_on_gpu(gpu, oracle, case):
+    tree, rays = case.build()
+    flat = tree.flatten()
+    gpu.upload(flat)
+    o = np.array([r[0] for r in rays], np.float32).reshape(-1, 3)
+    d = np.array([r[1] for r in rays], np.float32).reshape(-1, 3)
+    got = gpu.trace_rays(o, d, count_bytes=True)
+    ref = oracle.trace_rays(flat, o, d, count_bytes=True)
+    assert_same(got, ref, case.name)
+    res = []
+    for i in range(len(rays)):
+        res.append(None if got["value"][i] == N.VHX_EMPTY else dict(
+            entry=vhx.entry_from_value(got["value"][i], flat.color_palette, flat.data_palette),
+            impact=got["impact"][i], normal=got["normal"][i]))
+    assert case.check(res), f"{case.name} ({case.lines}) failed on the GPU"
+
+
+def test_get_by_ray_api(gpu):
+    """BoxTree.get_by_ray returns (entry, impact, normal) like src/raytracing/cpu.rs:296."""
+    t = vhx.BoxTree(4, 1)
+    t.insert((0, 3, 0), vhx.voxel_data(5))
+    o = np.array([2.0, 2.0, -5.0], np.float32)
+    hit = t.get_by_ray(vhx.Ray(vhx.V3c(*o), vhx.V3c(*kat_cases.normalized(np.array([0, 3, 0], np.float32) - o))))
+    assert hit is not None and hit[0] == vhx.voxel_data(5)
+    miss = t.get_by_ray(vhx.Ray(vhx.V3c(10.0, 10.0, 10.0), vhx.V3c(1.0, 0.0, 0.0)))
+    assert miss is None
+
+
+SCENE_TREES = [(N.VHX_SCENE_LATTICE_CUBE, 32, 8), (N.VHX_SCENE_LATTICE_CUBE, 32, 2), (N.VHX_SCENE_LATTICE_CUBE, 64, 1),
+               (N.VHX_SCENE_LATTICE_CUBE, 256, 4), (N.VHX_SCENE_LATTICE_CUBE, 256, 16), (N.VHX_SCENE_LATTICE_CUBE, 128, 8),
+               (N.VHX_SCENE_BENCH_REGION, 512, 8), (N.VHX_SCENE_HEIGHTFIELD, 256, 4), (N.VHX_SCENE_BOUNDARY, 128, 8)]
+
+
+@pytest.mark.parametrize("scene,size,bd", SCENE_TREES)
+def test_random_rays_vs_oracle(gpu, oracle, scene, size, bd):
+    flat = vhx.FlatTree.build_scene(scene, size, bd)
+    gpu.upload(flat)
+    rng = np.random.default_rng(size * 131 + bd)
+    o, d = rand_rays(rng, size, 20000)
+    got = gpu.trace_rays(o, d, count_bytes=True)
+    ref = oracle.trace_rays(flat, o, d, count_bytes=True)
+    assert_same(got, ref, f"scene {scene} {size}/{bd}")
+    assert (got["value"] != N.VHX_EMPTY).sum() > 100
+
+
+def test_insert_built_tree_with_palettes(gpu, oracle):
+    """Complex / informative / updated voxels and an explicitly simplified tree (Solid bricks, UniformLeaf)."""
+    t = vhx.BoxTree(64, 4)
+    rng = np.random.default_rng(3)
+    for i in range(3000):
+        p = rng.integers(0, 64, 3)
+        k = i % 4
+        e = (vhx.Albedo(int(p[0] * 4), int(p[1] * 4), int(p[2] * 4), 255) if k == 0 else
+             int(1 + i % 7) if k == 1 else (vhx.Albedo(10, 20, 30, 255), 3) if k == 2 else vhx.Albedo.from_u32(0x11223344))
+        t.insert(p, e)
+    for x in range(16, 32):  # a solid 16^3 block, simplified into UniformLeaf/Solid bricks below
+        for y in range(16, 32):
+            for z in range(16, 32):
+                t.insert((x, y, z), vhx.Albedo(200, 100, 50, 255))
+    t.update((17, 17, 17), 9)
+    for flat in (t.flatten(),):
+        gpu.upload(flat)
+        o, d = rand_rays(rng, 64, 20000)
+        assert_same(gpu.trace_rays(o, d, count_bytes=True), oracle.trace_rays(flat, o, d, count_bytes=True), "insert")
+    t.simplify(recursive=True)
+    flat = t.flatten()
+    assert (flat.node_type == N.VHX_NODE_UNIFORM_LEAF).any() or flat.solid_values.size > 0
+    gpu.upload(flat)
+    o, d = rand_rays(rng, 64, 20000)
+    assert_same(gpu.trace_rays(o, d, count_bytes=True), oracle.trace_rays(flat, o, d, count_bytes=True), "simplified")
+
+
+FRAMES = [(N.VHX_SCENE_LATTICE_CUBE, 32, 8, 256, 256), (N.VHX_SCENE_LATTICE_CUBE, 256, 4, 256, 256),
+          (N.VHX_SCENE_LATTICE_CUBE, 256, 16, 192, 128), (N.VHX_SCENE_BENCH_REGION, 512, 8, 128, 128)]
+
+
+@pytest.mark.parametrize("scene,size,bd,w,h", FRAMES)
+def test_primary_frame_glass_vs_oracle(gpu, oracle, scene, size, bd, w, h):
+    flat = vhx.FlatTree.build_scene(scene, size, bd)
+    gpu.upload(flat)
+    tgt = None if scene == N.VHX_SCENE_BENCH_REGION else (size / 2,) * 3
+    cam = vhx.glass_camera(size, w, h, target=tgt)
+    got = gpu.trace_primary(cam, count_bytes=True)
+    ref = oracle.trace_primary(flat, cam, 0, 0, w, h, count_bytes=True)
+    assert_same(got, ref, f"frame {size}/{bd}")
+    assert (got["value"] != N.VHX_EMPTY).sum() > w * h // 20
+
+
+def test_primary_frame_inverse_vp_vs_oracle(gpu, oracle):
+    """examples/gpu_render.rs camera: Viewport(origin (0,100,0), dir (0,0,-10), frustum (10,10,1024), fov 50)."""
+    flat = vhx.FlatTree.build_scene(N.VHX_SCENE_LATTICE_CUBE, 128, 8)
+    gpu.upload(flat)
+    vp = vhx.Viewport((150.0, 140.0, 170.0), tuple(kat_cases.normalized(np.array([-1.0, -0.8, -1.1], np.float32))),
+                      (10.0, 10.0, 1024.0), 50.0)
+    cam = vp.camera(200, 120)
+    got = gpu.trace_primary(cam)
+    ref = oracle.trace_primary(flat, cam, 0, 0, 200, 120)
+    assert_same(got, ref, "inverse-vp")
+    assert (got["value"] != N.VHX_EMPTY).sum() > 1000
+
+
+def test_tiles_and_untile_match_framebuffer(gpu):
+    import torch
+    flat = vhx.FlatTree.build_scene(N.VHX_SCENE_LATTICE_CUBE, 64, 4)
+    gpu.upload(flat)
+    W, H, T, R = 200, 136, 64, 3
+    cam = vhx.glass_camera(64, W, H, target=(32.0, 32.0, 32.0))
+    full = gpu.trace_primary(cam, fields=("rgba",))["rgba"]
+    ntiles = ((W + T - 1) // T) * ((H + T - 1) // T)
+    per = (ntiles + R - 1) // R
+    gathered = torch.zeros(R * per * T * T, dtype=torch.int32, device="cuda")
+    for r in range(R):
+        part = gpu.trace_primary(cam, tile_size=T, tile_start=r, tile_stride=R, layout=N.VHX_LAYOUT_TILES,
+                                 fields=("rgba",))["rgba"]
+        gathered[r * per * T * T: r * per * T * T + part.size] = torch.from_numpy(part.view(np.int32)).cuda()
+    fb = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+    gpu.untile_rgba(gathered.data_ptr(), R, per, T, W, H, fb.data_ptr())
+    gpu.sync()
+    assert np.array_equal(fb.cpu().numpy().view(np.uint32), full)
+
+
+def test_update_range(gpu, oracle):
+    """vhx_update_range (write_range_to_buffer, src/raytracing/bevy/streaming/mod.rs:344-370)."""
+    t = vhx.BoxTree(32, 4)
+    t.insert_scene(N.VHX_SCENE_LATTICE_CUBE)
+    flat = t.flatten()
+    gpu.upload(flat)
+    rng = np.random.default_rng(5)
+    o, d = rand_rays(rng, 32, 5000)
+    before = gpu.trace_rays(o, d)
+    vox = flat.voxels.copy()
+    vox[: vox.size // 2] = N.VHX_EMPTY  # clear half of the bricks
+    gpu.update_range(N.VHX_BUF_VOXELS, 0, vox[: vox.size // 2])
+    after = gpu.trace_rays(o, d)
+    flat.voxels[: vox.size // 2] = N.VHX_EMPTY  # same edit on the host copy, checked by the oracle
+    assert_same(after, oracle.trace_rays(flat, o, d), "update_range")
+    assert not np.array_equal(before["value"], after["value"])
+    with pytest.raises(N.VhxError):
+        gpu.update_range(N.VHX_BUF_VOXELS, vox.size - 4, np.zeros(8, np.uint32))
+
+
+def test_full_size_frame_crops(gpu, oracle):
+    """BASELINE config 3 geometry (1024^3, brick_dim 4, 3840x2160): GPU frame checked on oracle crops, plus
+    run-to-run idempotence of the whole frame."""
+    flat = vhx.FlatTree.build_scene(N.VHX_SCENE_LATTICE_CUBE, 1024, 4)
+    gpu.upload(flat)
+    W, H = 3840, 2160
+    cam = vhx.glass_camera(1024, W, H, target=(512.0, 512.0, 512.0))
+    a = gpu.trace_primary(cam, fields=("value", "cell", "voxel", "depth", "rgba"))
+    b = gpu.trace_primary(cam, fields=("value", "cell", "voxel", "depth", "rgba"))
+    assert_same(a, b, "idempotence")
+    for (x0, y0) in ((0, 0), (1888, 1048), (3776, 2096), (1000, 300)):
+        ref = oracle.trace_primary(flat, cam, x0, y0, 64, 64, fields=("value", "cell", "voxel", "depth", "rgba"))
+        idx = (np.arange(y0, y0 + 64)[:, None] * W + np.arange(x0, x0 + 64)[None, :]).reshape(-1)
+        assert_same({k: v[idx] for k, v in a.items()}, ref, f"crop {x0},{y0}")
+    assert (a["value"] != N.VHX_EMPTY).mean() > 0.2

@@ -1,0 +1,47 @@
+"""The bulk scene builder produces exactly the flattened tree that the reference insert loop produces.
+
+vhx_scene_build (canonical image written directly) vs vhx_scene_insert (BoxTree::insert per voxel, x outer / z
+inner, as the reference examples and tests do) + vhx_boxtree_flatten, compared buffer by buffer.
+"""
+import numpy as np
+import pytest
+
+from voxelhex_amd import BoxTree, FlatTree
+from voxelhex_amd import _native as N
+
+SCENES = [N.VHX_SCENE_LATTICE_CUBE, N.VHX_SCENE_BENCH_REGION, N.VHX_SCENE_LATTICE, N.VHX_SCENE_CUBE,
+          N.VHX_SCENE_BOUNDARY, N.VHX_SCENE_HEIGHTFIELD]
+SIZES = [(4, 1), (16, 1), (8, 2), (32, 2), (16, 4), (64, 4), (32, 8), (64, 16)]
+
+
+def _arrays(f):
+    return dict(node_type=f.node_type, node_ocbits=f.node_ocbits, node_children=f.node_children, voxels=f.voxels,
+                solid_values=f.solid_values, color_palette=f.color_palette, data_palette=f.data_palette)
+
+
+@pytest.mark.parametrize("size,bd", SIZES)
+@pytest.mark.parametrize("scene", SCENES)
+def test_bulk_equals_insert(scene, size, bd):
+    t = BoxTree(size, bd)
+    t.insert_scene(scene, seed=7)
+    a = _arrays(t.flatten())
+    b = _arrays(FlatTree.build_scene(scene, size, bd, seed=7, threads=4))
+    for k in a:
+        assert a[k].shape == b[k].shape, k
+        assert np.array_equal(a[k], b[k]), k
+
+
+def test_scene_s_structure():
+    """Scene S at 64^3, brick_dim 4: leaves are the 16^3 nodes, only Parted bricks, no solid values."""
+    f = FlatTree.build_scene(N.VHX_SCENE_LATTICE_CUBE, 64, 4)
+    assert f.node_type[0] == N.VHX_NODE_INTERNAL
+    assert set(np.unique(f.node_type)) <= {N.VHX_NODE_INTERNAL, N.VHX_NODE_LEAF}
+    assert f.solid_values.size == 0
+    leaves = np.flatnonzero(f.node_type == N.VHX_NODE_LEAF)
+    bricks = f.node_children.reshape(-1, 64)[leaves]
+    assert ((bricks != N.VHX_EMPTY).sum(axis=1) == np.array([bin(int(o)).count("1") for o in f.node_ocbits[leaves]])).all()
+
+
+def test_invalid_sizes():
+    with pytest.raises(Exception):
+        FlatTree.build_scene(N.VHX_SCENE_LATTICE_CUBE, 256, 8)

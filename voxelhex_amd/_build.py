@@ -1,0 +1,70 @@
+"""Builds libvhx.so in-tree (voxelhex_amd/_lib/) for gfx950: host C++ with g++, HIP kernels with hipcc.
+
+Float semantics matter for parity with the reference raytracer: every unit is compiled with -ffp-contract=off and
+without fast-math (IEEE division / sqrt, f32 denormals kept on the GPU).
+"""
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+LIBDIR = os.path.join(HERE, "_lib")
+BUILD = os.path.join(ROOT, "build", "vhx")
+LIB = os.path.join(LIBDIR, "libvhx.so")
+ARCH = os.environ.get("VHX_OFFLOAD_ARCH", "gfx950")
+
+HOST_SRCS = ["boxtree.cpp", "flatten.cpp"]
+DEV_SRCS = ["vhx_device.hip"]
+HEADERS = ["boxtree.hpp", "trace.hpp"]
+
+
+def _hipcc():
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found")
+
+
+def _run(cmd, verbose):
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+
+
+def _stale(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(verbose=False, force=False):
+    os.makedirs(LIBDIR, exist_ok=True)
+    os.makedirs(BUILD, exist_ok=True)
+    inc = os.path.join(ROOT, "include")
+    common_deps = [os.path.join(inc, h) for h in ("vhx.h", "vhx_boxtree.h")] + [os.path.join(CSRC, h) for h in HEADERS]
+    objs = []
+    for src in HOST_SRCS:
+        s = os.path.join(CSRC, src)
+        o = os.path.join(BUILD, src + ".o")
+        if force or _stale(o, [s] + common_deps):
+            _run(["g++", "-O3", "-std=c++17", "-fPIC", "-pthread", "-ffp-contract=off", "-fno-fast-math",
+                  "-Wall", "-Wextra", "-I", inc, "-c", s, "-o", o], verbose)
+        objs.append(o)
+    for src in DEV_SRCS:
+        s = os.path.join(CSRC, src)
+        o = os.path.join(BUILD, src + ".o")
+        if force or _stale(o, [s] + common_deps):
+            _run([_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
+                  "-fno-fast-math", "-Wall", "-I", inc, "-c", s, "-o", o], verbose)
+        objs.append(o)
+    if force or _stale(LIB, objs):
+        _run([_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-pthread", "-o", LIB] + objs, verbose)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(verbose=True, force="--force" in sys.argv)

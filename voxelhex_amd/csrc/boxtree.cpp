@@ -1,0 +1,937 @@
+// Host-side BoxTree<u32>: see boxtree.hpp for the list of restated reference functions.
+// Float arithmetic follows the reference op order (compiled with -ffp-contract=off).
+#include "boxtree.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <functional>
+
+#include "../../include/vhx_boxtree.h"
+
+namespace vhx {
+
+// ---------------------------------------------------------------------------------------------- scalar helpers
+static inline F3 f3(float x, float y, float z) { return F3{x, y, z}; }
+static inline F3 add(F3 a, F3 b) { return f3(a.x + b.x, a.y + b.y, a.z + b.z); }
+static inline F3 sub(F3 a, F3 b) { return f3(a.x - b.x, a.y - b.y, a.z - b.z); }
+static inline F3 mul(F3 a, float s) { return f3(a.x * s, a.y * s, a.z * s); }
+static inline F3 divs(F3 a, float s) { return f3(a.x / s, a.y / s, a.z / s); }
+static inline F3 floor3(F3 a) { return f3(std::floor(a.x), std::floor(a.y), std::floor(a.z)); }
+static inline F3 from_u3(U3 a) { return f3((float)a.x, (float)a.y, (float)a.z); }
+static inline uint32_t as_u32(float f) {  // Rust `as u32` (saturating, NaN -> 0)
+    if (std::isnan(f) || f <= 0.f) return 0;
+    if (f >= 4294967296.0f) return 0xFFFFFFFFu;
+    return (uint32_t)f;
+}
+static inline size_t as_usize(float f) {
+    if (std::isnan(f) || f <= 0.f) return 0;
+    if (f >= 18446744073709551616.0f) return SIZE_MAX;
+    return (size_t)f;
+}
+static inline uint8_t as_u8(float f) {
+    if (std::isnan(f) || f <= 0.f) return 0;
+    if (f >= 255.f) return 255;
+    return (uint8_t)f;
+}
+// From<V3c<f32>> for V3c<u32>/V3c<usize> rounds (src/spatial/math/vector.rs:325-355)
+static inline U3 round_u3(F3 a) { return U3{as_u32(std::round(a.x)), as_u32(std::round(a.y)), as_u32(std::round(a.z))}; }
+// derived PartialOrd on V3c compares lexicographically (src/spatial/math/vector.rs:3)
+static inline bool lex_le(F3 a, F3 b) {
+    if (a.x != b.x) return a.x < b.x;
+    if (a.y != b.y) return a.y < b.y;
+    return a.z <= b.z;
+}
+static inline size_t flat_projection(size_t x, size_t y, size_t z, size_t size) { return x + (y * size) + (z * size * size); }
+
+static float SECTANT_OFFSET_LUT[64][3];
+static const bool kLutInit = [] {
+    for (int x = 0; x < 4; ++x)
+        for (int y = 0; y < 4; ++y)
+            for (int z = 0; z < 4; ++z) {
+                int s = x + y * 4 + z * 16;
+                SECTANT_OFFSET_LUT[s][0] = (float)x / 4.f;
+                SECTANT_OFFSET_LUT[s][1] = (float)y / 4.f;
+                SECTANT_OFFSET_LUT[s][2] = (float)z / 4.f;
+            }
+    return true;
+}();
+const float *sectant_offset(uint32_t s) { return SECTANT_OFFSET_LUT[s]; }
+static inline F3 lut(uint32_t s) { return f3(SECTANT_OFFSET_LUT[s][0], SECTANT_OFFSET_LUT[s][1], SECTANT_OFFSET_LUT[s][2]); }
+
+// offset_sectant, src/spatial/math/mod.rs:27-44
+uint8_t offset_sectant(F3 off, float size) {
+    F3 idx = floor3(divs(mul(off, 4.f), size));
+    idx = f3(std::fmin(idx.x, 3.f), std::fmin(idx.y, 3.f), std::fmin(idx.z, 3.f));
+    return as_u8(idx.x + (idx.y * 4.f) + (idx.z * 16.f));
+}
+// Cube::child_bounds_for, src/spatial/mod.rs:72-77
+Cube child_bounds_for(const Cube &c, uint8_t s) { return Cube{add(c.min, mul(lut(s), c.size)), c.size / 4.f}; }
+static inline bool cube_contains(const Cube &c, F3 p) {  // src/spatial/mod.rs:54-61
+    return p.x >= c.min.x && p.y >= c.min.y && p.z >= c.min.z && p.x < (c.min.x + c.size) &&
+           p.y < (c.min.y + c.size) && p.z < (c.min.z + c.size);
+}
+static inline uint8_t sectant_for(const Cube &c, F3 p) { return offset_sectant(sub(p, c.min), c.size); }
+// matrix_index_for, src/spatial/math/mod.rs:64-96
+static inline std::array<size_t, 3> matrix_index_for(const Cube &b, U3 pos, uint32_t dim) {
+    F3 m = floor3(divs(mul(sub(from_u3(pos), b.min), (float)dim), b.size));
+    return {as_usize(std::round(m.x)), as_usize(std::round(m.y)), as_usize(std::round(m.z))};
+}
+// `(x as f32).log(base).fract() != 0.0` (src/boxtree/mod.rs:189, 194); Rust f32::log = ln(x) / ln(base)
+bool rust_log_is_integral(float x, float base) {
+    float l = std::log(x) / std::log(base);
+    return (l - std::trunc(l)) == 0.f;
+}
+
+// pix_* (src/boxtree/node.rs:260-309)
+static inline uint32_t pix_visual(uint32_t c) { return c | (0xFFFFu << 16); }
+static inline uint32_t pix_informal(uint32_t d) { return 0xFFFFu | (d << 16); }
+static inline uint32_t pix_complex(uint32_t c, uint32_t d) { return c | (d << 16); }
+static inline uint32_t pix_color_index(uint32_t v) { return v & 0xFFFFu; }
+static inline uint32_t pix_data_index(uint32_t v) { return (v & 0xFFFF0000u) >> 16; }
+static inline bool pix_color_is_some(uint32_t v) { return pix_color_index(v) < 0xFFFFu; }
+static inline bool pix_data_is_some(uint32_t v) { return pix_data_index(v) != 0xFFFFu; }
+
+// execute_for_relevant_sectants, src/boxtree/iterate.rs:40-121
+using SectantFn = std::function<void(U3, U3, uint8_t, const Cube &)>;
+static std::array<size_t, 3> execute_for_relevant_sectants(const Cube &nb, U3 position_, uint32_t update_size_,
+                                                           const SectantFn &fun) {
+    if ((float)position_.x > nb.min.x + nb.size || (float)position_.y > nb.min.y + nb.size ||
+        (float)position_.z > nb.min.z + nb.size)
+        return {0, 0, 0};
+    F3 position = f3(std::fmax((float)position_.x, nb.min.x), std::fmax((float)position_.y, nb.min.y),
+                     std::fmax((float)position_.z, nb.min.z));
+    F3 update_size = sub(add(from_u3(position_), f3((float)update_size_, (float)update_size_, (float)update_size_)), position);
+    float cell_size = nb.size / 4.f;
+    F3 shifted = position;
+    while (shifted.x <= (position.x + update_size.x)) {
+        shifted.y = position.y;
+        while (shifted.y <= (position.y + update_size.y)) {
+            shifted.z = position.z;
+            while (shifted.z <= (position.z + update_size.z)) {
+                if (!cube_contains(nb, shifted)) {
+                    shifted.z += cell_size;
+                    continue;
+                }
+                uint8_t s = sectant_for(nb, shifted);
+                Cube tb = child_bounds_for(nb, s);
+                tb = Cube{floor3(tb.min), std::ceil(tb.size)};
+                F3 pit = f3(std::fmax(position.x, tb.min.x), std::fmax(position.y, tb.min.y), std::fmax(position.z, tb.min.z));
+                F3 remains = sub(add(position, update_size), pit);
+                F3 uit = sub(add(tb.min, f3(tb.size, tb.size, tb.size)), pit);
+                uit = f3(std::fmin(uit.x, remains.x), std::fmin(uit.y, remains.y), std::fmin(uit.z, remains.z));
+                if (0.f < uit.x && 0.f < uit.y && 0.f < uit.z) fun(round_u3(pit), round_u3(uit), s, tb);
+                shifted.z += cell_size;
+            }
+            shifted.y += cell_size;
+        }
+        shifted.x += cell_size;
+    }
+    return {as_usize(std::round(update_size.x)), as_usize(std::round(update_size.y)), as_usize(std::round(update_size.z))};
+}
+
+// ---------------------------------------------------------------------------------------------- ObjectPool
+bool ObjectPool::try_set_next_available() {  // src/object_pool.rs:168-183
+    if ((first_available_ + 1) < buffer_.size() && !reserved_[first_available_]) return true;
+    if ((first_available_ + 1) < buffer_.size() && !reserved_[first_available_ + 1]) {
+        first_available_ += 1;
+        return true;
+    }
+    return false;
+}
+size_t ObjectPool::allocate() {  // src/object_pool.rs:198-222
+    size_t key;
+    if (try_set_next_available()) {
+        size_t fa = first_available_;
+        reserved_[fa] = true;
+        try_set_next_available();
+        key = fa;
+    } else {
+        reserved_.push_back(true);
+        buffer_.emplace_back();
+        key = buffer_.size() - 1;
+    }
+    try_set_next_available();
+    return key;
+}
+size_t ObjectPool::push(Node item) {
+    size_t key = allocate();
+    buffer_[key] = std::move(item);
+    return key;
+}
+bool ObjectPool::free(size_t key) {
+    if (!key_is_valid(key)) return false;
+    reserved_[key] = false;
+    first_available_ = std::min(first_available_, key);
+    return true;
+}
+
+// ---------------------------------------------------------------------------------------------- node constructors
+static Node empty_node() { return Node{}; }
+static Node uniform_solid_node(uint32_t v) {
+    Node n;
+    n.content = Content::UniformLeaf;
+    n.bricks.resize(1);
+    n.bricks[0].kind = BrickKind::Solid;
+    n.bricks[0].solid = v;
+    n.occupied_bits = ~0ull;
+    return n;
+}
+static Node uniform_parted_node(std::vector<uint32_t> brick, uint64_t occ) {
+    Node n;
+    n.content = Content::UniformLeaf;
+    n.bricks.resize(1);
+    n.bricks[0].kind = BrickKind::Parted;
+    n.bricks[0].parted = std::move(brick);
+    n.occupied_bits = occ;
+    return n;
+}
+static Brick parted(std::vector<uint32_t> v) {
+    Brick b;
+    b.kind = BrickKind::Parted;
+    b.parted = std::move(v);
+    return b;
+}
+static Brick solid(uint32_t v) {
+    Brick b;
+    b.kind = BrickKind::Solid;
+    b.solid = v;
+    return b;
+}
+
+// ---------------------------------------------------------------------------------------------- BoxTree
+int BoxTree::create(uint32_t size, uint32_t bd, BoxTree **out) {  // src/boxtree/mod.rs:188-219
+    if (0 == size || !rust_log_is_integral((float)bd, 2.0f)) return VHX_E_TREE_INVALID_BRICK_DIMENSION;
+    if (bd > size || 0 == size || !rust_log_is_integral((float)size / (float)bd, 4.0f)) return VHX_E_TREE_INVALID_SIZE;
+    if (size < bd * 4u) return VHX_E_TREE_INVALID_STRUCTURE;
+    BoxTree *t = new BoxTree();
+    t->boxtree_size = size;
+    t->brick_dim = bd;
+    size_t root = t->nodes.push(empty_node());
+    (void)root;
+    *out = t;
+    return 0;
+}
+
+bool BoxTree::points_to_empty(uint32_t v) const {  // src/boxtree/node.rs:311-333
+    uint32_t ci = pix_color_index(v), di = pix_data_index(v);
+    bool color_none = !pix_color_is_some(v) || ci >= color_palette.size() || ((color_palette[ci] >> 24) & 0xFFu) == 0;
+    bool data_none = !pix_data_is_some(v) || di >= data_palette.size() || data_palette[di] == 0;
+    return color_none && data_none;
+}
+
+size_t BoxTree::child(size_t key, uint8_t s) const {  // src/boxtree/node.rs:214-219
+    const Node &n = nodes.get(key);
+    return n.has_children ? (size_t)n.children[s] : SIZE_MAX;
+}
+uint32_t &BoxTree::child_mut(size_t key, size_t index) {  // src/boxtree/node.rs:222-230
+    Node &n = nodes.get(key);
+    if (!n.has_children) {
+        n.has_children = true;
+        n.children.fill(kEmpty32);
+    }
+    return n.children[index];
+}
+
+static bool entry_is_none(const Entry &e) {  // src/boxtree/mod.rs:99-106
+    switch (e.kind) {
+        case VHX_ENTRY_EMPTY: return true;
+        case VHX_ENTRY_VISUAL: return ((e.albedo >> 24) & 0xFFu) == 0;
+        case VHX_ENTRY_INFORMATIVE: return e.data == 0;
+        default: return ((e.albedo >> 24) & 0xFFu) == 0 && e.data == 0;
+    }
+}
+
+uint32_t BoxTree::add_to_palette(Entry e) {  // src/boxtree/update/mod.rs:39-120
+    auto color = [&](uint32_t albedo) {
+        size_t potential = color_index_.size();
+        auto it = color_index_.find(albedo);
+        if (it == color_index_.end()) {
+            color_index_.emplace(albedo, potential);
+            color_palette.push_back(albedo);
+            return potential;
+        }
+        return it->second;
+    };
+    auto data = [&](uint32_t d) {
+        size_t potential = data_index_.size();
+        auto it = data_index_.find(d);
+        if (it == data_index_.end()) {
+            data_index_.emplace(d, potential);
+            data_palette.push_back(d);
+            return potential;
+        }
+        return it->second;
+    };
+    switch (e.kind) {
+        case VHX_ENTRY_EMPTY: return kEmpty32;
+        case VHX_ENTRY_VISUAL:
+            if (e.albedo == 0) return kEmpty32;
+            return pix_visual((uint32_t)color(e.albedo));
+        case VHX_ENTRY_INFORMATIVE:
+            if (e.data == 0) return kEmpty32;
+            return pix_informal((uint32_t)data(e.data));
+        default:
+            if (e.albedo == 0) return add_to_palette(Entry{VHX_ENTRY_INFORMATIVE, 0, e.data});
+            if (e.data == 0) return add_to_palette(Entry{VHX_ENTRY_VISUAL, e.albedo, 0});
+            {
+                size_t ci = color(e.albedo);
+                size_t di = data(e.data);
+                return pix_complex((uint32_t)ci, (uint32_t)di);
+            }
+    }
+}
+
+// ------------------------------------------------------------------------------------- BrickData (node.rs:34-145)
+uint64_t BoxTree::calculate_brick_occupied_bits(const std::vector<uint32_t> &brick) const {
+    uint64_t bitmap = 0;
+    size_t bd = brick_dim;
+    for (size_t x = 0; x < bd; ++x)
+        for (size_t y = 0; y < bd; ++y)
+            for (size_t z = 0; z < bd; ++z) {
+                if (points_to_empty(brick[flat_projection(x, y, z, bd)])) continue;
+                // set_occupied_bitmap_value(&V3c(x,y,z), 1, bd, true, bitmap), src/spatial/math/mod.rs:104-155
+                if (bd == 1) {
+                    bitmap = ~0ull;
+                    continue;
+                }
+                size_t count = (size_t)std::ceil((float)1 * 4.f / (float)bd);
+                size_t sx = as_usize(std::round(std::floor((float)(x * 4) / (float)bd)));
+                size_t sy = as_usize(std::round(std::floor((float)(y * 4) / (float)bd)));
+                size_t sz = as_usize(std::round(std::floor((float)(z * 4) / (float)bd)));
+                for (size_t ax = sx; ax < std::min(sx + count, (size_t)4); ++ax)
+                    for (size_t ay = sy; ay < std::min(sy + count, (size_t)4); ++ay)
+                        for (size_t az = sz; az < std::min(sz + count, (size_t)4); ++az)
+                            bitmap |= 1ull << offset_sectant(f3((float)ax, (float)ay, (float)az), 4.f);
+            }
+    return bitmap;
+}
+uint64_t BoxTree::calculate_occupied_bits(const Brick &b) const {
+    switch (b.kind) {
+        case BrickKind::Empty: return 0;
+        case BrickKind::Solid: return points_to_empty(b.solid) ? 0 : ~0ull;
+        default: return calculate_brick_occupied_bits(b.parted);
+    }
+}
+static const uint32_t *homogeneous(const Brick &b) {
+    switch (b.kind) {
+        case BrickKind::Empty: return nullptr;
+        case BrickKind::Solid: return &b.solid;
+        default:
+            for (uint32_t v : b.parted)
+                if (v != b.parted[0]) return nullptr;
+            return &b.parted[0];
+    }
+}
+bool BoxTree::brick_contains_nothing(const Brick &b) const {
+    switch (b.kind) {
+        case BrickKind::Empty: return true;
+        case BrickKind::Solid: return points_to_empty(b.solid);
+        default:
+            for (uint32_t v : b.parted)
+                if (!points_to_empty(v)) return false;
+            return true;
+    }
+}
+bool BoxTree::brick_simplify(Brick &b) const {
+    const uint32_t *h = homogeneous(b);
+    if (!h) return false;
+    uint32_t v = *h;
+    if (points_to_empty(v)) {
+        b = Brick{};
+    } else {
+        b = solid(v);
+    }
+    return true;
+}
+bool BoxTree::content_is_all(const Node &n, uint32_t data) const {  // node.rs:424-458
+    auto brick_is = [&](const Brick &b) {
+        switch (b.kind) {
+            case BrickKind::Empty: return false;
+            case BrickKind::Solid: return b.solid == data;
+            default: {
+                const uint32_t *h = homogeneous(b);
+                return h && *h == data;
+            }
+        }
+    };
+    switch (n.content) {
+        case Content::UniformLeaf: return brick_is(n.bricks[0]);
+        case Content::Leaf:
+            for (const Brick &b : n.bricks)
+                if (!brick_is(b)) return false;
+            return true;
+        default: return false;
+    }
+}
+
+// ------------------------------------------------------------------------------------- detail.rs
+bool BoxTree::node_empty_at(size_t key, uint8_t s) const {  // detail.rs:156-224
+    const Node &n = nodes.get(key);
+    switch (n.content) {
+        case Content::Nothing: return true;
+        case Content::Leaf: {
+            const Brick &b = n.bricks[s];
+            if (b.kind == BrickKind::Empty) return true;
+            if (b.kind == BrickKind::Solid) return points_to_empty(b.solid);
+            const uint32_t *h = homogeneous(b);
+            return h ? points_to_empty(*h) : false;
+        }
+        case Content::UniformLeaf: {
+            const Brick &b = n.bricks[0];
+            if (b.kind == BrickKind::Empty) return true;
+            if (b.kind == BrickKind::Solid) return points_to_empty(b.solid);
+            const float *o = sectant_offset(s);
+            F3 cs = floor3(f3(o[0] * (float)brick_dim, o[1] * (float)brick_dim, o[2] * (float)brick_dim));
+            U3 start = round_u3(cs);
+            size_t check = as_usize(std::fmax((float)brick_dim / 4.f, 1.f));
+            for (size_t x = start.x; x < start.x + check; ++x)
+                for (size_t y = start.y; y < start.y + check; ++y)
+                    for (size_t z = start.z; z < start.z + check; ++z)
+                        if (!points_to_empty(b.parted[flat_projection(x, y, z, brick_dim)])) return false;
+            return true;
+        }
+        default: {
+            size_t ck = child(key, s);
+            if (!nodes.key_is_valid(ck)) return true;
+            for (uint32_t cs = 0; cs < kChildren; ++cs)
+                if (!node_empty_at(ck, (uint8_t)cs)) return false;
+            return true;
+        }
+    }
+}
+bool BoxTree::compare_nodes(size_t l, size_t r) const {  // detail.rs:229-243, node.rs:460-479
+    if (nodes.key_is_valid(l) != nodes.key_is_valid(r)) return false;
+    if (!nodes.key_is_valid(l)) return true;
+    const Node &a = nodes.get(l), &b = nodes.get(r);
+    switch (a.content) {
+        case Content::Nothing: return b.content == Content::Nothing;
+        case Content::Internal: return false;
+        case Content::UniformLeaf: return b.content == Content::UniformLeaf && a.bricks[0] == b.bricks[0];
+        default: return b.content == Content::Leaf && a.bricks == b.bricks;
+    }
+}
+void BoxTree::deallocate_children_of(size_t key) {  // detail.rs:352-370
+    if (!nodes.key_is_valid(key)) return;
+    std::vector<size_t> to_free;
+    const Node &n = nodes.get(key);
+    if (n.has_children)
+        for (uint32_t c : n.children)
+            if (nodes.key_is_valid(c)) to_free.push_back(c);
+    for (size_t c : to_free) {
+        deallocate_children_of(c);
+        nodes.free(c);
+    }
+}
+Brick BoxTree::try_brick_from_node(size_t key) const {  // detail.rs:340-349
+    if (!nodes.key_is_valid(key)) return Brick{};
+    const Node &n = nodes.get(key);
+    if (n.content == Content::UniformLeaf) return n.bricks[0];
+    return Brick{};
+}
+
+std::array<std::vector<uint32_t>, kChildren> BoxTree::dilute_brick_data(const std::vector<uint32_t> &bdata) const {
+    // src/boxtree/update/mod.rs:478-555
+    std::array<std::vector<uint32_t>, kChildren> result;
+    size_t bd = brick_dim, n3 = bd * bd * bd;
+    if (bd == 1) {
+        for (auto &r : result) r = bdata;
+        return result;
+    }
+    if (bd == 2) {
+        for (uint32_t s = 0; s < kChildren; ++s) {
+            // octant_in_sectants (src/spatial/math/mod.rs:56-59)
+            const float *o = sectant_offset(s);
+            float ox = o[0] * 2.f, oy = o[1] * 2.f, oz = o[2] * 2.f;
+            size_t oct = (size_t)(ox >= 1.f) + (size_t)(oz >= 1.f) * 2 + (size_t)(oy >= 1.f) * 4;
+            result[s].assign(n3, bdata[oct]);
+        }
+        return result;
+    }
+    for (uint32_t s = 0; s < kChildren; ++s) result[s].assign(n3, bdata[s]);
+    if (bd == 4) return result;
+    for (uint32_t s = 0; s < kChildren; ++s) {
+        const float *o = sectant_offset(s);
+        U3 off = round_u3(f3(o[0] * (float)bd, o[1] * (float)bd, o[2] * (float)bd));
+        std::vector<uint32_t> nb(n3, bdata[flat_projection(off.x, off.y, off.z, bd)]);
+        for (size_t x = 0; x < bd; ++x)
+            for (size_t y = 0; y < bd; ++y)
+                for (size_t z = 0; z < bd; ++z) {
+                    if (x < 4 && y < 4 && z < 4) continue;
+                    nb[flat_projection(x, y, z, bd)] = bdata[flat_projection(off.x + x / 4, off.y + y / 4, off.z + z / 4, bd)];
+                }
+        result[s] = std::move(nb);
+    }
+    return result;
+}
+
+void BoxTree::update_brick(bool overwrite, std::vector<uint32_t> &brick, const Cube &bb, U3 position, U3 size,
+                           uint32_t data) const {  // src/boxtree/update/mod.rs:564-603
+    auto mi = matrix_index_for(bb, position, brick_dim);
+    size_t bd = brick_dim;
+    for (size_t x = mi[0]; x < std::min(mi[0] + size.x, bd); ++x)
+        for (size_t y = mi[1]; y < std::min(mi[1] + size.y, bd); ++y)
+            for (size_t z = mi[2]; z < std::min(mi[2] + size.z, bd); ++z) {
+                size_t f = flat_projection(x, y, z, bd);
+                if (overwrite) {
+                    brick[f] = data;
+                } else {
+                    if (pix_color_is_some(data)) brick[f] = (brick[f] & 0xFFFF0000u) | (data & 0x0000FFFFu);
+                    if (pix_data_is_some(data)) brick[f] = (brick[f] & 0x0000FFFFu) | (data & 0xFFFF0000u);
+                }
+            }
+}
+
+void BoxTree::subdivide_leaf_to_nodes(size_t key, size_t target_sectant) {  // detail.rs:248-337
+    Node &n0 = nodes.get(key);
+    Content content = n0.content;
+    std::vector<Brick> bricks = std::move(n0.bricks);
+    n0.content = Content::Internal;
+    n0.bricks.clear();
+    std::array<uint32_t, kChildren> new_children;
+    new_children.fill(kEmpty32);
+    if (content == Content::Leaf) {
+        for (size_t s = 0; s < kChildren; ++s) {
+            Brick brick = std::move(bricks[s]);
+            bricks[s] = Brick{};  // std::mem::swap leaves BrickData::Empty behind
+            if (!brick_contains_nothing(brick) || s == target_sectant)
+                new_children[s] = (uint32_t)nodes.push(empty_node());
+            if (brick.kind == BrickKind::Solid) {
+                Node &c = nodes.get(new_children[s]);
+                c.occupied_bits = ~0ull;
+                c.content = Content::UniformLeaf;
+                c.bricks.assign(1, solid(brick.solid));
+            } else if (brick.kind == BrickKind::Parted) {
+                // detail.rs:283-289 computes the occupancy of bricks[sectant] after the swap, i.e. of Empty -> 0
+                uint64_t occ = calculate_occupied_bits(bricks[s]);
+                Node &c = nodes.get(new_children[s]);
+                c.occupied_bits = occ;
+                c.content = Content::UniformLeaf;
+                c.bricks.assign(1, parted(brick.parted));
+            }
+        }
+    } else if (content == Content::UniformLeaf) {
+        Brick brick = std::move(bricks[0]);
+        if (brick.kind == BrickKind::Empty) {
+            new_children[target_sectant] = (uint32_t)nodes.push(empty_node());
+        } else if (brick.kind == BrickKind::Solid) {
+            for (size_t s = 0; s < kChildren; ++s) new_children[s] = (uint32_t)nodes.push(uniform_solid_node(brick.solid));
+        } else {
+            auto cb = dilute_brick_data(brick.parted);
+            for (size_t s = 0; s < kChildren; ++s) {
+                uint64_t occ = calculate_brick_occupied_bits(cb[s]);
+                new_children[s] = (uint32_t)nodes.push(uniform_parted_node(std::move(cb[s]), occ));
+            }
+        }
+    }  // Nothing / Internal: the reference panics
+    Node &n = nodes.get(key);
+    n.has_children = true;
+    n.children = new_children;
+}
+
+size_t BoxTree::get_node_internal(size_t key, Cube &bounds, F3 position) const {  // iterate.rs:293-343
+    for (;;) {
+        const Node &n = nodes.get(key);
+        if (n.content != Content::Internal) return key;
+        uint8_t s = sectant_for(bounds, position);
+        size_t c = child(key, s);
+        if (!nodes.key_is_valid(c)) return key;
+        key = c;
+        bounds = child_bounds_for(bounds, s);
+    }
+}
+
+uint32_t BoxTree::get_raw(U3 pos) const {  // src/boxtree/mod.rs:247-317
+    Cube bounds{f3(0.f, 0.f, 0.f), (float)boxtree_size};
+    F3 p = from_u3(pos);
+    if (!cube_contains(bounds, p)) return kEmpty32;
+    size_t key = get_node_internal(0, bounds, p);
+    const Node &n = nodes.get(key);
+    switch (n.content) {
+        case Content::Leaf: {
+            uint8_t s = sectant_for(bounds, p);
+            const Brick &b = n.bricks[s];
+            if (b.kind == BrickKind::Empty) return kEmpty32;
+            if (b.kind == BrickKind::Solid) return b.solid;
+            Cube cb = child_bounds_for(bounds, s);
+            auto mi = matrix_index_for(cb, pos, brick_dim);
+            uint32_t v = b.parted[flat_projection(mi[0], mi[1], mi[2], brick_dim)];
+            return points_to_empty(v) ? kEmpty32 : v;
+        }
+        case Content::UniformLeaf: {
+            const Brick &b = n.bricks[0];
+            if (b.kind == BrickKind::Empty) return kEmpty32;
+            if (b.kind == BrickKind::Solid) return b.solid;
+            auto mi = matrix_index_for(bounds, pos, brick_dim);
+            return b.parted[flat_projection(mi[0], mi[1], mi[2], brick_dim)];
+        }
+        default: return kEmpty32;
+    }
+}
+Entry BoxTree::get(U3 pos) const {  // pix_get_ref, src/boxtree/node.rs:335-373
+    uint32_t v = get_raw(pos);
+    bool cn = !pix_color_is_some(v), dn = !pix_data_is_some(v);
+    Entry e{VHX_ENTRY_EMPTY, 0, 0};
+    if (cn && dn) return e;
+    if (!cn) e.albedo = pix_color_index(v) < color_palette.size() ? color_palette[pix_color_index(v)] : 0;
+    if (!dn) e.data = pix_data_index(v) < data_palette.size() ? data_palette[pix_data_index(v)] : 0;
+    e.kind = dn ? VHX_ENTRY_VISUAL : (cn ? VHX_ENTRY_INFORMATIVE : VHX_ENTRY_COMPLEX);
+    return e;
+}
+
+bool BoxTree::leaf_update(bool overwrite, size_t key, const Cube &node_bounds, const Cube &target_bounds, size_t tcs,
+                          U3 position, U3 size, uint32_t tc) {  // src/boxtree/update/mod.rs:144-464
+    Node &node = nodes.get(key);
+    switch (node.content) {
+        case Content::Leaf: {
+            Brick &b = node.bricks[tcs];
+            if (b.kind == BrickKind::Empty) {
+                std::vector<uint32_t> nb((size_t)brick_dim * brick_dim * brick_dim, kEmpty32);
+                update_brick(overwrite, nb, target_bounds, position, size, tc);
+                nodes.get(key).bricks[tcs] = parted(std::move(nb));
+                return true;
+            }
+            if (b.kind == BrickKind::Solid) {
+                uint32_t v = b.solid;
+                if ((points_to_empty(tc) && !points_to_empty(v)) || (!points_to_empty(tc) && v != tc)) {
+                    std::vector<uint32_t> nb((size_t)brick_dim * brick_dim * brick_dim, v);
+                    update_brick(overwrite, nb, target_bounds, position, size, tc);
+                    nodes.get(key).bricks[tcs] = parted(std::move(nb));
+                    return true;
+                }
+                return false;
+            }
+            update_brick(overwrite, b.parted, target_bounds, position, size, tc);
+            return true;
+        }
+        case Content::UniformLeaf: {
+            Brick &mat = node.bricks[0];
+            if (mat.kind == BrickKind::Empty) {
+                if (!points_to_empty(tc)) {
+                    std::vector<Brick> leaf(kChildren);
+                    std::vector<uint32_t> nb((size_t)brick_dim * brick_dim * brick_dim, add_to_palette(Entry{VHX_ENTRY_EMPTY, 0, 0}));
+                    update_brick(overwrite, nb, target_bounds, position, size, tc);
+                    leaf[tcs] = parted(std::move(nb));
+                    Node &n = nodes.get(key);
+                    n.content = Content::Leaf;
+                    n.bricks = std::move(leaf);
+                    return true;
+                }
+                break;  // falls through to the recursive call below (unreachable for insert: data is never empty)
+            }
+            if (mat.kind == BrickKind::Solid) {
+                uint32_t v = mat.solid;
+                if (points_to_empty(tc) && points_to_empty(v)) {
+                    node.content = Content::Nothing;
+                    node.bricks.clear();
+                    return false;
+                }
+                if ((!points_to_empty(tc) && v != tc) || (points_to_empty(tc) && !points_to_empty(v))) {
+                    mat = parted(std::vector<uint32_t>((size_t)brick_dim * brick_dim * brick_dim, v));
+                    return leaf_update(overwrite, key, node_bounds, target_bounds, tcs, position, size, tc);
+                }
+                return false;
+            }
+            {
+                auto mi = matrix_index_for(node_bounds, position, brick_dim);
+                size_t f = flat_projection(mi[0], mi[1], mi[2], brick_dim);
+                if (1 < brick_dim && ((points_to_empty(tc) && points_to_empty(mat.parted[f])) ||
+                                      (!points_to_empty(tc) && mat.parted[f] == tc)))
+                    return false;
+                if (node_bounds.size <= (float)brick_dim && brick_dim > 1) {
+                    update_brick(overwrite, mat.parted, node_bounds, position, size, tc);
+                    return true;
+                }
+                std::vector<Brick> leaf(kChildren);
+                std::vector<uint32_t> taken = std::move(mat.parted);
+                mat.parted.clear();
+                auto cb = dilute_brick_data(taken);
+                bool updated = false;
+                for (size_t s = 0; s < kChildren; ++s) {
+                    if (s == tcs) {
+                        update_brick(overwrite, cb[s], target_bounds, position, size, tc);
+                        updated = true;
+                    }
+                    leaf[s] = parted(std::move(cb[s]));
+                }
+                Node &n = nodes.get(key);
+                n.content = Content::Leaf;
+                n.bricks = std::move(leaf);
+                return updated;
+            }
+        }
+        case Content::Internal: {
+            node.has_children = false;  // children = NoChildren before the bricks are gathered (update/mod.rs:420)
+            std::vector<Brick> leaf(kChildren);
+            for (size_t s = 0; s < kChildren; ++s) leaf[s] = try_brick_from_node(child(key, (uint8_t)s));
+            Node &n = nodes.get(key);
+            n.content = Content::Leaf;
+            n.bricks = std::move(leaf);
+            deallocate_children_of(key);
+            return leaf_update(overwrite, key, node_bounds, target_bounds, tcs, position, size, tc);
+        }
+        case Content::Nothing: {
+            std::vector<Brick> leaf(kChildren);
+            for (size_t s = 0; s < kChildren; ++s) leaf[s] = try_brick_from_node(child(key, (uint8_t)s));
+            Node &n = nodes.get(key);
+            n.content = Content::Leaf;
+            n.bricks = std::move(leaf);
+            deallocate_children_of(key);
+            return leaf_update(overwrite, key, node_bounds, target_bounds, tcs, position, size, tc);
+        }
+    }
+    return leaf_update(overwrite, key, node_bounds, target_bounds, tcs, position, size, tc);
+}
+
+void BoxTree::post_process_node_insert(size_t key, const Cube &nb, const std::array<size_t, 3> &aus, U3 pos,
+                                       uint32_t insert_size) {  // src/boxtree/update/insert.rs:411-495
+    Node &n = nodes.get(key);
+    if (n.content == Content::Nothing) {
+        n.content = Content::Internal;
+        n.occupied_bits = 0;
+    }
+    uint64_t occ = n.occupied_bits;
+    size_t ns = as_usize(nb.size);
+    if (ns == aus[0] && ns == aus[1] && ns == aus[2]) {
+        occ = ~0ull;
+    } else {
+        execute_for_relevant_sectants(nb, pos, insert_size, [&](U3, U3, uint8_t cs, const Cube &) {
+            if (!node_empty_at(key, cs)) occ |= 1ull << cs;
+        });
+    }
+    nodes.get(key).occupied_bits = occ;
+}
+
+int BoxTree::insert_at_lod_internal(bool overwrite, U3 pos_u32, uint32_t insert_size, Entry data) {
+    // src/boxtree/update/insert.rs:73-407
+    Cube root{f3(0.f, 0.f, 0.f), (float)boxtree_size};
+    F3 position = from_u3(pos_u32);
+    if (!cube_contains(root, position)) return VHX_E_TREE_INVALID_POSITION;
+    if (entry_is_none(data) || insert_size == 0) return 0;
+
+    std::vector<std::pair<size_t, uint8_t>> node_stack{{0, sectant_for(root, position)}};
+    std::vector<Cube> bounds_stack{root};
+    std::vector<uint8_t> modified_bottom;
+    std::array<size_t, 3> actual_update_size{0, 0, 0};
+    bool updated = false;
+    uint32_t tc = add_to_palette(data);
+    for (;;) {
+        size_t cur = node_stack.back().first;
+        uint8_t tcs = node_stack.back().second;
+        Cube cb = bounds_stack.back();
+        Cube tb = child_bounds_for(cb, tcs);
+        size_t tck = child(cur, tcs);
+
+        if (tb.size > 1.f && insert_size > 1 && tb.size <= (float)insert_size && lex_le(position, tb.min)) {
+            actual_update_size = execute_for_relevant_sectants(cb, pos_u32, insert_size, [&](U3 pit, U3 uit, uint8_t cs, const Cube &ctb) {
+                U3 ctb_min = round_u3(ctb.min);
+                uint32_t csz = as_u32(ctb.size);
+                if (pit.x == ctb_min.x && pit.y == ctb_min.y && pit.z == ctb_min.z && uit.x == csz && uit.y == csz && uit.z == csz) {
+                    updated = true;
+                    tck = child(cur, cs);
+                    if (nodes.get(cur).content == Content::Leaf || nodes.get(cur).content == Content::UniformLeaf) {
+                        subdivide_leaf_to_nodes(cur, cs);
+                        tck = child(cur, cs);
+                    }
+                    if (nodes.key_is_valid(tck)) {
+                        deallocate_children_of(tck);
+                        Node &t = nodes.get(tck);
+                        t.content = Content::UniformLeaf;
+                        t.bricks.assign(1, solid(tc));
+                        t.occupied_bits = ~0ull;
+                    } else {
+                        uint32_t nk = (uint32_t)nodes.push(uniform_solid_node(tc));
+                        child_mut(cur, cs) = nk;
+                    }
+                    modified_bottom.push_back(cs);
+                }
+            });
+            break;
+        }
+
+        if (tb.size > 1.f && (tb.size > (float)brick_dim || nodes.key_is_valid(tck))) {
+            if (nodes.key_is_valid(tck)) {
+                node_stack.push_back({child(cur, tcs), sectant_for(tb, position)});
+                bounds_stack.push_back(tb);
+            } else {
+                const Node &cn = nodes.get(cur);
+                if (cn.content == Content::Leaf || cn.content == Content::UniformLeaf) {
+                    bool target_match = false;
+                    if (cn.content == Content::UniformLeaf) {
+                        const Brick &b = cn.bricks[0];
+                        if (b.kind == BrickKind::Solid) target_match = b.solid == tc;
+                        else if (b.kind == BrickKind::Parted) {
+                            auto mi = matrix_index_for(cb, round_u3(position), brick_dim);
+                            target_match = b.parted[flat_projection(mi[0], mi[1], mi[2], brick_dim)] == tc;
+                        }
+                    } else {
+                        const Brick &b = cn.bricks[tcs];
+                        if (b.kind == BrickKind::Solid) target_match = b.solid == tc;
+                        else if (b.kind == BrickKind::Parted) {
+                            auto mi = matrix_index_for(tb, round_u3(position), brick_dim);
+                            target_match = b.parted[flat_projection(mi[0], mi[1], mi[2], brick_dim)] == tc;
+                        }
+                    }
+                    if (target_match || content_is_all(cn, tc)) break;
+                    subdivide_leaf_to_nodes(cur, tcs);
+                    node_stack.push_back({child(cur, tcs), sectant_for(tb, position)});
+                    bounds_stack.push_back(tb);
+                } else {
+                    Node &n = nodes.get(cur);
+                    if (n.content == Content::Nothing) {
+                        n.content = Content::Internal;
+                        n.occupied_bits = 0;
+                    }
+                    size_t nc = nodes.push(empty_node());
+                    child_mut(cur, tcs) = (uint32_t)nc;
+                    node_stack.push_back({nc, sectant_for(tb, position)});
+                    bounds_stack.push_back(tb);
+                }
+            }
+        } else {
+            actual_update_size = execute_for_relevant_sectants(cb, pos_u32, insert_size, [&](U3 pit, U3 uit, uint8_t cs, const Cube &ctb) {
+                updated |= leaf_update(overwrite, cur, cb, ctb, cs, pit, uit, tc);
+                modified_bottom.push_back(cs);
+            });
+            break;
+        }
+    }
+
+    if (!updated) return 0;
+    bool simplifyable = auto_simplify;
+    for (uint8_t mbs : modified_bottom) {
+        size_t node_key = node_stack.back().first;
+        uint8_t original = node_stack.back().second;
+        Cube nbounds = bounds_stack.back();
+        size_t ck = child(node_key, mbs);
+        if (nodes.key_is_valid(ck)) {
+            Cube cbounds = child_bounds_for(nbounds, mbs);
+            node_stack.push_back({ck, sectant_for(cbounds, f3(std::fmax(position.x, cbounds.min.x),
+                                                              std::fmax(position.y, cbounds.min.y),
+                                                              std::fmax(position.z, cbounds.min.z)))});
+            post_process_node_insert(ck, cbounds, actual_update_size, pos_u32, insert_size);
+            node_stack.pop_back();
+        } else {
+            node_stack.back().second = mbs;
+            post_process_node_insert(node_key, nbounds, actual_update_size, pos_u32, insert_size);
+            node_stack.back().second = original;
+        }
+        if (simplifyable) simplifyable &= simplify(ck, false);
+    }
+    while (!node_stack.empty()) {
+        size_t node_key = node_stack.back().first;
+        if (!nodes.key_is_valid(node_key)) {  // the reference `continue`s here without popping (never reached)
+            node_stack.pop_back();
+            bounds_stack.pop_back();
+            continue;
+        }
+        post_process_node_insert(node_key, bounds_stack.back(), actual_update_size, pos_u32, insert_size);
+        if (simplifyable) simplifyable = simplify(node_key, false);
+        node_stack.pop_back();
+        bounds_stack.pop_back();
+    }
+    return 0;
+}
+
+bool BoxTree::simplify(size_t key, bool recursive) {  // src/boxtree/update/mod.rs:617-867
+    if (!nodes.key_is_valid(key)) return false;
+    Node &node = nodes.get(key);
+    switch (node.content) {
+        case Content::Nothing: return true;
+        case Content::UniformLeaf: {
+            Brick &b = node.bricks[0];
+            if (b.kind == BrickKind::Empty) return true;
+            if (b.kind == BrickKind::Solid) {
+                if (points_to_empty(b.solid)) {
+                    node.content = Content::Nothing;
+                    node.bricks.clear();
+                    node.has_children = false;
+                    return true;
+                }
+                return false;
+            }
+            return brick_simplify(b);
+        }
+        case Content::Leaf: {
+            bool simplified = false, uniform_solid = true, have_usv = false;
+            uint32_t usv = 0;
+            for (Brick &b : node.bricks) {
+                simplified |= brick_simplify(b);
+                if (uniform_solid) {
+                    if (b.kind == BrickKind::Solid) {
+                        if (have_usv) {
+                            if (usv != b.solid) uniform_solid = false;
+                        } else {
+                            usv = b.solid;
+                            have_usv = true;
+                        }
+                    } else {
+                        uniform_solid = false;
+                    }
+                }
+            }
+            if (uniform_solid) {
+                node.content = Content::UniformLeaf;
+                node.bricks.assign(1, solid(usv));
+                return true;
+            }
+            if (brick_dim == 1) return false;  // update/mod.rs:721-723 (even if bricks were simplified)
+            size_t bd = brick_dim;
+            std::vector<uint32_t> unified(bd * bd * bd, kEmpty32);
+            bool uniform = true;
+            float sbs = (float)brick_dim * 4.f;
+            auto voxel_of = [&](size_t s, F3 pic) -> uint32_t {
+                const Brick &b = node.bricks[s];
+                if (b.kind == BrickKind::Empty) return kEmpty32;
+                if (b.kind == BrickKind::Solid) return b.solid;
+                return b.parted[flat_projection(as_usize(pic.x), as_usize(pic.y), as_usize(pic.z), bd)];
+            };
+            for (size_t x = 0; x < bd && uniform; ++x)
+                for (size_t y = 0; y < bd && uniform; ++y)
+                    for (size_t z = 0; z < bd && uniform; ++z) {
+                        F3 cell_start = mul(f3((float)x, (float)y, (float)z), 4.f);
+                        uint8_t rs = offset_sectant(cell_start, sbs);
+                        F3 pic = sub(cell_start, mul(lut(rs), sbs));
+                        uint32_t ref = voxel_of(rs, pic);
+                        for (int cx = 0; cx < 4 && uniform; ++cx)
+                            for (int cy = 0; cy < 4 && uniform; ++cy)
+                                for (int cz = 0; cz < 4 && uniform; ++cz) {
+                                    F3 p = add(cell_start, f3((float)cx, (float)cy, (float)cz));
+                                    uint8_t s = offset_sectant(p, sbs);
+                                    F3 pc = sub(p, mul(lut(s), sbs));
+                                    uniform = uniform && (ref == voxel_of(s, pc));
+                                }
+                        if (uniform) unified[flat_projection(x, y, z, bd)] = ref;
+                    }
+            if (uniform) {
+                node.content = Content::UniformLeaf;
+                node.bricks.assign(1, parted(std::move(unified)));
+                simplified = true;
+            }
+            return simplified;
+        }
+        case Content::Internal: {
+            if (node.occupied_bits == 0 || !node.has_children) {
+                node.content = Content::Nothing;
+                return true;
+            }
+            std::array<uint32_t, kChildren> ck = node.children;
+            if (recursive)
+                for (uint32_t c : ck) simplify(c, true);
+            // update/mod.rs:833-844 tests the *parent's* content for UniformLeaf(Solid); the parent is Internal,
+            // so the collapse below never happens and the function returns false.
+            for (size_t s = 1; s < kChildren; ++s) {
+                size_t c0 = ck[0];
+                const Node &self = nodes.get(key);
+                bool parent_uniform_solid = self.content == Content::UniformLeaf && self.bricks[0].kind == BrickKind::Solid;
+                if (!nodes.key_is_valid(c0) || !parent_uniform_solid || !compare_nodes(c0, ck[s])) return false;
+            }
+            nodes.swap(key, ck[0]);
+            deallocate_children_of(key);
+            nodes.get(key).has_children = false;
+            return true;
+        }
+    }
+    return false;
+}
+
+}  // namespace vhx

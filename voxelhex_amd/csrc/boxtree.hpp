@@ -1,0 +1,142 @@
+// Host-side BoxTree<u32> — C++ restatement of VoxelHex's voxel container (the host half of the raytracing
+// drop-in; the reference's Rust toolchain is not available to this build).
+//
+// Restated (paths relative to the VoxelHex repository):
+//   ObjectPool                 src/object_pool.rs:51-266 (same key allocation, so node keys match the reference)
+//   BoxTree::new / get         src/boxtree/mod.rs:188-317
+//   insert / insert_at_lod     src/boxtree/update/insert.rs:21-407, post_process_node_insert 411-495
+//   add_to_palette             src/boxtree/update/mod.rs:39-120
+//   leaf_update                src/boxtree/update/mod.rs:144-464
+//   dilute_brick_data          src/boxtree/update/mod.rs:478-555, update_brick 564-603
+//   simplify                   src/boxtree/update/mod.rs:617-867
+//   subdivide_leaf_to_nodes    src/boxtree/detail.rs:248-337, node_empty_at 156-224, deallocate_children_of 352-370
+//   execute_for_relevant_sectants src/boxtree/iterate.rs:40-121, get_node_internal 293-343
+//   BrickData helpers          src/boxtree/node.rs:34-145, NodeContent pix_* 259-373, is_all 424-458
+// Not restated (no effect on what the raytracer reads): occlusion bits (insert.rs:451-469), MIP maps (disabled by
+// default, mipmap.rs:42-44, 351-353), update triggers (insert.rs:401-404; streaming is out of scope).
+#pragma once
+
+#include <array>
+#include <cstddef>
+#include <utility>
+#include <cstdint>
+#include <unordered_map>
+#include <vector>
+
+namespace vhx {
+
+constexpr uint32_t kChildren = 64;
+constexpr uint32_t kEmpty32 = 0xFFFFFFFFu;
+
+struct F3 {
+    float x, y, z;
+};
+struct U3 {
+    uint32_t x, y, z;
+};
+struct Cube {
+    F3 min;
+    float size;
+};
+
+enum class BrickKind : uint8_t { Empty, Parted, Solid };
+struct Brick {
+    BrickKind kind = BrickKind::Empty;
+    uint32_t solid = 0;
+    std::vector<uint32_t> parted;
+    bool operator==(const Brick &o) const {
+        if (kind != o.kind) return false;
+        if (kind == BrickKind::Solid) return solid == o.solid;
+        if (kind == BrickKind::Parted) return parted == o.parted;
+        return true;
+    }
+};
+
+enum class Content : uint8_t { Nothing, Internal, Leaf, UniformLeaf };
+struct Node {
+    Content content = Content::Nothing;
+    std::vector<Brick> bricks;  // Leaf: 64, UniformLeaf: 1
+    bool has_children = false;  // NodeChildren::Children vs NoChildren
+    std::array<uint32_t, kChildren> children{};
+    uint64_t occupied_bits = 0;
+};
+
+// BoxTreeEntry<u32>
+struct Entry {
+    uint32_t kind;  // VHX_ENTRY_*
+    uint32_t albedo;  // r | g<<8 | b<<16 | a<<24
+    uint32_t data;
+};
+
+class ObjectPool {
+   public:
+    size_t push(Node item);
+    size_t allocate();
+    bool free(size_t key);
+    void swap(size_t a, size_t b) { std::swap(buffer_[a], buffer_[b]); }
+    bool key_is_valid(size_t key) const { return key < buffer_.size() && reserved_[key]; }
+    Node &get(size_t key) { return buffer_[key]; }
+    const Node &get(size_t key) const { return buffer_[key]; }
+    size_t len() const { return buffer_.size(); }
+
+   private:
+    bool try_set_next_available();
+    std::vector<Node> buffer_;
+    std::vector<bool> reserved_;
+    size_t first_available_ = 0;
+};
+
+class BoxTree {
+   public:
+    // returns 0 or a VHX_E_TREE_* code (OctreeError)
+    static int create(uint32_t size, uint32_t brick_dim, BoxTree **out);
+
+    int insert(U3 pos, Entry e) { return insert_at_lod_internal(true, pos, 1, e); }
+    int insert_at_lod(U3 pos, uint32_t size, Entry e) { return insert_at_lod_internal(true, pos, size, e); }
+    int update(U3 pos, Entry e) { return insert_at_lod_internal(false, pos, 1, e); }
+    uint32_t get_raw(U3 pos) const;
+    Entry get(U3 pos) const;
+    bool simplify(size_t node_key, bool recursive);
+
+    bool auto_simplify = true;
+    uint32_t brick_dim = 0, boxtree_size = 0;
+    ObjectPool nodes;
+    std::vector<uint32_t> color_palette;
+    std::vector<uint32_t> data_palette;
+
+    bool points_to_empty(uint32_t v) const;
+
+   private:
+    std::unordered_map<uint32_t, size_t> color_index_, data_index_;
+
+    uint32_t add_to_palette(Entry e);
+    int insert_at_lod_internal(bool overwrite_if_empty, U3 pos, uint32_t insert_size, Entry e);
+    void post_process_node_insert(size_t node_key, const Cube &node_bounds, const std::array<size_t, 3> &aus,
+                                  U3 pos, uint32_t insert_size);
+    bool leaf_update(bool overwrite_if_empty, size_t node_key, const Cube &node_bounds, const Cube &target_bounds,
+                     size_t target_child_sectant, U3 position, U3 size, uint32_t target_content);
+    void subdivide_leaf_to_nodes(size_t node_key, size_t target_sectant);
+    bool node_empty_at(size_t node_key, uint8_t sectant) const;
+    bool compare_nodes(size_t l, size_t r) const;
+    void deallocate_children_of(size_t node_key);
+    Brick try_brick_from_node(size_t node_key) const;
+    size_t child(size_t node_key, uint8_t sectant) const;
+    uint32_t &child_mut(size_t node_key, size_t index);
+    size_t get_node_internal(size_t key, Cube &bounds, F3 position) const;
+    uint64_t calculate_brick_occupied_bits(const std::vector<uint32_t> &brick) const;
+    uint64_t calculate_occupied_bits(const Brick &b) const;
+    bool brick_contains_nothing(const Brick &b) const;
+    bool brick_simplify(Brick &b) const;
+    bool content_is_all(const Node &n, uint32_t data) const;
+    std::array<std::vector<uint32_t>, kChildren> dilute_brick_data(const std::vector<uint32_t> &brick) const;
+    void update_brick(bool overwrite_if_empty, std::vector<uint32_t> &brick, const Cube &bb, U3 position, U3 size,
+                      uint32_t data) const;
+};
+
+// spatial helpers shared with the flattener / scene builder (src/spatial/math/mod.rs, src/spatial/mod.rs)
+const float *sectant_offset(uint32_t s);
+uint8_t offset_sectant(F3 off, float size);
+Cube child_bounds_for(const Cube &c, uint8_t s);
+bool rust_log_is_integral(float x, float base);
+
+}  // namespace vhx

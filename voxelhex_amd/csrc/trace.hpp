@@ -1,0 +1,370 @@
+// Device-side traversal of the flattened BoxTree for gfx950 — the per-ray state machine of the reference CPU
+// raytracer BoxTree::get_by_ray (src/raytracing/cpu.rs:296-458), restated for one ray per lane of a wave64.
+//
+// Bit-exactness with the reference needs its float semantics: every f32 op is issued in the reference order
+// (the library is compiled with -ffp-contract=off, IEEE-correct division and sqrt, f32 denormals kept),
+// fminf/fmaxf ignore NaN like f32::min/max, signum(+-0) = +-1, and `as` casts saturate.
+//
+// Departures from a transliteration, none of which changes a result:
+//  * node type + 64-bit occupancy are one 16-byte record per node (one global_load_dwordx4 per node visit);
+//  * emptiness of brick cells is read from a per-brick occupancy bitmap (brick_dim^3 bits, built at upload from
+//    pix_points_to_empty, src/boxtree/node.rs:311-333), so the DDA through a brick issues no voxel loads; the voxel
+//    value is loaded once, on the hit;
+//  * the 4-entry NodeStack ring (cpu.rs:18-76) lives in four scalar registers, selected without dynamic indexing;
+//  * LUTs come from constant memory, except the 64-bit occupancy LUT which is computed from its closed form.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/vhx.h"
+
+namespace vhx {
+
+#define VHX_MAX_ITERS (1u << 22)  // same bound as the oracle (iteration bound)
+
+struct DevTree {
+    const uint4 *hdr;          // {occ_lo, occ_hi, type, 0} per node
+    const uint32_t *children;  // 64 per node
+    const uint32_t *voxels;    // raw PaletteIndexValues, bd^3 per brick
+    const uint64_t *brick_occ; // occ_words per brick; bit = flat cell index
+    const uint32_t *solid;
+    const uint32_t *color;
+    uint32_t color_count;
+    uint32_t node_count;
+    uint32_t size;
+    uint32_t bd;
+    uint32_t occ_words;  // max(1, bd^3/64)
+};
+
+struct HitOut {
+    uint32_t value, cell, vx, vy, vz, bytes;
+    float ix, iy, iz, nx, ny, nz;
+    bool hit;
+};
+
+struct F3d {
+    float x, y, z;
+};
+
+__device__ __forceinline__ F3d mk(float x, float y, float z) { return F3d{x, y, z}; }
+__device__ __forceinline__ F3d vadd(F3d a, F3d b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ F3d vsub(F3d a, F3d b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ F3d vmul(F3d a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
+__device__ __forceinline__ F3d vdiv(F3d a, float s) { return mk(a.x / s, a.y / s, a.z / s); }
+__device__ __forceinline__ float vlen(F3d a) { return __builtin_sqrtf((a.x * a.x + a.y * a.y) + a.z * a.z); }
+__device__ __forceinline__ F3d vnorm(F3d a) { return vdiv(a, vlen(a)); }
+
+__device__ __forceinline__ float rsignum(float a) { return __builtin_isnan(a) ? a : __builtin_copysignf(1.0f, a); }
+__device__ __forceinline__ int32_t ras_i32(float f) {
+    if (__builtin_isnan(f)) return 0;
+    if (f >= 2147483648.0f) return INT32_MAX;
+    if (f <= -2147483648.0f) return INT32_MIN;
+    return (int32_t)f;
+}
+__device__ __forceinline__ uint32_t ras_u32(float f) {
+    if (__builtin_isnan(f) || f <= 0.0f) return 0;
+    if (f >= 4294967296.0f) return 0xFFFFFFFFu;
+    return (uint32_t)f;
+}
+__device__ __forceinline__ uint32_t ras_u8(float f) {
+    if (__builtin_isnan(f) || f <= 0.0f) return 0;
+    if (f >= 255.0f) return 255;
+    return (uint32_t)f;
+}
+
+// SECTANT_STEP_RESULT_LUT, packed [sectant][x+1][y+1][z+1] (src/spatial/lut.rs:27-92); filled at library load.
+extern __constant__ uint8_t c_step_lut[64 * 27];
+
+// offset of sectant s = (s&3, (s>>2)&3, s>>4) / 4 (SECTANT_OFFSET_LUT, src/spatial/lut.rs:4-24)
+__device__ __forceinline__ F3d sect_off(uint32_t s) {
+    return mk((float)(s & 3u) * 0.25f, (float)((s >> 2) & 3u) * 0.25f, (float)(s >> 4) * 0.25f);
+}
+// RAY_TO_NODE_OCCUPANCY_BITMASK_LUT[s][o] (src/spatial/lut.rs:96-161): sectants t with t_k on the ray's side of
+// s_k on every axis; o = (dx>=0) + 2(dz>=0) + 4(dy>=0). Pinned against the reference table in the tests.
+__device__ __forceinline__ uint64_t occ_lut(uint32_t s, uint32_t o) {
+    const uint32_t sx = s & 3u, sy = (s >> 2) & 3u, sz = s >> 4;
+    // per-axis 4-bit masks of admissible coordinates
+    const uint32_t mx = (o & 1u) ? (0xFu << sx) & 0xFu : (0xFu >> (3u - sx));
+    const uint32_t my = (o & 4u) ? (0xFu << sy) & 0xFu : (0xFu >> (3u - sy));
+    const uint32_t mz = (o & 2u) ? (0xFu << sz) & 0xFu : (0xFu >> (3u - sz));
+    // expand: row mask over x (4 bits) replicated across admissible y rows, then across admissible z slabs
+    uint32_t row16 = 0;
+#pragma unroll
+    for (uint32_t y = 0; y < 4; ++y) row16 |= ((my >> y) & 1u) ? (mx << (4u * y)) : 0u;
+    uint64_t m = 0;
+#pragma unroll
+    for (uint32_t z = 0; z < 4; ++z) m |= ((mz >> z) & 1u) ? ((uint64_t)row16 << (16u * z)) : 0ull;
+    return m;
+}
+
+__device__ __forceinline__ uint32_t step_sectant(uint32_t s, F3d st) {
+    const int32_t ix = ras_i32(st.x), iy = ras_i32(st.y), iz = ras_i32(st.z);
+    const int32_t sx = (ix > 0) - (ix < 0), sy = (iy > 0) - (iy < 0), sz = (iz > 0) - (iz < 0);
+    return c_step_lut[s * 27u + (uint32_t)(sx + 1) * 9u + (uint32_t)(sy + 1) * 3u + (uint32_t)(sz + 1)];
+}
+// offset_sectant, src/spatial/math/mod.rs:27-44
+__device__ __forceinline__ uint32_t offset_sectant(F3d off, float size) {
+    F3d idx = vdiv(vmul(off, 4.0f), size);
+    idx = mk(__builtin_floorf(idx.x), __builtin_floorf(idx.y), __builtin_floorf(idx.z));
+    idx = mk(__builtin_fminf(idx.x, 3.0f), __builtin_fminf(idx.y, 3.0f), __builtin_fminf(idx.z, 3.0f));
+    return ras_u8(idx.x + (idx.y * 4.0f) + (idx.z * 16.0f));
+}
+
+struct CubeD {
+    F3d min;
+    float size;
+};
+__device__ __forceinline__ CubeD child_bounds(CubeD c, uint32_t s) {
+    CubeD r;
+    r.min = vadd(c.min, vmul(sect_off(s), c.size));
+    r.size = c.size / 4.0f;
+    return r;
+}
+// cube_impact_normal, src/spatial/raytracing/mod.rs:97-125
+__device__ __forceinline__ F3d impact_normal(CubeD c, F3d p) {
+    const float h = c.size / 2.0f;
+    F3d m = vsub(vadd(c.min, mk(h, h, h)), p);
+    const float mc = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(m.x), __builtin_fabsf(m.y)), __builtin_fabsf(m.z));
+    F3d n = mk(__builtin_fabsf(m.x) == mc ? -m.x : 0.0f, __builtin_fabsf(m.y) == mc ? -m.y : 0.0f,
+               __builtin_fabsf(m.z) == mc ? -m.z : 0.0f);
+    return vnorm(n);
+}
+
+struct RayD {
+    F3d o, d, sf, sg, sgmax;
+};
+
+// dda_step_to_next_sibling, src/raytracing/cpu.rs:104-132
+__device__ __forceinline__ F3d dda_step(const RayD &r, F3d &p, CubeD b) {
+    const F3d diff = vsub(p, b.min);
+    const F3d st = mk(b.size * r.sgmax.x - r.sg.x * diff.x, b.size * r.sgmax.y - r.sg.y * diff.y,
+                      b.size * r.sgmax.z - r.sg.z * diff.z);
+    const float dx = __builtin_fabsf(st.x * r.sf.x), dy = __builtin_fabsf(st.y * r.sf.y),
+                dz = __builtin_fabsf(st.z * r.sf.z);
+    const float m = __builtin_fminf(__builtin_fminf(dx, dy), dz);
+    p = vadd(p, vmul(r.d, m));
+    return mk(m == dx ? r.sg.x : 0.0f, m == dy ? r.sg.y : 0.0f, m == dz ? r.sg.z : 0.0f);
+}
+
+template <bool COUNT>
+__device__ __forceinline__ bool probe_brick(const DevTree &t, const RayD &r, F3d &p, uint32_t desc, CubeD bb,
+                                            HitOut &h, uint32_t &iters) {
+    if (desc == VHX_EMPTY) return false;
+    if (desc & VHX_SOLID_BIT) {  // BrickData::Solid, cpu.rs:249-260
+        if (COUNT) h.bytes += 4;
+        h.value = t.solid[desc & 0x7FFFFFFFu];
+        h.cell = VHX_EMPTY;
+        h.ix = p.x;
+        h.iy = p.y;
+        h.iz = p.z;
+        F3d n = impact_normal(bb, p);
+        h.nx = n.x;
+        h.ny = n.y;
+        h.nz = n.z;
+        h.vx = ras_u32(bb.min.x);
+        h.vy = ras_u32(bb.min.y);
+        h.vz = ras_u32(bb.min.z);
+        return true;
+    }
+    // BrickData::Parted -> traverse_brick, cpu.rs:136-232
+    const int32_t bd = (int32_t)t.bd;
+    const float fbd = (float)t.bd;
+    const F3d pib = vdiv(vmul(vsub(p, bb.min), fbd), bb.size);
+    int32_t ix = ras_i32(pib.x), iy = ras_i32(pib.y), iz = ras_i32(pib.z);
+    ix = ix < 0 ? 0 : (ix > bd - 1 ? bd - 1 : ix);
+    iy = iy < 0 ? 0 : (iy > bd - 1 ? bd - 1 : iy);
+    iz = iz < 0 ? 0 : (iz > bd - 1 ? bd - 1 : iz);
+    int32_t flat = ix + iy * bd + iz * bd * bd;
+    const float unit = bb.size / fbd;
+    CubeD cur;
+    cur.min = vadd(bb.min, vmul(mk((float)ix, (float)iy, (float)iz), unit));
+    cur.size = unit;
+    const uint64_t *occw = t.brick_occ + (uint64_t)desc * t.occ_words;
+    uint64_t word = occw[0];
+    int32_t word_idx = 0;
+    F3d step = mk(0.0f, 0.0f, 0.0f);
+    for (;;) {
+        if (ix < 0 || ix >= bd || iy < 0 || iy >= bd || iz < 0 || iz >= bd) return false;
+        flat += ras_i32(step.x) * 1 + ras_i32(step.y) * bd + ras_i32(step.z) * (bd * bd);
+        const int32_t wi = flat >> 6;
+        if (wi != word_idx) {
+            word_idx = wi;
+            word = occw[wi];
+        }
+        if (COUNT) h.bytes += 4;
+        if ((word >> (flat & 63)) & 1ull) {
+            const uint32_t v = t.voxels[(uint64_t)desc * (uint64_t)(bd * bd * bd) + (uint32_t)flat];
+            if (COUNT) h.bytes += ((v & 0xFFFFu) != 0xFFFFu ? 4u : 0u) + ((v >> 16) != 0xFFFFu ? 4u : 0u);
+            CubeD hb;
+            hb.size = bb.size / fbd;
+            hb.min = vadd(bb.min, vdiv(vmul(mk((float)ix, (float)iy, (float)iz), bb.size), fbd));
+            h.value = v;
+            h.cell = (uint32_t)flat;
+            h.ix = p.x;
+            h.iy = p.y;
+            h.iz = p.z;
+            F3d n = impact_normal(hb, p);
+            h.nx = n.x;
+            h.ny = n.y;
+            h.nz = n.z;
+            h.vx = ras_u32(hb.min.x);
+            h.vy = ras_u32(hb.min.y);
+            h.vz = ras_u32(hb.min.z);
+            return true;
+        }
+        if (COUNT) {
+            // the reference reads the palettes for every cell whose indices are not none (node.rs:329-332),
+            // even when they turn out empty; the instrumented build reloads the raw value to account for it
+            const uint32_t v = t.voxels[(uint64_t)desc * (uint64_t)(bd * bd * bd) + (uint32_t)flat];
+            h.bytes += ((v & 0xFFFFu) != 0xFFFFu ? 4u : 0u) + ((v >> 16) != 0xFFFFu ? 4u : 0u);
+        }
+        if (++iters > VHX_MAX_ITERS) return false;
+        step = dda_step(r, p, cur);
+        cur.min = vadd(cur.min, vmul(step, unit));
+        ix += ras_i32(__builtin_roundf(step.x));
+        iy += ras_i32(__builtin_roundf(step.y));
+        iz += ras_i32(__builtin_roundf(step.z));
+    }
+}
+
+// BoxTree::get_by_ray, src/raytracing/cpu.rs:296-458
+template <bool COUNT>
+__device__ __forceinline__ void get_by_ray(const DevTree &t, F3d o, F3d d, HitOut &h) {
+    h.hit = false;
+    h.bytes = 0;
+    RayD r;
+    r.o = o;
+    r.d = d;
+    {
+        const float zx = d.z / d.x, yx = d.y / d.x, xy = d.x / d.y, zy = d.z / d.y, xz = d.x / d.z, yz = d.y / d.z;
+        r.sf = mk(__builtin_sqrtf((1.0f + zx * zx) + yx * yx), __builtin_sqrtf((xy * xy + 1.0f) + zy * zy),
+                  __builtin_sqrtf((xz * xz + 1.0f) + yz * yz));
+    }
+    r.sg = mk(rsignum(d.x), rsignum(d.y), rsignum(d.z));
+    r.sgmax = mk(__builtin_fmaxf(r.sg.x, 0.0f), __builtin_fmaxf(r.sg.y, 0.0f), __builtin_fmaxf(r.sg.z, 0.0f));
+    uint32_t dir_idx;
+    {
+        const F3d od = vadd(mk(1.0f, 1.0f, 1.0f), d);
+        dir_idx = (uint32_t)(od.x >= 1.0f) + (uint32_t)(od.z >= 1.0f) * 2u + (uint32_t)(od.y >= 1.0f) * 4u;
+    }
+    const float tsize = (float)t.size;
+    CubeD cur;
+    cur.min = mk(0.0f, 0.0f, 0.0f);
+    cur.size = tsize;
+    F3d p;
+    uint32_t target;
+    CubeD tb;
+    {
+        // Cube::intersect_ray, src/spatial/raytracing/mod.rs:33-62
+        const F3d mx = vadd(cur.min, mk(cur.size, cur.size, cur.size));
+        const float t1 = (cur.min.x - o.x) / d.x, t2 = (mx.x - o.x) / d.x;
+        const float t3 = (cur.min.y - o.y) / d.y, t4 = (mx.y - o.y) / d.y;
+        const float t5 = (cur.min.z - o.z) / d.z, t6 = (mx.z - o.z) / d.z;
+        const float tmin = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(t1, t2), __builtin_fminf(t3, t4)),
+                                           __builtin_fminf(t5, t6));
+        const float tmax = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(t1, t2), __builtin_fmaxf(t3, t4)),
+                                           __builtin_fmaxf(t5, t6));
+        if (tmax < 0.0f || tmin > tmax) {
+            p = o;
+            target = 64;
+            tb = cur;
+        } else {
+            p = vadd(o, vmul(d, tmin < 0.0f ? 0.0f : tmin));
+            target = offset_sectant(p, cur.size);
+            tb = child_bounds(cur, target);
+        }
+    }
+    // NodeStack<u32, 4> ring in registers
+    uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0, head = 0, count = 0;
+    uint32_t node = 0;
+    uint32_t iters = 0;
+    while (target < 64) {
+        node = 0;
+        cur.min = mk(0.0f, 0.0f, 0.0f);
+        cur.size = tsize;
+        // push(ROOT)
+        head = (head + 1) & 3u;
+        count = count + 1 < 4 ? count + 1 : 4;
+        s0 = head == 0 ? 0u : s0;
+        s1 = head == 1 ? 0u : s1;
+        s2 = head == 2 ? 0u : s2;
+        s3 = head == 3 ? 0u : s3;
+        while (count != 0) {
+            if (++iters > VHX_MAX_ITERS) return;
+            const uint32_t last = head == 0 ? s0 : (head == 1 ? s1 : (head == 2 ? s2 : s3));
+            const uint4 lh = t.hdr[last];
+            const uint64_t occ = ((uint64_t)lh.y << 32) | (uint64_t)lh.x;
+            const uint32_t ntype = last == node ? lh.z : t.hdr[node].z;
+            if (COUNT) h.bytes += 12;
+            bool backtrack = ntype == VHX_NODE_UNIFORM_LEAF;
+            if (target < 64) {
+                if (ntype == VHX_NODE_UNIFORM_LEAF) {
+                    if (COUNT) h.bytes += 4;
+                    if (probe_brick<COUNT>(t, r, p, t.children[(uint64_t)node * 64u], cur, h, iters)) {
+                        h.hit = true;
+                        return;
+                    }
+                    backtrack = true;
+                } else if (ntype == VHX_NODE_LEAF) {
+                    if (COUNT) h.bytes += 4;
+                    if (probe_brick<COUNT>(t, r, p, t.children[(uint64_t)node * 64u + target], child_bounds(cur, target),
+                                           h, iters)) {
+                        h.hit = true;
+                        return;
+                    }
+                }
+            }
+            if (backtrack || target >= 64 || occ == 0 || (occ & occ_lut(target, dir_idx)) == 0) {
+                // POP (cpu.rs:368-393)
+                if (count != 0) {
+                    count -= 1;
+                    head = (head - 1) & 3u;
+                }
+                tb = cur;
+                cur.size *= 4.0f;
+                cur.min = vsub(cur.min, mk(__builtin_fmodf(cur.min.x, cur.size), __builtin_fmodf(cur.min.y, cur.size),
+                                           __builtin_fmodf(cur.min.z, cur.size)));
+                const float hs = tb.size / 2.0f;
+                target = offset_sectant(vsub(vadd(tb.min, mk(hs, hs, hs)), cur.min), cur.size);
+                const F3d sv = dda_step(r, p, tb);
+                target = step_sectant(target, sv);
+                tb.min = vadd(tb.min, vmul(sv, tb.size));
+                if (count != 0) node = head == 0 ? s0 : (head == 1 ? s1 : (head == 2 ? s2 : s3));
+                continue;
+            }
+            if (ntype == VHX_NODE_INTERNAL && (occ & (1ull << target)) != 0) {
+                // PUSH (cpu.rs:401-411)
+                if (COUNT) h.bytes += 4;
+                const uint32_t child = t.children[(uint64_t)node * 64u + target];
+                if (child >= t.node_count) return;  // the reference would panic on an invalid key
+                node = child;
+                cur = tb;
+                target = offset_sectant(vsub(p, tb.min), tb.size);
+                tb = child_bounds(cur, target);
+                head = (head + 1) & 3u;
+                count = count + 1 < 4 ? count + 1 : 4;
+                s0 = head == 0 ? child : s0;
+                s1 = head == 1 ? child : s1;
+                s2 = head == 2 ? child : s2;
+                s3 = head == 3 ? child : s3;
+            } else {
+                // ADVANCE (cpu.rs:416-437)
+                for (;;) {
+                    if (++iters > VHX_MAX_ITERS) return;
+                    const F3d sv = dda_step(r, p, tb);
+                    target = step_sectant(target, sv);
+                    if (target < 64) tb.min = vadd(tb.min, vmul(sv, tb.size));
+                    if (target >= 64 || (occ & (1ull << target)) != 0) break;
+                }
+            }
+        }
+        // restart from the root (cpu.rs:441-455)
+        p = vadd(p, vmul(d, 0.1f));
+        if (p.x < tsize && p.y < tsize && p.z < tsize && p.x > 0.0f && p.y > 0.0f && p.z > 0.0f)
+            target = offset_sectant(p, tsize);
+        else
+            target = 64;
+    }
+}
+
+}  // namespace vhx

@@ -1,0 +1,628 @@
+// libvhx device side: HIP kernels for gfx950 and the C ABI of include/vhx.h.
+//
+// Kernels
+//   k_trace_primary  per-pixel primary rays (examples/gpu_render.rs:196-257, benches/performance.rs:29-66) traced with
+//                    get_by_ray semantics (src/raytracing/cpu.rs:296-458); replaces the WGSL `update` kernel dispatched
+//                    by VhxRenderNode::run (src/raytracing/bevy/pipeline/mod.rs:96-155)
+//   k_trace_rays     explicit ray batch (BoxTree::get_by_ray over many rays)
+//   k_brick_occ_*    upload-time brick occupancy bitmaps from pix_points_to_empty (src/boxtree/node.rs:311-333)
+//   k_pack_hdr       node type + occupied_bits -> one 16-byte record per node
+//   k_untile_rgba    scatters rank-gathered tile buffers into the framebuffer (multi-GPU screen-tile split)
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/vhx.h"
+#include "trace.hpp"
+
+namespace vhx {
+__constant__ uint8_t c_step_lut[64 * 27];
+}
+
+using namespace vhx;
+
+// ------------------------------------------------------------------------------------------------ device context
+struct DevBuf {
+    void *ptr = nullptr;
+    uint64_t bytes = 0;
+};
+
+struct vhx_ctx {
+    int device = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    bool timed = false;
+    std::string err;
+    bool uploaded = false;
+    vhx_tree_desc desc{};  // counts of the uploaded tree (pointers unused)
+    DevBuf raw[7];         // VHX_BUF_* raw copies
+    DevBuf hdr, brick_occ, scratch;
+    uint32_t occ_words = 1;
+};
+
+#define VHX_HIP(ctx, call)                                                                                         \
+    do {                                                                                                           \
+        hipError_t e_ = (call);                                                                                    \
+        if (e_ != hipSuccess) {                                                                                    \
+            (ctx)->err = std::string(#call) + ": " + hipGetErrorString(e_);                                        \
+            return VHX_E_HIP;                                                                                      \
+        }                                                                                                          \
+    } while (0)
+
+static int fail(vhx_ctx *ctx, int code, const char *msg) {
+    if (ctx) ctx->err = msg;
+    return code;
+}
+
+// SECTANT_STEP_RESULT_LUT generator (src/bin/sectant_step_result_lut.rs:48-114), host side
+static void make_step_lut(uint8_t *lut) {
+    for (int s = 0; s < 64; ++s)
+        for (int x = -1; x <= 1; ++x)
+            for (int y = -1; y <= 1; ++y)
+                for (int z = -1; z <= 1; ++z) {
+                    float off[3] = {(float)(s % 4) / 4.f, (float)((s / 4) % 4) / 4.f, (float)(s / 16) / 4.f};
+                    float st[3] = {(float)x, (float)y, (float)z};
+                    float after[3];
+                    bool out = false;
+                    for (int k = 0; k < 3; ++k) {
+                        after[k] = (off[k] + 0.25f / 2.f) + 0.25f * st[k];
+                        out |= after[k] < 0.f || after[k] > 1.f;
+                    }
+                    int base = 0;
+                    if (out) {
+                        for (int k = 0; k < 3; ++k) {
+                            after[k] = std::fmod(after[k], 1.f);
+                            if (after[k] < 0.f) after[k] += 1.f;
+                        }
+                        base = 64;
+                    }
+                    int ix = (int)std::floor(after[0] * 4.f), iy = (int)std::floor(after[1] * 4.f),
+                        iz = (int)std::floor(after[2] * 4.f);
+                    lut[s * 27 + (x + 1) * 9 + (y + 1) * 3 + (z + 1)] = (uint8_t)(base + ix + iy * 4 + iz * 16);
+                }
+}
+
+// ------------------------------------------------------------------------------------------------ upload kernels
+__device__ __forceinline__ bool cell_empty(uint32_t v, const uint32_t *color, uint32_t ncolor, const uint32_t *data,
+                                           uint32_t ndata) {
+    const uint32_t ci = v & 0xFFFFu, di = v >> 16;
+    const bool cn = ci == 0xFFFFu || ci >= ncolor || ((color[ci] >> 24) & 0xFFu) == 0;
+    const bool dn = di == 0xFFFFu || di >= ndata || data[di] == 0;
+    return cn && dn;
+}
+
+// bd^3 >= 64: one lane per cell, the wave's ballot is one 64-bit occupancy word
+__global__ void __launch_bounds__(256) k_brick_occ_ballot(const uint32_t *__restrict__ vox, uint64_t ncells,
+                                                          uint64_t cell0, const uint32_t *__restrict__ color,
+                                                          uint32_t ncolor, const uint32_t *__restrict__ data,
+                                                          uint32_t ndata, uint64_t *__restrict__ words) {
+    const uint64_t i = cell0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool in = i < cell0 + ncells;
+    const bool full = in && !cell_empty(vox[in ? i : cell0], color, ncolor, data, ndata);
+    const uint64_t m = __ballot(full);
+    if ((threadIdx.x & 63u) == 0 && in) words[i >> 6] = m;
+}
+
+// bd^3 < 64 (bd = 1, 2): one lane per brick
+__global__ void __launch_bounds__(256) k_brick_occ_small(const uint32_t *__restrict__ vox, uint32_t nbricks,
+                                                         uint32_t brick0, uint32_t n3,
+                                                         const uint32_t *__restrict__ color, uint32_t ncolor,
+                                                         const uint32_t *__restrict__ data, uint32_t ndata,
+                                                         uint64_t *__restrict__ words) {
+    const uint32_t b = brick0 + blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= brick0 + nbricks) return;
+    uint64_t m = 0;
+    for (uint32_t c = 0; c < n3; ++c)
+        if (!cell_empty(vox[(uint64_t)b * n3 + c], color, ncolor, data, ndata)) m |= 1ull << c;
+    words[b] = m;
+}
+
+__global__ void __launch_bounds__(256) k_pack_hdr(const uint32_t *__restrict__ type, const uint64_t *__restrict__ occ,
+                                                  uint32_t n0, uint32_t n, uint4 *__restrict__ hdr) {
+    const uint32_t i = n0 + blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n0 + n) return;
+    const uint64_t o = occ[i];
+    hdr[i] = make_uint4((uint32_t)o, (uint32_t)(o >> 32), type[i], 0u);
+}
+
+// ------------------------------------------------------------------------------------------------ trace kernels
+struct CamD {
+    uint32_t model, width, height;
+    float ox, oy, oz;
+    float blx, bly, blz, rx, ry, rz, ux, uy, uz, pw, ph;
+    float m[16];
+};
+
+struct OutD {
+    uint32_t *value, *cell, *voxel, *rgba, *bytes;
+    float *impact, *normal, *depth;
+};
+
+// examples/gpu_render.rs:199, 236-251
+__device__ __forceinline__ uint32_t shade(const DevTree &t, const HitOut &h) {
+    if (!h.hit) return 128u | (128u << 8) | (128u << 16) | (255u << 24);
+    const uint32_t ci = h.value & 0xFFFFu;
+    if (ci == 0xFFFFu || ci >= t.color_count) return 255u << 24;
+    const uint32_t c = t.color[ci];
+    const F3d L = vnorm(mk(0.0f, -1.0f, 1.0f));
+    const float dot = (h.nx * L.x + h.ny * L.y) + h.nz * L.z;
+    const float s = 1.0f - (dot / 2.0f + 0.5f);
+    const uint32_t r = ras_u8((float)(c & 0xFFu) * s), g = ras_u8((float)((c >> 8) & 0xFFu) * s),
+                   b = ras_u8((float)((c >> 16) & 0xFFu) * s);
+    return r | (g << 8) | (b << 16) | (255u << 24);
+}
+
+__device__ __forceinline__ void store(const DevTree &t, const OutD &o, uint64_t i, F3d org, const HitOut &h) {
+    if (o.value) o.value[i] = h.hit ? h.value : VHX_EMPTY;
+    if (o.cell) o.cell[i] = h.hit ? h.cell : VHX_EMPTY;
+    if (o.voxel) {
+        o.voxel[3 * i] = h.hit ? h.vx : VHX_EMPTY;
+        o.voxel[3 * i + 1] = h.hit ? h.vy : VHX_EMPTY;
+        o.voxel[3 * i + 2] = h.hit ? h.vz : VHX_EMPTY;
+    }
+    if (o.impact) {
+        o.impact[3 * i] = h.hit ? h.ix : 0.0f;
+        o.impact[3 * i + 1] = h.hit ? h.iy : 0.0f;
+        o.impact[3 * i + 2] = h.hit ? h.iz : 0.0f;
+    }
+    if (o.normal) {
+        o.normal[3 * i] = h.hit ? h.nx : 0.0f;
+        o.normal[3 * i + 1] = h.hit ? h.ny : 0.0f;
+        o.normal[3 * i + 2] = h.hit ? h.nz : 0.0f;
+    }
+    if (o.depth) o.depth[i] = h.hit ? vlen(vsub(mk(h.ix, h.iy, h.iz), org)) : __builtin_huge_valf();
+    if (o.rgba) o.rgba[i] = shade(t, h);
+    if (o.bytes) o.bytes[i] = h.bytes;
+}
+
+// benches/performance.rs:54-61 (glass) and examples/gpu_render.rs:203-224 (inverse VP, glam op order)
+__device__ __forceinline__ void primary_ray(const CamD &c, uint32_t px, uint32_t py, F3d &o, F3d &d) {
+    const uint32_t x = px, y = c.height - 1u - py;
+    o = mk(c.ox, c.oy, c.oz);
+    if (c.model == VHX_RAY_GLASS) {
+        const F3d gp = vadd(vadd(mk(c.blx, c.bly, c.blz), vmul(vmul(mk(c.rx, c.ry, c.rz), (float)x), c.pw)),
+                            vmul(vmul(mk(c.ux, c.uy, c.uz), (float)y), c.ph));
+        d = vnorm(vsub(gp, o));
+    } else {
+        const float nx = ((float)x + 0.5f) / (float)c.width * 2.0f - 1.0f;
+        const float ny = ((float)y + 0.5f) / (float)c.height * 2.0f - 1.0f;
+        float nr[4], fr[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            nr[k] = ((c.m[k] * nx + c.m[4 + k] * ny) + c.m[8 + k] * -1.0f) + c.m[12 + k] * 1.0f;
+            fr[k] = ((c.m[k] * nx + c.m[4 + k] * ny) + c.m[8 + k] * 1.0f) + c.m[12 + k] * 1.0f;
+        }
+        const F3d np = mk(nr[0] / nr[3], nr[1] / nr[3], nr[2] / nr[3]);
+        const F3d fp = mk(fr[0] / fr[3], fr[1] / fr[3], fr[2] / fr[3]);
+        const F3d dd = vsub(fp, np);
+        const float rcp = 1.0f / __builtin_sqrtf((dd.x * dd.x + dd.y * dd.y) + dd.z * dd.z);
+        d = vmul(dd, rcp);
+    }
+}
+
+// One workgroup = 256 lanes = a 16x16 pixel block made of four 8x8 wave tiles (wave64-coherent ray bundles, the
+// 8x8 footprint of the reference's @workgroup_size(8, 8, 1)). Blocks are dealt tile by tile.
+template <bool COUNT>
+__global__ void __launch_bounds__(256) k_trace_primary(DevTree t, CamD cam, OutD out, uint32_t T, uint32_t tiles_x,
+                                                       uint32_t tile_start, uint32_t tile_stride, uint32_t layout,
+                                                       uint32_t blocks_per_tile_x, uint32_t blocks_per_tile) {
+    const uint32_t j = blockIdx.x / blocks_per_tile;  // j-th tile of this rank
+    const uint32_t sb = blockIdx.x - j * blocks_per_tile;
+    const uint32_t tile = tile_start + j * tile_stride;
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    const uint32_t lx = (sb % blocks_per_tile_x) * 16u + (wave & 1u) * 8u + (lane & 7u);
+    const uint32_t ly = (sb / blocks_per_tile_x) * 16u + (wave >> 1) * 8u + (lane >> 3);
+    if (lx >= T || ly >= T) return;
+    const uint32_t px = (tile % tiles_x) * T + lx, py = (tile / tiles_x) * T + ly;
+    if (px >= cam.width || py >= cam.height) return;
+    F3d o, d;
+    primary_ray(cam, px, py, o, d);
+    HitOut h;
+    get_by_ray<COUNT>(t, o, d, h);
+    const uint64_t idx = layout == VHX_LAYOUT_FRAMEBUFFER ? (uint64_t)py * cam.width + px
+                                                          : (uint64_t)j * T * T + (uint64_t)ly * T + lx;
+    store(t, out, idx, o, h);
+}
+
+template <bool COUNT>
+__global__ void __launch_bounds__(256) k_trace_rays(DevTree t, const float *__restrict__ rays, uint64_t n, OutD out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const F3d o = mk(rays[6 * i], rays[6 * i + 1], rays[6 * i + 2]);
+    const F3d d = mk(rays[6 * i + 3], rays[6 * i + 4], rays[6 * i + 5]);
+    HitOut h;
+    get_by_ray<COUNT>(t, o, d, h);
+    store(t, out, i, o, h);
+}
+
+__global__ void __launch_bounds__(256) k_untile_rgba(const uint32_t *__restrict__ gathered, uint32_t ranks,
+                                                     uint32_t tiles_per_rank, uint32_t T, uint32_t tiles_x,
+                                                     uint32_t ntiles, uint32_t width, uint32_t height,
+                                                     uint32_t *__restrict__ fb) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t per_rank = (uint64_t)tiles_per_rank * T * T;
+    if (i >= per_rank * ranks) return;
+    const uint32_t r = (uint32_t)(i / per_rank);
+    const uint64_t k = i - (uint64_t)r * per_rank;
+    const uint32_t j = (uint32_t)(k / ((uint64_t)T * T));
+    const uint32_t local = (uint32_t)(k - (uint64_t)j * T * T);
+    const uint32_t tile = r + j * ranks;
+    if (tile >= ntiles) return;
+    const uint32_t px = (tile % tiles_x) * T + local % T, py = (tile / tiles_x) * T + local / T;
+    if (px >= width || py >= height) return;
+    fb[(uint64_t)py * width + px] = gathered[i];
+}
+
+// ------------------------------------------------------------------------------------------------ host helpers
+static DevTree dev_tree(const vhx_ctx *c) {
+    DevTree t;
+    t.hdr = (const uint4 *)c->hdr.ptr;
+    t.children = (const uint32_t *)c->raw[VHX_BUF_NODE_CHILDREN].ptr;
+    t.voxels = (const uint32_t *)c->raw[VHX_BUF_VOXELS].ptr;
+    t.brick_occ = (const uint64_t *)c->brick_occ.ptr;
+    t.solid = (const uint32_t *)c->raw[VHX_BUF_SOLID_VALUES].ptr;
+    t.color = (const uint32_t *)c->raw[VHX_BUF_COLOR_PALETTE].ptr;
+    t.color_count = c->desc.color_count;
+    t.node_count = c->desc.node_count;
+    t.size = c->desc.boxtree_size;
+    t.bd = c->desc.brick_dim;
+    t.occ_words = c->occ_words;
+    return t;
+}
+
+static int ensure(vhx_ctx *c, DevBuf &b, uint64_t bytes) {
+    if (b.bytes >= bytes && b.ptr) return VHX_OK;
+    if (b.ptr) VHX_HIP(c, hipFree(b.ptr));
+    b.ptr = nullptr;
+    b.bytes = 0;
+    if (bytes == 0) bytes = 16;
+    VHX_HIP(c, hipMalloc(&b.ptr, bytes));
+    b.bytes = bytes;
+    return VHX_OK;
+}
+
+static uint64_t elem_size(int id) {
+    switch (id) {
+        case VHX_BUF_NODE_OCBITS: return 8;
+        default: return 4;
+    }
+}
+static uint64_t elem_count(const vhx_tree_desc &d, int id) {
+    const uint64_t n3 = (uint64_t)d.brick_dim * d.brick_dim * d.brick_dim;
+    switch (id) {
+        case VHX_BUF_NODE_TYPE: return d.node_count;
+        case VHX_BUF_NODE_OCBITS: return d.node_count;
+        case VHX_BUF_NODE_CHILDREN: return (uint64_t)d.node_count * 64;
+        case VHX_BUF_VOXELS: return (uint64_t)d.brick_count * n3;
+        case VHX_BUF_SOLID_VALUES: return d.solid_count;
+        case VHX_BUF_COLOR_PALETTE: return d.color_count;
+        case VHX_BUF_DATA_PALETTE: return d.data_count;
+    }
+    return 0;
+}
+
+static int rebuild_hdr(vhx_ctx *c, uint32_t n0, uint32_t n) {
+    if (n == 0) return VHX_OK;
+    k_pack_hdr<<<(n + 255) / 256, 256, 0, c->stream>>>((const uint32_t *)c->raw[VHX_BUF_NODE_TYPE].ptr,
+                                                       (const uint64_t *)c->raw[VHX_BUF_NODE_OCBITS].ptr, n0, n,
+                                                       (uint4 *)c->hdr.ptr);
+    VHX_HIP(c, hipGetLastError());
+    return VHX_OK;
+}
+
+static int rebuild_occ(vhx_ctx *c, uint32_t brick0, uint32_t nbricks) {
+    if (nbricks == 0) return VHX_OK;
+    const uint32_t bd = c->desc.brick_dim;
+    const uint32_t n3 = bd * bd * bd;
+    const uint32_t *vox = (const uint32_t *)c->raw[VHX_BUF_VOXELS].ptr;
+    const uint32_t *col = (const uint32_t *)c->raw[VHX_BUF_COLOR_PALETTE].ptr;
+    const uint32_t *dat = (const uint32_t *)c->raw[VHX_BUF_DATA_PALETTE].ptr;
+    if (n3 >= 64) {
+        const uint64_t cell0 = (uint64_t)brick0 * n3, ncells = (uint64_t)nbricks * n3;
+        // grid-stride chunks keep gridDim.x within range for multi-GB voxel buffers
+        const uint64_t chunk = 1ull << 30;
+        for (uint64_t s = 0; s < ncells; s += chunk) {
+            const uint64_t n = std::min(chunk, ncells - s);
+            k_brick_occ_ballot<<<(unsigned)((n + 255) / 256), 256, 0, c->stream>>>(
+                vox, n, cell0 + s, col, c->desc.color_count, dat, c->desc.data_count, (uint64_t *)c->brick_occ.ptr);
+            VHX_HIP(c, hipGetLastError());
+        }
+    } else {
+        k_brick_occ_small<<<(nbricks + 255) / 256, 256, 0, c->stream>>>(vox, nbricks, brick0, n3, col,
+                                                                         c->desc.color_count, dat, c->desc.data_count,
+                                                                         (uint64_t *)c->brick_occ.ptr);
+        VHX_HIP(c, hipGetLastError());
+    }
+    return VHX_OK;
+}
+
+struct HostOut {
+    OutD dev{};
+    std::vector<std::pair<void *, std::pair<void *, uint64_t>>> copies;  // (host dst, (dev src, bytes))
+};
+
+// Maps the caller's vhx_hits onto device pointers (scratch-backed when the caller passed host memory).
+static int map_out(vhx_ctx *c, const vhx_hits *h, uint64_t n, int on_device, HostOut &ho) {
+    struct F {
+        void *user;
+        uint64_t per;
+        void **dst;
+    } fields[] = {{h->value, 4, (void **)&ho.dev.value},   {h->cell, 4, (void **)&ho.dev.cell},
+                  {h->voxel, 12, (void **)&ho.dev.voxel},  {h->impact, 12, (void **)&ho.dev.impact},
+                  {h->normal, 12, (void **)&ho.dev.normal}, {h->depth, 4, (void **)&ho.dev.depth},
+                  {h->rgba, 4, (void **)&ho.dev.rgba},     {h->bytes, 4, (void **)&ho.dev.bytes}};
+    if (on_device) {
+        for (auto &f : fields) *f.dst = f.user;
+        return VHX_OK;
+    }
+    uint64_t total = 0;
+    for (auto &f : fields)
+        if (f.user) total += (f.per * n + 255) & ~255ull;
+    int rc = ensure(c, c->scratch, total);
+    if (rc) return rc;
+    uint64_t off = 0;
+    for (auto &f : fields) {
+        if (!f.user) continue;
+        void *p = (char *)c->scratch.ptr + off;
+        *f.dst = p;
+        ho.copies.push_back({f.user, {p, f.per * n}});
+        off += (f.per * n + 255) & ~255ull;
+    }
+    return VHX_OK;
+}
+
+static int finish_out(vhx_ctx *c, HostOut &ho) {
+    for (auto &cp : ho.copies)
+        VHX_HIP(c, hipMemcpyAsync(cp.first, cp.second.first, cp.second.second, hipMemcpyDeviceToHost, c->stream));
+    if (!ho.copies.empty()) VHX_HIP(c, hipStreamSynchronize(c->stream));
+    return VHX_OK;
+}
+
+// ------------------------------------------------------------------------------------------------ C ABI
+extern "C" {
+
+uint32_t vhx_abi_version(void) { return VHX_ABI_VERSION; }
+
+int vhx_device_count(int *count) {
+    if (!count) return VHX_E_INVALID_ARG;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    *count = n;
+    return VHX_OK;
+}
+
+int vhx_create(int hip_device, vhx_ctx **out) {
+    if (!out) return VHX_E_INVALID_ARG;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return VHX_E_NO_DEVICE;
+    if (hip_device < 0 || hip_device >= n) return VHX_E_INVALID_ARG;
+    vhx_ctx *c = new vhx_ctx();
+    c->device = hip_device;
+    auto bail = [&](const char *what, hipError_t e) {
+        fprintf(stderr, "vhx_create: %s: %s\n", what, hipGetErrorString(e));
+        delete c;
+        return VHX_E_HIP;
+    };
+    hipError_t e;
+    if ((e = hipSetDevice(hip_device)) != hipSuccess) return bail("hipSetDevice", e);
+    if ((e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking)) != hipSuccess)
+        return bail("hipStreamCreate", e);
+    c->stream = c->own_stream;
+    if ((e = hipEventCreate(&c->ev0)) != hipSuccess) return bail("hipEventCreate", e);
+    if ((e = hipEventCreate(&c->ev1)) != hipSuccess) return bail("hipEventCreate", e);
+    uint8_t lut[64 * 27];
+    make_step_lut(lut);
+    if ((e = hipMemcpyToSymbol(HIP_SYMBOL(vhx::c_step_lut), lut, sizeof(lut))) != hipSuccess)
+        return bail("hipMemcpyToSymbol", e);
+    *out = c;
+    return VHX_OK;
+}
+
+void vhx_destroy(vhx_ctx *c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (auto &b : c->raw)
+        if (b.ptr) (void)hipFree(b.ptr);
+    for (DevBuf *b : {&c->hdr, &c->brick_occ, &c->scratch})
+        if (b->ptr) (void)hipFree(b->ptr);
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    delete c;
+}
+
+const char *vhx_last_error(const vhx_ctx *c) { return c ? c->err.c_str() : "null context"; }
+
+int vhx_set_stream(vhx_ctx *c, void *s) {
+    if (!c) return VHX_E_INVALID_ARG;
+    c->stream = s ? (hipStream_t)s : c->own_stream;
+    return VHX_OK;
+}
+
+int vhx_sync(vhx_ctx *c, float *ms) {
+    if (!c) return VHX_E_INVALID_ARG;
+    VHX_HIP(c, hipSetDevice(c->device));
+    VHX_HIP(c, hipStreamSynchronize(c->stream));
+    if (ms) {
+        *ms = 0.f;
+        if (c->timed) VHX_HIP(c, hipEventElapsedTime(ms, c->ev0, c->ev1));
+    }
+    return VHX_OK;
+}
+
+int vhx_upload_tree(vhx_ctx *c, const vhx_tree_desc *t) {
+    if (!c || !t) return VHX_E_INVALID_ARG;
+    const uint32_t bd = t->brick_dim;
+    if (t->node_count == 0 || bd == 0 || t->boxtree_size == 0 || (bd & (bd - 1)) != 0 || bd > 32)
+        return fail(c, VHX_E_INVALID_ARG, "vhx_upload_tree: invalid sizes");
+    const void *src[7] = {t->node_type, t->node_ocbits, t->node_children, t->voxels,
+                          t->solid_values, t->color_palette, t->data_palette};
+    VHX_HIP(c, hipSetDevice(c->device));
+    for (int id = 0; id < 7; ++id) {
+        const uint64_t n = elem_count(*t, id), bytes = n * elem_size(id);
+        if (n && !src[id]) return fail(c, VHX_E_INVALID_ARG, "vhx_upload_tree: null array with non-zero count");
+        int rc = ensure(c, c->raw[id], bytes);
+        if (rc) return rc;
+        if (bytes) VHX_HIP(c, hipMemcpyAsync(c->raw[id].ptr, src[id], bytes, hipMemcpyHostToDevice, c->stream));
+    }
+    c->desc = *t;
+    const uint64_t n3 = (uint64_t)bd * bd * bd;
+    c->occ_words = n3 >= 64 ? (uint32_t)(n3 / 64) : 1u;
+    int rc = ensure(c, c->hdr, (uint64_t)t->node_count * 16);
+    if (rc) return rc;
+    rc = ensure(c, c->brick_occ, (uint64_t)t->brick_count * c->occ_words * 8);
+    if (rc) return rc;
+    if ((rc = rebuild_hdr(c, 0, t->node_count))) return rc;
+    if ((rc = rebuild_occ(c, 0, t->brick_count))) return rc;
+    VHX_HIP(c, hipStreamSynchronize(c->stream));
+    c->uploaded = true;
+    return VHX_OK;
+}
+
+int vhx_update_range(vhx_ctx *c, int id, uint64_t off, uint64_t count, const void *src) {
+    if (!c || id < 0 || id > 6 || (!src && count)) return VHX_E_INVALID_ARG;
+    if (!c->uploaded) return fail(c, VHX_E_STATE, "vhx_update_range before vhx_upload_tree");
+    const uint64_t cap = elem_count(c->desc, id);
+    if (off + count > cap) return fail(c, VHX_E_CAPACITY, "vhx_update_range: range beyond the uploaded buffer");
+    if (count == 0) return VHX_OK;
+    VHX_HIP(c, hipSetDevice(c->device));
+    const uint64_t es = elem_size(id);
+    VHX_HIP(c, hipMemcpyAsync((char *)c->raw[id].ptr + off * es, src, count * es, hipMemcpyHostToDevice, c->stream));
+    int rc = VHX_OK;
+    const uint64_t n3 = (uint64_t)c->desc.brick_dim * c->desc.brick_dim * c->desc.brick_dim;
+    if (id == VHX_BUF_NODE_TYPE || id == VHX_BUF_NODE_OCBITS) rc = rebuild_hdr(c, (uint32_t)off, (uint32_t)count);
+    else if (id == VHX_BUF_VOXELS) {
+        const uint64_t b0 = off / n3, b1 = (off + count + n3 - 1) / n3;
+        rc = rebuild_occ(c, (uint32_t)b0, (uint32_t)(b1 - b0));
+    } else if (id == VHX_BUF_COLOR_PALETTE || id == VHX_BUF_DATA_PALETTE)
+        rc = rebuild_occ(c, 0, c->desc.brick_count);
+    if (rc) return rc;
+    VHX_HIP(c, hipStreamSynchronize(c->stream));
+    return VHX_OK;
+}
+
+int vhx_tree_device_bytes(const vhx_ctx *c, uint64_t *bytes) {
+    if (!c || !bytes) return VHX_E_INVALID_ARG;
+    uint64_t b = c->hdr.bytes + c->brick_occ.bytes;
+    for (auto &r : c->raw) b += r.bytes;
+    *bytes = b;
+    return VHX_OK;
+}
+
+static CamD cam_of(const vhx_camera *cam) {
+    CamD d;
+    d.model = cam->ray_model;
+    d.width = cam->width;
+    d.height = cam->height;
+    d.ox = cam->origin[0];
+    d.oy = cam->origin[1];
+    d.oz = cam->origin[2];
+    d.blx = cam->glass_bottom_left[0];
+    d.bly = cam->glass_bottom_left[1];
+    d.blz = cam->glass_bottom_left[2];
+    d.rx = cam->glass_right[0];
+    d.ry = cam->glass_right[1];
+    d.rz = cam->glass_right[2];
+    d.ux = cam->glass_up[0];
+    d.uy = cam->glass_up[1];
+    d.uz = cam->glass_up[2];
+    d.pw = cam->pixel_width;
+    d.ph = cam->pixel_height;
+    std::memcpy(d.m, cam->inv_view_proj, sizeof(d.m));
+    return d;
+}
+
+int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t tile_start, uint32_t tile_stride,
+                      uint32_t layout, const vhx_hits *out, int on_device) {
+    if (!c || !cam || !out) return VHX_E_INVALID_ARG;
+    if (!c->uploaded) return fail(c, VHX_E_STATE, "vhx_trace_primary before vhx_upload_tree");
+    if (cam->width == 0 || cam->height == 0 || cam->ray_model > VHX_RAY_GLASS || layout > VHX_LAYOUT_TILES)
+        return fail(c, VHX_E_INVALID_ARG, "vhx_trace_primary: bad camera or layout");
+    if (T == 0) {
+        if (layout != VHX_LAYOUT_FRAMEBUFFER) return fail(c, VHX_E_INVALID_ARG, "tile_size 0 needs the framebuffer layout");
+        T = 16;
+        tile_start = 0;
+        tile_stride = 1;
+    }
+    if (tile_stride == 0) return fail(c, VHX_E_INVALID_ARG, "tile_stride 0");
+    const uint32_t tiles_x = (cam->width + T - 1) / T, tiles_y = (cam->height + T - 1) / T;
+    const uint32_t ntiles = tiles_x * tiles_y;
+    if (tile_start >= ntiles) return VHX_OK;
+    const uint32_t my_tiles = (ntiles - tile_start + tile_stride - 1) / tile_stride;
+    const uint32_t bpx = (T + 15) / 16, bpt = bpx * bpx;
+    const uint64_t nblocks = (uint64_t)my_tiles * bpt;
+    if (nblocks > 0x7FFFFFFFull) return fail(c, VHX_E_INVALID_ARG, "frame too large");
+    const uint64_t nout = layout == VHX_LAYOUT_FRAMEBUFFER ? (uint64_t)cam->width * cam->height
+                                                           : (uint64_t)my_tiles * T * T;
+    VHX_HIP(c, hipSetDevice(c->device));
+    HostOut ho;
+    int rc = map_out(c, out, nout, on_device, ho);
+    if (rc) return rc;
+    const DevTree t = dev_tree(c);
+    const CamD cd = cam_of(cam);
+    VHX_HIP(c, hipEventRecord(c->ev0, c->stream));
+    if (ho.dev.bytes)
+        k_trace_primary<true><<<(unsigned)nblocks, 256, 0, c->stream>>>(t, cd, ho.dev, T, tiles_x, tile_start,
+                                                                        tile_stride, layout, bpx, bpt);
+    else
+        k_trace_primary<false><<<(unsigned)nblocks, 256, 0, c->stream>>>(t, cd, ho.dev, T, tiles_x, tile_start,
+                                                                         tile_stride, layout, bpx, bpt);
+    VHX_HIP(c, hipGetLastError());
+    VHX_HIP(c, hipEventRecord(c->ev1, c->stream));
+    c->timed = true;
+    return finish_out(c, ho);
+}
+
+int vhx_trace_rays(vhx_ctx *c, const float *rays, uint64_t n, const vhx_hits *out, int on_device) {
+    if (!c || !out || (!rays && n)) return VHX_E_INVALID_ARG;
+    if (!c->uploaded) return fail(c, VHX_E_STATE, "vhx_trace_rays before vhx_upload_tree");
+    if (n == 0) return VHX_OK;
+    if ((n + 255) / 256 > 0x7FFFFFFFull) return fail(c, VHX_E_INVALID_ARG, "too many rays");
+    VHX_HIP(c, hipSetDevice(c->device));
+    HostOut ho;
+    int rc = map_out(c, out, n, on_device, ho);
+    if (rc) return rc;
+    const float *drays = rays;
+    void *tmp = nullptr;
+    if (!on_device) {
+        VHX_HIP(c, hipMallocAsync(&tmp, n * 24, c->stream));
+        VHX_HIP(c, hipMemcpyAsync(tmp, rays, n * 24, hipMemcpyHostToDevice, c->stream));
+        drays = (const float *)tmp;
+    }
+    const DevTree t = dev_tree(c);
+    VHX_HIP(c, hipEventRecord(c->ev0, c->stream));
+    if (ho.dev.bytes)
+        k_trace_rays<true><<<(unsigned)((n + 255) / 256), 256, 0, c->stream>>>(t, drays, n, ho.dev);
+    else
+        k_trace_rays<false><<<(unsigned)((n + 255) / 256), 256, 0, c->stream>>>(t, drays, n, ho.dev);
+    VHX_HIP(c, hipGetLastError());
+    VHX_HIP(c, hipEventRecord(c->ev1, c->stream));
+    c->timed = true;
+    rc = finish_out(c, ho);
+    if (tmp) VHX_HIP(c, hipFreeAsync(tmp, c->stream));
+    if (tmp) VHX_HIP(c, hipStreamSynchronize(c->stream));
+    return rc;
+}
+
+int vhx_untile_rgba(vhx_ctx *c, const uint32_t *gathered, uint32_t ranks, uint32_t tiles_per_rank, uint32_t T,
+                    uint32_t width, uint32_t height, uint32_t *fb, int on_device) {
+    if (!c || !gathered || !fb || ranks == 0 || T == 0 || width == 0 || height == 0) return VHX_E_INVALID_ARG;
+    if (!on_device) return fail(c, VHX_E_INVALID_ARG, "vhx_untile_rgba works on device buffers");
+    const uint32_t tiles_x = (width + T - 1) / T, tiles_y = (height + T - 1) / T;
+    const uint64_t n = (uint64_t)ranks * tiles_per_rank * T * T;
+    if ((n + 255) / 256 > 0x7FFFFFFFull) return fail(c, VHX_E_INVALID_ARG, "too many pixels");
+    VHX_HIP(c, hipSetDevice(c->device));
+    k_untile_rgba<<<(unsigned)((n + 255) / 256), 256, 0, c->stream>>>(gathered, ranks, tiles_per_rank, T, tiles_x,
+                                                                      tiles_x * tiles_y, width, height, fb);
+    VHX_HIP(c, hipGetLastError());
+    return VHX_OK;
+}
+
+}  // extern "C"

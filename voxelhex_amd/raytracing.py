@@ -1,0 +1,299 @@
+"""GPU raytracing API: the MI355X replacement of VoxelHex's `src/raytracing` module.
+
+    Ray                      voxelhex::raytracing::Ray (src/spatial/raytracing/mod.rs:8-22)
+    Raytracer                a libvhx context: one device, the tree resident in HBM (BoxTreeGPUHost + view,
+                             src/raytracing/bevy/mod.rs:164-180, src/raytracing/bevy/view.rs:36-137)
+    Raytracer.trace_rays     BoxTree::get_by_ray over a batch (src/raytracing/cpu.rs:296)
+    Raytracer.trace_primary  one frame of per-pixel primary rays (VhxRenderNode::run,
+                             src/raytracing/bevy/pipeline/mod.rs:96-155, with the CPU frame semantics of
+                             examples/gpu_render.rs:196-257)
+    Viewport                 src/raytracing/bevy/types.rs:60-88 with update_matrices (src/raytracing/bevy/view.rs:211-239)
+    glass_camera             the pinhole camera of benches/performance.rs:29-61
+
+Every call goes through the HIP kernels of libvhx; there is no CPU path here.
+"""
+import ctypes
+from dataclasses import dataclass, field
+import math
+
+import numpy as np
+
+from . import _native as N
+from .boxtree import V3c, FlatTree
+
+f32 = np.float32
+_libm = ctypes.CDLL("libm.so.6")
+_libm.sinf.restype = ctypes.c_float
+_libm.sinf.argtypes = [ctypes.c_float]
+_libm.cosf.restype = ctypes.c_float
+_libm.cosf.argtypes = [ctypes.c_float]
+_libm.tanf.restype = ctypes.c_float
+_libm.tanf.argtypes = [ctypes.c_float]
+
+
+@dataclass
+class Ray:
+    origin: V3c
+    direction: V3c
+
+    def is_valid(self):
+        d = np.array(list(self.direction), f32)
+        return abs(f32(1) - _len(d)) < f32(0.000001)
+
+
+# ---------------------------------------------------------------------------------------------- f32 V3c helpers
+def _v(*a):
+    return np.array(a, f32)
+
+
+def _len(v):
+    """V3c::length (src/spatial/math/vector.rs:71-73): sqrt((x*x + y*y) + z*z) in f32."""
+    return f32(np.sqrt(f32(f32(v[0] * v[0]) + f32(v[1] * v[1])) + f32(v[2] * v[2])))
+
+
+def _normalized(v):
+    """V3c::normalized: v / length (three f32 divisions)."""
+    l = _len(v)
+    return np.array([v[0] / l, v[1] / l, v[2] / l], f32)
+
+
+def _cross(a, b):
+    """V3c::cross (src/spatial/math/vector.rs:196-202)."""
+    return np.array([f32(a[1] * b[2]) - f32(a[2] * b[1]), f32(a[2] * b[0]) - f32(a[0] * b[2]),
+                     f32(a[0] * b[1]) - f32(a[1] * b[0])], f32)
+
+
+def glass_camera(tree_size, width, height, angle=40.0, radius=None, target=None, glass_width=4.0,
+                 glass_height=None, fov=3.0):
+    """Pinhole 'glass' camera of benches/performance.rs:32-61.
+
+    The reference bench renders 128x128 rays through a 4x4 glass at distance 3 from a camera at
+    (sin(40) R, R, cos(40) R), R = 2*tree_size, aimed at (0,0,0). Defaults keep that geometry; `target` re-aims it
+    (SURVEY.md 8d aims at the tree centre) and glass_height defaults to 4*height/width so pixels stay square.
+    Arithmetic is f32 in the reference's op order; sin/cos come from libm's sinf/cosf like Rust's f32::sin.
+    """
+    S = f32(tree_size)
+    R = f32(2.0) * S if radius is None else f32(radius)
+    a = f32(angle)
+    origin = _v(f32(_libm.sinf(a)) * R, R, f32(_libm.cosf(a)) * R)
+    tgt = _v(0, 0, 0) if target is None else np.array(target, f32)
+    direction = _normalized(tgt - origin)
+    up = _v(0, 1, 0)
+    right = _normalized(_cross(up, direction))
+    gw = f32(glass_width)
+    gh = f32(glass_width * height / width) if glass_height is None else f32(glass_height)
+    pw = f32(gw / f32(width))
+    ph = f32(gh / f32(height))
+    bl = ((origin + direction * f32(fov)) - up * f32(gh / f32(2))) - right * f32(gw / f32(2))
+    cam = N.Camera()
+    cam.ray_model = N.VHX_RAY_GLASS
+    cam.width, cam.height = width, height
+    cam.origin[:] = [float(v) for v in origin]
+    cam.glass_bottom_left[:] = [float(v) for v in bl]
+    cam.glass_right[:] = [float(v) for v in right]
+    cam.glass_up[:] = [float(v) for v in up]
+    cam.pixel_width = float(pw)
+    cam.pixel_height = float(ph)
+    return cam
+
+
+@dataclass
+class Viewport:
+    """Viewport (src/raytracing/bevy/types.rs:60-88)."""
+    origin: tuple
+    direction: tuple
+    frustum: tuple
+    fov: float
+    view_matrix: np.ndarray = field(default_factory=lambda: np.eye(4, dtype=f32))
+    projection_matrix: np.ndarray = field(default_factory=lambda: np.eye(4, dtype=f32))
+    inverse_view_projection_matrix: np.ndarray = field(default_factory=lambda: np.eye(4, dtype=f32))
+
+    def update_matrices(self, resolution):
+        """Viewport::update_matrices (src/raytracing/bevy/view.rs:211-239); matrices stored column-major like glam.
+
+        look_at_rh and perspective_rh follow glam 0.29's formulas in f32; the inverse is computed in f64 and
+        rounded (glam's cofactor order is not restated: parity for this matrix is unpinned)."""
+        fwd = np.array(self.direction, f32)
+        right = _normalized(_cross(fwd, _v(0, 1, 0)))
+        up = _normalized(_cross(right, fwd))
+        eye = np.array(self.origin, f32)
+        center = eye + fwd
+        f = _normalized(center - eye)
+        s = _normalized(_cross(f, up))
+        u = _cross(s, f)
+        view = np.zeros((4, 4), f32)  # [col][row]
+        view[0] = [s[0], u[0], -f[0], 0]
+        view[1] = [s[1], u[1], -f[1], 0]
+        view[2] = [s[2], u[2], -f[2], 0]
+        view[3] = [-np.dot(eye, s), -np.dot(eye, u), np.dot(eye, f), 1]
+        aspect = f32(resolution[0]) / f32(resolution[1])
+        fov_r = f32(math.radians(self.fov))
+        near = f32(self.frustum[1]) / f32(2.0) / f32(_libm.tanf(fov_r / f32(2.0)))
+        far = f32(self.frustum[2])
+        half = f32(0.5) * fov_r
+        h = f32(_libm.cosf(half)) / f32(_libm.sinf(half))
+        w = h / aspect
+        r = far / (near - far)
+        proj = np.zeros((4, 4), f32)
+        proj[0] = [w, 0, 0, 0]
+        proj[1] = [0, h, 0, 0]
+        proj[2] = [0, 0, r, -1]
+        proj[3] = [0, 0, r * near, 0]
+        # column-major storage: M[col][row]; math matrix = storage.T
+        vp = (proj.T.astype(np.float64) @ view.T.astype(np.float64))
+        self.view_matrix, self.projection_matrix = view, proj
+        self.inverse_view_projection_matrix = np.linalg.inv(vp).T.astype(f32)
+
+    def camera(self, width, height):
+        self.update_matrices((width, height))
+        cam = N.Camera()
+        cam.ray_model = N.VHX_RAY_INVERSE_VP
+        cam.width, cam.height = width, height
+        cam.origin[:] = [float(v) for v in self.origin]
+        cam.inv_view_proj[:] = [float(v) for v in self.inverse_view_projection_matrix.reshape(-1)]
+        return cam
+
+
+HIT_FIELDS = (("value", np.uint32, 1), ("cell", np.uint32, 1), ("voxel", np.uint32, 3), ("impact", np.float32, 3),
+              ("normal", np.float32, 3), ("depth", np.float32, 1), ("rgba", np.uint32, 1), ("bytes", np.uint32, 1))
+
+
+def _hits_struct(arrays):
+    h = N.Hits()
+    for name, _, _ in HIT_FIELDS:
+        a = arrays.get(name)
+        setattr(h, name, None if a is None else _ptr(a))
+    return h
+
+
+def _ptr(a):
+    if hasattr(a, "data_ptr"):  # torch tensor (device or host)
+        return a.data_ptr()
+    return a.ctypes.data
+
+
+class Raytracer:
+    """A libvhx context on one HIP device with a tree resident in HBM."""
+
+    def __init__(self, device=0):
+        lib = N.lib()
+        n = ctypes.c_int()
+        N.check(lib.vhx_device_count(ctypes.byref(n)))
+        if n.value == 0:
+            raise RuntimeError("voxelhex_amd: no HIP device is visible (the raytracer has no CPU fallback)")
+        h = ctypes.c_void_p()
+        N.check(lib.vhx_create(device, ctypes.byref(h)))
+        self._h = h
+        self.device = device
+        self._tree = None
+
+    def close(self):
+        if getattr(self, "_h", None) and self._h.value:
+            N.lib().vhx_destroy(self._h)
+            self._h = ctypes.c_void_p(None)
+
+    def __del__(self):
+        self.close()
+
+    def _check(self, rc):
+        return N.check(rc, self._h)
+
+    def upload(self, flat: FlatTree):
+        if self._tree is flat:
+            return
+        self._check(N.lib().vhx_upload_tree(self._h, ctypes.byref(flat.desc)))
+        self._tree = flat
+
+    def update_range(self, buffer_id, elem_offset, values):
+        values = np.ascontiguousarray(values)
+        self._check(N.lib().vhx_update_range(self._h, buffer_id, elem_offset, values.size, values.ctypes.data))
+
+    def device_bytes(self):
+        b = ctypes.c_uint64()
+        self._check(N.lib().vhx_tree_device_bytes(self._h, ctypes.byref(b)))
+        return b.value
+
+    def set_stream(self, stream_ptr):
+        self._check(N.lib().vhx_set_stream(self._h, ctypes.c_void_p(stream_ptr)))
+
+    def sync(self):
+        ms = ctypes.c_float()
+        self._check(N.lib().vhx_sync(self._h, ctypes.byref(ms)))
+        return ms.value
+
+    def trace_rays(self, origins, directions, fields=("value", "cell", "voxel", "impact", "normal", "depth", "rgba"),
+                   count_bytes=False):
+        """Traces rays given as (n,3) f32 origins and directions on the host; returns numpy hit arrays."""
+        o = np.ascontiguousarray(origins, f32).reshape(-1, 3)
+        d = np.ascontiguousarray(directions, f32).reshape(-1, 3)
+        n = o.shape[0]
+        rays = np.ascontiguousarray(np.concatenate([o, d], axis=1), f32)
+        fields = tuple(fields) + (("bytes",) if count_bytes else ())
+        out = {name: np.empty((n, k) if k > 1 else (n,), dt) for name, dt, k in HIT_FIELDS if name in fields}
+        hs = _hits_struct(out)
+        self._check(N.lib().vhx_trace_rays(self._h, rays.ctypes.data, n, ctypes.byref(hs), 0))
+        return out
+
+    def trace_primary(self, cam, tile_size=0, tile_start=0, tile_stride=1, layout=N.VHX_LAYOUT_FRAMEBUFFER,
+                      fields=("value", "cell", "voxel", "impact", "normal", "depth", "rgba"), count_bytes=False,
+                      out=None):
+        """Traces one frame (or this rank's tiles). With out=dict of device tensors nothing is copied back."""
+        if out is not None:
+            hs = _hits_struct(out)
+            self._check(N.lib().vhx_trace_primary(self._h, ctypes.byref(cam), tile_size, tile_start, tile_stride,
+                                                  layout, ctypes.byref(hs), 1))
+            return out
+        if layout == N.VHX_LAYOUT_FRAMEBUFFER:
+            n = cam.width * cam.height
+        else:
+            T = tile_size
+            ntiles = ((cam.width + T - 1) // T) * ((cam.height + T - 1) // T)
+            n = max(0, (ntiles - tile_start + tile_stride - 1) // tile_stride) * T * T
+        fields = tuple(fields) + (("bytes",) if count_bytes else ())
+        alloc = np.empty if layout == N.VHX_LAYOUT_FRAMEBUFFER else np.zeros  # tiles past the frame edge stay 0
+        res = {name: alloc((n, k) if k > 1 else (n,), dt) for name, dt, k in HIT_FIELDS if name in fields}
+        hs = _hits_struct(res)
+        self._check(N.lib().vhx_trace_primary(self._h, ctypes.byref(cam), tile_size, tile_start, tile_stride, layout,
+                                              ctypes.byref(hs), 0))
+        return res
+
+    def untile_rgba(self, gathered_dev_ptr, ranks, tiles_per_rank, tile_size, width, height, fb_dev_ptr):
+        self._check(N.lib().vhx_untile_rgba(self._h, ctypes.c_void_p(gathered_dev_ptr), ranks, tiles_per_rank,
+                                            tile_size, width, height, ctypes.c_void_p(fb_dev_ptr), 1))
+
+
+_default = {}
+
+
+def default_raytracer(device=None):
+    dev = 0 if device is None else device
+    if dev not in _default:
+        _default[dev] = Raytracer(dev)
+    return _default[dev]
+
+
+class BoxTreeGPUHost:
+    """BoxTreeGPUHost (src/raytracing/bevy/types.rs:91-103): owns the tree and renders views of it on a GPU."""
+
+    def __init__(self, tree, device=0):
+        self.tree = tree
+        self.raytracer = Raytracer(device)
+
+    def create_new_view(self, viewport, resolution):
+        return BoxTreeGPUView(self, viewport, resolution)
+
+
+class BoxTreeGPUView:
+    """A view (src/raytracing/bevy/types.rs:134-180): viewport + output resolution, rendered to RGBA8."""
+
+    def __init__(self, host, viewport, resolution):
+        self.host, self.viewport, self.resolution = host, viewport, tuple(resolution)
+
+    def render(self, fields=("rgba", "depth")):
+        flat = self.host.tree.flatten() if hasattr(self.host.tree, "flatten") else self.host.tree
+        self.host.raytracer.upload(flat)
+        w, h = self.resolution
+        res = self.host.raytracer.trace_primary(self.viewport.camera(w, h), fields=fields)
+        if "rgba" in res:
+            res["image"] = res["rgba"].view(np.uint8).reshape(h, w, 4)
+        return res
