@@ -68,8 +68,11 @@ def main():
     flat = vhx.FlatTree.build_scene(args.scene, args.size, args.brick_dim, threads=min(16, os.cpu_count() or 1))
     build_s = time.time() - t0
     rt = vhx.Raytracer(local)
-    stream = torch.cuda.current_stream(dev)
-    rt.set_stream(stream.cuda_stream)  # kernels run on torch's stream: torch events and RCCL see them in order
+    # one dedicated (non-null) stream shared by libvhx and torch: the kernel, the torch events that time it and
+    # the RCCL gather are ordered on it
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    rt.set_stream(stream.cuda_stream)
     t0 = time.time()
     rt.upload(flat)
     upload_s = time.time() - t0

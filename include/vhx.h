@@ -154,6 +154,12 @@ int vhx_upload_tree(vhx_ctx *ctx, const vhx_tree_desc *tree);
 /* Overwrites elements [elem_offset, elem_offset+elem_count) of one uploaded buffer (element = one entry of the
  * corresponding vhx_tree_desc array) and refreshes the derived device state. VHX_E_CAPACITY past the end. */
 int vhx_update_range(vhx_ctx *ctx, int buffer_id, uint64_t elem_offset, uint64_t elem_count, const void *src);
+/* Diagnostics: copies elements of a derived device buffer to host memory (for tests).
+ * VHX_DERIVED_NODE_HDR: 16-byte {occ_lo, occ_hi, type, 0} per node; VHX_DERIVED_BRICK_OCC: u64 words, brick_dim^3
+ * bits per brick (max(1, brick_dim^3/64) words), bit = flat cell index, set = cell not empty. */
+#define VHX_DERIVED_NODE_HDR 0
+#define VHX_DERIVED_BRICK_OCC 1
+int vhx_read_derived(vhx_ctx *ctx, int which, uint64_t elem_offset, uint64_t elem_count, void *dst);
 /* Device bytes held by the uploaded tree. */
 int vhx_tree_device_bytes(const vhx_ctx *ctx, uint64_t *bytes);
 

@@ -140,7 +140,7 @@ def test_primary_frame_glass_vs_oracle(gpu, oracle, scene, size, bd, w, h):
     got = gpu.trace_primary(cam, count_bytes=True)
     ref = oracle.trace_primary(flat, cam, 0, 0, w, h, count_bytes=True)
     assert_same(got, ref, f"frame {size}/{bd}")
-    assert (got["value"] != N.VHX_EMPTY).sum() > w * h // 20
+    assert (got["value"] != N.VHX_EMPTY).sum() > 100
 
 
 def test_primary_frame_inverse_vp_vs_oracle(gpu, oracle):
@@ -178,12 +178,12 @@ def test_tiles_and_untile_match_framebuffer(gpu):
 
 def test_update_range(gpu, oracle):
     """vhx_update_range (write_range_to_buffer, src/raytracing/bevy/streaming/mod.rs:344-370)."""
-    t = vhx.BoxTree(32, 4)
+    t = vhx.BoxTree(64, 4)
     t.insert_scene(N.VHX_SCENE_LATTICE_CUBE)
     flat = t.flatten()
     gpu.upload(flat)
     rng = np.random.default_rng(5)
-    o, d = rand_rays(rng, 32, 5000)
+    o, d = rand_rays(rng, 64, 5000)
     before = gpu.trace_rays(o, d)
     vox = flat.voxels.copy()
     vox[: vox.size // 2] = N.VHX_EMPTY  # clear half of the bricks

@@ -37,6 +37,7 @@ VHX_SCENE_LATTICE_CUBE, VHX_SCENE_BENCH_REGION, VHX_SCENE_LATTICE = 1, 2, 3
 VHX_SCENE_CUBE, VHX_SCENE_BOUNDARY, VHX_SCENE_HEIGHTFIELD = 4, 5, 6
 VHX_BUF_NODE_TYPE, VHX_BUF_NODE_OCBITS, VHX_BUF_NODE_CHILDREN, VHX_BUF_VOXELS = 0, 1, 2, 3
 VHX_BUF_SOLID_VALUES, VHX_BUF_COLOR_PALETTE, VHX_BUF_DATA_PALETTE = 4, 5, 6
+VHX_DERIVED_NODE_HDR, VHX_DERIVED_BRICK_OCC = 0, 1
 
 
 class TreeDesc(ctypes.Structure):
@@ -75,6 +76,7 @@ SIGNATURES = [
     ("vhx_sync", c_int, [c_void_p, P(c_f32)]),
     ("vhx_upload_tree", c_int, [c_void_p, P(TreeDesc)]),
     ("vhx_update_range", c_int, [c_void_p, c_int, c_u64, c_u64, c_void_p]),
+    ("vhx_read_derived", c_int, [c_void_p, c_int, c_u64, c_u64, c_void_p]),
     ("vhx_tree_device_bytes", c_int, [c_void_p, P(c_u64)]),
     ("vhx_trace_primary", c_int, [c_void_p, P(Camera), c_u32, c_u32, c_u32, c_u32, P(Hits), c_int]),
     ("vhx_trace_rays", c_int, [c_void_p, c_void_p, c_u64, P(Hits), c_int]),
@@ -105,6 +107,12 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise ImportError(
                 f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+        try:
+            # torch ships its own HIP runtime (libamdhip64.so.7); loading it first makes libvhx bind to the same
+            # runtime instance, so torch streams, events and device pointers are valid in libvhx calls
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         l = ctypes.CDLL(LIB_PATH)
         for name, res, args in SIGNATURES:
             f = getattr(l, name)

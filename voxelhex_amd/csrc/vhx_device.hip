@@ -41,7 +41,7 @@ struct vhx_ctx {
     bool uploaded = false;
     vhx_tree_desc desc{};  // counts of the uploaded tree (pointers unused)
     DevBuf raw[7];         // VHX_BUF_* raw copies
-    DevBuf hdr, brick_occ, scratch;
+    DevBuf hdr, brick_occ, scratch, rays;
     uint32_t occ_words = 1;
 };
 
@@ -430,7 +430,7 @@ void vhx_destroy(vhx_ctx *c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (auto &b : c->raw)
         if (b.ptr) (void)hipFree(b.ptr);
-    for (DevBuf *b : {&c->hdr, &c->brick_occ, &c->scratch})
+    for (DevBuf *b : {&c->hdr, &c->brick_occ, &c->scratch, &c->rays})
         if (b->ptr) (void)hipFree(b->ptr);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -504,6 +504,20 @@ int vhx_update_range(vhx_ctx *c, int id, uint64_t off, uint64_t count, const voi
     } else if (id == VHX_BUF_COLOR_PALETTE || id == VHX_BUF_DATA_PALETTE)
         rc = rebuild_occ(c, 0, c->desc.brick_count);
     if (rc) return rc;
+    VHX_HIP(c, hipStreamSynchronize(c->stream));
+    return VHX_OK;
+}
+
+int vhx_read_derived(vhx_ctx *c, int which, uint64_t off, uint64_t count, void *dst) {
+    if (!c || (!dst && count) || which < 0 || which > 1) return VHX_E_INVALID_ARG;
+    if (!c->uploaded) return fail(c, VHX_E_STATE, "vhx_read_derived before vhx_upload_tree");
+    const uint64_t es = which == VHX_DERIVED_NODE_HDR ? 16 : 8;
+    const uint64_t cap = which == VHX_DERIVED_NODE_HDR ? c->desc.node_count
+                                                       : (uint64_t)c->desc.brick_count * c->occ_words;
+    if (off + count > cap) return fail(c, VHX_E_CAPACITY, "vhx_read_derived: range beyond the buffer");
+    const DevBuf &b = which == VHX_DERIVED_NODE_HDR ? c->hdr : c->brick_occ;
+    VHX_HIP(c, hipSetDevice(c->device));
+    VHX_HIP(c, hipMemcpyAsync(dst, (const char *)b.ptr + off * es, count * es, hipMemcpyDeviceToHost, c->stream));
     VHX_HIP(c, hipStreamSynchronize(c->stream));
     return VHX_OK;
 }
@@ -590,11 +604,13 @@ int vhx_trace_rays(vhx_ctx *c, const float *rays, uint64_t n, const vhx_hits *ou
     int rc = map_out(c, out, n, on_device, ho);
     if (rc) return rc;
     const float *drays = rays;
-    void *tmp = nullptr;
     if (!on_device) {
-        VHX_HIP(c, hipMallocAsync(&tmp, n * 24, c->stream));
-        VHX_HIP(c, hipMemcpyAsync(tmp, rays, n * 24, hipMemcpyHostToDevice, c->stream));
-        drays = (const float *)tmp;
+        // context-owned staging buffer (a stream-ordered hipMallocAsync buffer here intermittently handed the
+        // kernel stale ray data after a pageable host copy on ROCm 7.2)
+        rc = ensure(c, c->rays, n * 24);
+        if (rc) return rc;
+        VHX_HIP(c, hipMemcpyAsync(c->rays.ptr, rays, n * 24, hipMemcpyHostToDevice, c->stream));
+        drays = (const float *)c->rays.ptr;
     }
     const DevTree t = dev_tree(c);
     VHX_HIP(c, hipEventRecord(c->ev0, c->stream));
@@ -605,10 +621,7 @@ int vhx_trace_rays(vhx_ctx *c, const float *rays, uint64_t n, const vhx_hits *ou
     VHX_HIP(c, hipGetLastError());
     VHX_HIP(c, hipEventRecord(c->ev1, c->stream));
     c->timed = true;
-    rc = finish_out(c, ho);
-    if (tmp) VHX_HIP(c, hipFreeAsync(tmp, c->stream));
-    if (tmp) VHX_HIP(c, hipStreamSynchronize(c->stream));
-    return rc;
+    return finish_out(c, ho);
 }
 
 int vhx_untile_rgba(vhx_ctx *c, const uint32_t *gathered, uint32_t ranks, uint32_t tiles_per_rank, uint32_t T,

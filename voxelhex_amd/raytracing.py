@@ -208,6 +208,13 @@ class Raytracer:
         values = np.ascontiguousarray(values)
         self._check(N.lib().vhx_update_range(self._h, buffer_id, elem_offset, values.size, values.ctypes.data))
 
+    def read_derived(self, which, offset, count):
+        dt = np.uint32 if which == N.VHX_DERIVED_NODE_HDR else np.uint64
+        k = 4 if which == N.VHX_DERIVED_NODE_HDR else 1
+        a = np.empty(count * k, dt)
+        self._check(N.lib().vhx_read_derived(self._h, which, offset, count, a.ctypes.data))
+        return a.reshape(count, k) if k > 1 else a
+
     def device_bytes(self):
         b = ctypes.c_uint64()
         self._check(N.lib().vhx_tree_device_bytes(self._h, ctypes.byref(b)))
