@@ -42,6 +42,7 @@
 #endif
 
 #define VHX_ORACLE_MAX_ITERS (1u << 22)
+static _Thread_local uint32_t g_brick_steps; /* per-thread scratch for the work statistics */
 
 typedef struct { float x, y, z; } v3;
 typedef struct { v3 min; float size; } cube;
@@ -202,6 +203,7 @@ typedef struct {
 typedef struct {
     uint32_t value, cell, voxel[3], bytes, hit;
     v3 impact, normal;
+    uint32_t n_node, n_advance, n_brick, n_pop, n_push, n_restart, n_probe; /* work statistics */
 } hit_t;
 
 /* get_dda_scale_factors, cpu.rs:79-92 */
@@ -261,6 +263,8 @@ static int traverse_brick(const vhx_tree_desc *t, const ray_t *r, v3 *p, const u
             return 1;
         }
         if (++*iters > VHX_ORACLE_MAX_ITERS) return 0;
+        (*bytes) += 0; /* keep byte model unchanged */
+        g_brick_steps += 1;
         step = dda_step(r, p, cur);
         cur.min = v_add(cur.min, v_mul(step, unit));
         ix += r_as_i32(roundf(step.x));
@@ -351,6 +355,7 @@ static void get_by_ray(const vhx_tree_desc *t, v3 o, v3 d, hit_t *h) {
         ns_push(&stack, 0);
         while (stack.count != 0) {
             if (++iters > VHX_ORACLE_MAX_ITERS) return;
+            h->n_node++;
             uint64_t occ = t->node_ocbits[stack.data[stack.head]];
             uint32_t ntype = t->node_type[node];
             h->bytes += 12;
@@ -358,6 +363,7 @@ static void get_by_ray(const vhx_tree_desc *t, v3 o, v3 d, hit_t *h) {
             if (target < 64) {
                 if (ntype == VHX_NODE_UNIFORM_LEAF) {
                     h->bytes += 4;
+                    h->n_probe++;
                     if (probe_brick(t, &r, &p, t->node_children[(uint64_t)node * 64], cur, h, &iters)) {
                         h->hit = 1;
                         return;
@@ -365,6 +371,7 @@ static void get_by_ray(const vhx_tree_desc *t, v3 o, v3 d, hit_t *h) {
                     backtrack = 1;
                 } else if (ntype == VHX_NODE_LEAF) {
                     h->bytes += 4;
+                    h->n_probe++;
                     if (probe_brick(t, &r, &p, t->node_children[(uint64_t)node * 64 + target],
                                     child_bounds_for(cur, target), h, &iters)) {
                         h->hit = 1;
@@ -374,6 +381,7 @@ static void get_by_ray(const vhx_tree_desc *t, v3 o, v3 d, hit_t *h) {
             }
             if (backtrack || target >= 64 || occ == 0 || (occ & OCC_LUT[target][dir_idx]) == 0) {
                 /* POP */
+                h->n_pop++;
                 ns_pop(&stack);
                 tb = cur;
                 cur.size *= 4.0f;
@@ -389,6 +397,7 @@ static void get_by_ray(const vhx_tree_desc *t, v3 o, v3 d, hit_t *h) {
             }
             if (ntype == VHX_NODE_INTERNAL && (occ & ((uint64_t)1 << target)) != 0) {
                 /* PUSH */
+                h->n_push++;
                 h->bytes += 4;
                 uint32_t child = t->node_children[(uint64_t)node * 64 + target];
                 if (child >= t->node_count) return; /* reference would panic on the invalid key */
@@ -401,6 +410,7 @@ static void get_by_ray(const vhx_tree_desc *t, v3 o, v3 d, hit_t *h) {
                 /* ADVANCE */
                 for (;;) {
                     if (++iters > VHX_ORACLE_MAX_ITERS) return;
+                    h->n_advance++;
                     v3 sv = dda_step(&r, &p, tb);
                     target = step_sectant(target, sv);
                     if (target < 64) tb.min = v_add(tb.min, v_mul(sv, tb.size));
@@ -408,6 +418,7 @@ static void get_by_ray(const vhx_tree_desc *t, v3 o, v3 d, hit_t *h) {
                 }
             }
         }
+        h->n_restart++;
         p = v_add(p, v_mul(d, 0.1f));
         if (p.x < tsize && p.y < tsize && p.z < tsize && p.x > 0.f && p.y > 0.f && p.z > 0.f)
             target = offset_sectant(p, tsize);
@@ -571,5 +582,55 @@ int vhx_oracle_nodestack_run(int size, const int32_t *ops, int n, int32_t *resul
             results[i] = data[head];
         }
     }
+    return VHX_OK;
+}
+
+/* Work statistics over a pixel rectangle (instrumentation for DESIGN.md): sums of per-ray counters
+ * [rays, hits, node iterations, advance steps, brick steps, pops, pushes, restarts, probes, bytes] and the max of
+ * node+advance+brick steps over rays in stats[10]. */
+int vhx_oracle_work_stats(const vhx_tree_desc *t, const vhx_camera *cam, uint32_t x0, uint32_t y0, uint32_t w,
+                          uint32_t h, double stats[11]) {
+    ensure_luts();
+    for (int k = 0; k < 11; ++k) stats[k] = 0;
+    for (uint32_t row = 0; row < h; ++row)
+        for (uint32_t col = 0; col < w; ++col) {
+            hit_t hh;
+            v3 o, d;
+            primary_ray(cam, x0 + col, y0 + row, &o, &d);
+            g_brick_steps = 0;
+            get_by_ray(t, o, d, &hh);
+            stats[0] += 1;
+            stats[1] += hh.hit;
+            stats[2] += hh.n_node;
+            stats[3] += hh.n_advance;
+            stats[4] += g_brick_steps;
+            stats[5] += hh.n_pop;
+            stats[6] += hh.n_push;
+            stats[7] += hh.n_restart;
+            stats[8] += hh.n_probe;
+            stats[9] += hh.bytes;
+            double tot = (double)hh.n_node + hh.n_advance + g_brick_steps;
+            if (tot > stats[10]) stats[10] = tot;
+        }
+    return VHX_OK;
+}
+
+/* Per-ray total steps (node iterations + advance steps + brick steps) over a pixel rectangle, row-major. */
+int vhx_oracle_ray_steps(const vhx_tree_desc *t, const vhx_camera *cam, uint32_t x0, uint32_t y0, uint32_t w,
+                         uint32_t h, uint32_t *steps, int threads) {
+    ensure_luts();
+#ifdef _OPENMP
+    if (threads <= 0) threads = omp_get_max_threads();
+#pragma omp parallel for schedule(dynamic, 64) num_threads(threads)
+#endif
+    for (int64_t i = 0; i < (int64_t)w * (int64_t)h; ++i) {
+        hit_t hh;
+        v3 o, d;
+        primary_ray(cam, x0 + (uint32_t)(i % w), y0 + (uint32_t)(i / w), &o, &d);
+        g_brick_steps = 0;
+        get_by_ray(t, o, d, &hh);
+        steps[i] = hh.n_node + hh.n_advance + g_brick_steps;
+    }
+    (void)threads;
     return VHX_OK;
 }

@@ -104,3 +104,30 @@ def test_nodestack_ring(oracle):  # src/raytracing/tests.rs:816-851: SIZE=3, pus
     assert r[3] == 30 and r[5] == 40
     r = oracle.nodestack(3, [5, 15, 25, pop, pop, pop, pop])  # 887-901
     assert r[3:] == [25, 15, 5, None]
+
+
+def test_closed_form_step_rule_matches_reference_lut():
+    """The GPU evaluates SECTANT_STEP_RESULT_LUT in closed form (voxelhex_amd/csrc/trace.hpp step_sectant_i)."""
+    g = np.array(json.load(open(GOLDEN))["sectant_step_result"]).reshape(64, 3, 3, 3)
+    for s in range(64):
+        sx, sy, sz = s & 3, (s >> 2) & 3, s >> 4
+        for dx in (-1, 0, 1):
+            for dy in (-1, 0, 1):
+                for dz in (-1, 0, 1):
+                    x, y, z = sx + dx, sy + dy, sz + dz
+                    out = not (0 <= x <= 3 and 0 <= y <= 3 and 0 <= z <= 3)
+                    assert g[s, dx + 1, dy + 1, dz + 1] == (64 if out else 0) + (x & 3) + (y & 3) * 4 + (z & 3) * 16
+
+
+def test_closed_form_occupancy_rule_matches_reference_lut():
+    """RAY_TO_NODE_OCCUPANCY_BITMASK_LUT as evaluated by trace.hpp occ_lut (per-axis 4-bit masks)."""
+    g = [int(v) for v in json.load(open(GOLDEN))["ray_to_node_occupancy_bitmask"]]
+    for s in range(64):
+        sx, sy, sz = s & 3, (s >> 2) & 3, s >> 4
+        for o in range(8):
+            mx = (0xF << sx) & 0xF if o & 1 else 0xF >> (3 - sx)
+            my = (0xF << sy) & 0xF if o & 4 else 0xF >> (3 - sy)
+            mz = (0xF << sz) & 0xF if o & 2 else 0xF >> (3 - sz)
+            row16 = sum((mx << (4 * y)) for y in range(4) if (my >> y) & 1)
+            m = sum((row16 << (16 * z)) for z in range(4) if (mz >> z) & 1)
+            assert m == g[s * 8 + o]

@@ -1,17 +1,24 @@
 // Device-side traversal of the flattened BoxTree for gfx950 — the per-ray state machine of the reference CPU
 // raytracer BoxTree::get_by_ray (src/raytracing/cpu.rs:296-458), restated for one ray per lane of a wave64.
 //
-// Bit-exactness with the reference needs its float semantics: every f32 op is issued in the reference order
-// (the library is compiled with -ffp-contract=off, IEEE-correct division and sqrt, f32 denormals kept),
+// Bit-exactness with the reference needs its float semantics: every f32 op that produces a value is issued in the
+// reference order (the library is compiled with -ffp-contract=off, IEEE division and sqrt, f32 denormals kept),
 // fminf/fmaxf ignore NaN like f32::min/max, signum(+-0) = +-1, and `as` casts saturate.
 //
-// Departures from a transliteration, none of which changes a result:
+// Strength reductions that leave every result bit-identical:
+//  * every cube size is a power of two (boxtree_size = brick_dim * 4^k, children are /4, cells /brick_dim, POP *4),
+//    so x / size == x * (1/size) exactly; 1/size is formed from the exponent bits (rcp_pow2) and fmod by a size is
+//    x - trunc(x / size) * size, exact by Sterbenz (fmod_pow2);
+//  * brick_dim is a template parameter, so / brick_dim is a multiply by an exact constant;
+//  * SECTANT_STEP_RESULT_LUT (src/spatial/lut.rs:27-92) and RAY_TO_NODE_OCCUPANCY_BITMASK_LUT (lut.rs:96-161) are
+//    evaluated in closed form (both forms are checked against the reference tables in tests/test_oracle_spatial.py);
+//  * a DDA step's float result is always (+-1 or 0) per axis, selected from signum(direction): the steps are carried
+//    as a 3-bit axis mask, and the integer index updates use the precomputed `as i32` of the signs;
 //  * node type + 64-bit occupancy are one 16-byte record per node (one global_load_dwordx4 per node visit);
-//  * emptiness of brick cells is read from a per-brick occupancy bitmap (brick_dim^3 bits, built at upload from
-//    pix_points_to_empty, src/boxtree/node.rs:311-333), so the DDA through a brick issues no voxel loads; the voxel
+//  * emptiness of brick cells comes from a per-brick occupancy bitmap (brick_dim^3 bits, built at upload from
+//    pix_points_to_empty, src/boxtree/node.rs:311-333): the DDA through a brick issues no voxel loads, the voxel
 //    value is loaded once, on the hit;
-//  * the 4-entry NodeStack ring (cpu.rs:18-76) lives in four scalar registers, selected without dynamic indexing;
-//  * LUTs come from constant memory, except the 64-bit occupancy LUT which is computed from its closed form.
+//  * the 4-entry NodeStack ring (cpu.rs:18-76) lives in four scalar registers, selected without dynamic indexing.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -72,22 +79,23 @@ __device__ __forceinline__ uint32_t ras_u8(float f) {
     return (uint32_t)f;
 }
 
-// SECTANT_STEP_RESULT_LUT, packed [sectant][x+1][y+1][z+1] (src/spatial/lut.rs:27-92); filled at library load.
-extern __constant__ uint8_t c_step_lut[64 * 27];
-
-// offset of sectant s = (s&3, (s>>2)&3, s>>4) / 4 (SECTANT_OFFSET_LUT, src/spatial/lut.rs:4-24)
-__device__ __forceinline__ F3d sect_off(uint32_t s) {
-    return mk((float)(s & 3u) * 0.25f, (float)((s >> 2) & 3u) * 0.25f, (float)(s >> 4) * 0.25f);
+// exact 1/s for s a normal power of two: exponent e -> -e
+__device__ __forceinline__ float rcp_pow2(float s) { return __uint_as_float(0x7F000000u - __float_as_uint(s)); }
+// fmodf(x, s) for s a power of two (exact: x*(1/s) and trunc(.)*s are exact scalings, the difference is exact by
+// Sterbenz); the sign of a zero result follows x like C fmod
+__device__ __forceinline__ float fmod_pow2(float x, float s) {
+    const float q = __builtin_truncf(x * rcp_pow2(s));
+    const float r = x - q * s;
+    return r == 0.0f ? __builtin_copysignf(0.0f, x) : r;
 }
+
 // RAY_TO_NODE_OCCUPANCY_BITMASK_LUT[s][o] (src/spatial/lut.rs:96-161): sectants t with t_k on the ray's side of
-// s_k on every axis; o = (dx>=0) + 2(dz>=0) + 4(dy>=0). Pinned against the reference table in the tests.
+// s_k on every axis; o = (dx>=0) + 2(dz>=0) + 4(dy>=0).
 __device__ __forceinline__ uint64_t occ_lut(uint32_t s, uint32_t o) {
     const uint32_t sx = s & 3u, sy = (s >> 2) & 3u, sz = s >> 4;
-    // per-axis 4-bit masks of admissible coordinates
     const uint32_t mx = (o & 1u) ? (0xFu << sx) & 0xFu : (0xFu >> (3u - sx));
     const uint32_t my = (o & 4u) ? (0xFu << sy) & 0xFu : (0xFu >> (3u - sy));
     const uint32_t mz = (o & 2u) ? (0xFu << sz) & 0xFu : (0xFu >> (3u - sz));
-    // expand: row mask over x (4 bits) replicated across admissible y rows, then across admissible z slabs
     uint32_t row16 = 0;
 #pragma unroll
     for (uint32_t y = 0; y < 4; ++y) row16 |= ((my >> y) & 1u) ? (mx << (4u * y)) : 0u;
@@ -97,14 +105,18 @@ __device__ __forceinline__ uint64_t occ_lut(uint32_t s, uint32_t o) {
     return m;
 }
 
-__device__ __forceinline__ uint32_t step_sectant(uint32_t s, F3d st) {
-    const int32_t ix = ras_i32(st.x), iy = ras_i32(st.y), iz = ras_i32(st.z);
-    const int32_t sx = (ix > 0) - (ix < 0), sy = (iy > 0) - (iy < 0), sz = (iz > 0) - (iz < 0);
-    return c_step_lut[s * 27u + (uint32_t)(sx + 1) * 9u + (uint32_t)(sy + 1) * 3u + (uint32_t)(sz + 1)];
+// step_sectant (src/spatial/mod.rs:23-26) for s < 64 and integer steps dk in {-1,0,1}: move each coordinate;
+// if any leaves [0,3] the result is 64 + the wrapped sectant (sectant_step_result_lut.rs:48-93)
+__device__ __forceinline__ uint32_t step_sectant_i(uint32_t s, int32_t dx, int32_t dy, int32_t dz) {
+    const int32_t x = (int32_t)(s & 3u) + dx, y = (int32_t)((s >> 2) & 3u) + dy, z = (int32_t)(s >> 4) + dz;
+    const uint32_t out = ((uint32_t)x > 3u) | ((uint32_t)y > 3u) | ((uint32_t)z > 3u);
+    return ((uint32_t)x & 3u) | (((uint32_t)y & 3u) << 2) | (((uint32_t)z & 3u) << 4) | (out << 6);
 }
-// offset_sectant, src/spatial/math/mod.rs:27-44
+
+// offset_sectant, src/spatial/math/mod.rs:27-44 ((off * 4) / size with size a power of two)
 __device__ __forceinline__ uint32_t offset_sectant(F3d off, float size) {
-    F3d idx = vdiv(vmul(off, 4.0f), size);
+    const float rs = rcp_pow2(size);
+    F3d idx = mk((off.x * 4.0f) * rs, (off.y * 4.0f) * rs, (off.z * 4.0f) * rs);
     idx = mk(__builtin_floorf(idx.x), __builtin_floorf(idx.y), __builtin_floorf(idx.z));
     idx = mk(__builtin_fminf(idx.x, 3.0f), __builtin_fminf(idx.y, 3.0f), __builtin_fminf(idx.z, 3.0f));
     return ras_u8(idx.x + (idx.y * 4.0f) + (idx.z * 16.0f));
@@ -114,15 +126,17 @@ struct CubeD {
     F3d min;
     float size;
 };
+// Cube::child_bounds_for, src/spatial/mod.rs:72-77; SECTANT_OFFSET_LUT[s] = (s&3, (s>>2)&3, s>>4) / 4
 __device__ __forceinline__ CubeD child_bounds(CubeD c, uint32_t s) {
     CubeD r;
-    r.min = vadd(c.min, vmul(sect_off(s), c.size));
-    r.size = c.size / 4.0f;
+    r.min = vadd(c.min, vmul(mk((float)(s & 3u) * 0.25f, (float)((s >> 2) & 3u) * 0.25f, (float)(s >> 4) * 0.25f),
+                             c.size));
+    r.size = c.size * 0.25f;
     return r;
 }
 // cube_impact_normal, src/spatial/raytracing/mod.rs:97-125
 __device__ __forceinline__ F3d impact_normal(CubeD c, F3d p) {
-    const float h = c.size / 2.0f;
+    const float h = c.size * 0.5f;
     F3d m = vsub(vadd(c.min, mk(h, h, h)), p);
     const float mc = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(m.x), __builtin_fabsf(m.y)), __builtin_fabsf(m.z));
     F3d n = mk(__builtin_fabsf(m.x) == mc ? -m.x : 0.0f, __builtin_fabsf(m.y) == mc ? -m.y : 0.0f,
@@ -132,10 +146,29 @@ __device__ __forceinline__ F3d impact_normal(CubeD c, F3d p) {
 
 struct RayD {
     F3d o, d, sf, sg, sgmax;
+    int32_t isx, isy, isz;  // `as i32` of signum(d) (= of round(signum(d))): the integer DDA steps
 };
 
-// dda_step_to_next_sibling, src/raytracing/cpu.rs:104-132
-__device__ __forceinline__ F3d dda_step(const RayD &r, F3d &p, CubeD b) {
+__device__ __forceinline__ void ray_setup(RayD &r, F3d o, F3d d) {
+    r.o = o;
+    r.d = d;
+    r.sg = mk(rsignum(d.x), rsignum(d.y), rsignum(d.z));
+    r.sgmax = mk(__builtin_fmaxf(r.sg.x, 0.0f), __builtin_fmaxf(r.sg.y, 0.0f), __builtin_fmaxf(r.sg.z, 0.0f));
+    r.isx = ras_i32(r.sg.x);
+    r.isy = ras_i32(r.sg.y);
+    r.isz = ras_i32(r.sg.z);
+}
+// get_dda_scale_factors, cpu.rs:79-92 (only needed once the ray enters the root cube)
+__device__ __forceinline__ void ray_scale_factors(RayD &r) {
+    const F3d d = r.d;
+    const float zx = d.z / d.x, yx = d.y / d.x, xy = d.x / d.y, zy = d.z / d.y, xz = d.x / d.z, yz = d.y / d.z;
+    r.sf = mk(__builtin_sqrtf((1.0f + zx * zx) + yx * yx), __builtin_sqrtf((xy * xy + 1.0f) + zy * zy),
+              __builtin_sqrtf((xz * xz + 1.0f) + yz * yz));
+}
+
+// dda_step_to_next_sibling, src/raytracing/cpu.rs:104-132. Returns the axis mask of the step (bit k set where
+// min_step == d_k); the float step of the reference is sg_k on those axes and 0.0 elsewhere.
+__device__ __forceinline__ uint32_t dda_step(const RayD &r, F3d &p, CubeD b) {
     const F3d diff = vsub(p, b.min);
     const F3d st = mk(b.size * r.sgmax.x - r.sg.x * diff.x, b.size * r.sgmax.y - r.sg.y * diff.y,
                       b.size * r.sgmax.z - r.sg.z * diff.z);
@@ -143,105 +176,107 @@ __device__ __forceinline__ F3d dda_step(const RayD &r, F3d &p, CubeD b) {
                 dz = __builtin_fabsf(st.z * r.sf.z);
     const float m = __builtin_fminf(__builtin_fminf(dx, dy), dz);
     p = vadd(p, vmul(r.d, m));
-    return mk(m == dx ? r.sg.x : 0.0f, m == dy ? r.sg.y : 0.0f, m == dz ? r.sg.z : 0.0f);
+    return (m == dx ? 1u : 0u) | (m == dy ? 2u : 0u) | (m == dz ? 4u : 0u);
+}
+__device__ __forceinline__ F3d step_vec(const RayD &r, uint32_t sel) {
+    return mk((sel & 1u) ? r.sg.x : 0.0f, (sel & 2u) ? r.sg.y : 0.0f, (sel & 4u) ? r.sg.z : 0.0f);
+}
+__device__ __forceinline__ uint32_t step_sectant(const RayD &r, uint32_t s, uint32_t sel) {
+    return step_sectant_i(s, (sel & 1u) ? r.isx : 0, (sel & 2u) ? r.isy : 0, (sel & 4u) ? r.isz : 0);
 }
 
+// brick geometry helpers
+template <int BD>
+struct Brick {
+    static constexpr int N3 = BD * BD * BD;
+    static constexpr uint32_t WORDS = N3 >= 64 ? (uint32_t)(N3 / 64) : 1u;
+    static constexpr float INV = 1.0f / (float)BD;  // exact: BD is a power of two
+};
+
 template <bool COUNT>
+__device__ __forceinline__ uint32_t pal_bytes(uint32_t v) {
+    return COUNT ? ((v & 0xFFFFu) != 0xFFFFu ? 4u : 0u) + ((v >> 16) != 0xFFFFu ? 4u : 0u) : 0u;
+}
+
+__device__ __forceinline__ void fill_hit(HitOut &h, uint32_t v, uint32_t cell, F3d p, CubeD hb) {
+    h.value = v;
+    h.cell = cell;
+    h.ix = p.x;
+    h.iy = p.y;
+    h.iz = p.z;
+    const F3d n = impact_normal(hb, p);
+    h.nx = n.x;
+    h.ny = n.y;
+    h.nz = n.z;
+    h.vx = ras_u32(hb.min.x);
+    h.vy = ras_u32(hb.min.y);
+    h.vz = ras_u32(hb.min.z);
+}
+
+// probe_brick (cpu.rs:236-292) incl. traverse_brick (cpu.rs:136-232)
+template <bool COUNT, int BD>
 __device__ __forceinline__ bool probe_brick(const DevTree &t, const RayD &r, F3d &p, uint32_t desc, CubeD bb,
                                             HitOut &h, uint32_t &iters) {
     if (desc == VHX_EMPTY) return false;
     if (desc & VHX_SOLID_BIT) {  // BrickData::Solid, cpu.rs:249-260
         if (COUNT) h.bytes += 4;
-        h.value = t.solid[desc & 0x7FFFFFFFu];
-        h.cell = VHX_EMPTY;
-        h.ix = p.x;
-        h.iy = p.y;
-        h.iz = p.z;
-        F3d n = impact_normal(bb, p);
-        h.nx = n.x;
-        h.ny = n.y;
-        h.nz = n.z;
-        h.vx = ras_u32(bb.min.x);
-        h.vy = ras_u32(bb.min.y);
-        h.vz = ras_u32(bb.min.z);
+        fill_hit(h, t.solid[desc & 0x7FFFFFFFu], VHX_EMPTY, p, bb);
         return true;
     }
-    // BrickData::Parted -> traverse_brick, cpu.rs:136-232
-    const int32_t bd = (int32_t)t.bd;
-    const float fbd = (float)t.bd;
-    const F3d pib = vdiv(vmul(vsub(p, bb.min), fbd), bb.size);
+    using B = Brick<BD>;
+    const float rs = rcp_pow2(bb.size);
+    const F3d pib = vmul(vmul(vsub(p, bb.min), (float)BD), rs);
     int32_t ix = ras_i32(pib.x), iy = ras_i32(pib.y), iz = ras_i32(pib.z);
-    ix = ix < 0 ? 0 : (ix > bd - 1 ? bd - 1 : ix);
-    iy = iy < 0 ? 0 : (iy > bd - 1 ? bd - 1 : iy);
-    iz = iz < 0 ? 0 : (iz > bd - 1 ? bd - 1 : iz);
-    int32_t flat = ix + iy * bd + iz * bd * bd;
-    const float unit = bb.size / fbd;
+    ix = ix < 0 ? 0 : (ix > BD - 1 ? BD - 1 : ix);
+    iy = iy < 0 ? 0 : (iy > BD - 1 ? BD - 1 : iy);
+    iz = iz < 0 ? 0 : (iz > BD - 1 ? BD - 1 : iz);
+    int32_t flat = ix + iy * BD + iz * BD * BD;
+    const float unit = bb.size * B::INV;
     CubeD cur;
     cur.min = vadd(bb.min, vmul(mk((float)ix, (float)iy, (float)iz), unit));
     cur.size = unit;
-    const uint64_t *occw = t.brick_occ + (uint64_t)desc * t.occ_words;
-    uint64_t word = occw[0];
-    int32_t word_idx = 0;
-    F3d step = mk(0.0f, 0.0f, 0.0f);
+    const uint64_t *occw = t.brick_occ + (uint64_t)desc * B::WORDS;
+    const uint32_t *vox = t.voxels + (uint64_t)desc * (uint64_t)B::N3;
+    int32_t word_idx = flat >> 6;
+    uint64_t word = occw[word_idx];
+    uint32_t sel = 0;
     for (;;) {
-        if (ix < 0 || ix >= bd || iy < 0 || iy >= bd || iz < 0 || iz >= bd) return false;
-        flat += ras_i32(step.x) * 1 + ras_i32(step.y) * bd + ras_i32(step.z) * (bd * bd);
-        const int32_t wi = flat >> 6;
-        if (wi != word_idx) {
-            word_idx = wi;
-            word = occw[wi];
+        if ((uint32_t)ix >= (uint32_t)BD || (uint32_t)iy >= (uint32_t)BD || (uint32_t)iz >= (uint32_t)BD) return false;
+        flat += ((sel & 1u) ? r.isx : 0) + ((sel & 2u) ? r.isy * BD : 0) + ((sel & 4u) ? r.isz * (BD * BD) : 0);
+        if (B::WORDS > 1) {
+            const int32_t wi = flat >> 6;
+            if (wi != word_idx) {
+                word_idx = wi;
+                word = occw[wi];
+            }
         }
         if (COUNT) h.bytes += 4;
         if ((word >> (flat & 63)) & 1ull) {
-            const uint32_t v = t.voxels[(uint64_t)desc * (uint64_t)(bd * bd * bd) + (uint32_t)flat];
-            if (COUNT) h.bytes += ((v & 0xFFFFu) != 0xFFFFu ? 4u : 0u) + ((v >> 16) != 0xFFFFu ? 4u : 0u);
+            const uint32_t v = vox[flat];
+            if (COUNT) h.bytes += pal_bytes<COUNT>(v);
             CubeD hb;
-            hb.size = bb.size / fbd;
-            hb.min = vadd(bb.min, vdiv(vmul(mk((float)ix, (float)iy, (float)iz), bb.size), fbd));
-            h.value = v;
-            h.cell = (uint32_t)flat;
-            h.ix = p.x;
-            h.iy = p.y;
-            h.iz = p.z;
-            F3d n = impact_normal(hb, p);
-            h.nx = n.x;
-            h.ny = n.y;
-            h.nz = n.z;
-            h.vx = ras_u32(hb.min.x);
-            h.vy = ras_u32(hb.min.y);
-            h.vz = ras_u32(hb.min.z);
+            hb.size = bb.size * B::INV;
+            hb.min = vadd(bb.min, vmul(vmul(mk((float)ix, (float)iy, (float)iz), bb.size), B::INV));
+            fill_hit(h, v, (uint32_t)flat, p, hb);
             return true;
         }
-        if (COUNT) {
-            // the reference reads the palettes for every cell whose indices are not none (node.rs:329-332),
-            // even when they turn out empty; the instrumented build reloads the raw value to account for it
-            const uint32_t v = t.voxels[(uint64_t)desc * (uint64_t)(bd * bd * bd) + (uint32_t)flat];
-            h.bytes += ((v & 0xFFFFu) != 0xFFFFu ? 4u : 0u) + ((v >> 16) != 0xFFFFu ? 4u : 0u);
-        }
+        if (COUNT) h.bytes += pal_bytes<COUNT>(vox[flat]);  // the reference reads the palettes of such cells too
         if (++iters > VHX_MAX_ITERS) return false;
-        step = dda_step(r, p, cur);
-        cur.min = vadd(cur.min, vmul(step, unit));
-        ix += ras_i32(__builtin_roundf(step.x));
-        iy += ras_i32(__builtin_roundf(step.y));
-        iz += ras_i32(__builtin_roundf(step.z));
+        sel = dda_step(r, p, cur);
+        cur.min = vadd(cur.min, vmul(step_vec(r, sel), unit));
+        ix += (sel & 1u) ? r.isx : 0;
+        iy += (sel & 2u) ? r.isy : 0;
+        iz += (sel & 4u) ? r.isz : 0;
     }
 }
 
 // BoxTree::get_by_ray, src/raytracing/cpu.rs:296-458
-template <bool COUNT>
+template <bool COUNT, int BD>
 __device__ __forceinline__ void get_by_ray(const DevTree &t, F3d o, F3d d, HitOut &h) {
     h.hit = false;
     h.bytes = 0;
     RayD r;
-    r.o = o;
-    r.d = d;
-    {
-        const float zx = d.z / d.x, yx = d.y / d.x, xy = d.x / d.y, zy = d.z / d.y, xz = d.x / d.z, yz = d.y / d.z;
-        r.sf = mk(__builtin_sqrtf((1.0f + zx * zx) + yx * yx), __builtin_sqrtf((xy * xy + 1.0f) + zy * zy),
-                  __builtin_sqrtf((xz * xz + 1.0f) + yz * yz));
-    }
-    r.sg = mk(rsignum(d.x), rsignum(d.y), rsignum(d.z));
-    r.sgmax = mk(__builtin_fmaxf(r.sg.x, 0.0f), __builtin_fmaxf(r.sg.y, 0.0f), __builtin_fmaxf(r.sg.z, 0.0f));
+    ray_setup(r, o, d);
     uint32_t dir_idx;
     {
         const F3d od = vadd(mk(1.0f, 1.0f, 1.0f), d);
@@ -255,25 +290,20 @@ __device__ __forceinline__ void get_by_ray(const DevTree &t, F3d o, F3d d, HitOu
     uint32_t target;
     CubeD tb;
     {
-        // Cube::intersect_ray, src/spatial/raytracing/mod.rs:33-62
-        const F3d mx = vadd(cur.min, mk(cur.size, cur.size, cur.size));
-        const float t1 = (cur.min.x - o.x) / d.x, t2 = (mx.x - o.x) / d.x;
-        const float t3 = (cur.min.y - o.y) / d.y, t4 = (mx.y - o.y) / d.y;
-        const float t5 = (cur.min.z - o.z) / d.z, t6 = (mx.z - o.z) / d.z;
+        // Cube::intersect_ray, src/spatial/raytracing/mod.rs:33-62 (root: min 0, max = 0 + size = size)
+        const float t1 = (0.0f - o.x) / d.x, t2 = (tsize - o.x) / d.x;
+        const float t3 = (0.0f - o.y) / d.y, t4 = (tsize - o.y) / d.y;
+        const float t5 = (0.0f - o.z) / d.z, t6 = (tsize - o.z) / d.z;
         const float tmin = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(t1, t2), __builtin_fminf(t3, t4)),
                                            __builtin_fminf(t5, t6));
         const float tmax = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(t1, t2), __builtin_fmaxf(t3, t4)),
                                            __builtin_fmaxf(t5, t6));
-        if (tmax < 0.0f || tmin > tmax) {
-            p = o;
-            target = 64;
-            tb = cur;
-        } else {
-            p = vadd(o, vmul(d, tmin < 0.0f ? 0.0f : tmin));
-            target = offset_sectant(p, cur.size);
-            tb = child_bounds(cur, target);
-        }
+        if (tmax < 0.0f || tmin > tmax) return;  // target = 64: the outer loop never runs
+        p = vadd(o, vmul(d, tmin < 0.0f ? 0.0f : tmin));
+        target = offset_sectant(p, cur.size);
+        tb = child_bounds(cur, target);
     }
+    ray_scale_factors(r);
     // NodeStack<u32, 4> ring in registers
     uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0, head = 0, count = 0;
     uint32_t node = 0;
@@ -300,15 +330,15 @@ __device__ __forceinline__ void get_by_ray(const DevTree &t, F3d o, F3d d, HitOu
             if (target < 64) {
                 if (ntype == VHX_NODE_UNIFORM_LEAF) {
                     if (COUNT) h.bytes += 4;
-                    if (probe_brick<COUNT>(t, r, p, t.children[(uint64_t)node * 64u], cur, h, iters)) {
+                    if (probe_brick<COUNT, BD>(t, r, p, t.children[(uint64_t)node * 64u], cur, h, iters)) {
                         h.hit = true;
                         return;
                     }
                     backtrack = true;
                 } else if (ntype == VHX_NODE_LEAF) {
                     if (COUNT) h.bytes += 4;
-                    if (probe_brick<COUNT>(t, r, p, t.children[(uint64_t)node * 64u + target], child_bounds(cur, target),
-                                           h, iters)) {
+                    if (probe_brick<COUNT, BD>(t, r, p, t.children[(uint64_t)node * 64u + target],
+                                               child_bounds(cur, target), h, iters)) {
                         h.hit = true;
                         return;
                     }
@@ -322,17 +352,17 @@ __device__ __forceinline__ void get_by_ray(const DevTree &t, F3d o, F3d d, HitOu
                 }
                 tb = cur;
                 cur.size *= 4.0f;
-                cur.min = vsub(cur.min, mk(__builtin_fmodf(cur.min.x, cur.size), __builtin_fmodf(cur.min.y, cur.size),
-                                           __builtin_fmodf(cur.min.z, cur.size)));
-                const float hs = tb.size / 2.0f;
+                cur.min = vsub(cur.min, mk(fmod_pow2(cur.min.x, cur.size), fmod_pow2(cur.min.y, cur.size),
+                                           fmod_pow2(cur.min.z, cur.size)));
+                const float hs = tb.size * 0.5f;
                 target = offset_sectant(vsub(vadd(tb.min, mk(hs, hs, hs)), cur.min), cur.size);
-                const F3d sv = dda_step(r, p, tb);
-                target = step_sectant(target, sv);
-                tb.min = vadd(tb.min, vmul(sv, tb.size));
+                const uint32_t sel = dda_step(r, p, tb);
+                target = step_sectant(r, target, sel);
+                tb.min = vadd(tb.min, vmul(step_vec(r, sel), tb.size));
                 if (count != 0) node = head == 0 ? s0 : (head == 1 ? s1 : (head == 2 ? s2 : s3));
                 continue;
             }
-            if (ntype == VHX_NODE_INTERNAL && (occ & (1ull << target)) != 0) {
+            if (ntype == VHX_NODE_INTERNAL && ((occ >> target) & 1ull) != 0) {
                 // PUSH (cpu.rs:401-411)
                 if (COUNT) h.bytes += 4;
                 const uint32_t child = t.children[(uint64_t)node * 64u + target];
@@ -351,10 +381,10 @@ __device__ __forceinline__ void get_by_ray(const DevTree &t, F3d o, F3d d, HitOu
                 // ADVANCE (cpu.rs:416-437)
                 for (;;) {
                     if (++iters > VHX_MAX_ITERS) return;
-                    const F3d sv = dda_step(r, p, tb);
-                    target = step_sectant(target, sv);
-                    if (target < 64) tb.min = vadd(tb.min, vmul(sv, tb.size));
-                    if (target >= 64 || (occ & (1ull << target)) != 0) break;
+                    const uint32_t sel = dda_step(r, p, tb);
+                    target = step_sectant(r, target, sel);
+                    if (target < 64) tb.min = vadd(tb.min, vmul(step_vec(r, sel), tb.size));
+                    if (target >= 64 || ((occ >> target) & 1ull) != 0) break;
                 }
             }
         }

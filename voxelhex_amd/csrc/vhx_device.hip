@@ -12,6 +12,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -43,6 +44,7 @@ struct vhx_ctx {
     DevBuf raw[7];         // VHX_BUF_* raw copies
     DevBuf hdr, brick_occ, scratch, rays;
     uint32_t occ_words = 1;
+    bool simple_kernel = true;  // VHX_PERSISTENT=1 selects the persistent wave-refill kernel (A/B)
 };
 
 #define VHX_HIP(ctx, call)                                                                                         \
@@ -205,9 +207,90 @@ __device__ __forceinline__ void primary_ray(const CamD &c, uint32_t px, uint32_t
     }
 }
 
+#include "persistent.hpp"
+
+// Where the rays of a launch come from: 8x8 micro-tiles either over the whole frame (FRAMEBUFFER layout, raster order of
+// micro-tiles) or over this rank's T x T screen tiles (TILES layout, T % 8 == 0).
+struct FrameMap {
+    uint32_t layout, T, tiles_x, tile_start, tile_stride;
+    uint32_t mtx;          // micro-tiles per row (frame mode) or per tile row (tile mode)
+    uint32_t micro_per_tile;
+    uint32_t n_micro;      // micro-tiles of this launch
+};
+
+__device__ __forceinline__ bool map_ray(const CamD &cam, const FrameMap &fm, uint32_t micro, uint32_t l, uint32_t &px,
+                                        uint32_t &py, uint64_t &idx) {
+    if (fm.layout == VHX_LAYOUT_FRAMEBUFFER) {
+        px = (micro % fm.mtx) * 8u + (l & 7u);
+        py = (micro / fm.mtx) * 8u + (l >> 3);
+        if (px >= cam.width || py >= cam.height) return false;
+        idx = (uint64_t)py * cam.width + px;
+        return true;
+    }
+    const uint32_t j = micro / fm.micro_per_tile, m = micro - j * fm.micro_per_tile;
+    const uint32_t tile = fm.tile_start + j * fm.tile_stride;
+    const uint32_t lx = (m % fm.mtx) * 8u + (l & 7u), ly = (m / fm.mtx) * 8u + (l >> 3);
+    px = (tile % fm.tiles_x) * fm.T + lx;
+    py = (tile / fm.tiles_x) * fm.T + ly;
+    if (px >= cam.width || py >= cam.height) return false;
+    idx = (uint64_t)j * fm.T * fm.T + (uint64_t)ly * fm.T + lx;
+    return true;
+}
+
+// Persistent wave-refill kernel: one task of TASK rays (TASK/64 consecutive micro-tiles) per wave, 4 waves per block.
+template <bool COUNT, int BD, uint32_t TASK>
+__global__ void __launch_bounds__(256) k_trace_persistent(DevTree t, CamD cam, OutD out, FrameMap fm) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = blockIdx.x * 4u + (threadIdx.x >> 6);
+    const uint32_t micro0 = wave * (TASK / 64u);
+    if (micro0 >= fm.n_micro) return;  // wave-uniform
+    const uint32_t nrays = min(TASK, (fm.n_micro - micro0) * 64u);
+    const uint64_t below = (1ull << lane) - 1ull;
+    uint32_t next = 0;  // wave-uniform: rays of the task handed out so far
+    bool active = false;
+    uint64_t my_idx = 0;
+    LaneState s;
+    for (;;) {
+        const uint64_t idle = __ballot(!active);
+        if (idle != 0ull) {
+            if (!active) {
+                const uint32_t r = next + (uint32_t)__popcll(idle & below);
+                if (r < nrays) {
+                    uint32_t px, py;
+                    if (map_ray(cam, fm, micro0 + (r >> 6), r & 63u, px, py, my_idx)) {
+                        F3d o, d;
+                        primary_ray(cam, px, py, o, d);
+                        if (ls_begin(t, s, o, d)) {
+                            active = true;
+                        } else {
+                            HitOut h;
+                            h.hit = false;
+                            h.bytes = 0;
+                            store(t, out, my_idx, o, h);
+                        }
+                    }
+                }
+            }
+            next += (uint32_t)__popcll(idle);
+            if (__ballot(active) == 0ull) {
+                if (next >= nrays) break;
+                continue;
+            }
+        }
+        if (active) {
+            HitOut h;
+            if (ls_step<COUNT, BD>(t, s, h)) {
+                h.bytes = s.bytes;
+                store(t, out, my_idx, s.r.o, h);
+                active = false;
+            }
+        }
+    }
+}
+
 // One workgroup = 256 lanes = a 16x16 pixel block made of four 8x8 wave tiles (wave64-coherent ray bundles, the
 // 8x8 footprint of the reference's @workgroup_size(8, 8, 1)). Blocks are dealt tile by tile.
-template <bool COUNT>
+template <bool COUNT, int BD>
 __global__ void __launch_bounds__(256) k_trace_primary(DevTree t, CamD cam, OutD out, uint32_t T, uint32_t tiles_x,
                                                        uint32_t tile_start, uint32_t tile_stride, uint32_t layout,
                                                        uint32_t blocks_per_tile_x, uint32_t blocks_per_tile) {
@@ -223,20 +306,20 @@ __global__ void __launch_bounds__(256) k_trace_primary(DevTree t, CamD cam, OutD
     F3d o, d;
     primary_ray(cam, px, py, o, d);
     HitOut h;
-    get_by_ray<COUNT>(t, o, d, h);
+    get_by_ray<COUNT, BD>(t, o, d, h);
     const uint64_t idx = layout == VHX_LAYOUT_FRAMEBUFFER ? (uint64_t)py * cam.width + px
                                                           : (uint64_t)j * T * T + (uint64_t)ly * T + lx;
     store(t, out, idx, o, h);
 }
 
-template <bool COUNT>
+template <bool COUNT, int BD>
 __global__ void __launch_bounds__(256) k_trace_rays(DevTree t, const float *__restrict__ rays, uint64_t n, OutD out) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const F3d o = mk(rays[6 * i], rays[6 * i + 1], rays[6 * i + 2]);
     const F3d d = mk(rays[6 * i + 3], rays[6 * i + 4], rays[6 * i + 5]);
     HitOut h;
-    get_by_ray<COUNT>(t, o, d, h);
+    get_by_ray<COUNT, BD>(t, o, d, h);
     store(t, out, i, o, h);
 }
 
@@ -259,6 +342,23 @@ __global__ void __launch_bounds__(256) k_untile_rgba(const uint32_t *__restrict_
 }
 
 // ------------------------------------------------------------------------------------------------ host helpers
+template <int V>
+struct BdTag {
+    static constexpr int value = V;
+};
+// brick_dim is a template parameter of the traversal kernels (exact / brick_dim as a constant multiply)
+template <class F>
+static bool dispatch_bd(uint32_t bd, F &&f) {
+    switch (bd) {
+        case 1: f(BdTag<1>{}); return true;
+        case 2: f(BdTag<2>{}); return true;
+        case 4: f(BdTag<4>{}); return true;
+        case 8: f(BdTag<8>{}); return true;
+        case 16: f(BdTag<16>{}); return true;
+        case 32: f(BdTag<32>{}); return true;
+        default: return false;
+    }
+}
 static DevTree dev_tree(const vhx_ctx *c) {
     DevTree t;
     t.hdr = (const uint4 *)c->hdr.ptr;
@@ -414,6 +514,10 @@ int vhx_create(int hip_device, vhx_ctx **out) {
     if ((e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking)) != hipSuccess)
         return bail("hipStreamCreate", e);
     c->stream = c->own_stream;
+    {
+        const char *pk = getenv("VHX_PERSISTENT");
+        c->simple_kernel = !(pk && pk[0] == '1');
+    }
     if ((e = hipEventCreate(&c->ev0)) != hipSuccess) return bail("hipEventCreate", e);
     if ((e = hipEventCreate(&c->ev1)) != hipSuccess) return bail("hipEventCreate", e);
     uint8_t lut[64 * 27];
@@ -460,7 +564,8 @@ int vhx_sync(vhx_ctx *c, float *ms) {
 int vhx_upload_tree(vhx_ctx *c, const vhx_tree_desc *t) {
     if (!c || !t) return VHX_E_INVALID_ARG;
     const uint32_t bd = t->brick_dim;
-    if (t->node_count == 0 || bd == 0 || t->boxtree_size == 0 || (bd & (bd - 1)) != 0 || bd > 32)
+    if (t->node_count == 0 || bd == 0 || t->boxtree_size == 0 || (bd & (bd - 1)) != 0 || bd > 32 ||
+        (t->boxtree_size & (t->boxtree_size - 1)) != 0 || t->boxtree_size > (1u << 24))
         return fail(c, VHX_E_INVALID_ARG, "vhx_upload_tree: invalid sizes");
     const void *src[7] = {t->node_type, t->node_ocbits, t->node_children, t->voxels,
                           t->solid_values, t->color_palette, t->data_palette};
@@ -581,13 +686,47 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
     if (rc) return rc;
     const DevTree t = dev_tree(c);
     const CamD cd = cam_of(cam);
+    FrameMap fm{};
+    fm.layout = layout;
+    fm.T = T;
+    fm.tiles_x = tiles_x;
+    fm.tile_start = tile_start;
+    fm.tile_stride = tile_stride;
+    if (layout == VHX_LAYOUT_FRAMEBUFFER) {
+        fm.mtx = (cam->width + 7) / 8;
+        fm.micro_per_tile = 0;
+        fm.n_micro = fm.mtx * ((cam->height + 7) / 8);
+    } else {
+        if (T % 8 != 0) return fail(c, VHX_E_INVALID_ARG, "tile_size must be a multiple of 8");
+        fm.mtx = T / 8;
+        fm.micro_per_tile = fm.mtx * fm.mtx;
+        fm.n_micro = my_tiles * fm.micro_per_tile;
+    }
+    constexpr uint32_t TASK = 512;
+    const uint32_t nwaves = (fm.n_micro + TASK / 64 - 1) / (TASK / 64);
+    const uint32_t pblocks = (nwaves + 3) / 4;
+    (void)nblocks;
     VHX_HIP(c, hipEventRecord(c->ev0, c->stream));
-    if (ho.dev.bytes)
-        k_trace_primary<true><<<(unsigned)nblocks, 256, 0, c->stream>>>(t, cd, ho.dev, T, tiles_x, tile_start,
-                                                                        tile_stride, layout, bpx, bpt);
-    else
-        k_trace_primary<false><<<(unsigned)nblocks, 256, 0, c->stream>>>(t, cd, ho.dev, T, tiles_x, tile_start,
-                                                                         tile_stride, layout, bpx, bpt);
+    const bool count = ho.dev.bytes != nullptr;
+    const bool simple = c->simple_kernel;
+    auto launch = [&](auto bd_tag) {
+        constexpr int BD = decltype(bd_tag)::value;
+        if (simple) {
+            if (count)
+                k_trace_primary<true, BD><<<(unsigned)nblocks, 256, 0, c->stream>>>(t, cd, ho.dev, T, tiles_x,
+                                                                                    tile_start, tile_stride, layout,
+                                                                                    bpx, bpt);
+            else
+                k_trace_primary<false, BD><<<(unsigned)nblocks, 256, 0, c->stream>>>(t, cd, ho.dev, T, tiles_x,
+                                                                                     tile_start, tile_stride, layout,
+                                                                                     bpx, bpt);
+        } else if (count) {
+            k_trace_persistent<true, BD, TASK><<<pblocks, 256, 0, c->stream>>>(t, cd, ho.dev, fm);
+        } else {
+            k_trace_persistent<false, BD, TASK><<<pblocks, 256, 0, c->stream>>>(t, cd, ho.dev, fm);
+        }
+    };
+    if (!dispatch_bd(c->desc.brick_dim, launch)) return fail(c, VHX_E_INVALID_ARG, "unsupported brick_dim");
     VHX_HIP(c, hipGetLastError());
     VHX_HIP(c, hipEventRecord(c->ev1, c->stream));
     c->timed = true;
@@ -614,10 +753,15 @@ int vhx_trace_rays(vhx_ctx *c, const float *rays, uint64_t n, const vhx_hits *ou
     }
     const DevTree t = dev_tree(c);
     VHX_HIP(c, hipEventRecord(c->ev0, c->stream));
-    if (ho.dev.bytes)
-        k_trace_rays<true><<<(unsigned)((n + 255) / 256), 256, 0, c->stream>>>(t, drays, n, ho.dev);
-    else
-        k_trace_rays<false><<<(unsigned)((n + 255) / 256), 256, 0, c->stream>>>(t, drays, n, ho.dev);
+    const bool count = ho.dev.bytes != nullptr;
+    auto launch = [&](auto bd_tag) {
+        constexpr int BD = decltype(bd_tag)::value;
+        if (count)
+            k_trace_rays<true, BD><<<(unsigned)((n + 255) / 256), 256, 0, c->stream>>>(t, drays, n, ho.dev);
+        else
+            k_trace_rays<false, BD><<<(unsigned)((n + 255) / 256), 256, 0, c->stream>>>(t, drays, n, ho.dev);
+    };
+    if (!dispatch_bd(c->desc.brick_dim, launch)) return fail(c, VHX_E_INVALID_ARG, "unsupported brick_dim");
     VHX_HIP(c, hipGetLastError());
     VHX_HIP(c, hipEventRecord(c->ev1, c->stream));
     c->timed = true;
