@@ -52,6 +52,7 @@ def main():
 
     import voxelhex_amd as vhx
     from voxelhex_amd import _native as N
+    from voxelhex_amd import multigpu as M
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -85,8 +86,7 @@ def main():
         trace_kw = dict(tile_size=0, tile_start=0, tile_stride=1, layout=N.VHX_LAYOUT_FRAMEBUFFER)
         tiles_per_rank = 0
     else:
-        ntiles = ((W + T - 1) // T) * ((H + T - 1) // T)
-        tiles_per_rank = (ntiles + world - 1) // world
+        tiles_per_rank = M.tiles_per_rank(W, H, T, world)
         n_out = tiles_per_rank * T * T
         trace_kw = dict(tile_size=T, tile_start=rank, tile_stride=world, layout=N.VHX_LAYOUT_TILES)
     rgba = torch.zeros(n_out, dtype=torch.int32, device=dev)
@@ -141,12 +141,7 @@ def main():
     if not args.no_roofline:
         res = rt.trace_primary(cam, fields=(), count_bytes=True, **trace_kw)
         tree_bytes = float(res["bytes"].astype(np.float64).sum())
-        if world == 1:
-            my_rays = W * H
-        else:
-            tx = (W + T - 1) // T
-            my_rays = sum(min(T, W - (k % tx) * T) * min(T, H - (k // tx) * T)
-                          for k in range(rank, ((W + T - 1) // T) * ((H + T - 1) // T), world))
+        my_rays = W * H if world == 1 else M.rank_rays(W, H, T, rank, world)
         out_bytes = 8.0 * my_rays  # rgba8 + f32 depth per ray
         launch_bytes = tree_bytes + out_bytes
         achieved = launch_bytes / (kernel_ms * 1e-3) / 1e9
