@@ -211,3 +211,44 @@ def test_full_size_frame_crops(gpu, oracle):
         idx = (np.arange(y0, y0 + 64)[:, None] * W + np.arange(x0, x0 + 64)[None, :]).reshape(-1)
         assert_same({k: v[idx] for k, v in a.items()}, ref, f"crop {x0},{y0}")
     assert (a["value"] != N.VHX_EMPTY).mean() > 0.2
+
+
+DEFAULT_BUDGETS = (64,)
+
+
+@pytest.mark.parametrize("budgets", [(), (1,), (1, 2, 3), (4, 40), (8, 64, 512), DEFAULT_BUDGETS])
+def test_multipass_schedule_is_bit_identical(gpu, oracle, budgets):
+    """The multi-pass scheduler (vhx_set_pass_budgets) abandons and re-traces rays; every schedule, down to a
+    1-step first budget that requeues nearly every ray, must give the oracle's results (incl. byte counts)."""
+    flat = vhx.FlatTree.build_scene(N.VHX_SCENE_LATTICE_CUBE, 256, 4)
+    gpu.upload(flat)
+    rng = np.random.default_rng(len(budgets) * 7 + sum(budgets))
+    o, d = rand_rays(rng, 256, 20000)
+    cam = vhx.glass_camera(256, 200, 136, target=(128.0, 128.0, 128.0))
+    ref_rays = oracle.trace_rays(flat, o, d, count_bytes=True)
+    ref_frame = oracle.trace_primary(flat, cam, 0, 0, 200, 136, count_bytes=True)
+    try:
+        gpu.set_pass_budgets(budgets)
+        assert_same(gpu.trace_rays(o, d, count_bytes=True), ref_rays, f"rays {budgets}")
+        assert_same(gpu.trace_primary(cam, count_bytes=True), ref_frame, f"frame {budgets}")
+        # tile layout: queue indices map back through the tile numbering
+        T, R = 64, 2
+        full = ref_frame["rgba"].reshape(136, 200)
+        for r in range(R):
+            part = gpu.trace_primary(cam, tile_size=T, tile_start=r, tile_stride=R, layout=N.VHX_LAYOUT_TILES,
+                                     fields=("rgba",))["rgba"].reshape(-1, T, T)
+            tiles_x = (200 + T - 1) // T
+            for j in range(part.shape[0]):
+                tile = r + j * R
+                tx, ty = (tile % tiles_x) * T, (tile // tiles_x) * T
+                want = full[ty:ty + T, tx:tx + T]
+                assert np.array_equal(part[j, :want.shape[0], :want.shape[1]], want), (budgets, tile)
+    finally:
+        gpu.set_pass_budgets(DEFAULT_BUDGETS)
+
+
+def test_pass_budget_validation(gpu):
+    for bad in ((0,), (5, 5), (9, 3), (1, 2, 3, 4), (1 << 22,)):
+        with pytest.raises(N.VhxError):
+            gpu.set_pass_budgets(bad)
+    gpu.set_pass_budgets(DEFAULT_BUDGETS)

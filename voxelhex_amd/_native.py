@@ -74,6 +74,7 @@ SIGNATURES = [
     ("vhx_last_error", ctypes.c_char_p, [c_void_p]),
     ("vhx_set_stream", c_int, [c_void_p, c_void_p]),
     ("vhx_sync", c_int, [c_void_p, P(c_f32)]),
+    ("vhx_set_pass_budgets", c_int, [c_void_p, P(c_u32), c_u32]),
     ("vhx_upload_tree", c_int, [c_void_p, P(TreeDesc)]),
     ("vhx_update_range", c_int, [c_void_p, c_int, c_u64, c_u64, c_void_p]),
     ("vhx_read_derived", c_int, [c_void_p, c_int, c_u64, c_u64, c_void_p]),

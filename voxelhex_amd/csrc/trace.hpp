@@ -62,21 +62,22 @@ __device__ __forceinline__ float vlen(F3d a) { return __builtin_sqrtf((a.x * a.x
 __device__ __forceinline__ F3d vnorm(F3d a) { return vdiv(a, vlen(a)); }
 
 __device__ __forceinline__ float rsignum(float a) { return __builtin_isnan(a) ? a : __builtin_copysignf(1.0f, a); }
+// Rust `as` casts (saturating, NaN -> 0). CDNA's v_cvt_i32_f32 / v_cvt_u32_f32 implement exactly this (out-of-range
+// inputs incl. infinities saturate, NaN converts to 0), so each cast is one instruction; written as inline asm because
+// the C++ conversion is undefined out of range and the compiler would otherwise guard it with branches.
 __device__ __forceinline__ int32_t ras_i32(float f) {
-    if (__builtin_isnan(f)) return 0;
-    if (f >= 2147483648.0f) return INT32_MAX;
-    if (f <= -2147483648.0f) return INT32_MIN;
-    return (int32_t)f;
+    int32_t r;
+    asm("v_cvt_i32_f32 %0, %1" : "=v"(r) : "v"(f));
+    return r;
 }
 __device__ __forceinline__ uint32_t ras_u32(float f) {
-    if (__builtin_isnan(f) || f <= 0.0f) return 0;
-    if (f >= 4294967296.0f) return 0xFFFFFFFFu;
-    return (uint32_t)f;
+    uint32_t r;
+    asm("v_cvt_u32_f32 %0, %1" : "=v"(r) : "v"(f));
+    return r;
 }
 __device__ __forceinline__ uint32_t ras_u8(float f) {
-    if (__builtin_isnan(f) || f <= 0.0f) return 0;
-    if (f >= 255.0f) return 255;
-    return (uint32_t)f;
+    const uint32_t r = ras_u32(f);
+    return r < 255u ? r : 255u;
 }
 
 // exact 1/s for s a normal power of two: exponent e -> -e
@@ -213,10 +214,16 @@ __device__ __forceinline__ void fill_hit(HitOut &h, uint32_t v, uint32_t cell, F
     h.vz = ras_u32(hb.min.z);
 }
 
-// probe_brick (cpu.rs:236-292) incl. traverse_brick (cpu.rs:136-232)
+// probe_brick (cpu.rs:236-292) incl. traverse_brick (cpu.rs:136-232).
+// The cell walk is a single-exit loop: an iteration that stops (hit, or step budget spent) computes its DDA step but
+// does not commit it, which costs four selects instead of the exec-mask bookkeeping of extra loop exits. Per-brick
+// constants: unit * max(signum, 0) (the dda_step term size * signum.max(0)) and signum * unit (the bounds step).
+// st_k = usg_k - sg_k * diff_k is formed with one fma: sg_k is +-1, the product is exact, so fma rounds once exactly
+// where the reference's separate multiply and subtract do.
+// Returns true on a hit; a walk that ran out of budget returns false with iters > budget for the caller to see.
 template <bool COUNT, int BD>
 __device__ __forceinline__ bool probe_brick(const DevTree &t, const RayD &r, F3d &p, uint32_t desc, CubeD bb,
-                                            HitOut &h, uint32_t &iters) {
+                                            HitOut &h, uint32_t &iters, uint32_t budget) {
     if (desc == VHX_EMPTY) return false;
     if (desc & VHX_SOLID_BIT) {  // BrickData::Solid, cpu.rs:249-260
         if (COUNT) h.bytes += 4;
@@ -230,19 +237,18 @@ __device__ __forceinline__ bool probe_brick(const DevTree &t, const RayD &r, F3d
     ix = ix < 0 ? 0 : (ix > BD - 1 ? BD - 1 : ix);
     iy = iy < 0 ? 0 : (iy > BD - 1 ? BD - 1 : iy);
     iz = iz < 0 ? 0 : (iz > BD - 1 ? BD - 1 : iz);
-    int32_t flat = ix + iy * BD + iz * BD * BD;
     const float unit = bb.size * B::INV;
-    CubeD cur;
-    cur.min = vadd(bb.min, vmul(mk((float)ix, (float)iy, (float)iz), unit));
-    cur.size = unit;
+    F3d cmin = vadd(bb.min, vmul(mk((float)ix, (float)iy, (float)iz), unit));
+    const F3d usg = mk(unit * r.sgmax.x, unit * r.sgmax.y, unit * r.sgmax.z);
+    const F3d sgu = mk(r.sg.x * unit, r.sg.y * unit, r.sg.z * unit);
     const uint64_t *occw = t.brick_occ + (uint64_t)desc * B::WORDS;
     const uint32_t *vox = t.voxels + (uint64_t)desc * (uint64_t)B::N3;
+    int32_t flat = ix + iy * BD + iz * (BD * BD);
     int32_t word_idx = flat >> 6;
     uint64_t word = occw[word_idx];
-    uint32_t sel = 0;
+    bool hit;
     for (;;) {
-        if ((uint32_t)ix >= (uint32_t)BD || (uint32_t)iy >= (uint32_t)BD || (uint32_t)iz >= (uint32_t)BD) return false;
-        flat += ((sel & 1u) ? r.isx : 0) + ((sel & 2u) ? r.isy * BD : 0) + ((sel & 4u) ? r.isz * (BD * BD) : 0);
+        flat = ix + iy * BD + iz * (BD * BD);
         if (B::WORDS > 1) {
             const int32_t wi = flat >> 6;
             if (wi != word_idx) {
@@ -250,29 +256,56 @@ __device__ __forceinline__ bool probe_brick(const DevTree &t, const RayD &r, F3d
                 word = occw[wi];
             }
         }
-        if (COUNT) h.bytes += 4;
-        if ((word >> (flat & 63)) & 1ull) {
-            const uint32_t v = vox[flat];
-            if (COUNT) h.bytes += pal_bytes<COUNT>(v);
-            CubeD hb;
-            hb.size = bb.size * B::INV;
-            hb.min = vadd(bb.min, vmul(vmul(mk((float)ix, (float)iy, (float)iz), bb.size), B::INV));
-            fill_hit(h, v, (uint32_t)flat, p, hb);
-            return true;
-        }
-        if (COUNT) h.bytes += pal_bytes<COUNT>(vox[flat]);  // the reference reads the palettes of such cells too
-        if (++iters > VHX_MAX_ITERS) return false;
-        sel = dda_step(r, p, cur);
-        cur.min = vadd(cur.min, vmul(step_vec(r, sel), unit));
-        ix += (sel & 1u) ? r.isx : 0;
-        iy += (sel & 2u) ? r.isy : 0;
-        iz += (sel & 4u) ? r.isz : 0;
+        hit = ((word >> (flat & 63)) & 1ull) != 0ull;
+        if (COUNT) h.bytes += 4 + pal_bytes<COUNT>(vox[flat]);  // the reference reads the palettes of every cell
+        ++iters;
+        const bool stop = hit || iters > budget;
+        // dda_step_to_next_sibling (cpu.rs:104-132) on the cell bounds {cmin, unit}
+        const F3d diff = vsub(p, cmin);
+        const float stx = __builtin_fmaf(-r.sg.x, diff.x, usg.x), sty = __builtin_fmaf(-r.sg.y, diff.y, usg.y),
+                    stz = __builtin_fmaf(-r.sg.z, diff.z, usg.z);
+        const float dx = __builtin_fabsf(stx * r.sf.x), dy = __builtin_fabsf(sty * r.sf.y),
+                    dz = __builtin_fabsf(stz * r.sf.z);
+        const float m = __builtin_fminf(__builtin_fminf(dx, dy), dz);
+        const float pnx = p.x + r.d.x * m, pny = p.y + r.d.y * m, pnz = p.z + r.d.z * m;
+        const bool mx = !stop && m == dx, my = !stop && m == dy, mz = !stop && m == dz;
+        p.x = stop ? p.x : pnx;  // component-wise: a struct select becomes a pointer select through scratch
+        p.y = stop ? p.y : pny;
+        p.z = stop ? p.z : pnz;
+        cmin = mk(mx ? cmin.x + sgu.x : cmin.x, my ? cmin.y + sgu.y : cmin.y, mz ? cmin.z + sgu.z : cmin.z);
+        ix += mx ? r.isx : 0;
+        iy += my ? r.isy : 0;
+        iz += mz ? r.isz : 0;
+        if (stop || (uint32_t)(ix | iy | iz) >= (uint32_t)BD) break;
     }
+    if (!hit) return false;
+    const uint32_t v = vox[flat];
+    CubeD hb;
+    hb.size = bb.size * B::INV;
+    hb.min = vadd(bb.min, vmul(vmul(mk((float)ix, (float)iy, (float)iz), bb.size), B::INV));
+    fill_hit(h, v, (uint32_t)flat, p, hb);
+    return true;
 }
 
-// BoxTree::get_by_ray, src/raytracing/cpu.rs:296-458
+// RAY_TO_NODE_OCCUPANCY_BITMASK_LUT in LDS: occ_tab[s * 8 + o] = occ_lut(s, o); filled by the block before tracing.
+__device__ __forceinline__ void fill_occ_tab(uint64_t *occ_tab) {
+    for (uint32_t i = threadIdx.x; i < 512u; i += blockDim.x) occ_tab[i] = occ_lut(i >> 3, i & 7u);
+}
+
+// BoxTree::get_by_ray, src/raytracing/cpu.rs:296-458.
+// `budget` bounds the loop iterations (node, advance and brick steps). With budget == VHX_MAX_ITERS this is the full
+// traversal (a ray exceeding the bound is a miss, as in the oracle) and the return value is always true. A smaller
+// budget makes a pass of the multi-pass scheduler: false = the ray was abandoned after `budget` steps and has to be
+// traced again from scratch with a larger budget (the traversal is deterministic, so the re-trace is bit-identical
+// to an uninterrupted one).
+//
+// Control flow: the reference's two nested loops (restart from the root / walk the NodeStack) are one loop here, and
+// every way out of it sets `done` and leaves through a single exit at the bottom of the iteration. The NodeStack<u32,
+// 4> ring (cpu.rs:18-76) is a shift register: `node` is its top, s1..s3 the entries below; a push onto a full stack
+// drops the oldest entry, a pop that empties it ends the walk and restarts from the root.
 template <bool COUNT, int BD>
-__device__ __forceinline__ void get_by_ray(const DevTree &t, F3d o, F3d d, HitOut &h) {
+__device__ __forceinline__ bool get_by_ray(const DevTree &t, const uint64_t *occ_tab, F3d o, F3d d, HitOut &h,
+                                           uint32_t budget) {
     h.hit = false;
     h.bytes = 0;
     RayD r;
@@ -298,58 +331,38 @@ __device__ __forceinline__ void get_by_ray(const DevTree &t, F3d o, F3d d, HitOu
                                            __builtin_fminf(t5, t6));
         const float tmax = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(t1, t2), __builtin_fmaxf(t3, t4)),
                                            __builtin_fmaxf(t5, t6));
-        if (tmax < 0.0f || tmin > tmax) return;  // target = 64: the outer loop never runs
+        if (tmax < 0.0f || tmin > tmax) return true;  // target = 64: the outer loop never runs
         p = vadd(o, vmul(d, tmin < 0.0f ? 0.0f : tmin));
         target = offset_sectant(p, cur.size);
         tb = child_bounds(cur, target);
     }
     ray_scale_factors(r);
-    // NodeStack<u32, 4> ring in registers
-    uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0, head = 0, count = 0;
-    uint32_t node = 0;
-    uint32_t iters = 0;
-    while (target < 64) {
-        node = 0;
-        cur.min = mk(0.0f, 0.0f, 0.0f);
-        cur.size = tsize;
-        // push(ROOT)
-        head = (head + 1) & 3u;
-        count = count + 1 < 4 ? count + 1 : 4;
-        s0 = head == 0 ? 0u : s0;
-        s1 = head == 1 ? 0u : s1;
-        s2 = head == 2 ? 0u : s2;
-        s3 = head == 3 ? 0u : s3;
-        while (count != 0) {
-            if (++iters > VHX_MAX_ITERS) return;
-            const uint32_t last = head == 0 ? s0 : (head == 1 ? s1 : (head == 2 ? s2 : s3));
-            const uint4 lh = t.hdr[last];
-            const uint64_t occ = ((uint64_t)lh.y << 32) | (uint64_t)lh.x;
-            const uint32_t ntype = last == node ? lh.z : t.hdr[node].z;
-            if (COUNT) h.bytes += 12;
-            bool backtrack = ntype == VHX_NODE_UNIFORM_LEAF;
-            if (target < 64) {
-                if (ntype == VHX_NODE_UNIFORM_LEAF) {
-                    if (COUNT) h.bytes += 4;
-                    if (probe_brick<COUNT, BD>(t, r, p, t.children[(uint64_t)node * 64u], cur, h, iters)) {
-                        h.hit = true;
-                        return;
-                    }
-                    backtrack = true;
-                } else if (ntype == VHX_NODE_LEAF) {
-                    if (COUNT) h.bytes += 4;
-                    if (probe_brick<COUNT, BD>(t, r, p, t.children[(uint64_t)node * 64u + target],
-                                               child_bounds(cur, target), h, iters)) {
-                        h.hit = true;
-                        return;
-                    }
-                }
-            }
-            if (backtrack || target >= 64 || occ == 0 || (occ & occ_lut(target, dir_idx)) == 0) {
+    uint32_t node = 0, s1 = 0, s2 = 0, s3 = 0, count = 1;  // push(ROOT)
+    uint32_t iters = 1;  // the first node iteration
+    bool ok = true;
+    for (;;) {
+        const uint4 lh = t.hdr[node];
+        // the child slot is read by both the leaf probe and the push: issue it with the header load so the
+        // iteration waits for one memory latency instead of two
+        const uint32_t slot = t.children[(uint64_t)node * 64u + (target & 63u)];
+        const uint64_t occ = ((uint64_t)lh.y << 32) | (uint64_t)lh.x;
+        const uint32_t ntype = lh.z;
+        if (COUNT) h.bytes += 12;
+        const bool uniform = ntype == VHX_NODE_UNIFORM_LEAF;
+        bool done = false;
+        if (target < 64u && (uniform || ntype == VHX_NODE_LEAF)) {
+            if (COUNT) h.bytes += 4;
+            const uint32_t desc = uniform ? t.children[(uint64_t)node * 64u] : slot;
+            done = probe_brick<COUNT, BD>(t, r, p, desc, uniform ? cur : child_bounds(cur, target), h, iters, budget);
+            h.hit = done;
+        }
+        if (!done) {
+            if (uniform || target >= 64u || occ == 0 || (occ & occ_tab[(target & 63u) * 8u + dir_idx]) == 0) {
                 // POP (cpu.rs:368-393)
-                if (count != 0) {
-                    count -= 1;
-                    head = (head - 1) & 3u;
-                }
+                count -= 1;
+                node = s1;
+                s1 = s2;
+                s2 = s3;
                 tb = cur;
                 cur.size *= 4.0f;
                 cur.min = vsub(cur.min, mk(fmod_pow2(cur.min.x, cur.size), fmod_pow2(cur.min.y, cur.size),
@@ -359,42 +372,54 @@ __device__ __forceinline__ void get_by_ray(const DevTree &t, F3d o, F3d d, HitOu
                 const uint32_t sel = dda_step(r, p, tb);
                 target = step_sectant(r, target, sel);
                 tb.min = vadd(tb.min, vmul(step_vec(r, sel), tb.size));
-                if (count != 0) node = head == 0 ? s0 : (head == 1 ? s1 : (head == 2 ? s2 : s3));
-                continue;
-            }
-            if (ntype == VHX_NODE_INTERNAL && ((occ >> target) & 1ull) != 0) {
+                if (count == 0) {
+                    // the stack ran empty: restart from the root (cpu.rs:441-455); target_bounds stays stale
+                    p = vadd(p, vmul(d, 0.1f));
+                    if (p.x < tsize && p.y < tsize && p.z < tsize && p.x > 0.0f && p.y > 0.0f && p.z > 0.0f) {
+                        target = offset_sectant(p, tsize);
+                        node = 0;
+                        count = 1;
+                        cur.min = mk(0.0f, 0.0f, 0.0f);
+                        cur.size = tsize;
+                    } else {
+                        // a brick walk that ran out of budget can end in a pop + restart that leaves the root cube
+                        done = true;
+                        ok = iters <= budget || budget >= VHX_MAX_ITERS;
+                    }
+                }
+            } else if (ntype == VHX_NODE_INTERNAL && ((occ >> target) & 1ull) != 0) {
                 // PUSH (cpu.rs:401-411)
                 if (COUNT) h.bytes += 4;
-                const uint32_t child = t.children[(uint64_t)node * 64u + target];
-                if (child >= t.node_count) return;  // the reference would panic on an invalid key
-                node = child;
-                cur = tb;
-                target = offset_sectant(vsub(p, tb.min), tb.size);
-                tb = child_bounds(cur, target);
-                head = (head + 1) & 3u;
-                count = count + 1 < 4 ? count + 1 : 4;
-                s0 = head == 0 ? child : s0;
-                s1 = head == 1 ? child : s1;
-                s2 = head == 2 ? child : s2;
-                s3 = head == 3 ? child : s3;
+                if (slot >= t.node_count) {
+                    done = true;  // the reference would panic on an invalid key
+                } else {
+                    s3 = s2;
+                    s2 = s1;
+                    s1 = node;
+                    node = slot;
+                    count = count + 1 < 4 ? count + 1 : 4;
+                    cur = tb;
+                    target = offset_sectant(vsub(p, tb.min), tb.size);
+                    tb = child_bounds(cur, target);
+                }
             } else {
-                // ADVANCE (cpu.rs:416-437)
+                // ADVANCE (cpu.rs:416-437); a step past the budget is harmless: the next check abandons the ray
                 for (;;) {
-                    if (++iters > VHX_MAX_ITERS) return;
+                    ++iters;
                     const uint32_t sel = dda_step(r, p, tb);
                     target = step_sectant(r, target, sel);
-                    if (target < 64) tb.min = vadd(tb.min, vmul(step_vec(r, sel), tb.size));
-                    if (target >= 64 || ((occ >> target) & 1ull) != 0) break;
+                    if (target < 64u) tb.min = vadd(tb.min, vmul(step_vec(r, sel), tb.size));
+                    if (iters > budget || target >= 64u || ((occ >> target) & 1ull) != 0) break;
                 }
             }
+            if (!done && ++iters > budget) {  // the next node iteration
+                done = true;
+                ok = budget >= VHX_MAX_ITERS;
+            }
         }
-        // restart from the root (cpu.rs:441-455)
-        p = vadd(p, vmul(d, 0.1f));
-        if (p.x < tsize && p.y < tsize && p.z < tsize && p.x > 0.0f && p.y > 0.0f && p.z > 0.0f)
-            target = offset_sectant(p, tsize);
-        else
-            target = 64;
+        if (done) break;
     }
+    return ok;
 }
 
 }  // namespace vhx

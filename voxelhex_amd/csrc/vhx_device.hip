@@ -43,8 +43,15 @@ struct vhx_ctx {
     vhx_tree_desc desc{};  // counts of the uploaded tree (pointers unused)
     DevBuf raw[7];         // VHX_BUF_* raw copies
     DevBuf hdr, brick_occ, scratch, rays;
+    DevBuf queue[2];  // multi-pass ray queues (ping-pong), one u32 output index per abandoned ray
+    DevBuf qctl;      // [0..3] queue lengths written by pass p, [4..7] work counters of the queue passes
     uint32_t occ_words = 1;
     bool simple_kernel = true;  // VHX_PERSISTENT=1 selects the persistent wave-refill kernel (A/B)
+    // step budgets of the passes before the final (unbounded) one; VHX_BUDGETS="64" / "32,256" style override
+    uint32_t budgets[3] = {64u, 0u, 0u};
+    uint32_t npass = 2;         // passes including the final one (1 = single pass)
+    uint32_t rpw[4] = {64u, 64u, 64u, 64u};  // rays per wave of each pass (VHX_RPW="64,16" style override)
+    uint32_t queue_blocks = 2048;  // workgroups of a queue pass (CUs x resident workgroups)
 };
 
 #define VHX_HIP(ctx, call)                                                                                         \
@@ -288,12 +295,67 @@ __global__ void __launch_bounds__(256) k_trace_persistent(DevTree t, CamD cam, O
     }
 }
 
+// ------------------------------------------------------------------------------------------- multi-pass scheduling
+// Per-ray work is heavy-tailed (bench frame: mean 14 steps, p99 311, max 2160), and a wave64 runs as long as its
+// longest lane. Pass 0 traces every ray with a small step budget; the rays that exhaust it hand their output index to
+// a queue (one atomic per wave) and are traced again from scratch, 64 long rays per wave, by the next pass with a
+// larger budget; the last pass is unbounded (VHX_MAX_ITERS). Every ray's result comes from one uninterrupted,
+// deterministic traversal, so the output is bit-identical to a single pass.
+__device__ __forceinline__ void enqueue(uint32_t *items, uint32_t *count, bool push, uint32_t idx) {
+    const uint64_t m = __ballot(push);
+    if (m == 0ull) return;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t leader = (uint32_t)__ffsll((unsigned long long)m) - 1u;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(count, (uint32_t)__popcll(m));
+    base = __shfl(base, (int)leader);
+    if (push) items[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = idx;
+}
+
+struct PassQ {
+    uint32_t budget;   // VHX_MAX_ITERS on the final pass
+    uint32_t rpw;      // queue passes: rays per wave (lanes >= rpw idle: less divergence on the latency-bound tail)
+    uint32_t *out;     // queue of abandoned rays (null on the final pass)
+    uint32_t *out_n;
+};
+
+// Where a queued output index comes from: a primary-ray frame (framebuffer or tile layout) or an explicit ray batch.
+struct RaySrc {
+    uint32_t kind;  // 0 framebuffer, 1 tiles, 2 explicit rays
+    uint32_t T, tiles_x, tile_start, tile_stride;
+    const float *rays;
+};
+
+__device__ __forceinline__ void ray_of(const CamD &cam, const RaySrc &src, uint32_t idx, F3d &o, F3d &d) {
+    if (src.kind == 2u) {
+        o = mk(src.rays[6ull * idx], src.rays[6ull * idx + 1], src.rays[6ull * idx + 2]);
+        d = mk(src.rays[6ull * idx + 3], src.rays[6ull * idx + 4], src.rays[6ull * idx + 5]);
+        return;
+    }
+    uint32_t px, py;
+    if (src.kind == 0u) {
+        py = idx / cam.width;
+        px = idx - py * cam.width;
+    } else {
+        const uint32_t tt = src.T * src.T;
+        const uint32_t j = idx / tt, local = idx - j * tt;
+        const uint32_t tile = src.tile_start + j * src.tile_stride;
+        px = (tile % src.tiles_x) * src.T + local % src.T;
+        py = (tile / src.tiles_x) * src.T + local / src.T;
+    }
+    primary_ray(cam, px, py, o, d);
+}
+
 // One workgroup = 256 lanes = a 16x16 pixel block made of four 8x8 wave tiles (wave64-coherent ray bundles, the
 // 8x8 footprint of the reference's @workgroup_size(8, 8, 1)). Blocks are dealt tile by tile.
 template <bool COUNT, int BD>
 __global__ void __launch_bounds__(256) k_trace_primary(DevTree t, CamD cam, OutD out, uint32_t T, uint32_t tiles_x,
                                                        uint32_t tile_start, uint32_t tile_stride, uint32_t layout,
-                                                       uint32_t blocks_per_tile_x, uint32_t blocks_per_tile) {
+                                                       uint32_t blocks_per_tile_x, uint32_t blocks_per_tile,
+                                                       PassQ q) {
+    __shared__ uint64_t occ_tab[512];
+    fill_occ_tab(occ_tab);
+    __syncthreads();
     const uint32_t j = blockIdx.x / blocks_per_tile;  // j-th tile of this rank
     const uint32_t sb = blockIdx.x - j * blocks_per_tile;
     const uint32_t tile = tile_start + j * tile_stride;
@@ -306,21 +368,60 @@ __global__ void __launch_bounds__(256) k_trace_primary(DevTree t, CamD cam, OutD
     F3d o, d;
     primary_ray(cam, px, py, o, d);
     HitOut h;
-    get_by_ray<COUNT, BD>(t, o, d, h);
+    const bool done = get_by_ray<COUNT, BD>(t, occ_tab, o, d, h, q.budget);
     const uint64_t idx = layout == VHX_LAYOUT_FRAMEBUFFER ? (uint64_t)py * cam.width + px
                                                           : (uint64_t)j * T * T + (uint64_t)ly * T + lx;
-    store(t, out, idx, o, h);
+    if (done) store(t, out, idx, o, h);
+    if (q.out) enqueue(q.out, q.out_n, !done, (uint32_t)idx);
 }
 
 template <bool COUNT, int BD>
-__global__ void __launch_bounds__(256) k_trace_rays(DevTree t, const float *__restrict__ rays, uint64_t n, OutD out) {
+__global__ void __launch_bounds__(256) k_trace_rays(DevTree t, const float *__restrict__ rays, uint64_t n, OutD out,
+                                                    PassQ q) {
+    __shared__ uint64_t occ_tab[512];
+    fill_occ_tab(occ_tab);
+    __syncthreads();
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const F3d o = mk(rays[6 * i], rays[6 * i + 1], rays[6 * i + 2]);
     const F3d d = mk(rays[6 * i + 3], rays[6 * i + 4], rays[6 * i + 5]);
     HitOut h;
-    get_by_ray<COUNT, BD>(t, o, d, h);
-    store(t, out, i, o, h);
+    const bool done = get_by_ray<COUNT, BD>(t, occ_tab, o, d, h, q.budget);
+    if (done) store(t, out, i, o, h);
+    if (q.out) enqueue(q.out, q.out_n, !done, (uint32_t)i);
+}
+
+// Queue pass: each wave takes 64 consecutive queue entries at a time from a shared counter until the queue written
+// by the previous pass is drained (its length is read on the device; the host never synchronises between passes).
+template <bool COUNT, int BD>
+__global__ void __launch_bounds__(256) k_trace_queue(DevTree t, CamD cam, RaySrc src, OutD out,
+                                                     const uint32_t *__restrict__ in, const uint32_t *in_n,
+                                                     uint32_t *grab, PassQ q) {
+    __shared__ uint64_t occ_tab[512];
+    fill_occ_tab(occ_tab);
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t n = *in_n;
+    for (;;) {
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(grab, q.rpw);
+        base = __shfl(base, 0);
+        if (base >= n) break;  // wave-uniform
+        const uint32_t i = base + lane;
+        bool push = false;
+        uint32_t idx = 0;
+        if (lane < q.rpw && i < n) {
+            idx = in[i];
+            F3d o, d;
+            ray_of(cam, src, idx, o, d);
+            HitOut h;
+            if (get_by_ray<COUNT, BD>(t, occ_tab, o, d, h, q.budget))
+                store(t, out, idx, o, h);
+            else
+                push = true;
+        }
+        if (q.out) enqueue(q.out, q.out_n, push, idx);
+    }
 }
 
 __global__ void __launch_bounds__(256) k_untile_rgba(const uint32_t *__restrict__ gathered, uint32_t ranks,
@@ -483,6 +584,39 @@ static int finish_out(vhx_ctx *c, HostOut &ho) {
     return VHX_OK;
 }
 
+// Multi-pass plumbing: queue buffers + counters for `nout` rays; returns the number of passes to run.
+static int prepare_passes(vhx_ctx *c, uint64_t nout, uint32_t &npass) {
+    npass = nout < 0xFFFFFFFFull ? c->npass : 1u;
+    if (npass < 2) return VHX_OK;
+    int rc = ensure(c, c->queue[0], nout * 4);
+    if (!rc && npass > 2) rc = ensure(c, c->queue[1], nout * 4);
+    if (!rc) rc = ensure(c, c->qctl, 8 * sizeof(uint32_t));
+    if (rc) return rc;
+    VHX_HIP(c, hipMemsetAsync(c->qctl.ptr, 0, 8 * sizeof(uint32_t), c->stream));
+    return VHX_OK;
+}
+
+static PassQ pass_q(const vhx_ctx *c, uint32_t p, uint32_t npass) {
+    PassQ q;
+    const bool last = p + 1 >= npass;
+    q.budget = last ? VHX_MAX_ITERS : c->budgets[p];
+    q.rpw = c->rpw[p];
+    q.out = last ? nullptr : (uint32_t *)c->queue[p & 1u].ptr;
+    q.out_n = last ? nullptr : (uint32_t *)c->qctl.ptr + p;
+    return q;
+}
+
+template <bool COUNT, int BD>
+static void launch_queue_passes(vhx_ctx *c, const DevTree &t, const CamD &cam, const RaySrc &src, const OutD &o,
+                                uint32_t npass) {
+    for (uint32_t p = 1; p < npass; ++p) {
+        const uint32_t *in = (const uint32_t *)c->queue[(p - 1) & 1u].ptr;
+        uint32_t *ctl = (uint32_t *)c->qctl.ptr;
+        k_trace_queue<COUNT, BD><<<c->queue_blocks, 256, 0, c->stream>>>(t, cam, src, o, in, ctl + (p - 1),
+                                                                         ctl + 4 + p, pass_q(c, p, npass));
+    }
+}
+
 // ------------------------------------------------------------------------------------------------ C ABI
 extern "C" {
 
@@ -517,6 +651,32 @@ int vhx_create(int hip_device, vhx_ctx **out) {
     {
         const char *pk = getenv("VHX_PERSISTENT");
         c->simple_kernel = !(pk && pk[0] == '1');
+        const char *pb = getenv("VHX_BUDGETS");  // "32,256" = three passes; "" or "0" = one pass
+        if (pb) {
+            uint32_t b[3], nb = 0;
+            for (const char *q = pb; *q && nb < 3;) {
+                char *end = nullptr;
+                const unsigned long v = strtoul(q, &end, 10);
+                if (end == q) break;
+                if (v > 0 && v < VHX_MAX_ITERS) b[nb++] = (uint32_t)v;
+                q = *end == ',' ? end + 1 : end;
+            }
+            vhx_set_pass_budgets(c, b, nb);
+        }
+        const char *pr = getenv("VHX_RPW");  // rays per wave of the queue passes 1.., e.g. "64,16"
+        if (pr) {
+            uint32_t k = 1;
+            for (const char *q = pr; *q && k < 4;) {
+                char *end = nullptr;
+                const unsigned long v = strtoul(q, &end, 10);
+                if (end == q) break;
+                if (v >= 1 && v <= 64) c->rpw[k++] = (uint32_t)v;
+                q = *end == ',' ? end + 1 : end;
+            }
+        }
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, hip_device) == hipSuccess && prop.multiProcessorCount > 0)
+            c->queue_blocks = (uint32_t)prop.multiProcessorCount * 8u;
     }
     if ((e = hipEventCreate(&c->ev0)) != hipSuccess) return bail("hipEventCreate", e);
     if ((e = hipEventCreate(&c->ev1)) != hipSuccess) return bail("hipEventCreate", e);
@@ -534,12 +694,22 @@ void vhx_destroy(vhx_ctx *c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (auto &b : c->raw)
         if (b.ptr) (void)hipFree(b.ptr);
-    for (DevBuf *b : {&c->hdr, &c->brick_occ, &c->scratch, &c->rays})
+    for (DevBuf *b : {&c->hdr, &c->brick_occ, &c->scratch, &c->rays, &c->queue[0], &c->queue[1], &c->qctl})
         if (b->ptr) (void)hipFree(b->ptr);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
+}
+
+int vhx_set_pass_budgets(vhx_ctx *c, const uint32_t *budgets, uint32_t n) {
+    if (!c || n > 3 || (n && !budgets)) return VHX_E_INVALID_ARG;
+    for (uint32_t i = 0; i < n; ++i)
+        if (budgets[i] == 0 || budgets[i] >= VHX_MAX_ITERS || (i && budgets[i] <= budgets[i - 1]))
+            return fail(c, VHX_E_INVALID_ARG, "pass budgets must be increasing, > 0 and < 2^22");
+    for (uint32_t i = 0; i < 3; ++i) c->budgets[i] = i < n ? budgets[i] : 0u;
+    c->npass = n + 1;
+    return VHX_OK;
 }
 
 const char *vhx_last_error(const vhx_ctx *c) { return c ? c->err.c_str() : "null context"; }
@@ -705,21 +875,33 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
     constexpr uint32_t TASK = 512;
     const uint32_t nwaves = (fm.n_micro + TASK / 64 - 1) / (TASK / 64);
     const uint32_t pblocks = (nwaves + 3) / 4;
-    (void)nblocks;
+    const bool simple = c->simple_kernel;
+    uint32_t npass = 1;
+    if (simple) {
+        rc = prepare_passes(c, nout, npass);
+        if (rc) return rc;
+    }
+    RaySrc src{};
+    src.kind = layout == VHX_LAYOUT_FRAMEBUFFER ? 0u : 1u;
+    src.T = T;
+    src.tiles_x = tiles_x;
+    src.tile_start = tile_start;
+    src.tile_stride = tile_stride;
     VHX_HIP(c, hipEventRecord(c->ev0, c->stream));
     const bool count = ho.dev.bytes != nullptr;
-    const bool simple = c->simple_kernel;
     auto launch = [&](auto bd_tag) {
         constexpr int BD = decltype(bd_tag)::value;
+        const PassQ q0 = pass_q(c, 0, npass);
         if (simple) {
-            if (count)
-                k_trace_primary<true, BD><<<(unsigned)nblocks, 256, 0, c->stream>>>(t, cd, ho.dev, T, tiles_x,
-                                                                                    tile_start, tile_stride, layout,
-                                                                                    bpx, bpt);
-            else
-                k_trace_primary<false, BD><<<(unsigned)nblocks, 256, 0, c->stream>>>(t, cd, ho.dev, T, tiles_x,
-                                                                                     tile_start, tile_stride, layout,
-                                                                                     bpx, bpt);
+            if (count) {
+                k_trace_primary<true, BD><<<(unsigned)nblocks, 256, 0, c->stream>>>(
+                    t, cd, ho.dev, T, tiles_x, tile_start, tile_stride, layout, bpx, bpt, q0);
+                launch_queue_passes<true, BD>(c, t, cd, src, ho.dev, npass);
+            } else {
+                k_trace_primary<false, BD><<<(unsigned)nblocks, 256, 0, c->stream>>>(
+                    t, cd, ho.dev, T, tiles_x, tile_start, tile_stride, layout, bpx, bpt, q0);
+                launch_queue_passes<false, BD>(c, t, cd, src, ho.dev, npass);
+            }
         } else if (count) {
             k_trace_persistent<true, BD, TASK><<<pblocks, 256, 0, c->stream>>>(t, cd, ho.dev, fm);
         } else {
@@ -752,14 +934,26 @@ int vhx_trace_rays(vhx_ctx *c, const float *rays, uint64_t n, const vhx_hits *ou
         drays = (const float *)c->rays.ptr;
     }
     const DevTree t = dev_tree(c);
+    uint32_t npass = 1;
+    rc = prepare_passes(c, n, npass);
+    if (rc) return rc;
+    RaySrc src{};
+    src.kind = 2u;
+    src.rays = drays;
+    CamD cd{};
     VHX_HIP(c, hipEventRecord(c->ev0, c->stream));
     const bool count = ho.dev.bytes != nullptr;
+    const unsigned nb = (unsigned)((n + 255) / 256);
     auto launch = [&](auto bd_tag) {
         constexpr int BD = decltype(bd_tag)::value;
-        if (count)
-            k_trace_rays<true, BD><<<(unsigned)((n + 255) / 256), 256, 0, c->stream>>>(t, drays, n, ho.dev);
-        else
-            k_trace_rays<false, BD><<<(unsigned)((n + 255) / 256), 256, 0, c->stream>>>(t, drays, n, ho.dev);
+        const PassQ q0 = pass_q(c, 0, npass);
+        if (count) {
+            k_trace_rays<true, BD><<<nb, 256, 0, c->stream>>>(t, drays, n, ho.dev, q0);
+            launch_queue_passes<true, BD>(c, t, cd, src, ho.dev, npass);
+        } else {
+            k_trace_rays<false, BD><<<nb, 256, 0, c->stream>>>(t, drays, n, ho.dev, q0);
+            launch_queue_passes<false, BD>(c, t, cd, src, ho.dev, npass);
+        }
     };
     if (!dispatch_bd(c->desc.brick_dim, launch)) return fail(c, VHX_E_INVALID_ARG, "unsupported brick_dim");
     VHX_HIP(c, hipGetLastError());

@@ -223,6 +223,11 @@ class Raytracer:
     def set_stream(self, stream_ptr):
         self._check(N.lib().vhx_set_stream(self._h, ctypes.c_void_p(stream_ptr)))
 
+    def set_pass_budgets(self, budgets):
+        """Step budgets of the multi-pass ray scheduler (vhx_set_pass_budgets); () = one unbounded pass."""
+        b = (ctypes.c_uint32 * max(1, len(budgets)))(*budgets)
+        self._check(N.lib().vhx_set_pass_budgets(self._h, b, len(budgets)))
+
     def sync(self):
         ms = ctypes.c_float()
         self._check(N.lib().vhx_sync(self._h, ctypes.byref(ms)))
