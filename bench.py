@@ -3,16 +3,18 @@
 One step = one frame: every pixel's primary ray traced with get_by_ray semantics (src/raytracing/cpu.rs:296-458)
 through the HIP kernel, shaded to RGBA8 + f32 depth in HBM. With N GPUs (torchrun, one process per GPU, RCCL) the
 frame is split into 64x64 screen tiles dealt round-robin over the ranks; each rank traces its tiles into a
-contiguous buffer, rank 0 gathers the RGBA tiles over RCCL and scatters them into the framebuffer (strong scaling:
-the frame is fixed, N GPUs share it).
+contiguous buffer, rank 0 gathers the RGBA tiles over RCCL and scatters them into the framebuffer. Weak scaling:
+the camera's field of view is fixed and the resolution grows with N so every rank keeps 3840x2160 rays
+(N=4 is config 4's 7680x4320 frame; N=2 5432x3056, N=8 10864x6112).
 
 Workload: the reference's lattice+cube scene S (examples/gpu_render.rs:57-82) at 1024^3
 with brick_dim 4 (1024 is not a valid size for brick_dim 8, src/boxtree/mod.rs:188-202; the 1024^3 .vox model is not
 in the reference checkout), glass camera of benches/performance.rs on radius 2S at 40 rad aimed at the centre.
 
 Also printed: roofline (algorithmic bytes per launch, counted by the instrumented kernel, / measured kernel time vs
-8 TB/s), and cpu_baseline: the CPU restatement of the reference raytracer (oracle/) on the host cores over the
-same frame.
+8 TB/s; `traffic` = the PMC-measured memory-side read bytes of the same launch from profiles/, see
+scripts/pmc_traffic.py), and cpu_baseline: the CPU restatement of the reference raytracer (oracle/) on the host
+cores over the same frame.
 """
 import argparse
 import json
@@ -36,13 +38,34 @@ def parse():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--size", type=int, default=1024)
     p.add_argument("--brick-dim", type=int, default=4)
-    p.add_argument("--width", type=int, default=3840)
+    p.add_argument("--width", type=int, default=3840, help="per-rank-equivalent frame width (N=1 frame)")
     p.add_argument("--height", type=int, default=2160)
     p.add_argument("--scene", type=int, default=1, help="VHX_SCENE_* (1 = lattice+cube scene S)")
     p.add_argument("--tile", type=int, default=64)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-roofline", action="store_true")
     return p.parse_args()
+
+
+def frame_size(w, h, world):
+    """Weak scaling: same field of view, w*h rays per rank (dimensions rounded to multiples of 8)."""
+    if world == 1:
+        return w, h
+    f = world ** 0.5
+    return int(round(w * f / 8.0)) * 8, int(round(h * f / 8.0)) * 8
+
+
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic.json")
+
+
+def pmc_traffic(workload):
+    """Memory-side read bytes per launch for this workload, from the committed PMC summary (or None)."""
+    try:
+        d = json.load(open(TRAFFIC_FILE))
+    except (OSError, ValueError):
+        return None
+    e = d.get(workload)
+    return None if e is None else e
 
 
 def main():
@@ -78,7 +101,7 @@ def main():
     rt.upload(flat)
     upload_s = time.time() - t0
 
-    W, H, T = args.width, args.height, args.tile
+    (W, H), T = frame_size(args.width, args.height, world), args.tile
     c = args.size / 2.0
     cam = vhx.glass_camera(args.size, W, H, target=(c, c, c))
     if world == 1:
@@ -132,6 +155,7 @@ def main():
         elapsed = float(tt.item())
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
 
+    workload = f"primary {W}x{H} S{args.scene} {args.size}^3 bd{args.brick_dim} ranks{world}"
     total_rays = W * H
     mrays = total_rays * args.steps / elapsed / 1e6
     ms_per_step = elapsed * 1e3 / args.steps
@@ -145,9 +169,14 @@ def main():
         out_bytes = 8.0 * my_rays  # rgba8 + f32 depth per ray
         launch_bytes = tree_bytes + out_bytes
         achieved = launch_bytes / (kernel_ms * 1e-3) / 1e9
+        tr = pmc_traffic(workload)
         roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-                "kernel": "k_trace_primary<false>", "kernel_ms": round(kernel_ms, 4),
+                "frac": round(achieved / HBM_PEAK_GBS, 5),
+                "traffic": None if tr is None else tr["read_bytes_per_launch"],
+                "traffic_source": None if tr is None else tr["source"],
+                "kernel": "vhx_trace_primary launch = k_trace_primary (pass 0, step budget) + k_trace_queue "
+                          "(re-trace of the rays over budget), timed together with HIP events on the trace stream",
+                "kernel_ms": round(kernel_ms, 4),
                 "algorithmic_bytes_per_launch": launch_bytes, "tree_bytes_per_ray": round(tree_bytes / max(1, my_rays), 2)}
 
     # ---- CPU baseline: the oracle (reference semantics) on the host cores, rank 0 at N=1 only ----------------------
@@ -167,10 +196,12 @@ def main():
         line = {
             "metric": BASELINE["metric"], "value": round(mrays, 3), "unit": "Mrays/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
-            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic",
             "config": {"workload": f"primary rays {W}x{H}, {args.size}^3 procedural scene S (lattice+cube), "
-                                   f"brick_dim {args.brick_dim}, glass camera",
+                                   f"brick_dim {args.brick_dim}, glass camera"
+                                   + (f", {W * H // world} rays per rank" if world > 1 else ""),
+                       "workload_key": workload,
                        "tree_size": args.size, "brick_dim": args.brick_dim, "width": W, "height": H,
                        "scene": args.scene, "tile": T if world > 1 else None,
                        "parallelism": f"screen-tile split x{world} + RCCL gather" if world > 1 else "single GPU",

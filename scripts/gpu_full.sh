@@ -1,11 +1,11 @@
 #!/bin/bash
-# Full GPU pass: parity tests, smoke, default bench, rocprofv3 kernel-trace summary of the bench command.
+# Full GPU pass: parity tests, smoke, default bench, rocprofv3 kernel-trace summary of the bench command, PMC traffic.
 cd "$GRAFT_REPO_ROOT" || exit 1
 R="$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 timeout -k 10 900 python -m pytest tests -m gpu -q > gpurun_out/pytest_gpu.log 2>&1; rc=$?
 echo "pytest rc=$rc"; tail -4 gpurun_out/pytest_gpu.log
-[ $rc -gt 1 ] && exit $rc
+[ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; rc=$?
 echo "smoke rc=$rc"; tail -1 gpurun_out/smoke.log
 [ $rc -ne 0 ] && exit $rc
@@ -15,5 +15,5 @@ echo "bench rc=$rc"; tail -1 gpurun_out/bench.log
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$R/gpurun_out/prof" -o bench -- python3 "$R/bench.py" --steps 10 --warmup 2 --no-cpu-baseline > "$R/gpurun_out/prof_bench.log" 2>&1; rc=$?
 echo "rocprof rc=$rc"; tail -1 "$R/gpurun_out/prof_bench.log"
-find "$R/gpurun_out/prof" -name "*stats*" | head
-exit $rc
+[ $rc -ne 0 ] && exit $rc
+bash "$R/scripts/gpu_pmc_traffic.sh"
