@@ -25,12 +25,13 @@ def main():
     for sched in ((), (32, 256)):
         rt.set_pass_budgets(sched)
         for name, pix in (("longest", z["top64"][:1]), ("top64", z["top64"]), ("top64x16", np.tile(z["top64"], 16)),
-                          ("tail>256", z["tail"]), ("tail>1024", z["tail"][z["steps"] > 1024])):
+                          ("tail>256", z["tail"]), ("tail>1024", z["tail"][z["steps"] > 1024]),
+                          ("tail>256 shuffled", z["tail_shuf"]), ("tail>64", z["t64"]), ("tail>64 shuffled", z["t64_shuf"])):
             oo, dd = rays(pix)
             ts = []
             for _ in range(4):
                 rt.trace_rays(oo, dd, fields=("value",))
                 ts.append(rt.sync())
-            print(f"sched={sched} {name:10s} n={len(pix):7d} ms={min(ts[1:]):.3f}", flush=True)
+            print(f"sched={sched} {name:18s} n={len(pix):7d} ms={min(ts[1:]):.3f}", flush=True)
 
 main()

@@ -80,6 +80,10 @@ __device__ __forceinline__ uint32_t ras_u8(float f) {
     return r < 255u ? r : 255u;
 }
 
+// x - fmod(x, s) for s a power of two: fmod(x, s) = x - q*s with q = trunc(x/s) exact, so the difference is q*s
+// exactly, except that x - x is +0 where q*s may be -0; adding +0.0 maps -0 to +0 and leaves every other value alone
+__device__ __forceinline__ float floor_to_pow2(float x, float s);
+
 // exact 1/s for s a normal power of two: exponent e -> -e
 __device__ __forceinline__ float rcp_pow2(float s) { return __uint_as_float(0x7F000000u - __float_as_uint(s)); }
 // fmodf(x, s) for s a power of two (exact: x*(1/s) and trunc(.)*s are exact scalings, the difference is exact by
@@ -88,6 +92,10 @@ __device__ __forceinline__ float fmod_pow2(float x, float s) {
     const float q = __builtin_truncf(x * rcp_pow2(s));
     const float r = x - q * s;
     return r == 0.0f ? __builtin_copysignf(0.0f, x) : r;
+}
+
+__device__ __forceinline__ float floor_to_pow2(float x, float s) {
+    return __builtin_truncf(x * rcp_pow2(s)) * s + 0.0f;
 }
 
 // RAY_TO_NODE_OCCUPANCY_BITMASK_LUT[s][o] (src/spatial/lut.rs:96-161): sectants t with t_k on the ray's side of
@@ -340,7 +348,15 @@ __device__ __forceinline__ bool get_by_ray(const DevTree &t, const uint64_t *occ
     uint32_t node = 0, s1 = 0, s2 = 0, s3 = 0, count = 1;  // push(ROOT)
     uint32_t iters = 1;  // the first node iteration
     bool ok = true;
+    uint32_t trips = 0;  // wave-uniform count of node-loop trips
     for (;;) {
+        // Long-running waves raise their issue priority (SIMD arbitration is by priority, then age), so the waves
+        // that hold the frame's longest rays are not slowed by the shorter waves sharing their SIMD.
+        if ((++trips & 127u) == 0u) {
+            if (trips == 128u) __builtin_amdgcn_s_setprio(1);
+            if (trips == 512u) __builtin_amdgcn_s_setprio(2);
+            if (trips == 1024u) __builtin_amdgcn_s_setprio(3);
+        }
         const uint4 lh = t.hdr[node];
         // the child slot is read by both the leaf probe and the push: issue it with the header load so the
         // iteration waits for one memory latency instead of two
@@ -365,8 +381,8 @@ __device__ __forceinline__ bool get_by_ray(const DevTree &t, const uint64_t *occ
                 s2 = s3;
                 tb = cur;
                 cur.size *= 4.0f;
-                cur.min = vsub(cur.min, mk(fmod_pow2(cur.min.x, cur.size), fmod_pow2(cur.min.y, cur.size),
-                                           fmod_pow2(cur.min.z, cur.size)));
+                cur.min = mk(floor_to_pow2(cur.min.x, cur.size), floor_to_pow2(cur.min.y, cur.size),
+                             floor_to_pow2(cur.min.z, cur.size));  // min -= min % size
                 const float hs = tb.size * 0.5f;
                 target = offset_sectant(vsub(vadd(tb.min, mk(hs, hs, hs)), cur.min), cur.size);
                 const uint32_t sel = dda_step(r, p, tb);
@@ -408,8 +424,12 @@ __device__ __forceinline__ bool get_by_ray(const DevTree &t, const uint64_t *occ
                     ++iters;
                     const uint32_t sel = dda_step(r, p, tb);
                     target = step_sectant(r, target, sel);
-                    if (target < 64u) tb.min = vadd(tb.min, vmul(step_vec(r, sel), tb.size));
-                    if (iters > budget || target >= 64u || ((occ >> target) & 1ull) != 0) break;
+                    const F3d nmin = vadd(tb.min, vmul(step_vec(r, sel), tb.size));
+                    const bool in = target < 64u;
+                    tb.min.x = in ? nmin.x : tb.min.x;  // component-wise select, no branch
+                    tb.min.y = in ? nmin.y : tb.min.y;
+                    tb.min.z = in ? nmin.z : tb.min.z;
+                    if (iters > budget || !in || ((occ >> target) & 1ull) != 0) break;
                 }
             }
             if (!done && ++iters > budget) {  // the next node iteration
