@@ -175,6 +175,16 @@ int vhx_trace_primary(vhx_ctx *ctx, const vhx_camera *cam, uint32_t tile_size, u
                       uint32_t tile_stride, uint32_t layout, const vhx_hits *out, int on_device);
 /* Traces n explicit rays; rays = 6 f32 per ray (origin xyz, direction xyz), host or device per on_device. */
 int vhx_trace_rays(vhx_ctx *ctx, const float *rays, uint64_t n, const vhx_hits *out, int on_device);
+/* Hard shadows (BASELINE config 5; the reference has no shadow rays — semantics defined in DESIGN.md §10): for
+ * every ray i < n of a previous trace with a hit (value[i] != VHX_EMPTY), one shadow ray from
+ * impact[i] + normal[i] * 1e-3 toward `light` (e.g. the reference's ambient_light_position = (size, size, size),
+ * src/raytracing/bevy/view.rs:81-85) is traced with get_by_ray semantics; shadowed[i] = 1 if it hits a voxel, else 0
+ * (0 for primary misses). rgba (optional) is darkened in place (rgb >> 1) where shadowed; bytes (optional) receives
+ * the algorithmic bytes of each shadow ray. All pointers are device memory (the on_device output of
+ * vhx_trace_primary / vhx_trace_rays); hit pixels are compacted first so waves trace only shadow rays. */
+int vhx_trace_shadows(vhx_ctx *ctx, const float light[3], uint64_t n, const uint32_t *value, const float *impact,
+                      const float *normal, uint32_t *shadowed, uint32_t *rgba, uint32_t *bytes);
+
 /* Scatters tile-major RGBA buffers gathered from `ranks` ranks (rank r traced tiles r, r+ranks, ...; each rank's
  * buffer holds tiles_per_rank*T*T pixels, concatenated by rank) into a width x height framebuffer.       */
 int vhx_untile_rgba(vhx_ctx *ctx, const uint32_t *gathered, uint32_t ranks, uint32_t tiles_per_rank,

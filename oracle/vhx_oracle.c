@@ -43,6 +43,14 @@
 
 #define VHX_ORACLE_MAX_ITERS (1u << 22)
 static _Thread_local uint32_t g_brick_steps; /* per-thread scratch for the work statistics */
+/* optional per-ray event trace (diagnostics: wave-divergence simulation in scripts/sim_divergence.py):
+ * N node iteration, P brick probe, B brick cell step, O pop, U push, A advance step, R restart */
+static _Thread_local uint8_t *g_ev;
+static _Thread_local uint32_t g_ev_n, g_ev_cap;
+#define EV(ch)                                                     \
+    do {                                                           \
+        if (g_ev && g_ev_n < g_ev_cap) g_ev[g_ev_n++] = (uint8_t)(ch); \
+    } while (0)
 
 typedef struct { float x, y, z; } v3;
 typedef struct { v3 min; float size; } cube;
@@ -265,6 +273,7 @@ static int traverse_brick(const vhx_tree_desc *t, const ray_t *r, v3 *p, const u
         if (++*iters > VHX_ORACLE_MAX_ITERS) return 0;
         (*bytes) += 0; /* keep byte model unchanged */
         g_brick_steps += 1;
+        EV('B');
         step = dda_step(r, p, cur);
         cur.min = v_add(cur.min, v_mul(step, unit));
         ix += r_as_i32(roundf(step.x));
@@ -356,6 +365,7 @@ static void get_by_ray(const vhx_tree_desc *t, v3 o, v3 d, hit_t *h) {
         while (stack.count != 0) {
             if (++iters > VHX_ORACLE_MAX_ITERS) return;
             h->n_node++;
+            EV('N');
             uint64_t occ = t->node_ocbits[stack.data[stack.head]];
             uint32_t ntype = t->node_type[node];
             h->bytes += 12;
@@ -364,6 +374,7 @@ static void get_by_ray(const vhx_tree_desc *t, v3 o, v3 d, hit_t *h) {
                 if (ntype == VHX_NODE_UNIFORM_LEAF) {
                     h->bytes += 4;
                     h->n_probe++;
+                    EV('P');
                     if (probe_brick(t, &r, &p, t->node_children[(uint64_t)node * 64], cur, h, &iters)) {
                         h->hit = 1;
                         return;
@@ -372,6 +383,7 @@ static void get_by_ray(const vhx_tree_desc *t, v3 o, v3 d, hit_t *h) {
                 } else if (ntype == VHX_NODE_LEAF) {
                     h->bytes += 4;
                     h->n_probe++;
+                    EV('P');
                     if (probe_brick(t, &r, &p, t->node_children[(uint64_t)node * 64 + target],
                                     child_bounds_for(cur, target), h, &iters)) {
                         h->hit = 1;
@@ -382,6 +394,7 @@ static void get_by_ray(const vhx_tree_desc *t, v3 o, v3 d, hit_t *h) {
             if (backtrack || target >= 64 || occ == 0 || (occ & OCC_LUT[target][dir_idx]) == 0) {
                 /* POP */
                 h->n_pop++;
+                EV('O');
                 ns_pop(&stack);
                 tb = cur;
                 cur.size *= 4.0f;
@@ -398,6 +411,7 @@ static void get_by_ray(const vhx_tree_desc *t, v3 o, v3 d, hit_t *h) {
             if (ntype == VHX_NODE_INTERNAL && (occ & ((uint64_t)1 << target)) != 0) {
                 /* PUSH */
                 h->n_push++;
+                EV('U');
                 h->bytes += 4;
                 uint32_t child = t->node_children[(uint64_t)node * 64 + target];
                 if (child >= t->node_count) return; /* reference would panic on the invalid key */
@@ -411,6 +425,7 @@ static void get_by_ray(const vhx_tree_desc *t, v3 o, v3 d, hit_t *h) {
                 for (;;) {
                     if (++iters > VHX_ORACLE_MAX_ITERS) return;
                     h->n_advance++;
+                    EV('A');
                     v3 sv = dda_step(&r, &p, tb);
                     target = step_sectant(target, sv);
                     if (target < 64) tb.min = v_add(tb.min, v_mul(sv, tb.size));
@@ -419,6 +434,7 @@ static void get_by_ray(const vhx_tree_desc *t, v3 o, v3 d, hit_t *h) {
             }
         }
         h->n_restart++;
+        EV('R');
         p = v_add(p, v_mul(d, 0.1f));
         if (p.x < tsize && p.y < tsize && p.z < tsize && p.x > 0.f && p.y > 0.f && p.z > 0.f)
             target = offset_sectant(p, tsize);
@@ -529,6 +545,36 @@ int vhx_oracle_trace_primary(const vhx_tree_desc *t, const vhx_camera *cam, uint
     return VHX_OK;
 }
 
+/* Hard shadows (BASELINE config 5; no reference counterpart — DESIGN.md §10 defines them): for every hit record i
+ * (value[i] != 0xFFFFFFFF) one shadow ray from impact + normal * 1e-3 (multiply, then add) toward `light`, direction
+ * normalised like V3c::normalized; shadowed[i] = hit ? 1 : 0; rgba (optional) gets rgb >> 1 where shadowed; bytes
+ * (optional) the shadow ray's algorithmic bytes. */
+int vhx_oracle_trace_shadows(const vhx_tree_desc *t, const float light[3], uint64_t n, const uint32_t *value,
+                             const float *impact, const float *normal, uint32_t *shadowed, uint32_t *rgba,
+                             uint32_t *bytes, int threads) {
+    if (!t || !light || (n && (!value || !impact || !normal || !shadowed))) return VHX_E_INVALID_ARG;
+    ensure_luts();
+#ifdef _OPENMP
+    if (threads <= 0) threads = omp_get_max_threads();
+#pragma omp parallel for schedule(dynamic, 64) num_threads(threads)
+#endif
+    for (int64_t i = 0; i < (int64_t)n; ++i) {
+        shadowed[i] = 0;
+        if (bytes) bytes[i] = 0;
+        if (value[i] == VHX_EMPTY) continue;
+        const float *ip = impact + 3 * i, *np = normal + 3 * i;
+        v3 o = V(ip[0] + np[0] * 1e-3f, ip[1] + np[1] * 1e-3f, ip[2] + np[2] * 1e-3f);
+        v3 d = v_normalized(V(light[0] - o.x, light[1] - o.y, light[2] - o.z));
+        hit_t h;
+        get_by_ray(t, o, d, &h);
+        shadowed[i] = h.hit ? 1u : 0u;
+        if (rgba && h.hit) rgba[i] = ((rgba[i] >> 1) & 0x007F7F7Fu) | (rgba[i] & 0xFF000000u);
+        if (bytes) bytes[i] = h.bytes;
+    }
+    (void)threads;
+    return VHX_OK;
+}
+
 /* Generates the three lookup tables (for pinning against the reference tables in tests/golden). */
 void vhx_oracle_luts(float offset[64 * 3], uint8_t step[64 * 27], uint64_t occ[64 * 8]) {
     ensure_luts();
@@ -633,4 +679,30 @@ int vhx_oracle_ray_steps(const vhx_tree_desc *t, const vhx_camera *cam, uint32_t
     }
     (void)threads;
     return VHX_OK;
+}
+
+/* Per-ray event sequences (see EV above) for the primary rays of the given pixels: events of ray i are
+ * buf[off[i] .. off[i+1]); returns the total length, or -1 if cap was too small. Diagnostics only. */
+int64_t vhx_oracle_ray_events(const vhx_tree_desc *t, const vhx_camera *cam, const uint32_t *px, const uint32_t *py,
+                              uint64_t n, uint8_t *buf, uint64_t cap, uint64_t *off) {
+    ensure_luts();
+    uint64_t used = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        hit_t hh;
+        v3 o, d;
+        primary_ray(cam, px[i], py[i], &o, &d);
+        g_ev = buf + used;
+        g_ev_n = 0;
+        g_ev_cap = (uint32_t)(cap - used > 0xFFFFFFFFull ? 0xFFFFFFFFull : cap - used);
+        get_by_ray(t, o, d, &hh);
+        off[i] = used;
+        if (g_ev_n >= g_ev_cap) {
+            g_ev = 0;
+            return -1;
+        }
+        used += g_ev_n;
+    }
+    off[n] = used;
+    g_ev = 0;
+    return (int64_t)used;
 }

@@ -18,6 +18,8 @@ class Oracle:
         l.vhx_oracle_trace_rays.argtypes = [P(N.TreeDesc), ctypes.c_void_p, ctypes.c_uint64, P(N.Hits), ctypes.c_int]
         l.vhx_oracle_trace_primary.argtypes = [P(N.TreeDesc), P(N.Camera), ctypes.c_uint32, ctypes.c_uint32,
                                                ctypes.c_uint32, ctypes.c_uint32, P(N.Hits), ctypes.c_int]
+        l.vhx_oracle_trace_shadows.argtypes = [P(N.TreeDesc), ctypes.c_void_p, ctypes.c_uint64] + \
+            [ctypes.c_void_p] * 6 + [ctypes.c_int]
         l.vhx_oracle_luts.argtypes = [ctypes.c_void_p] * 3
         l.vhx_oracle_luts.restype = None
         l.vhx_oracle_offset_sectant.argtypes = [ctypes.c_void_p, ctypes.c_float]
@@ -55,6 +57,21 @@ class Oracle:
         assert self.lib.vhx_oracle_trace_primary(ctypes.byref(flat.desc), ctypes.byref(cam), x0, y0, w, h,
                                                  ctypes.byref(hs), threads) == 0
         return out
+
+    def trace_shadows(self, flat, light, hits, threads=0):
+        """Shadow flags, darkened rgba and bytes for host hit records (value, impact, normal, rgba)."""
+        n = hits["value"].shape[0]
+        lt = np.asarray(light, np.float32)
+        value = np.ascontiguousarray(hits["value"], np.uint32)
+        imp = np.ascontiguousarray(hits["impact"], np.float32)
+        nrm = np.ascontiguousarray(hits["normal"], np.float32)
+        sh = np.empty(n, np.uint32)
+        rgba = np.array(hits["rgba"], np.uint32, copy=True)
+        by = np.empty(n, np.uint32)
+        assert self.lib.vhx_oracle_trace_shadows(ctypes.byref(flat.desc), lt.ctypes.data, n, value.ctypes.data,
+                                                 imp.ctypes.data, nrm.ctypes.data, sh.ctypes.data, rgba.ctypes.data,
+                                                 by.ctypes.data, threads) == 0
+        return {"shadowed": sh, "rgba": rgba, "bytes": by}
 
     # -- primitives -----------------------------------------------------------------------------------------------
     def luts(self):

@@ -252,3 +252,47 @@ def test_pass_budget_validation(gpu):
         with pytest.raises(N.VhxError):
             gpu.set_pass_budgets(bad)
     gpu.set_pass_budgets(DEFAULT_BUDGETS)
+
+
+def _device_hits(n):
+    import torch
+    return {"value": torch.empty(n, dtype=torch.int32, device="cuda"),
+            "impact": torch.empty((n, 3), dtype=torch.float32, device="cuda"),
+            "normal": torch.empty((n, 3), dtype=torch.float32, device="cuda"),
+            "rgba": torch.empty(n, dtype=torch.int32, device="cuda")}
+
+
+SHADOW_CASES = [(N.VHX_SCENE_LATTICE_CUBE, 256, 4, 256, 192, ()), (N.VHX_SCENE_LATTICE_CUBE, 256, 4, 256, 192, (1,)),
+                (N.VHX_SCENE_LATTICE_CUBE, 128, 8, 160, 120, (4, 40)), (N.VHX_SCENE_HEIGHTFIELD, 256, 4, 200, 150, ()),
+                (N.VHX_SCENE_BENCH_REGION, 512, 8, 128, 128, DEFAULT_BUDGETS)]
+
+
+@pytest.mark.parametrize("scene,size,bd,w,h,budgets", SHADOW_CASES)
+def test_shadow_rays_vs_oracle(gpu, oracle, scene, size, bd, w, h, budgets):
+    """vhx_trace_shadows (BASELINE config 5): shadow flags, darkened rgba and byte counts equal the oracle's on the
+    same primary hits, for single- and multi-pass schedules."""
+    flat = vhx.FlatTree.build_scene(scene, size, bd)
+    gpu.upload(flat)
+    tgt = None if scene == N.VHX_SCENE_BENCH_REGION else (size / 2,) * 3
+    cam = vhx.glass_camera(size, w, h, target=tgt)
+    light = (float(size),) * 3
+    try:
+        gpu.set_pass_budgets(budgets)
+        hits = gpu.trace_primary(cam, out=_device_hits(w * h))
+        res = gpu.trace_shadows(light, hits, count_bytes=True)
+        gpu.sync()
+        host = {k: v.cpu().numpy() for k, v in hits.items()}
+        ref_primary = oracle.trace_primary(flat, cam, 0, 0, w, h, fields=("value", "impact", "normal", "rgba"))
+        assert_same({k: host[k].view(np.uint32) if k in ("value", "rgba") else host[k] for k in ("value", "impact",
+                     "normal")}, {k: ref_primary[k] for k in ("value", "impact", "normal")}, "primary")
+        ref = oracle.trace_shadows(flat, light, ref_primary)
+        sh = res["shadowed"].cpu().numpy().view(np.uint32)
+        assert np.array_equal(sh, ref["shadowed"]), f"shadow flags differ at {np.count_nonzero(sh != ref['shadowed'])}"
+        assert np.array_equal(host["rgba"].view(np.uint32), ref["rgba"])
+        assert np.array_equal(res["bytes"].cpu().numpy().view(np.uint32), ref["bytes"])
+        hit = ref_primary["value"] != N.VHX_EMPTY
+        assert sh[~hit].sum() == 0
+        if scene != N.VHX_SCENE_BENCH_REGION:
+            assert 0 < sh[hit].sum() < hit.sum(), "expected both lit and shadowed hits"
+    finally:
+        gpu.set_pass_budgets(DEFAULT_BUDGETS)

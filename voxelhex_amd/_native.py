@@ -81,6 +81,8 @@ SIGNATURES = [
     ("vhx_tree_device_bytes", c_int, [c_void_p, P(c_u64)]),
     ("vhx_trace_primary", c_int, [c_void_p, P(Camera), c_u32, c_u32, c_u32, c_u32, P(Hits), c_int]),
     ("vhx_trace_rays", c_int, [c_void_p, c_void_p, c_u64, P(Hits), c_int]),
+    ("vhx_trace_shadows", c_int, [c_void_p, P(c_f32), c_u64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                  c_void_p]),
     ("vhx_untile_rgba", c_int, [c_void_p, c_void_p, c_u32, c_u32, c_u32, c_u32, c_u32, c_void_p, c_int]),
     ("vhx_boxtree_new", c_int, [c_u32, c_u32, P(c_void_p)]),
     ("vhx_boxtree_free", None, [c_void_p]),

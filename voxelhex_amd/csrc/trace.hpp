@@ -348,15 +348,7 @@ __device__ __forceinline__ bool get_by_ray(const DevTree &t, const uint64_t *occ
     uint32_t node = 0, s1 = 0, s2 = 0, s3 = 0, count = 1;  // push(ROOT)
     uint32_t iters = 1;  // the first node iteration
     bool ok = true;
-    uint32_t trips = 0;  // wave-uniform count of node-loop trips
     for (;;) {
-        // Long-running waves raise their issue priority (SIMD arbitration is by priority, then age), so the waves
-        // that hold the frame's longest rays are not slowed by the shorter waves sharing their SIMD.
-        if ((++trips & 127u) == 0u) {
-            if (trips == 128u) __builtin_amdgcn_s_setprio(1);
-            if (trips == 512u) __builtin_amdgcn_s_setprio(2);
-            if (trips == 1024u) __builtin_amdgcn_s_setprio(3);
-        }
         const uint4 lh = t.hdr[node];
         // the child slot is read by both the leaf probe and the push: issue it with the header load so the
         // iteration waits for one memory latency instead of two

@@ -46,7 +46,7 @@ struct vhx_ctx {
     DevBuf raw[7];         // VHX_BUF_* raw copies
     DevBuf hdr, brick_occ, scratch, rays;
     DevBuf queue[2];  // multi-pass ray queues (ping-pong), output indices of abandoned rays in increasing order
-    DevBuf qctl;      // [0..3] queue lengths written after pass p, [4..7] work counters of the queue passes
+    DevBuf qctl;      // [0..7] queue lengths written after pass p (7: shadow hit list), [8..15] work counters
     DevBuf flags;     // one byte per output ray: abandoned by the current pass
     DevBuf seltmp;    // rocPRIM select scratch
     uint32_t occ_words = 1;
@@ -315,12 +315,26 @@ struct PassQ {
 
 // Where a queued output index comes from: a primary-ray frame (framebuffer or tile layout) or an explicit ray batch.
 struct RaySrc {
-    uint32_t kind;  // 0 framebuffer, 1 tiles, 2 explicit rays
+    uint32_t kind;  // 0 framebuffer, 1 tiles, 2 explicit rays, 3 shadow rays from hit records
     uint32_t T, tiles_x, tile_start, tile_stride;
     const float *rays;
+    const float *impact, *normal;  // kind 3
+    float lx, ly, lz;               // kind 3: light position
 };
 
+// Hard-shadow ray of hit record idx (BASELINE config 5; semantics in DESIGN.md §10): from impact + normal * 1e-3
+// toward the light, direction normalised like V3c::normalized (src/spatial/math/vector.rs).
+__device__ __forceinline__ void shadow_ray(const RaySrc &src, uint32_t idx, F3d &o, F3d &d) {
+    const float *ip = src.impact + 3ull * idx, *np = src.normal + 3ull * idx;
+    o = mk(ip[0] + np[0] * 1e-3f, ip[1] + np[1] * 1e-3f, ip[2] + np[2] * 1e-3f);
+    d = vnorm(mk(src.lx - o.x, src.ly - o.y, src.lz - o.z));
+}
+
 __device__ __forceinline__ void ray_of(const CamD &cam, const RaySrc &src, uint32_t idx, F3d &o, F3d &d) {
+    if (src.kind == 3u) {
+        shadow_ray(src, idx, o, d);
+        return;
+    }
     if (src.kind == 2u) {
         o = mk(src.rays[6ull * idx], src.rays[6ull * idx + 1], src.rays[6ull * idx + 2]);
         d = mk(src.rays[6ull * idx + 3], src.rays[6ull * idx + 4], src.rays[6ull * idx + 5]);
@@ -391,7 +405,14 @@ __global__ void __launch_bounds__(256) k_trace_rays(DevTree t, const float *__re
 
 // Queue pass: each wave takes 64 consecutive queue entries at a time from a shared counter until the queue written
 // by the previous pass is drained (its length is read on the device; the host never synchronises between passes).
-template <bool COUNT, int BD>
+// Store of a shadow ray's result: shadowed flag (in out.value), rgb halved in place when shadowed, byte count.
+__device__ __forceinline__ void store_shadow(const OutD &o, uint64_t i, const HitOut &h) {
+    o.value[i] = h.hit ? 1u : 0u;
+    if (o.rgba && h.hit) o.rgba[i] = ((o.rgba[i] >> 1) & 0x007F7F7Fu) | (o.rgba[i] & 0xFF000000u);
+    if (o.bytes) o.bytes[i] = h.bytes;
+}
+
+template <bool COUNT, int BD, bool SHADOW = false>
 __global__ void __launch_bounds__(256) k_trace_queue(DevTree t, CamD cam, RaySrc src, OutD out,
                                                      const uint32_t *__restrict__ in, const uint32_t *in_n,
                                                      uint32_t *grab, PassQ q) {
@@ -411,13 +432,21 @@ __global__ void __launch_bounds__(256) k_trace_queue(DevTree t, CamD cam, RaySrc
             F3d o, d;
             ray_of(cam, src, idx, o, d);
             HitOut h;
-            if (get_by_ray<COUNT, BD>(t, occ_tab, o, d, h, q.budget))
-                store(t, out, idx, o, h);
-            else
+            if (!get_by_ray<COUNT, BD>(t, occ_tab, o, d, h, q.budget))
                 q.flags[idx] = 1;
+            else if (SHADOW)
+                store_shadow(out, idx, h);
+            else
+                store(t, out, idx, o, h);
         }
     }
 }
+
+// Hit pixels of a previous trace (value != VHX_EMPTY): the shadow pass's first queue.
+struct IsHit {
+    const uint32_t *value;
+    __device__ bool operator()(uint32_t i) const { return value[i] != VHX_EMPTY; }
+};
 
 __global__ void __launch_bounds__(256) k_untile_rgba(const uint32_t *__restrict__ gathered, uint32_t ranks,
                                                      uint32_t tiles_per_rank, uint32_t T, uint32_t tiles_x,
@@ -581,24 +610,30 @@ static int finish_out(vhx_ctx *c, HostOut &ho) {
 
 // Multi-pass plumbing: allocates flags, queues, counters and compaction scratch for `nout` rays (may synchronise;
 // called before the trace is timed); returns the number of passes to run.
-static int prepare_passes(vhx_ctx *c, uint64_t nout, uint32_t &npass) {
+static int prepare_passes(vhx_ctx *c, uint64_t nout, uint32_t &npass, bool shadow = false) {
     npass = nout < 0x7FFFFFFFull ? c->npass : 1u;
-    if (npass < 2) return VHX_OK;
+    if (npass < 2 && !shadow) return VHX_OK;
     int rc = ensure(c, c->queue[0], nout * 4);
-    if (!rc && npass > 2) rc = ensure(c, c->queue[1], nout * 4);
-    if (!rc) rc = ensure(c, c->qctl, 8 * sizeof(uint32_t));
+    if (!rc && (npass > 2 || shadow)) rc = ensure(c, c->queue[1], nout * 4);
+    if (!rc) rc = ensure(c, c->qctl, 16 * sizeof(uint32_t));
     if (!rc) rc = ensure(c, c->flags, nout);
     if (rc) return rc;
     size_t tmp = 0;
     VHX_HIP(c, rocprim::select(nullptr, tmp, rocprim::counting_iterator<uint32_t>(0u), (const uint8_t *)nullptr,
                                (uint32_t *)nullptr, (uint32_t *)nullptr, (size_t)nout, c->stream));
+    if (shadow) {
+        size_t tmp2 = 0;
+        VHX_HIP(c, rocprim::select(nullptr, tmp2, rocprim::counting_iterator<uint32_t>(0u), (uint32_t *)nullptr,
+                                   (uint32_t *)nullptr, (size_t)nout, IsHit{nullptr}, c->stream));
+        tmp = tmp2 > tmp ? tmp2 : tmp;
+    }
     return ensure(c, c->seltmp, tmp);
 }
 
 // Stream-ordered per-trace reset of the pass state (inside the timed region).
-static int reset_passes(vhx_ctx *c, uint64_t nout, uint32_t npass) {
-    if (npass < 2) return VHX_OK;
-    VHX_HIP(c, hipMemsetAsync(c->qctl.ptr, 0, 8 * sizeof(uint32_t), c->stream));
+static int reset_passes(vhx_ctx *c, uint64_t nout, uint32_t npass, bool shadow = false) {
+    if (npass < 2 && !shadow) return VHX_OK;
+    VHX_HIP(c, hipMemsetAsync(c->qctl.ptr, 0, 16 * sizeof(uint32_t), c->stream));
     VHX_HIP(c, hipMemsetAsync(c->flags.ptr, 0, nout, c->stream));
     return VHX_OK;
 }
@@ -623,15 +658,19 @@ static int compact_queue(vhx_ctx *c, uint32_t p, uint32_t npass, uint64_t nout) 
     return VHX_OK;
 }
 
-template <bool COUNT, int BD>
+// Queue passes first..npass-1: pass p re-traces the queue of pass p-1 (pass 0's queue, for first == 0, is the list
+// in queue[1] with its length in qctl[7]), flags what exceeds its budget, and the flags are compacted into the next
+// pass's queue.
+template <bool COUNT, int BD, bool SHADOW = false>
 static int launch_queue_passes(vhx_ctx *c, const DevTree &t, const CamD &cam, const RaySrc &src, const OutD &o,
-                               uint32_t npass, uint64_t nout) {
-    int rc = compact_queue(c, 0, npass, nout);
-    for (uint32_t p = 1; p < npass && !rc; ++p) {
-        const uint32_t *in = (const uint32_t *)c->queue[(p - 1) & 1u].ptr;
-        uint32_t *ctl = (uint32_t *)c->qctl.ptr;
-        k_trace_queue<COUNT, BD><<<c->queue_blocks, 256, 0, c->stream>>>(t, cam, src, o, in, ctl + (p - 1),
-                                                                         ctl + 4 + p, pass_q(c, p, npass));
+                               uint32_t first, uint32_t npass, uint64_t nout) {
+    uint32_t *ctl = (uint32_t *)c->qctl.ptr;
+    int rc = first > 0 ? compact_queue(c, first - 1, npass, nout) : VHX_OK;
+    for (uint32_t p = first; p < npass && !rc; ++p) {
+        const uint32_t *in = (const uint32_t *)c->queue[(p - 1) & 1u].ptr;  // p = 0: queue[1]
+        const uint32_t *in_n = p > 0 ? ctl + (p - 1) : ctl + 7;
+        k_trace_queue<COUNT, BD, SHADOW><<<c->queue_blocks, 256, 0, c->stream>>>(t, cam, src, o, in, in_n,
+                                                                                 ctl + 8 + p, pass_q(c, p, npass));
         rc = compact_queue(c, p, npass, nout);
     }
     return rc;
@@ -920,11 +959,11 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
             if (count) {
                 k_trace_primary<true, BD><<<(unsigned)nblocks, 256, 0, c->stream>>>(
                     t, cd, ho.dev, T, tiles_x, tile_start, tile_stride, layout, bpx, bpt, q0);
-                qrc = launch_queue_passes<true, BD>(c, t, cd, src, ho.dev, npass, nout);
+                qrc = launch_queue_passes<true, BD>(c, t, cd, src, ho.dev, 1, npass, nout);
             } else {
                 k_trace_primary<false, BD><<<(unsigned)nblocks, 256, 0, c->stream>>>(
                     t, cd, ho.dev, T, tiles_x, tile_start, tile_stride, layout, bpx, bpt, q0);
-                qrc = launch_queue_passes<false, BD>(c, t, cd, src, ho.dev, npass, nout);
+                qrc = launch_queue_passes<false, BD>(c, t, cd, src, ho.dev, 1, npass, nout);
             }
         } else if (count) {
             k_trace_persistent<true, BD, TASK><<<pblocks, 256, 0, c->stream>>>(t, cd, ho.dev, fm);
@@ -977,10 +1016,10 @@ int vhx_trace_rays(vhx_ctx *c, const float *rays, uint64_t n, const vhx_hits *ou
         const PassQ q0 = pass_q(c, 0, npass);
         if (count) {
             k_trace_rays<true, BD><<<nb, 256, 0, c->stream>>>(t, drays, n, ho.dev, q0);
-            qrc = launch_queue_passes<true, BD>(c, t, cd, src, ho.dev, npass, n);
+            qrc = launch_queue_passes<true, BD>(c, t, cd, src, ho.dev, 1, npass, n);
         } else {
             k_trace_rays<false, BD><<<nb, 256, 0, c->stream>>>(t, drays, n, ho.dev, q0);
-            qrc = launch_queue_passes<false, BD>(c, t, cd, src, ho.dev, npass, n);
+            qrc = launch_queue_passes<false, BD>(c, t, cd, src, ho.dev, 1, npass, n);
         }
     };
     if (!dispatch_bd(c->desc.brick_dim, launch)) return fail(c, VHX_E_INVALID_ARG, "unsupported brick_dim");
@@ -989,6 +1028,55 @@ int vhx_trace_rays(vhx_ctx *c, const float *rays, uint64_t n, const vhx_hits *ou
     VHX_HIP(c, hipEventRecord(c->ev1, c->stream));
     c->timed = true;
     return finish_out(c, ho);
+}
+
+int vhx_trace_shadows(vhx_ctx *c, const float light[3], uint64_t n, const uint32_t *value, const float *impact,
+                      const float *normal, uint32_t *shadowed, uint32_t *rgba, uint32_t *bytes) {
+    if (!c || !light || (n && (!value || !impact || !normal || !shadowed))) return VHX_E_INVALID_ARG;
+    if (!c->uploaded) return fail(c, VHX_E_STATE, "vhx_trace_shadows before vhx_upload_tree");
+    if (n == 0) return VHX_OK;
+    if (n >= 0x7FFFFFFFull) return fail(c, VHX_E_INVALID_ARG, "too many rays");
+    VHX_HIP(c, hipSetDevice(c->device));
+    uint32_t npass = 1;
+    int rc = prepare_passes(c, n, npass, true);
+    if (rc) return rc;
+    const DevTree t = dev_tree(c);
+    RaySrc src{};
+    src.kind = 3u;
+    src.impact = impact;
+    src.normal = normal;
+    src.lx = light[0];
+    src.ly = light[1];
+    src.lz = light[2];
+    OutD so{};
+    so.value = shadowed;
+    so.rgba = rgba;
+    so.bytes = bytes;
+    CamD cd{};
+    VHX_HIP(c, hipEventRecord(c->ev0, c->stream));
+    rc = reset_passes(c, n, npass, true);
+    if (rc) return rc;
+    VHX_HIP(c, hipMemsetAsync(shadowed, 0, n * 4, c->stream));
+    if (bytes) VHX_HIP(c, hipMemsetAsync(bytes, 0, n * 4, c->stream));
+    // wave-dense secondary rays: the hit pixels, in frame order, are pass 0's queue
+    size_t tmp = c->seltmp.bytes;
+    VHX_HIP(c, rocprim::select(c->seltmp.ptr, tmp, rocprim::counting_iterator<uint32_t>(0u),
+                               (uint32_t *)c->queue[1].ptr, (uint32_t *)c->qctl.ptr + 7, (size_t)n, IsHit{value},
+                               c->stream));
+    int qrc = VHX_OK;
+    auto launch = [&](auto bd_tag) {
+        constexpr int BD = decltype(bd_tag)::value;
+        if (bytes)
+            qrc = launch_queue_passes<true, BD, true>(c, t, cd, src, so, 0, npass, n);
+        else
+            qrc = launch_queue_passes<false, BD, true>(c, t, cd, src, so, 0, npass, n);
+    };
+    if (!dispatch_bd(c->desc.brick_dim, launch)) return fail(c, VHX_E_INVALID_ARG, "unsupported brick_dim");
+    if (qrc) return qrc;
+    VHX_HIP(c, hipGetLastError());
+    VHX_HIP(c, hipEventRecord(c->ev1, c->stream));
+    c->timed = true;
+    return VHX_OK;
 }
 
 int vhx_untile_rgba(vhx_ctx *c, const uint32_t *gathered, uint32_t ranks, uint32_t tiles_per_rank, uint32_t T,

@@ -269,6 +269,26 @@ class Raytracer:
                                               ctypes.byref(hs), 0))
         return res
 
+    def trace_shadows(self, light, hits, shadowed=None, darken=True, count_bytes=False):
+        """Hard shadow rays (vhx_trace_shadows) for the device-resident hit records `hits` of a previous trace
+        (dict of torch tensors with value, impact, normal and optionally rgba). Returns a dict with the int32
+        `shadowed` flags (and `bytes`); hits["rgba"] is darkened in place when darken."""
+        import torch
+        n = hits["value"].numel()
+        if shadowed is None:
+            shadowed = torch.empty(n, dtype=torch.int32, device=hits["value"].device)
+        res = {"shadowed": shadowed}
+        if count_bytes:
+            res["bytes"] = torch.empty(n, dtype=torch.int32, device=hits["value"].device)
+        lt = (ctypes.c_float * 3)(*[float(v) for v in light])
+        rgba = hits.get("rgba") if darken else None
+        self._check(N.lib().vhx_trace_shadows(
+            self._h, lt, n, ctypes.c_void_p(_ptr(hits["value"])), ctypes.c_void_p(_ptr(hits["impact"])),
+            ctypes.c_void_p(_ptr(hits["normal"])), ctypes.c_void_p(_ptr(shadowed)),
+            ctypes.c_void_p(None if rgba is None else _ptr(rgba)),
+            ctypes.c_void_p(_ptr(res["bytes"]) if count_bytes else None)))
+        return res
+
     def untile_rgba(self, gathered_dev_ptr, ranks, tiles_per_rank, tile_size, width, height, fb_dev_ptr):
         self._check(N.lib().vhx_untile_rgba(self._h, ctypes.c_void_p(gathered_dev_ptr), ranks, tiles_per_rank,
                                             tile_size, width, height, ctypes.c_void_p(fb_dev_ptr), 1))
