@@ -42,6 +42,8 @@ def parse():
     p.add_argument("--height", type=int, default=2160)
     p.add_argument("--scene", type=int, default=1, help="VHX_SCENE_* (1 = lattice+cube scene S)")
     p.add_argument("--tile", type=int, default=64)
+    p.add_argument("--shadows", action="store_true",
+                   help="config 5: each step = primary frame + one hard-shadow ray per hit toward (S,S,S)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-roofline", action="store_true")
     return p.parse_args()
@@ -115,6 +117,13 @@ def main():
     rgba = torch.zeros(n_out, dtype=torch.int32, device=dev)
     depth = torch.zeros(n_out, dtype=torch.float32, device=dev)
     out = {"rgba": rgba, "depth": depth}
+    light = (float(args.size),) * 3  # ambient_light_position, src/raytracing/bevy/view.rs:81-85
+    if args.shadows:
+        # -1 = VHX_EMPTY: tile padding past the frame edge is never written and casts no shadow ray
+        out.update(value=torch.full((n_out,), -1, dtype=torch.int32, device=dev),
+                   impact=torch.zeros((n_out, 3), dtype=torch.float32, device=dev),
+                   normal=torch.zeros((n_out, 3), dtype=torch.float32, device=dev))
+        shadowed = torch.zeros(n_out, dtype=torch.int32, device=dev)
     if world > 1 and rank == 0:
         gathered = [torch.zeros(n_out, dtype=torch.int32, device=dev) for _ in range(world)]
         framebuffer = torch.zeros(W * H, dtype=torch.int32, device=dev)
@@ -126,6 +135,8 @@ def main():
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
         rt.trace_primary(cam, out=out, **trace_kw)
+        if args.shadows:
+            rt.trace_shadows(light, out, shadowed=shadowed)
         if timed:
             e1.record(stream)
             ev.append((e0, e1))
@@ -157,12 +168,21 @@ def main():
 
     workload = f"primary {W}x{H} S{args.scene} {args.size}^3 bd{args.brick_dim} ranks{world}"
     total_rays = W * H
+    n_shadow = 0
+    if args.shadows:
+        workload += " +shadows"
+        n_shadow = int((out["value"] != -1).sum().item())  # shadow rays this rank traced per frame
+        if world > 1:
+            ts = torch.tensor([n_shadow], dtype=torch.int64, device=dev)
+            dist.all_reduce(ts)
+            n_shadow = int(ts.item())
+        total_rays += n_shadow
     mrays = total_rays * args.steps / elapsed / 1e6
     ms_per_step = elapsed * 1e3 / args.steps
 
     # ---- roofline: algorithmic bytes of this rank's launch (instrumented kernel, untimed) -------------------------
     roof = None
-    if not args.no_roofline:
+    if not args.no_roofline and not args.shadows:
         res = rt.trace_primary(cam, fields=(), count_bytes=True, **trace_kw)
         tree_bytes = float(res["bytes"].astype(np.float64).sum())
         my_rays = W * H if world == 1 else M.rank_rays(W, H, T, rank, world)
@@ -181,7 +201,7 @@ def main():
 
     # ---- CPU baseline: the oracle (reference semantics) on the host cores, rank 0 at N=1 only ----------------------
     cpu = None
-    if world == 1 and rank == 0 and not args.no_cpu_baseline:
+    if world == 1 and rank == 0 and not args.no_cpu_baseline and not args.shadows:
         from tests._oracle import Oracle
         orc = Oracle()
         cores = max(1, min(16, len(os.sched_getaffinity(0))))
@@ -193,8 +213,11 @@ def main():
                "sample": f"full {W}x{H} frame, same tree and camera, OpenMP dynamic over pixels, {cpu_s:.2f} s"}
 
     if rank == 0:
+        metric = BASELINE["metric"]
+        if args.shadows:
+            metric = "primary + hard-shadow Mrays/s (BASELINE config 5)"
         line = {
-            "metric": BASELINE["metric"], "value": round(mrays, 3), "unit": "Mrays/s", "n_gpus": world,
+            "metric": metric, "value": round(mrays, 3), "unit": "Mrays/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic",
@@ -202,6 +225,7 @@ def main():
                                    f"brick_dim {args.brick_dim}, glass camera"
                                    + (f", {W * H // world} rays per rank" if world > 1 else ""),
                        "workload_key": workload,
+                       "shadow_rays_per_frame": n_shadow if args.shadows else None,
                        "tree_size": args.size, "brick_dim": args.brick_dim, "width": W, "height": H,
                        "scene": args.scene, "tile": T if world > 1 else None,
                        "parallelism": f"screen-tile split x{world} + RCCL gather" if world > 1 else "single GPU",

@@ -175,7 +175,7 @@ int vhx_trace_primary(vhx_ctx *ctx, const vhx_camera *cam, uint32_t tile_size, u
                       uint32_t tile_stride, uint32_t layout, const vhx_hits *out, int on_device);
 /* Traces n explicit rays; rays = 6 f32 per ray (origin xyz, direction xyz), host or device per on_device. */
 int vhx_trace_rays(vhx_ctx *ctx, const float *rays, uint64_t n, const vhx_hits *out, int on_device);
-/* Hard shadows (BASELINE config 5; the reference has no shadow rays — semantics defined in DESIGN.md §10): for
+/* Hard shadows (BASELINE config 5; the reference has no shadow rays — semantics defined in DESIGN.md §9): for
  * every ray i < n of a previous trace with a hit (value[i] != VHX_EMPTY), one shadow ray from
  * impact[i] + normal[i] * 1e-3 toward `light` (e.g. the reference's ambient_light_position = (size, size, size),
  * src/raytracing/bevy/view.rs:81-85) is traced with get_by_ray semantics; shadowed[i] = 1 if it hits a voxel, else 0

@@ -545,7 +545,7 @@ int vhx_oracle_trace_primary(const vhx_tree_desc *t, const vhx_camera *cam, uint
     return VHX_OK;
 }
 
-/* Hard shadows (BASELINE config 5; no reference counterpart — DESIGN.md §10 defines them): for every hit record i
+/* Hard shadows (BASELINE config 5; no reference counterpart — DESIGN.md §9 defines them): for every hit record i
  * (value[i] != 0xFFFFFFFF) one shadow ray from impact + normal * 1e-3 (multiply, then add) toward `light`, direction
  * normalised like V3c::normalized; shadowed[i] = hit ? 1 : 0; rgba (optional) gets rgb >> 1 where shadowed; bytes
  * (optional) the shadow ray's algorithmic bytes. */

@@ -322,7 +322,7 @@ struct RaySrc {
     float lx, ly, lz;               // kind 3: light position
 };
 
-// Hard-shadow ray of hit record idx (BASELINE config 5; semantics in DESIGN.md §10): from impact + normal * 1e-3
+// Hard-shadow ray of hit record idx (BASELINE config 5; semantics in DESIGN.md §9): from impact + normal * 1e-3
 // toward the light, direction normalised like V3c::normalized (src/spatial/math/vector.rs).
 __device__ __forceinline__ void shadow_ray(const RaySrc &src, uint32_t idx, F3d &o, F3d &d) {
     const float *ip = src.impact + 3ull * idx, *np = src.normal + 3ull * idx;
