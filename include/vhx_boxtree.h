@@ -12,6 +12,7 @@
  *   vhx_boxtree_simplify       <- BoxTree::simplify(ROOT, recursive) (src/boxtree/update/mod.rs:617-867)
  *   vhx_boxtree_flatten        <- BoxTreeGPUDataHandler::add_node/add_brick with every node resident
  *                                 (src/raytracing/bevy/streaming/cache.rs:226-455, 608-716)
+ *   vhx_boxtree_load_vox       <- BoxTree::load_vox_file  (src/convert/magicavoxel.rs:234-374)
  *   vhx_scene_build            <- bulk builder producing exactly the flattened tree that inserting a procedural
  *                                 scene voxel by voxel (x, then y, then z loops) would produce
  *
@@ -31,6 +32,9 @@ extern "C" {
 #define VHX_E_TREE_INVALID_BRICK_DIMENSION (-11)
 #define VHX_E_TREE_INVALID_STRUCTURE (-12)
 #define VHX_E_TREE_INVALID_POSITION (-13)
+/* .vox import */
+#define VHX_E_VOX_FORMAT (-14) /* not a .vox file the importer supports (see vhx_boxtree_load_vox) */
+#define VHX_E_VOX_IO (-15)     /* the file could not be read */
 
 /* BoxTreeEntry kinds (src/boxtree/types.rs:25-37) */
 #define VHX_ENTRY_EMPTY 0u
@@ -75,6 +79,19 @@ int vhx_scene_build(uint32_t scene, uint32_t size, uint32_t brick_dim, uint64_t 
 /* Fills *desc with pointers into the flat object (valid until vhx_flat_free). */
 int vhx_flat_desc(const vhx_flat *flat, vhx_tree_desc *desc);
 void vhx_flat_free(vhx_flat *flat);
+
+/* MagicaVoxel .vox import — BoxTree::<u32>::load_vox_file(filename, brick_dimension) (src/convert/magicavoxel.rs:
+ * 234-374): walks the scene graph at frame 0 (translations "_t", rotations "_r" composed like the reference, which
+ * resets to identity where "_r" is absent), sizes the tree with model_size_to_tree_size (magicavoxel.rs:55-60),
+ * converts Rz-up to Ly-up and inserts every voxel as BoxTreeEntry::Visual(palette colour), then simplifies the tree
+ * recursively when auto-simplify is on (the default). The .vox reader is restated from the file format (the
+ * reference's dot_vox 5.1.1 is not vendored): files without an RGBA palette or without a scene graph are rejected
+ * with VHX_E_VOX_FORMAT. Voxels landing outside the tree return VHX_E_TREE_INVALID_POSITION (the reference panics). */
+int vhx_boxtree_load_vox(const char *path, uint32_t brick_dim, vhx_boxtree **out);
+int vhx_boxtree_load_vox_memory(const uint8_t *data, uint64_t size, uint32_t brick_dim, vhx_boxtree **out);
+/* helpers of the import, exported for tests: model_size_to_tree_size and parse_rotation_matrix (row-major m[9]) */
+uint32_t vhx_vox_tree_size(int32_t sx, int32_t sy, int32_t sz, uint32_t brick_dim);
+int vhx_vox_rotation(uint8_t b, int32_t m[9]);
 
 #ifdef __cplusplus
 }

@@ -26,6 +26,8 @@ VHX_E_TREE_INVALID_SIZE = -10
 VHX_E_TREE_INVALID_BRICK_DIMENSION = -11
 VHX_E_TREE_INVALID_STRUCTURE = -12
 VHX_E_TREE_INVALID_POSITION = -13
+VHX_E_VOX_FORMAT = -14
+VHX_E_VOX_IO = -15
 
 VHX_EMPTY = 0xFFFFFFFF
 VHX_SOLID_BIT = 0x80000000
@@ -95,6 +97,10 @@ SIGNATURES = [
     ("vhx_boxtree_info", c_int, [c_void_p, P(c_u32 * 5)]),
     ("vhx_scene_insert", c_int, [c_void_p, c_u32, c_u64]),
     ("vhx_boxtree_flatten", c_int, [c_void_p, P(c_void_p)]),
+    ("vhx_boxtree_load_vox", c_int, [ctypes.c_char_p, c_u32, P(c_void_p)]),
+    ("vhx_boxtree_load_vox_memory", c_int, [c_void_p, c_u64, c_u32, P(c_void_p)]),
+    ("vhx_vox_tree_size", c_u32, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, c_u32]),
+    ("vhx_vox_rotation", c_int, [ctypes.c_uint8, P(ctypes.c_int32 * 9)]),
     ("vhx_scene_build", c_int, [c_u32, c_u32, c_u32, c_u64, c_int, P(c_void_p)]),
     ("vhx_flat_desc", c_int, [c_void_p, P(TreeDesc)]),
     ("vhx_flat_free", None, [c_void_p]),

@@ -232,6 +232,34 @@ class FlatTree:
         return sum(a.nbytes for a in (self.node_type, self.node_ocbits, self.node_children, self.voxels,
                                       self.solid_values, self.color_palette, self.data_palette))
 
+    @classmethod
+    def _from_handle(cls, h):
+        t = cls.__new__(cls)
+        t._h = h
+        t._version = 0
+        t._flat = None
+        t._flat_version = -1
+        return t
+
+    @classmethod
+    def load_vox_file(cls, filename, brick_dimension):
+        """BoxTree::load_vox_file (src/convert/magicavoxel.rs:234-265): MagicaVoxel .vox import (C++,
+        voxelhex_amd/csrc/vox.cpp). Raises VhxError for unreadable / unsupported files, InvalidPosition for voxels
+        outside the tree (the reference panics)."""
+        h = ctypes.c_void_p()
+        _tree_check(N.lib().vhx_boxtree_load_vox(str(filename).encode(), brick_dimension, ctypes.byref(h)),
+                    f"{filename}")
+        return cls._from_handle(h)
+
+    @classmethod
+    def load_vox_bytes(cls, data, brick_dimension):
+        """load_vox_file over an in-memory .vox image."""
+        buf = (ctypes.c_uint8 * len(data)).from_buffer_copy(bytes(data))
+        h = ctypes.c_void_p()
+        _tree_check(N.lib().vhx_boxtree_load_vox_memory(buf, len(data), brick_dimension, ctypes.byref(h)),
+                    "vox bytes")
+        return cls._from_handle(h)
+
     def __del__(self):
         if getattr(self, "_h", None) and self._h.value:
             N.lib().vhx_flat_free(self._h)
@@ -259,6 +287,34 @@ class BoxTree:
         self._version = 0
         self._flat = None
         self._flat_version = -1
+
+    @classmethod
+    def _from_handle(cls, h):
+        t = cls.__new__(cls)
+        t._h = h
+        t._version = 0
+        t._flat = None
+        t._flat_version = -1
+        return t
+
+    @classmethod
+    def load_vox_file(cls, filename, brick_dimension):
+        """BoxTree::load_vox_file (src/convert/magicavoxel.rs:234-265): MagicaVoxel .vox import (C++,
+        voxelhex_amd/csrc/vox.cpp). Raises VhxError for unreadable / unsupported files, InvalidPosition for voxels
+        outside the tree (the reference panics)."""
+        h = ctypes.c_void_p()
+        _tree_check(N.lib().vhx_boxtree_load_vox(str(filename).encode(), brick_dimension, ctypes.byref(h)),
+                    f"{filename}")
+        return cls._from_handle(h)
+
+    @classmethod
+    def load_vox_bytes(cls, data, brick_dimension):
+        """load_vox_file over an in-memory .vox image."""
+        buf = (ctypes.c_uint8 * len(data)).from_buffer_copy(bytes(data))
+        h = ctypes.c_void_p()
+        _tree_check(N.lib().vhx_boxtree_load_vox_memory(buf, len(data), brick_dimension, ctypes.byref(h)),
+                    "vox bytes")
+        return cls._from_handle(h)
 
     def __del__(self):
         if getattr(self, "_h", None) and self._h.value:

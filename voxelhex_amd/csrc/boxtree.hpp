@@ -140,3 +140,8 @@ Cube child_bounds_for(const Cube &c, uint8_t s);
 bool rust_log_is_integral(float x, float base);
 
 }  // namespace vhx
+
+// opaque handle of the C ABI (include/vhx_boxtree.h)
+struct vhx_boxtree {
+    vhx::BoxTree *tree;
+};

@@ -28,10 +28,6 @@
 
 using namespace vhx;
 
-struct vhx_boxtree {
-    BoxTree *tree;
-};
-
 struct vhx_flat {
     uint32_t size = 0, brick_dim = 0;
     std::vector<uint32_t> node_type;
