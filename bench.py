@@ -41,6 +41,8 @@ def parse():
     p.add_argument("--width", type=int, default=3840, help="per-rank-equivalent frame width (N=1 frame)")
     p.add_argument("--height", type=int, default=2160)
     p.add_argument("--scene", type=int, default=1, help="VHX_SCENE_* (1 = lattice+cube scene S)")
+    p.add_argument("--vox", default=None, help="trace a MagicaVoxel model instead (BoxTree::load_vox_file, bd = "
+                                              "--brick-dim; tree size from the model)")
     p.add_argument("--tile", type=int, default=64)
     p.add_argument("--shadows", action="store_true",
                    help="config 5: each step = primary frame + one hard-shadow ray per hit toward (S,S,S)")
@@ -91,7 +93,11 @@ def main():
     dev = torch.device("cuda", local)
 
     t0 = time.time()
-    flat = vhx.FlatTree.build_scene(args.scene, args.size, args.brick_dim, threads=min(16, os.cpu_count() or 1))
+    if args.vox:
+        flat = vhx.BoxTree.load_vox_file(args.vox, args.brick_dim).flatten()
+        args.size = int(flat.desc.boxtree_size)
+    else:
+        flat = vhx.FlatTree.build_scene(args.scene, args.size, args.brick_dim, threads=min(16, os.cpu_count() or 1))
     build_s = time.time() - t0
     rt = vhx.Raytracer(local)
     # one dedicated (non-null) stream shared by libvhx and torch: the kernel, the torch events that time it and
@@ -166,7 +172,8 @@ def main():
         elapsed = float(tt.item())
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
 
-    workload = f"primary {W}x{H} S{args.scene} {args.size}^3 bd{args.brick_dim} ranks{world}"
+    scene_tag = f"vox:{os.path.basename(args.vox)}" if args.vox else f"S{args.scene}"
+    workload = f"primary {W}x{H} {scene_tag} {args.size}^3 bd{args.brick_dim} ranks{world}"
     total_rays = W * H
     n_shadow = 0
     if args.shadows:
@@ -220,9 +227,11 @@ def main():
             "metric": metric, "value": round(mrays, 3), "unit": "Mrays/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic",
-            "config": {"workload": f"primary rays {W}x{H}, {args.size}^3 procedural scene S (lattice+cube), "
-                                   f"brick_dim {args.brick_dim}, glass camera"
+            "data": "model file" if args.vox else "synthetic",
+            "config": {"workload": f"primary rays {W}x{H}, {args.size}^3 "
+                                   + (f".vox model {os.path.basename(args.vox)}" if args.vox
+                                      else "procedural scene S (lattice+cube)")
+                                   + f", brick_dim {args.brick_dim}, glass camera"
                                    + (f", {W * H // world} rays per rank" if world > 1 else ""),
                        "workload_key": workload,
                        "shadow_rays_per_frame": n_shadow if args.shadows else None,

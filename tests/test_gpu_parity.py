@@ -296,3 +296,26 @@ def test_shadow_rays_vs_oracle(gpu, oracle, scene, size, bd, w, h, budgets):
             assert 0 < sh[hit].sum() < hit.sum(), "expected both lit and shadowed hits"
     finally:
         gpu.set_pass_budgets(DEFAULT_BUDGETS)
+
+
+def test_vox_model_frame_vs_oracle(gpu, oracle):
+    """A tree imported from a .vox file (vhx_boxtree_load_vox; written by tests/test_vox.py's writer with rotated,
+    translated models) traced on the GPU equals the oracle, incl. the simplified (Solid/UniformLeaf) parts."""
+    from tests.test_vox import PALETTE, write_vox
+    big = ((40, 24, 32), [(x, y, z, 1 + (x // 8 + (y // 8) * 5 + (z // 8) * 25) % 250 if x < 32 else 1 + (x * 7 + y) % 250)
+                          for x in range(40) for y in range(24) for z in range(32)
+                          if (x // 8 + y // 8 + z // 8) % 2 == 0 or x > 33])
+    rod = ((3, 30, 3), [(x, y, z, 9) for x in range(3) for y in range(30) for z in range(3)])
+    scene = [("T", {}, 1, [{}]), ("G", {}, [2, 4]),
+             ("T", {}, 3, [{"_t": "0 0 0", "_r": "17"}]), ("S", {}, [(0, {})]),
+             ("T", {}, 5, [{"_t": "30 -12 20"}]), ("S", {}, [(1, {})])]
+    t = vhx.BoxTree.load_vox_bytes(write_vox([big, rod], PALETTE, scene), 4)
+    flat = t.flatten()
+    assert (flat.node_type == N.VHX_NODE_UNIFORM_LEAF).any() or flat.solid_values.size > 0
+    gpu.upload(flat)
+    S = float(flat.desc.boxtree_size)
+    cam = vhx.glass_camera(int(S), 192, 128, target=(S / 4, S / 4, S / 4))
+    got = gpu.trace_primary(cam, count_bytes=True)
+    ref = oracle.trace_primary(flat, cam, 0, 0, 192, 128, count_bytes=True)
+    assert_same(got, ref, "vox frame")
+    assert (got["value"] != N.VHX_EMPTY).sum() > 500
