@@ -66,6 +66,10 @@ int vhx_boxtree_update(vhx_boxtree *tree, uint32_t x, uint32_t y, uint32_t z, ui
 int vhx_boxtree_get(const vhx_boxtree *tree, uint32_t x, uint32_t y, uint32_t z, uint32_t *kind, uint32_t *albedo,
                     uint32_t *data);
 int vhx_boxtree_simplify(vhx_boxtree *tree, int recursive);
+/* The deepest node containing a position (BoxTree::get_node_internal from the root, src/boxtree/iterate.rs:293-343):
+ * its pool key, content (0 Nothing, 1 Internal, 2 Leaf, 3 UniformLeaf), occupied bits and occlusion bits. */
+int vhx_boxtree_node_info(const vhx_boxtree *tree, float x, float y, float z, uint64_t *key, uint32_t *content,
+                          uint64_t *occupied_bits, uint32_t *occlusion_bits);
 /* size, brick_dim, node count (pool length), color and data palette sizes */
 int vhx_boxtree_info(const vhx_boxtree *tree, uint32_t info[5]);
 /* Runs the reference insert loop (x outer, z inner) of a procedural scene on `tree` (for cross-checking the bulk

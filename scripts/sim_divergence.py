@@ -118,3 +118,39 @@ def breakdown(lanes):
             if any(a[kk] for a in act):
                 comp[kk] += C[kk]
     return comp, K
+
+
+def tokens(seq):
+    """Per-trip tokens of a one-step-per-trip machine: N+outcome (O/U/R folded into the node trip), P, B, A."""
+    out = []
+    for ch in seq:
+        if ch == 'N':
+            out.append(['N'])
+        elif ch in "OUR":
+            if out and out[-1][0] == 'N':
+                out[-1].append(ch)
+            else:
+                out.append(['N', ch])
+        else:
+            out.append([ch])
+    return out
+
+
+def ifif_cost(lanes, merge_ba=False):
+    toks = [tokens(s) for s in lanes]
+    T = max(len(t) for t in toks)
+    total = 0
+    for k in range(T):
+        act = [t[k] for t in toks if k < len(t)]
+        kinds = set(a[0] for a in act)
+        c = 0
+        if 'N' in kinds:
+            c += C['N'] + sum(C[x] for x in "OUR" if any(x in a for a in act))
+        if 'P' in kinds:
+            c += C['P']
+        if merge_ba and ('B' in kinds or 'A' in kinds):
+            c += C['BA']
+        else:
+            c += (C['B'] if 'B' in kinds else 0) + (C['A'] if 'A' in kinds else 0)
+        total += c
+    return total

@@ -364,6 +364,15 @@ class BoxTree:
         N.check(N.lib().vhx_boxtree_simplify(self._h, int(recursive)))
         self._version += 1
 
+    def node_info(self, position):
+        """The deepest node containing `position` (get_node_internal): key, content, occupied and occlusion bits."""
+        key, content, occ, occl = ctypes.c_uint64(), ctypes.c_uint32(), ctypes.c_uint64(), ctypes.c_uint32()
+        _tree_check(N.lib().vhx_boxtree_node_info(self._h, *[float(v) for v in position], ctypes.byref(key),
+                                                  ctypes.byref(content), ctypes.byref(occ), ctypes.byref(occl)),
+                    f"{position}")
+        return {"key": key.value, "content": ("Nothing", "Internal", "Leaf", "UniformLeaf")[content.value],
+                "occupied_bits": occ.value, "occlusion_bits": occl.value}
+
     def info(self):
         a = (ctypes.c_uint32 * 5)()
         N.check(N.lib().vhx_boxtree_info(self._h, ctypes.byref(a)))

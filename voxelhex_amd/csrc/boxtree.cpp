@@ -93,8 +93,8 @@ static inline bool pix_data_is_some(uint32_t v) { return pix_data_index(v) != 0x
 
 // execute_for_relevant_sectants, src/boxtree/iterate.rs:40-121
 using SectantFn = std::function<void(U3, U3, uint8_t, const Cube &)>;
-static std::array<size_t, 3> execute_for_relevant_sectants(const Cube &nb, U3 position_, uint32_t update_size_,
-                                                           const SectantFn &fun) {
+std::array<size_t, 3> execute_for_relevant_sectants(const Cube &nb, U3 position_, uint32_t update_size_,
+                                                    const SectantFn &fun) {
     if ((float)position_.x > nb.min.x + nb.size || (float)position_.y > nb.min.y + nb.size ||
         (float)position_.z > nb.min.z + nb.size)
         return {0, 0, 0};
@@ -682,8 +682,75 @@ bool BoxTree::leaf_update(bool overwrite, size_t key, const Cube &node_bounds, c
     return leaf_update(overwrite, key, node_bounds, target_bounds, tcs, position, size, tc);
 }
 
-void BoxTree::post_process_node_insert(size_t key, const Cube &nb, const std::array<size_t, 3> &aus, U3 pos,
+uint8_t step_sectant_i(uint8_t s, int dx, int dy, int dz) {
+    const int x = (s & 3) + dx, y = ((s >> 2) & 3) + dy, z = (s >> 4) + dz;
+    const int out = (x < 0 || x > 3 || y < 0 || y > 3 || z < 0 || z > 3) ? 64 : 0;
+    return (uint8_t)(out + (x & 3) + ((y & 3) << 2) + ((z & 3) << 4));
+}
+
+// get_sibling_by_stack, src/boxtree/iterate.rs:186-290 (direction given as unit integer steps)
+bool BoxTree::get_sibling_by_stack(int dx, int dy, int dz, const std::vector<std::pair<size_t, uint8_t>> &ns_in,
+                                   size_t &sibling, uint8_t &sibling_sectant) const {
+    std::vector<std::pair<size_t, uint8_t>> ns = ns_in;
+    uint8_t current = ns.back().second;
+    uint8_t next = step_sectant_i(current, dx, dy, dz);
+    std::vector<uint8_t> mirror;  // front = mirror[0]
+    bool uniform_sibling = false;
+    uint8_t uniform_sibling_sectant = 0;
+    if (!ns.empty() && nodes.get(ns.back().first).content == Content::UniformLeaf) {
+        uint8_t ts = ns.back().second;
+        ns.pop_back();
+        while (ts < kChildren) ts = step_sectant_i(ts, dx, dy, dz);
+        uniform_sibling = true;
+        uniform_sibling_sectant = (uint8_t)(ts - kChildren);
+        if (!ns.empty()) next = step_sectant_i(ns.back().second, dx, dy, dz);
+    }
+    while (!ns.empty() && next >= kChildren) {
+        mirror.insert(mirror.begin(), (uint8_t)(next - kChildren));
+        const auto parent = ns.back();
+        ns.pop_back();
+        current = parent.second;
+        next = step_sectant_i(current, dx, dy, dz);
+        if (next < kChildren) ns.push_back({parent.first, next});
+    }
+    if (ns.empty()) return false;
+    mirror.insert(mirror.begin(), next);
+    if (uniform_sibling) {
+        const size_t sn = child(ns.back().first, next);
+        if (nodes.key_is_valid(sn)) {
+            sibling = sn;
+            sibling_sectant = uniform_sibling_sectant;
+            return true;
+        }
+        return false;
+    }
+    size_t key = ns.back().first;
+    for (uint8_t ts : mirror) {
+        const size_t c = child(key, ts);
+        if (nodes.key_is_valid(c)) {
+            key = c;
+            next = ts;
+        } else if (nodes.get(key).content == Content::Leaf) {
+            sibling = key;
+            sibling_sectant = ts;
+            return true;
+        } else if (nodes.get(key).content == Content::UniformLeaf) {
+            sibling = key;
+            sibling_sectant = kChildren;
+            return true;
+        } else {
+            return false;
+        }
+    }
+    sibling = key;
+    sibling_sectant = next;
+    return true;
+}
+
+void BoxTree::post_process_node_insert(const std::vector<std::pair<size_t, uint8_t>> &node_stack, const Cube &nb,
+                                       const std::array<size_t, 3> &aus, U3 pos,
                                        uint32_t insert_size) {  // src/boxtree/update/insert.rs:411-495
+    const size_t key = node_stack.back().first;
     Node &n = nodes.get(key);
     if (n.content == Content::Nothing) {
         n.content = Content::Internal;
@@ -697,6 +764,16 @@ void BoxTree::post_process_node_insert(size_t key, const Cube &nb, const std::ar
         execute_for_relevant_sectants(nb, pos, insert_size, [&](U3, U3, uint8_t cs, const Cube &) {
             if (!node_empty_at(key, cs)) occ |= 1ull << cs;
         });
+    }
+    if (occ == ~0ull) {  // a full node occludes the facing side of each sibling (insert.rs:451-468)
+        static const int dirs[6][4] = {{-1, 0, 0, 5 /*Right*/}, {1, 0, 0, 4 /*Left*/},  {0, -1, 0, 2 /*Top*/},
+                                       {0, 1, 0, 3 /*Bottom*/}, {0, 0, -1, 1 /*Front*/}, {0, 0, 1, 0 /*Back*/}};
+        for (const auto &dv : dirs) {
+            size_t sib;
+            uint8_t ss;
+            if (get_sibling_by_stack(dv[0], dv[1], dv[2], node_stack, sib, ss))
+                nodes.get(sib).occlusion_bits |= (uint8_t)(1u << dv[3]);
+        }
     }
     nodes.get(key).occupied_bits = occ;
 }
@@ -808,11 +885,11 @@ int BoxTree::insert_at_lod_internal(bool overwrite, U3 pos_u32, uint32_t insert_
             node_stack.push_back({ck, sectant_for(cbounds, f3(std::fmax(position.x, cbounds.min.x),
                                                               std::fmax(position.y, cbounds.min.y),
                                                               std::fmax(position.z, cbounds.min.z)))});
-            post_process_node_insert(ck, cbounds, actual_update_size, pos_u32, insert_size);
+            post_process_node_insert(node_stack, cbounds, actual_update_size, pos_u32, insert_size);
             node_stack.pop_back();
         } else {
             node_stack.back().second = mbs;
-            post_process_node_insert(node_key, nbounds, actual_update_size, pos_u32, insert_size);
+            post_process_node_insert(node_stack, nbounds, actual_update_size, pos_u32, insert_size);
             node_stack.back().second = original;
         }
         if (simplifyable) simplifyable &= simplify(ck, false);
@@ -824,7 +901,7 @@ int BoxTree::insert_at_lod_internal(bool overwrite, U3 pos_u32, uint32_t insert_
             bounds_stack.pop_back();
             continue;
         }
-        post_process_node_insert(node_key, bounds_stack.back(), actual_update_size, pos_u32, insert_size);
+        post_process_node_insert(node_stack, bounds_stack.back(), actual_update_size, pos_u32, insert_size);
         if (simplifyable) simplifyable = simplify(node_key, false);
         node_stack.pop_back();
         bounds_stack.pop_back();

@@ -17,6 +17,7 @@
 #pragma once
 
 #include <array>
+#include <functional>
 #include <cstddef>
 #include <utility>
 #include <cstdint>
@@ -59,6 +60,8 @@ struct Node {
     bool has_children = false;  // NodeChildren::Children vs NoChildren
     std::array<uint32_t, kChildren> children{};
     uint64_t occupied_bits = 0;
+    uint8_t occlusion_bits = 0;  // bit CubeSides: no ray enters from that side (src/boxtree/types.rs:189-200)
+    bool is_occluded() const { return (occlusion_bits & 0x3F) == 0x3F; }  // node.rs:176-178
 };
 
 // BoxTreeEntry<u32>
@@ -105,14 +108,18 @@ class BoxTree {
     std::vector<uint32_t> data_palette;
 
     bool points_to_empty(uint32_t v) const;
+    size_t get_node_internal(size_t key, Cube &bounds, F3 position) const;
+    size_t child(size_t node_key, uint8_t sectant) const;
 
    private:
     std::unordered_map<uint32_t, size_t> color_index_, data_index_;
 
     uint32_t add_to_palette(Entry e);
     int insert_at_lod_internal(bool overwrite_if_empty, U3 pos, uint32_t insert_size, Entry e);
-    void post_process_node_insert(size_t node_key, const Cube &node_bounds, const std::array<size_t, 3> &aus,
-                                  U3 pos, uint32_t insert_size);
+    void post_process_node_insert(const std::vector<std::pair<size_t, uint8_t>> &node_stack, const Cube &node_bounds,
+                                  const std::array<size_t, 3> &aus, U3 pos, uint32_t insert_size);
+    bool get_sibling_by_stack(int dx, int dy, int dz, const std::vector<std::pair<size_t, uint8_t>> &node_stack,
+                              size_t &sibling, uint8_t &sibling_sectant) const;
     bool leaf_update(bool overwrite_if_empty, size_t node_key, const Cube &node_bounds, const Cube &target_bounds,
                      size_t target_child_sectant, U3 position, U3 size, uint32_t target_content);
     void subdivide_leaf_to_nodes(size_t node_key, size_t target_sectant);
@@ -120,9 +127,7 @@ class BoxTree {
     bool compare_nodes(size_t l, size_t r) const;
     void deallocate_children_of(size_t node_key);
     Brick try_brick_from_node(size_t node_key) const;
-    size_t child(size_t node_key, uint8_t sectant) const;
     uint32_t &child_mut(size_t node_key, size_t index);
-    size_t get_node_internal(size_t key, Cube &bounds, F3 position) const;
     uint64_t calculate_brick_occupied_bits(const std::vector<uint32_t> &brick) const;
     uint64_t calculate_occupied_bits(const Brick &b) const;
     bool brick_contains_nothing(const Brick &b) const;
@@ -138,6 +143,11 @@ const float *sectant_offset(uint32_t s);
 uint8_t offset_sectant(F3 off, float size);
 Cube child_bounds_for(const Cube &c, uint8_t s);
 bool rust_log_is_integral(float x, float base);
+// step_sectant (src/spatial/mod.rs:23-26) for integer steps in {-1, 0, 1}: >= 64 means out of the node
+uint8_t step_sectant_i(uint8_t s, int dx, int dy, int dz);
+// execute_for_relevant_sectants (src/boxtree/iterate.rs:40-121)
+std::array<size_t, 3> execute_for_relevant_sectants(const Cube &nb, U3 position, uint32_t update_size,
+                                                    const std::function<void(U3, U3, uint8_t, const Cube &)> &fun);
 
 }  // namespace vhx
 

@@ -432,6 +432,23 @@ int vhx_boxtree_get(const vhx_boxtree *tree, uint32_t x, uint32_t y, uint32_t z,
     *data = e.data;
     return VHX_OK;
 }
+int vhx_boxtree_node_info(const vhx_boxtree *tree, float x, float y, float z, uint64_t *key, uint32_t *content,
+                          uint64_t *occupied_bits, uint32_t *occlusion_bits) {
+    if (!tree || !key || !content || !occupied_bits || !occlusion_bits) return VHX_E_INVALID_ARG;
+    const BoxTree &t = *tree->tree;
+    const float S = (float)t.boxtree_size;
+    if (!(x >= 0.f && y >= 0.f && z >= 0.f && x < S && y < S && z < S)) return VHX_E_TREE_INVALID_POSITION;
+    Cube bounds{F3{0.f, 0.f, 0.f}, S};
+    const size_t k = t.get_node_internal(0, bounds, F3{x, y, z});
+    if (k == SIZE_MAX) return VHX_E_TREE_INVALID_POSITION;
+    const Node &n = t.nodes.get(k);
+    *key = k;
+    *content = (uint32_t)n.content;
+    *occupied_bits = n.occupied_bits;
+    *occlusion_bits = n.occlusion_bits;
+    return VHX_OK;
+}
+
 int vhx_boxtree_simplify(vhx_boxtree *tree, int recursive) {
     if (!tree) return VHX_E_INVALID_ARG;
     tree->tree->simplify(0, recursive != 0);
