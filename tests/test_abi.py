@@ -10,7 +10,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def declared_functions():
     names = set()
-    for h in ("vhx.h", "vhx_boxtree.h"):
+    for h in ("vhx.h", "vhx_boxtree.h", "vhx_stream.h"):
         text = open(os.path.join(ROOT, "include", h)).read()
         text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
         for m in re.finditer(r"^\s*[A-Za-z_][\w \*]*?\b(vhx_\w+)\s*\(", text, flags=re.M):

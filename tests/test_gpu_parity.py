@@ -319,3 +319,34 @@ def test_vox_model_frame_vs_oracle(gpu, oracle):
     ref = oracle.trace_primary(flat, cam, 0, 0, 192, 128, count_bytes=True)
     assert_same(got, ref, "vox frame")
     assert (got["value"] != N.VHX_EMPTY).sum() > 500
+
+
+def test_streamed_view_on_device_matches_mirror(gpu, oracle):
+    """vhx_stream on a device context: after frames of ranged writes (nodes, children, voxels, solid values,
+    palettes) and a view resize, the GPU traces the device view exactly like the oracle traces the host mirror,
+    and like the full tree inside the streamed region."""
+    from tests.test_streaming import FIELDS, _rays_in_box, _tree
+    t = _tree(128, 8)
+    flat = t.flatten()
+    s = vhx.StreamingView(t, gpu, (40.0, 30.0, 50.0), 10.0)
+    s.set_rates(16, 64, 10)
+    s.set_viewport((40.0, 30.0, 50.0), 48.0)  # larger than the initial sizing: forces a resize
+    stats, frames, resizes = s.upload_all()
+    assert resizes >= 1 and frames > 2
+    rng = np.random.default_rng(11)
+    c = np.array((40.0, 30.0, 50.0), np.float32)
+    lo, hi = np.maximum(c - 23, 0), np.minimum(c + 23, 128)
+    o, d = _rays_in_box(rng, lo, hi, 20000)
+    got = gpu.trace_rays(o, d, fields=FIELDS, count_bytes=True)
+    mirror = oracle.trace_rays(s.view(), o, d, fields=FIELDS, count_bytes=True)
+    assert_same(got, mirror, "device view vs host mirror")
+    full = oracle.trace_rays(flat, o, d, fields=FIELDS)
+    inside = (full["value"] != N.VHX_EMPTY) & np.all((full["impact"] >= lo) & (full["impact"] <= hi), axis=1)
+    assert inside.sum() > 1000
+    assert_same({k: got[k][inside] for k in FIELDS}, {k: full[k][inside] for k in FIELDS}, "streamed region")
+    # move: slots are reused, the device follows the host mirror
+    s.set_viewport((100.0, 100.0, 90.0), 48.0)
+    s.upload_all()
+    o, d = _rays_in_box(rng, np.array([80.0, 80.0, 70.0]), np.array([120.0, 120.0, 110.0]), 20000)
+    assert_same(gpu.trace_rays(o, d, fields=FIELDS), oracle.trace_rays(s.view(), o, d, fields=FIELDS), "after move")
+    s.close()

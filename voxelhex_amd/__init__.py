@@ -6,6 +6,7 @@ Host side (BoxTree data model and flattening) and the HIP kernels for gfx950 bot
 from .boxtree import (Albedo, BoxTree, BoxTreeEntry, FlatTree, InvalidBrickDimension, InvalidPosition, InvalidSize,
                       InvalidStructure, OctreeError, V3c, entry_from_value, voxel_data)
 from .raytracing import BoxTreeGPUHost, BoxTreeGPUView, Ray, Raytracer, Viewport, default_raytracer, glass_camera
+from .streaming import StreamingView
 from . import _native as native
 
 __all__ = [

@@ -16,7 +16,7 @@ BUILD = os.path.join(ROOT, "build", "vhx")
 LIB = os.path.join(LIBDIR, "libvhx.so")
 ARCH = os.environ.get("VHX_OFFLOAD_ARCH", "gfx950")
 
-HOST_SRCS = ["boxtree.cpp", "flatten.cpp", "vox.cpp"]
+HOST_SRCS = ["boxtree.cpp", "flatten.cpp", "vox.cpp", "stream.cpp"]
 DEV_SRCS = ["vhx_device.hip"]
 HEADERS = ["boxtree.hpp", "trace.hpp"]
 

@@ -97,6 +97,14 @@ SIGNATURES = [
     ("vhx_boxtree_info", c_int, [c_void_p, P(c_u32 * 5)]),
     ("vhx_scene_insert", c_int, [c_void_p, c_u32, c_u64]),
     ("vhx_boxtree_flatten", c_int, [c_void_p, P(c_void_p)]),
+    ("vhx_stream_create", c_int, [c_void_p, c_void_p, P(c_f32), c_f32, P(c_void_p)]),
+    ("vhx_stream_destroy", None, [c_void_p]),
+    ("vhx_stream_set_rates", c_int, [c_void_p, c_u32, c_u32, c_u32]),
+    ("vhx_stream_set_viewport", c_int, [c_void_p, P(c_f32), c_f32]),
+    ("vhx_stream_upload", c_int, [c_void_p, c_void_p]),
+    ("vhx_stream_resize", c_int, [c_void_p]),
+    ("vhx_stream_reload", c_int, [c_void_p]),
+    ("vhx_stream_view", c_int, [c_void_p, P(TreeDesc)]),
     ("vhx_boxtree_node_info", c_int, [c_void_p, c_f32, c_f32, c_f32, P(c_u64), P(c_u32), P(c_u64), P(c_u32)]),
     ("vhx_boxtree_load_vox", c_int, [ctypes.c_char_p, c_u32, P(c_void_p)]),
     ("vhx_boxtree_load_vox_memory", c_int, [c_void_p, c_u64, c_u32, P(c_void_p)]),

@@ -1,0 +1,833 @@
+// Streaming producer: a device-resident *view* of a BoxTree with bounded node and brick capacity, filled around a
+// viewport with ranged writes — BoxTreeGPUDataHandler and its upload queue (src/raytracing/bevy/streaming/*.rs)
+// over the host BoxTree restatement, feeding vhx_update_range instead of wgpu's write_buffer.
+//
+//   rebuild                            upload_queue.rs:60-207   nodes to see around the viewport
+//   process / next_valid_node          upload_queue.rs:218-574  node uploads, then brick uploads, per frame
+//   process_node_child_bricks          upload_queue.rs:406-476
+//   add_node / first_available_node    cache.rs:188-455         node slots, victim = not in view
+//   add_brick / first_available_brick  cache.rs:460-716         brick slots, victim = unused / MIP / furthest
+//   erase_node_child                   cache.rs:41-145
+//   re_evaluate_view_size              streaming/mod.rs:292-340 grows capacities (caller re-creates buffers)
+//   upload                             streaming/mod.rs:420-635 cache updates -> ranged writes
+//   view sizing                        view.rs:50-69; set_viewport: bevy/mod.rs:110-155 (brick slot hysteresis)
+//
+// Behavioural deviation: rebuild puts the whole root -> center access path into the view set (see rebuild).
+// Differences in the layout the device kernel reads: node type is one u32 per node (not 2 bits
+// packed 16 per word), occupancy one u64, a Solid brick descriptor is 0x80000000 | index into a deduplicated solid
+// value table (the reference inlines the value, losing data-palette bits), MIP data is tracked for slot accounting
+// but never uploaded (the raytracer does not read MIPs). The reference computes the view set on a worker thread; here
+// `rebuild` runs synchronously when the viewport leaves its brick slot, so the upload order is deterministic.
+// Tree-change propagation (handle_tree_updates, streaming/mod.rs:36-288) is not restated: the tree must not be
+// modified while a stream uses it.
+#include <algorithm>
+#include <array>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <memory>
+#include <tuple>
+#include <unordered_map>
+#include <unordered_set>
+#include <vector>
+
+#include "../../include/vhx.h"
+#include "../../include/vhx_boxtree.h"
+#include "../../include/vhx_stream.h"
+#include "boxtree.hpp"
+
+using namespace vhx;
+
+namespace {
+
+constexpr uint32_t kEmpty = 0xFFFFFFFFu;
+constexpr uint32_t kSolidCapacity0 = 4096;
+constexpr uint32_t kPaletteCapacity = 65536;
+
+// BrickOwnedBy (streaming/types.rs:14-21); equality and hash ignore the brick position (streaming/mod.rs:561-590)
+struct Owned {
+    uint8_t kind = 0;  // 0 None, 1 NodeAsChild, 2 NodeAsMIP
+    uint32_t node = 0;
+    uint8_t sectant = 0;
+    F3 bl{0.f, 0.f, 0.f};  // V3c<u32> brick position, kept as floats
+    uint64_t key() const { return ((uint64_t)kind << 40) | ((uint64_t)sectant << 32) | node; }
+};
+
+struct CacheUpdate {  // CacheUpdatePackage (types.rs:35-47)
+    std::vector<std::pair<size_t, Owned>> brick_updates;
+    std::vector<std::pair<size_t, uint64_t>> modified_nodes;
+};
+
+struct StackItem {
+    size_t node;
+    uint8_t sectant;
+    Cube bounds;
+};
+
+inline F3 f3(float x, float y, float z) { return F3{x, y, z}; }
+inline F3 sub(F3 a, F3 b) { return f3(a.x - b.x, a.y - b.y, a.z - b.z); }
+inline F3 add(F3 a, F3 b) { return f3(a.x + b.x, a.y + b.y, a.z + b.z); }
+inline F3 unit(float v) { return f3(v, v, v); }
+inline float clampf(float v, float lo, float hi) { return std::fmin(std::fmax(v, lo), hi); }  // f32::clamp
+inline float length(F3 a) { return std::sqrt((a.x * a.x + a.y * a.y) + a.z * a.z); }
+inline bool contains(const Cube &c, F3 p) {  // Cube::contains, spatial/mod.rs:54-61
+    return p.x >= c.min.x && p.y >= c.min.y && p.z >= c.min.z && p.x < (c.min.x + c.size) &&
+           p.y < (c.min.y + c.size) && p.z < (c.min.z + c.size);
+}
+inline uint32_t round_u32(float v) {  // f32::round() as u32 (saturating)
+    const float r = std::round(v);
+    if (!(r > 0.f)) return 0;
+    if (r >= 4294967296.f) return 0xFFFFFFFFu;
+    return (uint32_t)r;
+}
+inline uint32_t as_u32(float v) {
+    if (!(v > 0.f)) return 0;
+    if (v >= 4294967296.f) return 0xFFFFFFFFu;
+    return (uint32_t)v;
+}
+
+}  // namespace
+
+struct vhx_stream {
+    const BoxTree *tree = nullptr;
+    vhx_ctx *ctx = nullptr;
+    // BoxTreeGPUDataHandler
+    size_t node_uploads_per_frame = 25, brick_uploads_per_frame = 50, brick_unload_search_perimeter = 10;
+    size_t nodes_in_view = 0, bricks_in_view = 0;
+    Cube upload_range{};
+    // render data: the host mirror of the device view
+    std::vector<uint32_t> node_type;
+    std::vector<uint64_t> node_ocbits;
+    std::vector<uint32_t> node_children;
+    std::vector<uint32_t> node_mips;  // host only
+    std::vector<uint32_t> voxels;
+    std::vector<uint32_t> solid_values;
+    std::unordered_map<uint32_t, uint32_t> solid_index;
+    size_t solid_capacity = kSolidCapacity0;
+    std::vector<uint32_t> color_palette, data_palette;  // device-side capacity kPaletteCapacity
+    // UploadQueueTargets
+    std::unordered_map<size_t, Owned> brick_by_index;
+    std::unordered_map<uint64_t, size_t> brick_by_owner;
+    std::unordered_map<size_t, size_t> meta_by_key, key_by_meta;
+    std::unordered_map<size_t, std::pair<size_t, uint8_t>> node_index_vs_parent;
+    std::unordered_set<size_t> nodes_to_see;
+    // UploadQueueStatus
+    std::vector<StackItem> target_node_stack;
+    std::vector<Owned> bricks_to_upload;
+    size_t victim_brick = 0, victim_node = 0;
+    size_t uploaded_color_palette_size = 0, uploaded_data_palette_size = 0, uploaded_solid_size = 0;
+    // view
+    F3 origin{0.f, 0.f, 0.f};
+    float view_distance = 0.f;
+    bool reload = true, resize = false, device_valid = false;
+    Cube brick_slot{f3(0.f, 0.f, 0.f), 0.f};
+    bool brick_slot_set = false;
+    // statistics of the last upload
+    uint64_t last_nodes = 0, last_bricks = 0, last_bytes = 0;
+    // completion tracking over the cyclic node walk: new work (node adds, brick requests) found in the current and
+    // in the last complete walk cycle (UINT64_MAX: no complete cycle since the last rebuild)
+    uint64_t cycle_work = 0, last_cycle_work = UINT64_MAX;
+    bool walk_started = false;
+
+    uint32_t bd() const { return tree->brick_dim; }
+    uint32_t max_mip_level() const {  // boxtree/mod.rs:320-324
+        const float l = std::ceil(std::log((float)tree->boxtree_size / (float)tree->brick_dim) / std::log(4.f));
+        return l <= 0.f ? 0u : (uint32_t)l;
+    }
+    bool key_valid(size_t k) const { return tree->nodes.key_is_valid(k); }
+    const Node &node(size_t k) const { return tree->nodes.get(k); }
+    size_t child(size_t k, uint8_t s) const {
+        const Node &n = node(k);
+        return n.has_children ? (size_t)n.children[s] : SIZE_MAX;
+    }
+    bool valid_child(size_t k, uint8_t s, size_t &c) const {
+        c = child(k, s);
+        return key_valid(c);
+    }
+
+    // --------------------------------------------------------------------------------- ownership bimap helpers
+    bool owner_has(const Owned &o) const { return brick_by_owner.count(o.key()) != 0; }
+    void owner_insert(size_t idx, const Owned &o) {  // BiHashMap::insert drops both old pairs
+        auto a = brick_by_index.find(idx);
+        if (a != brick_by_index.end()) brick_by_owner.erase(a->second.key());
+        auto b = brick_by_owner.find(o.key());
+        if (b != brick_by_owner.end()) brick_by_index.erase(b->second);
+        brick_by_index[idx] = o;
+        brick_by_owner[o.key()] = idx;
+    }
+    void owner_remove_index(size_t idx) {
+        auto a = brick_by_index.find(idx);
+        if (a == brick_by_index.end()) return;
+        brick_by_owner.erase(a->second.key());
+        brick_by_index.erase(a);
+    }
+    void meta_insert(size_t key, size_t meta) {
+        auto a = meta_by_key.find(key);
+        if (a != meta_by_key.end()) key_by_meta.erase(a->second);
+        auto b = key_by_meta.find(meta);
+        if (b != key_by_meta.end()) meta_by_key.erase(b->second);
+        meta_by_key[key] = meta;
+        key_by_meta[meta] = key;
+    }
+
+    uint32_t solid_descriptor(uint32_t value) {
+        auto it = solid_index.find(value);
+        if (it != solid_index.end()) return 0x80000000u | it->second;
+        const uint32_t i = (uint32_t)solid_values.size();
+        solid_values.push_back(value);
+        solid_index[value] = i;
+        return 0x80000000u | i;
+    }
+
+    // ------------------------------------------------------------------------------------------ view sizing
+    void size_view() {  // view.rs:50-69
+        const float dist = view_distance;
+        const uint32_t levels = max_mip_level();
+        size_t nodes = 0;
+        for (uint32_t level = 1; level <= levels; ++level) {
+            uint32_t cube = tree->brick_dim;
+            for (uint32_t k = 0; k < level; ++k) cube *= 4;
+            nodes += (size_t)std::pow(std::ceil(dist / (float)cube), 3.f);
+        }
+        const size_t per_axis = (size_t)std::ceil(dist / (float)tree->brick_dim);
+        nodes_in_view = std::max<size_t>(nodes, 1);
+        bricks_in_view = std::max<size_t>((per_axis * per_axis * per_axis + nodes_in_view) / 4, 1);
+    }
+    void alloc_mirror() {
+        node_type.assign(nodes_in_view, VHX_NODE_NOTHING);
+        node_ocbits.assign(nodes_in_view, 0);
+        node_children.assign(nodes_in_view * kChildren, kEmpty);
+        node_mips.assign(nodes_in_view, kEmpty);
+        voxels.assign(bricks_in_view * (size_t)bd() * bd() * bd(), 0u);
+    }
+    void reset_targets() {  // UploadQueueTargets::reset + view.reload (view.rs:141-145)
+        brick_by_index.clear();
+        brick_by_owner.clear();
+        meta_by_key.clear();
+        key_by_meta.clear();
+        node_index_vs_parent.clear();
+        nodes_to_see.clear();
+        bricks_to_upload.clear();
+        reload = true;
+    }
+
+    // --------------------------------------------------------------------------------------------- rebuild
+    void add_children_nodes_to_upload_queue(size_t key, Cube nb, uint32_t mip_level, F3 vc, float dist,
+                                            uint32_t min_mip) {  // upload_queue.rs:144-207
+        if (mip_level < min_mip) return;
+        const float include = dist * std::pow(4.f, (float)mip_level - 1.f);
+        const F3 c = sub(vc, unit(include / 2.f));
+        const U3 cbl{round_u32(c.x), round_u32(c.y), round_u32(c.z)};
+        if (node(key).content != Content::Internal) return;
+        execute_for_relevant_sectants(nb, cbl, as_u32(include), [&](U3, U3, uint8_t cs, const Cube &tb) {
+            size_t ck;
+            if (valid_child(key, cs, ck)) {
+                nodes_to_see.insert(ck);
+                add_children_nodes_to_upload_queue(ck, tb, mip_level - 1, vc, dist, min_mip);
+            }
+        });
+    }
+    void rebuild(F3 center_, float dist) {  // upload_queue.rs:60-142
+        nodes_to_see.clear();
+        walk_started = false;
+        last_cycle_work = UINT64_MAX;
+        const float S = (float)tree->boxtree_size;
+        const F3 vc = f3(clampf(center_.x, 0.f, S), clampf(center_.y, 0.f, S), clampf(center_.z, 0.f, S));
+        const F3 bl_ = sub(center_, unit(dist / 2.f));
+        const F3 bl = f3(clampf(bl_.x, 0.f, S), clampf(bl_.y, 0.f, S), clampf(bl_.z, 0.f, S));
+        F3 tr = add(bl, unit(dist));
+        tr = f3(clampf(tr.x, 0.f, S), clampf(tr.y, 0.f, S), clampf(tr.z, 0.f, S));
+        uint32_t deepest = as_u32(std::ceil(length(sub(bl_, bl)) / dist));
+        deepest = std::max(std::min(deepest, max_mip_level()), 1u);
+        bool have_parent = false;
+        size_t parent_key = 0;
+        Cube parent_bounds{};
+        uint32_t parent_mip = 0;
+        Cube nb{f3(0.f, 0.f, 0.f), S};
+        uint32_t mip = max_mip_level();
+        size_t key = 0;
+        // Deviation: the whole access path root -> center joins the view set. The reference marks only the center
+        // node and its parent's relevant children, which leaves the root's slot 0 evictable and makes a center two
+        // or more levels down unreachable for next_valid_node (it only descends into nodes of the view set).
+        nodes_to_see.insert(0);
+        for (;;) {
+            const Content c = node(key).content;
+            if (c != Content::Internal || (nb.size / 4.f) <= dist || !contains(nb, bl) || !contains(nb, tr)) break;
+            const uint8_t cs = offset_sectant(sub(vc, nb.min), nb.size);  // Cube::sectant_for
+            size_t ck;
+            if (!valid_child(key, cs, ck)) break;
+            have_parent = true;
+            parent_key = key;
+            parent_bounds = nb;
+            parent_mip = mip;
+            key = ck;
+            nodes_to_see.insert(ck);
+            nb = child_bounds_for(nb, cs);
+            mip -= 1;
+        }
+        nodes_to_see.insert(key);
+        if (have_parent)
+            add_children_nodes_to_upload_queue(parent_key, parent_bounds, parent_mip, vc, dist, deepest);
+        else
+            add_children_nodes_to_upload_queue(key, nb, mip, vc, dist, deepest);
+    }
+    std::vector<StackItem> node_stack_init() const {  // streaming/mod.rs:553-559
+        return {StackItem{0, (uint8_t)kChildren, Cube{f3(0.f, 0.f, 0.f), (float)tree->boxtree_size}}};
+    }
+
+    // -------------------------------------------------------------------------------------------- eviction
+    std::vector<std::pair<size_t, uint64_t>> erase_node_child(size_t meta, size_t cs) {  // cache.rs:41-145
+        std::vector<std::pair<size_t, uint64_t>> modified{{meta, 1ull << cs}};
+        auto pk = key_by_meta.find(meta);
+        if (pk == key_by_meta.end()) return modified;  // the reference unwraps (panics) here
+        const size_t parent_key = pk->second;
+        const size_t off = meta * kChildren + cs;
+        const uint32_t desc = node_children[off];
+        node_index_vs_parent.erase(desc);
+        node_children[off] = kEmpty;
+        const Content pc = node(parent_key).content;
+        if (pc == Content::Internal) {
+            // MIP connection of the erased child (MIP data is Empty in a tree without MIPs: nothing owned)
+            if (desc < node_mips.size() && node_mips[desc] != kEmpty) node_mips[desc] = kEmpty;
+            modified.push_back({desc, 0});
+        } else if (pc == Content::Leaf || pc == Content::UniformLeaf) {
+            if (desc != kEmpty && !(desc & 0x80000000u)) owner_remove_index(desc & 0x7FFFFFFFu);
+        }
+        return modified;
+    }
+    bool first_available_node(size_t &idx, bool &has_parent, std::pair<size_t, uint8_t> &parent) {  // cache.rs:159-185
+        size_t v = (victim_node + 1) % nodes_in_view;
+        while (v != victim_node) {
+            auto it = key_by_meta.find(v);
+            if (it == key_by_meta.end() || !nodes_to_see.count(it->second)) {
+                victim_node = v;
+                idx = v;
+                auto p = node_index_vs_parent.find(v);
+                has_parent = p != node_index_vs_parent.end();
+                if (has_parent) parent = p->second;
+                return true;
+            }
+            v = (v + 1) % nodes_in_view;
+        }
+        return false;
+    }
+    bool outside_range(F3 b, float s) const {  // cache.rs:462-469
+        const Cube &r = upload_range;
+        return (b.x + s) < r.min.x || (r.min.x + r.size) < b.x || (b.y + s) < r.min.y || (r.min.y + r.size) < b.y ||
+               (b.z + s) < r.min.z || (r.min.z + r.size) < b.z;
+    }
+    bool mip_children_all_empty(uint32_t node_key) const {
+        auto it = meta_by_key.find(node_key);
+        if (it == meta_by_key.end()) return true;
+        const size_t m = it->second;
+        for (size_t s = 0; s < kChildren; ++s)
+            if (node_children[m * kChildren + s] != kEmpty) return false;
+        return true;
+    }
+    bool first_available_brick(float brick_size, size_t &out) {  // cache.rs:460-573
+        const size_t start = (size_t)std::max<long long>((long long)victim_brick -
+                                                             (long long)brick_unload_search_perimeter / 2, 0);
+        const size_t end = std::min(start + brick_unload_search_perimeter, bricks_in_view);
+        bool have_priority = false, have_furthest = false;
+        size_t priority = 0, furthest = 0;
+        float furthest_d = 0.f;
+        const F3 half = unit(upload_range.size / 2.f);
+        for (size_t i = start; i < end; ++i) {
+            auto it = brick_by_index.find(i);
+            const Owned o = it == brick_by_index.end() ? Owned{} : it->second;
+            if (o.kind == 0) {
+                priority = i;
+                have_priority = true;
+                break;
+            } else if (o.kind == 2) {
+                if (!nodes_to_see.count(o.node) && mip_children_all_empty(o.node)) {
+                    priority = i;
+                    have_priority = true;
+                    break;
+                }
+            } else {
+                const float d = length(add(sub(o.bl, upload_range.min), half));
+                if (outside_range(o.bl, brick_size) && (!have_furthest || d > furthest_d)) {
+                    furthest_d = d;
+                    furthest = i;
+                    have_furthest = true;
+                }
+            }
+        }
+        if (have_priority || have_furthest) {
+            out = have_priority ? priority : furthest;
+            victim_brick = (out + 1) % bricks_in_view;
+            return true;
+        }
+        for (int pass = 0; pass < 2; ++pass) {
+            const size_t a = pass == 0 ? end : 0, b = pass == 0 ? bricks_in_view : start;
+            for (size_t i = a; i < b; ++i) {
+                auto it = brick_by_index.find(i);
+                const Owned o = it == brick_by_index.end() ? Owned{} : it->second;
+                const bool ok = o.kind == 0 || (o.kind == 2 && !nodes_to_see.count(o.node)) ||
+                                (o.kind == 1 && outside_range(o.bl, brick_size));
+                if (ok) {
+                    victim_brick = (i + 1) % bricks_in_view;
+                    out = i;
+                    return true;
+                }
+            }
+        }
+        return false;
+    }
+
+    // ------------------------------------------------------------------------------------------ add_node
+    bool add_node(size_t parent_key, uint8_t target_sectant, CacheUpdate &upd) {  // cache.rs:188-455
+        const size_t key = target_sectant < kChildren ? child(parent_key, target_sectant) : 0;
+        size_t idx = 0;
+        bool robbed = false;
+        std::pair<size_t, uint8_t> robbed_parent{0, 0};
+        if (key == 0) {
+            idx = 0;
+        } else if (meta_by_key.count(key)) {
+            idx = meta_by_key[key];
+        } else {
+            if (!first_available_node(idx, robbed, robbed_parent)) return false;
+        }
+        meta_insert(key, idx);
+        if (robbed) {
+            auto m = erase_node_child(robbed_parent.first, robbed_parent.second);
+            upd.modified_nodes.insert(upd.modified_nodes.end(), m.begin(), m.end());
+        }
+        const Node &n = node(key);
+        node_type[idx] = n.content == Content::Leaf          ? VHX_NODE_LEAF
+                         : n.content == Content::UniformLeaf ? VHX_NODE_UNIFORM_LEAF
+                         : n.content == Content::Internal    ? VHX_NODE_INTERNAL
+                                                             : VHX_NODE_NOTHING;
+        node_ocbits[idx] = n.occupied_bits;
+        std::fill(node_children.begin() + (ptrdiff_t)(idx * kChildren),
+                  node_children.begin() + (ptrdiff_t)((idx + 1) * kChildren), kEmpty);
+        if (key != 0) {
+            auto pmi = meta_by_key.find(parent_key);
+            if (pmi == meta_by_key.end()) return false;  // parent not resident (the reference panics)
+            const size_t pm = pmi->second;
+            node_children[pm * kChildren + target_sectant] = (uint32_t)idx;
+            node_index_vs_parent[idx] = {pm, target_sectant};
+            upd.modified_nodes.push_back({pm, 1ull << target_sectant});
+        }
+        upd.modified_nodes.push_back({idx, ~0ull});
+        const size_t first = idx * kChildren;
+        auto brick_desc = [&](const Brick &b, uint8_t s) -> uint32_t {
+            if (b.kind == BrickKind::Solid) return solid_descriptor(b.solid);
+            if (b.kind == BrickKind::Empty) return kEmpty;
+            Owned o;
+            o.kind = 1;
+            o.node = (uint32_t)key;
+            o.sectant = s;
+            auto it = brick_by_owner.find(o.key());
+            return it == brick_by_owner.end() ? kEmpty : (0x7FFFFFFFu & (uint32_t)it->second);
+        };
+        if (n.content == Content::Internal) {
+            for (uint8_t s = 0; s < kChildren; ++s) {
+                size_t ck;
+                if (valid_child(key, s, ck)) {
+                    auto it = meta_by_key.find(ck);
+                    node_children[first + s] = it == meta_by_key.end() ? kEmpty : (uint32_t)it->second;
+                } else {
+                    node_children[first + s] = kEmpty;
+                }
+            }
+        } else if (n.content == Content::UniformLeaf) {
+            node_children[first] = brick_desc(n.bricks[0], 0);
+        } else if (n.content == Content::Leaf) {
+            for (uint8_t s = 0; s < kChildren; ++s) node_children[first + s] = brick_desc(n.bricks[s], s);
+        }
+        node_mips[idx] = kEmpty;  // MIPs are not built by this restatement (BrickData::Empty)
+        return true;
+    }
+
+    // ----------------------------------------------------------------------------------------- add_brick
+    bool add_brick(const Owned &req, CacheUpdate &upd) {  // cache.rs:575-716
+        size_t bi;
+        if (!first_available_brick((float)tree->brick_dim, bi)) return false;
+        auto prev = brick_by_index.find(bi);
+        const Owned old = prev == brick_by_index.end() ? Owned{} : prev->second;
+        if (old.kind == 1) {
+            auto m = meta_by_key.find(old.node);
+            if (m != meta_by_key.end()) {
+                auto mod = erase_node_child(m->second, old.sectant);
+                upd.modified_nodes.insert(upd.modified_nodes.end(), mod.begin(), mod.end());
+            }
+        } else if (old.kind == 2) {
+            auto m = meta_by_key.find(old.node);
+            if (m != meta_by_key.end()) {
+                node_mips[m->second] = kEmpty;
+                upd.modified_nodes.push_back({m->second, 0});
+            }
+        }
+        auto pmi = meta_by_key.find(req.node);
+        if (pmi == meta_by_key.end()) return true;  // owner no longer resident: nothing to attach (reference panics)
+        const size_t pm = pmi->second;
+        if (req.kind == 1) {
+            upd.modified_nodes.push_back({pm, 1ull << req.sectant});
+            node_children[pm * kChildren + req.sectant] = 0x7FFFFFFFu & (uint32_t)bi;
+        } else {
+            upd.modified_nodes.push_back({pm, 0});
+            node_mips[pm] = 0x7FFFFFFFu & (uint32_t)bi;
+        }
+        owner_insert(bi, req);
+        upd.brick_updates.push_back({bi, req});
+        return true;
+    }
+
+    // ----------------------------------------------------------------------------------------- process
+    std::vector<Owned> process_node_child_bricks(size_t key, const Cube &nb, U3 vbl, float dist) const {
+        std::vector<Owned> res;  // upload_queue.rs:406-476
+        const Node &n = node(key);
+        if (n.content == Content::UniformLeaf) {
+            if (n.bricks[0].kind == BrickKind::Parted) {
+                Owned o;
+                o.kind = 1;
+                o.node = (uint32_t)key;
+                o.sectant = 0;
+                o.bl = f3(std::round(nb.min.x), std::round(nb.min.y), std::round(nb.min.z));
+                if (!owner_has(o)) res.push_back(o);
+            }
+        } else if (n.content == Content::Leaf) {
+            execute_for_relevant_sectants(nb, vbl, as_u32(dist), [&](U3, U3, uint8_t cs, const Cube &tb) {
+                if (n.bricks[cs].kind != BrickKind::Parted) return;
+                Owned o;
+                o.kind = 1;
+                o.node = (uint32_t)key;
+                o.sectant = cs;
+                o.bl = f3(std::round(tb.min.x), std::round(tb.min.y), std::round(tb.min.z));
+                if (!owner_has(o)) res.push_back(o);
+            });
+        }
+        return res;
+    }
+    bool next_valid_node(size_t &parent_out, uint8_t &sect_out, size_t &child_out, Cube &bounds_out) {
+        if (target_node_stack.empty()) return false;  // upload_queue.rs:480-574
+        auto &top = target_node_stack.back();
+        const size_t cur = top.node;
+        uint8_t ts = top.sectant;
+        const Cube cb = top.bounds;
+        // the root's cursor at 64 reads as "start": once the walk is through, it starts over from the root, so the
+        // reference streams continuously (and picks up bricks that were evicted or not yet uploaded)
+        if (cur == 0 && ts == kChildren) {
+            if (walk_started) last_cycle_work = cycle_work;
+            cycle_work = 0;
+            walk_started = true;
+            top.sectant = 0;
+            parent_out = cur;
+            sect_out = (uint8_t)kChildren;
+            child_out = cur;
+            bounds_out = cb;
+            return true;
+        }
+        for (;;) {
+            if (ts >= kChildren || !node(cur).has_children) {
+                target_node_stack.pop_back();
+                if (!target_node_stack.empty()) {
+                    auto &p = target_node_stack.back();
+                    p.sectant += 1;
+                    parent_out = p.node;
+                    sect_out = (uint8_t)(p.sectant - 1);
+                    child_out = cur;
+                    bounds_out = cb;
+                    return true;
+                }
+                return false;
+            }
+            size_t ck = child(cur, ts);
+            while (ts < kChildren && (!key_valid(ck) || !nodes_to_see.count(ck))) {
+                ts += 1;
+                if (ts < kChildren) ck = child(cur, ts);
+            }
+            if (ts >= kChildren) continue;
+            if (!node(ck).has_children || node(ck).is_occluded()) {
+                const uint8_t rs = ts;
+                const size_t rc = ck;
+                ts += 1;
+                ck = ts < kChildren ? child(cur, ts) : SIZE_MAX;
+                while (ts < kChildren && !key_valid(ck)) {
+                    ts += 1;
+                    if (ts < kChildren) ck = child(cur, ts);
+                }
+                target_node_stack.back().sectant = ts;
+                parent_out = cur;
+                sect_out = rs;
+                child_out = rc;
+                bounds_out = child_bounds_for(cb, rs);
+                return true;
+            }
+            target_node_stack.back().sectant = ts;
+            target_node_stack.push_back(StackItem{ck, 0, child_bounds_for(cb, ts)});
+            parent_out = cur;
+            sect_out = ts;
+            child_out = ck;
+            bounds_out = cb;
+            return true;
+        }
+    }
+    // returns false when the view ran out of capacity (re_evaluate_view_size was applied)
+    bool process(std::vector<CacheUpdate> &updates) {  // upload_queue.rs:218-404
+        if (reload) {
+            rebuild(origin, view_distance);
+            target_node_stack = node_stack_init();
+            reload = false;
+        }
+        for (size_t k = 0; k < node_uploads_per_frame && !target_node_stack.empty(); ++k) {
+            size_t parent, key;
+            uint8_t ts;
+            Cube nb;
+            if (!next_valid_node(parent, ts, key, nb)) break;
+            if (!meta_by_key.count(key)) {
+                CacheUpdate u;
+                if (!add_node(parent, ts, u)) return re_evaluate_view_size();
+                updates.push_back(std::move(u));
+                ++cycle_work;
+            }
+            {  // the MIP of every node takes a brick slot (empty MIPs upload no voxels)
+                Owned mip;
+                mip.kind = 2;
+                mip.node = (uint32_t)key;
+                CacheUpdate u;
+                if (!add_brick(mip, u)) return re_evaluate_view_size();
+                updates.push_back(std::move(u));
+            }
+            const F3 vbl_f = sub(origin, unit(view_distance / 2.f));
+            const U3 vbl{round_u32(vbl_f.x), round_u32(vbl_f.y), round_u32(vbl_f.z)};
+            auto more = process_node_child_bricks(key, nb, vbl, view_distance);
+            cycle_work += more.size();
+            bricks_to_upload.insert(bricks_to_upload.end(), more.begin(), more.end());
+        }
+        if (!bricks_to_upload.empty()) {
+            const size_t take = std::min(brick_uploads_per_frame, bricks_to_upload.size());
+            std::vector<Owned> reqs(bricks_to_upload.end() - (ptrdiff_t)take, bricks_to_upload.end());
+            bricks_to_upload.resize(bricks_to_upload.size() - take);
+            for (const Owned &r : reqs) {
+                if (owner_has(r)) continue;
+                CacheUpdate u;
+                if (!add_brick(r, u)) return re_evaluate_view_size();
+                updates.push_back(std::move(u));
+            }
+        }
+        return true;
+    }
+    bool re_evaluate_view_size() {  // streaming/mod.rs:292-340
+        const size_t need_nodes = nodes_to_see.size();
+        if (need_nodes > nodes_in_view) nodes_in_view = (size_t)((float)need_nodes * 1.2f);
+        const size_t need_bricks = bricks_to_upload.size() + brick_by_index.size() + need_nodes;
+        if (need_bricks > bricks_in_view) bricks_in_view = (size_t)((float)need_bricks * 1.2f);
+        node_type.resize(nodes_in_view, VHX_NODE_NOTHING);
+        node_ocbits.resize(nodes_in_view, 0);
+        node_children.resize(nodes_in_view * kChildren, kEmpty);
+        node_mips.resize(nodes_in_view, kEmpty);
+        voxels.resize(bricks_in_view * (size_t)bd() * bd() * bd(), 0u);
+        resize = true;
+        return false;
+    }
+
+    // ------------------------------------------------------------------------------------------- device side
+    vhx_tree_desc desc() const {
+        vhx_tree_desc d{};
+        d.boxtree_size = tree->boxtree_size;
+        d.brick_dim = tree->brick_dim;
+        d.node_count = (uint32_t)nodes_in_view;
+        d.brick_count = (uint32_t)bricks_in_view;
+        d.solid_count = (uint32_t)solid_capacity;
+        d.color_count = kPaletteCapacity;
+        d.data_count = kPaletteCapacity;
+        d.node_type = node_type.data();
+        d.node_ocbits = node_ocbits.data();
+        d.node_children = node_children.data();
+        d.voxels = voxels.data();
+        return d;
+    }
+    int upload_all() {  // (re)creates the device view from the host mirror (view creation / view.resize)
+        std::vector<uint32_t> solid(solid_capacity, 0u), color(kPaletteCapacity, 0u), data(kPaletteCapacity, 0u);
+        std::copy(solid_values.begin(), solid_values.end(), solid.begin());
+        std::copy(color_palette.begin(), color_palette.end(), color.begin());
+        std::copy(data_palette.begin(), data_palette.end(), data.begin());
+        vhx_tree_desc d = desc();
+        d.solid_values = solid.data();
+        d.color_palette = color.data();
+        d.data_palette = data.data();
+        const int rc = ctx ? vhx_upload_tree(ctx, &d) : VHX_OK;  // ctx == NULL: host-only view (tests)
+        if (rc) return rc;
+        uploaded_solid_size = solid_values.size();
+        device_valid = true;
+        resize = false;
+        return VHX_OK;
+    }
+    int write(int buf, size_t off, size_t n, const void *src) {
+        if (n == 0) return VHX_OK;
+        const size_t esz = buf == VHX_BUF_NODE_OCBITS ? 8 : 4;
+        last_bytes += n * esz;
+        return ctx ? vhx_update_range(ctx, buf, off, n, src) : VHX_OK;
+    }
+    int upload_frame() {  // streaming/mod.rs:420-635
+        last_nodes = last_bricks = last_bytes = 0;
+        if (resize) return VHX_E_CAPACITY;
+        std::vector<CacheUpdate> updates;
+        const bool fits = process(updates);
+        int rc = VHX_OK;
+        // palettes: deltas of the host tree's palettes (capacity kPaletteCapacity entries on the device)
+        if (tree->color_palette.size() > kPaletteCapacity || tree->data_palette.size() > kPaletteCapacity)
+            return VHX_E_CAPACITY;
+        if (tree->color_palette.size() > uploaded_color_palette_size) {
+            color_palette = tree->color_palette;
+            rc = write(VHX_BUF_COLOR_PALETTE, uploaded_color_palette_size,
+                       color_palette.size() - uploaded_color_palette_size, color_palette.data() + uploaded_color_palette_size);
+            if (rc) return rc;
+            uploaded_color_palette_size = color_palette.size();
+        }
+        if (tree->data_palette.size() > uploaded_data_palette_size) {
+            data_palette = tree->data_palette;
+            rc = write(VHX_BUF_DATA_PALETTE, uploaded_data_palette_size,
+                       data_palette.size() - uploaded_data_palette_size, data_palette.data() + uploaded_data_palette_size);
+            if (rc) return rc;
+            uploaded_data_palette_size = data_palette.size();
+        }
+        // voxel data of the uploaded bricks (Parted only: MIP slots upload nothing), before the nodes point at them
+        const size_t n3 = (size_t)bd() * bd() * bd();
+        for (const auto &u : updates)
+            for (const auto &bu : u.brick_updates) {
+                const Owned &o = bu.second;
+                if (o.kind != 1) continue;
+                const Node &n = node(o.node);
+                const Brick &b = n.content == Content::UniformLeaf ? n.bricks[0] : n.bricks[o.sectant];
+                if (b.kind != BrickKind::Parted) continue;
+                std::copy(b.parted.begin(), b.parted.end(), voxels.begin() + (ptrdiff_t)(bu.first * n3));
+                rc = write(VHX_BUF_VOXELS, bu.first * n3, n3, voxels.data() + bu.first * n3);
+                if (rc) return rc;
+                ++last_bricks;
+            }
+        if (solid_values.size() > solid_capacity) {  // grow the solid table: re-create the view
+            while (solid_capacity < solid_values.size()) solid_capacity *= 2;
+            resize = true;
+            return VHX_E_CAPACITY;
+        }
+        if (solid_values.size() > uploaded_solid_size) {
+            rc = write(VHX_BUF_SOLID_VALUES, uploaded_solid_size, solid_values.size() - uploaded_solid_size,
+                       solid_values.data() + uploaded_solid_size);
+            if (rc) return rc;
+            uploaded_solid_size = solid_values.size();
+        }
+        size_t meta_lo = SIZE_MAX, meta_hi = 0, ch_lo = SIZE_MAX, ch_hi = 0;
+        for (const auto &u : updates)
+            for (const auto &mn : u.modified_nodes) {
+                const size_t i = mn.first;
+                if (i >= nodes_in_view) continue;
+                meta_lo = std::min(meta_lo, i);
+                meta_hi = std::max(meta_hi, i + 1);
+                for (size_t s = 0; s < kChildren; ++s)
+                    if (mn.second & (1ull << s)) {
+                        ch_lo = std::min(ch_lo, i * kChildren + s);
+                        ch_hi = std::max(ch_hi, i * kChildren + s + 1);
+                    }
+            }
+        for (const auto &u : updates)
+            for (const auto &mn : u.modified_nodes) last_nodes += mn.second == ~0ull ? 1 : 0;  // nodes (re)written
+        if (meta_lo < meta_hi) {
+            rc = write(VHX_BUF_NODE_TYPE, meta_lo, meta_hi - meta_lo, node_type.data() + meta_lo);
+            if (!rc) rc = write(VHX_BUF_NODE_OCBITS, meta_lo, meta_hi - meta_lo, node_ocbits.data() + meta_lo);
+            if (rc) return rc;
+        }
+        if (ch_lo < ch_hi) {
+            rc = write(VHX_BUF_NODE_CHILDREN, ch_lo, ch_hi - ch_lo, node_children.data() + ch_lo);
+            if (rc) return rc;
+        }
+        return fits ? VHX_OK : VHX_E_CAPACITY;
+    }
+};
+
+extern "C" {
+
+int vhx_stream_create(const vhx_boxtree *tree, vhx_ctx *ctx, const float origin[3], float view_distance,
+                      vhx_stream **out) {
+    if (!tree || !origin || !out || !(view_distance > 0.f)) return VHX_E_INVALID_ARG;
+    *out = nullptr;
+    auto s = std::make_unique<vhx_stream>();
+    s->tree = tree->tree;
+    s->ctx = ctx;
+    s->origin = f3(origin[0], origin[1], origin[2]);
+    s->view_distance = view_distance;
+    s->upload_range = Cube{sub(s->origin, unit(view_distance / 2.f)), view_distance};
+    s->size_view();
+    s->alloc_mirror();
+    const int rc = s->upload_all();
+    if (rc) return rc;
+    *out = s.release();
+    return VHX_OK;
+}
+
+void vhx_stream_destroy(vhx_stream *s) { delete s; }
+
+int vhx_stream_set_rates(vhx_stream *s, uint32_t node_uploads_per_frame, uint32_t brick_uploads_per_frame,
+                         uint32_t brick_unload_search_perimeter) {
+    if (!s || node_uploads_per_frame == 0 || brick_uploads_per_frame == 0) return VHX_E_INVALID_ARG;
+    s->node_uploads_per_frame = node_uploads_per_frame;
+    s->brick_uploads_per_frame = brick_uploads_per_frame;
+    s->brick_unload_search_perimeter = brick_unload_search_perimeter;
+    return VHX_OK;
+}
+
+int vhx_stream_set_viewport(vhx_stream *s, const float origin[3], float view_distance) {
+    if (!s || !origin || !(view_distance > 0.f)) return VHX_E_INVALID_ARG;
+    const F3 o = f3(origin[0], origin[1], origin[2]);
+    s->origin = o;
+    const bool moved = !s->brick_slot_set || !contains(s->brick_slot, o) || view_distance != s->view_distance;
+    s->view_distance = view_distance;
+    if (moved) {  // bevy/mod.rs:110-155: a rebuild only when the origin leaves its brick slot
+        s->upload_range = Cube{sub(o, unit(view_distance / 2.f)), view_distance};
+        s->rebuild(o, view_distance);
+        s->target_node_stack = s->node_stack_init();
+        const float bd = (float)s->tree->brick_dim;  // Cube::brick_slot_for, spatial/raytracing/mod.rs:65-70
+        s->brick_slot = Cube{f3(o.x - std::fabs(std::fmod(o.x, bd)), o.y - std::fabs(std::fmod(o.y, bd)),
+                                o.z - std::fabs(std::fmod(o.z, bd))),
+                             bd};
+        s->brick_slot_set = true;
+    }
+    return VHX_OK;
+}
+
+int vhx_stream_upload(vhx_stream *s, vhx_stream_stats *stats) {
+    if (!s) return VHX_E_INVALID_ARG;
+    const int rc = s->upload_frame();
+    if (stats) {
+        stats->bytes_written = s->last_bytes;
+        stats->nodes_written = s->last_nodes;
+        stats->bricks_written = s->last_bricks;
+        stats->nodes_resident = s->meta_by_key.size();
+        stats->bricks_resident = s->brick_by_index.size();
+        stats->nodes_in_view = s->nodes_in_view;
+        stats->bricks_in_view = s->bricks_in_view;
+        stats->nodes_to_see = s->nodes_to_see.size();
+        uint64_t missing = 0;
+        for (size_t k : s->nodes_to_see) missing += s->meta_by_key.count(k) ? 0u : 1u;
+        stats->pending = missing + s->bricks_to_upload.size() + (s->last_cycle_work == 0 ? 0u : 1u);
+    }
+    return rc;
+}
+
+int vhx_stream_resize(vhx_stream *s) {
+    if (!s) return VHX_E_INVALID_ARG;
+    return s->upload_all();
+}
+
+int vhx_stream_reload(vhx_stream *s) {
+    if (!s) return VHX_E_INVALID_ARG;
+    s->reset_targets();
+    return VHX_OK;
+}
+
+int vhx_stream_view(const vhx_stream *s, vhx_tree_desc *out) {
+    if (!s || !out) return VHX_E_INVALID_ARG;
+    *out = s->desc();
+    out->solid_count = (uint32_t)s->solid_values.size();
+    out->solid_values = s->solid_values.data();
+    out->color_count = (uint32_t)s->color_palette.size();
+    out->color_palette = s->color_palette.data();
+    out->data_count = (uint32_t)s->data_palette.size();
+    out->data_palette = s->data_palette.data();
+    return VHX_OK;
+}
+
+}  // extern "C"

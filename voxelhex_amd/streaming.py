@@ -1,0 +1,94 @@
+"""Streaming view of a BoxTree on the GPU (vhx_stream, include/vhx_stream.h).
+
+Mirrors the reference's BoxTreeGPUDataHandler (src/raytracing/bevy/streaming/*.rs): a device buffer set with a bounded
+number of node and brick slots, filled around the viewport a few nodes/bricks per frame with ranged writes. A
+Raytracer that hosts a stream traces the streamed view.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _native as N
+
+STAT_FIELDS = ("bytes_written", "bricks_written", "nodes_written", "nodes_resident", "bricks_resident",
+               "nodes_in_view", "bricks_in_view", "nodes_to_see", "pending")
+
+
+class StreamStats(ctypes.Structure):
+    _fields_ = [(f, ctypes.c_uint64) for f in STAT_FIELDS]
+
+
+class ViewDesc:
+    """Host mirror of the device view, usable wherever a FlatTree's `desc` is read (e.g. the test oracle)."""
+
+    def __init__(self, stream, desc):
+        self._stream = stream  # the arrays live in the stream
+        self.desc = desc
+
+
+class StreamingView:
+    """A streamed view (vhx_stream). raytracer=None keeps it on the host (vhx_stream_view only)."""
+
+    def __init__(self, tree, raytracer, origin, view_distance):
+        self.tree = tree
+        self.raytracer = raytracer
+        h = ctypes.c_void_p()
+        ctx = raytracer._h if raytracer is not None else None
+        o = (ctypes.c_float * 3)(*[float(v) for v in origin])
+        N.check(N.lib().vhx_stream_create(tree._h, ctx, o, float(view_distance), ctypes.byref(h)), ctx)
+        self._h = h
+        if raytracer is not None:
+            raytracer._tree = self  # the context now holds the streamed view
+
+    def close(self):
+        if getattr(self, "_h", None) and self._h.value:
+            N.lib().vhx_stream_destroy(self._h)
+            self._h = ctypes.c_void_p(None)
+
+    def __del__(self):
+        self.close()
+
+    def _ctx(self):
+        return self.raytracer._h if self.raytracer is not None else None
+
+    def set_rates(self, node_uploads_per_frame=25, brick_uploads_per_frame=50, brick_unload_search_perimeter=10):
+        N.check(N.lib().vhx_stream_set_rates(self._h, node_uploads_per_frame, brick_uploads_per_frame,
+                                             brick_unload_search_perimeter))
+
+    def set_viewport(self, origin, view_distance):
+        o = (ctypes.c_float * 3)(*[float(v) for v in origin])
+        N.check(N.lib().vhx_stream_set_viewport(self._h, o, float(view_distance)))
+
+    def upload(self):
+        """One frame of uploads; returns (stats dict, needs_resize)."""
+        st = StreamStats()
+        rc = N.lib().vhx_stream_upload(self._h, ctypes.byref(st))
+        if rc not in (N.VHX_OK, N.VHX_E_CAPACITY):
+            N.check(rc, self._ctx())
+        return {f: getattr(st, f) for f in STAT_FIELDS}, rc == N.VHX_E_CAPACITY
+
+    def resize(self):
+        N.check(N.lib().vhx_stream_resize(self._h), self._ctx())
+
+    def reload(self):
+        N.check(N.lib().vhx_stream_reload(self._h))
+
+    def upload_all(self, max_frames=100000):
+        """Uploads frame by frame (resizing when the view is too small) until nothing is pending."""
+        frames = resizes = 0
+        stats = None
+        while frames < max_frames:
+            stats, grow = self.upload()
+            frames += 1
+            if grow:
+                self.resize()
+                resizes += 1
+                continue
+            if stats["pending"] == 0:
+                break
+        return stats, frames, resizes
+
+    def view(self):
+        d = N.TreeDesc()
+        N.check(N.lib().vhx_stream_view(self._h, ctypes.byref(d)))
+        return ViewDesc(self, d)
