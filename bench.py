@@ -84,10 +84,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal of the multi-GPU path on a single GPU: VHX_BENCH_REHEARSAL=1 puts every rank on cuda:0 and gathers
+    # over gloo through host memory (RCCL needs one GPU per rank); timings from such a run are not scaling numbers
+    rehearsal = world > 1 and os.environ.get("VHX_BENCH_REHEARSAL") == "1"
+    if rehearsal:
+        local = 0
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearsal:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -147,7 +155,15 @@ def main():
             e1.record(stream)
             ev.append((e0, e1))
         if world > 1:
-            dist.gather(rgba, gathered if rank == 0 else None, dst=0)
+            if rehearsal:
+                host = rgba.cpu()
+                hg = [torch.empty_like(host) for _ in range(world)] if rank == 0 else None
+                dist.gather(host, hg, dst=0)
+                if rank == 0:
+                    for g, h in zip(gathered, hg):
+                        g.copy_(h)
+            else:
+                dist.gather(rgba, gathered if rank == 0 else None, dst=0)
             if rank == 0:
                 flatg = torch.cat(gathered)
                 rt.untile_rgba(flatg.data_ptr(), world, tiles_per_rank, T, W, H, framebuffer.data_ptr())
@@ -167,7 +183,7 @@ def main():
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if rehearsal else dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
@@ -180,12 +196,19 @@ def main():
         workload += " +shadows"
         n_shadow = int((out["value"] != -1).sum().item())  # shadow rays this rank traced per frame
         if world > 1:
-            ts = torch.tensor([n_shadow], dtype=torch.int64, device=dev)
+            ts = torch.tensor([n_shadow], dtype=torch.int64, device="cpu" if rehearsal else dev)
             dist.all_reduce(ts)
             n_shadow = int(ts.item())
         total_rays += n_shadow
     mrays = total_rays * args.steps / elapsed / 1e6
     ms_per_step = elapsed * 1e3 / args.steps
+
+    # ---- multi-GPU check (untimed): the gathered, untiled frame equals rank 0 tracing the whole frame alone -------
+    mgpu = None
+    if world > 1 and rank == 0:
+        whole = rt.trace_primary(cam, fields=("rgba",))["rgba"]
+        got = framebuffer.cpu().numpy().view(np.uint32)
+        mgpu = {"frame_equal": bool(np.array_equal(got, whole)), "pixels": int(whole.size)}
 
     # ---- roofline: algorithmic bytes of this rank's launch (instrumented kernel, untimed) -------------------------
     roof = None
@@ -237,12 +260,15 @@ def main():
                        "shadow_rays_per_frame": n_shadow if args.shadows else None,
                        "tree_size": args.size, "brick_dim": args.brick_dim, "width": W, "height": H,
                        "scene": args.scene, "tile": T if world > 1 else None,
-                       "parallelism": f"screen-tile split x{world} + RCCL gather" if world > 1 else "single GPU",
+                       "parallelism": (f"screen-tile split x{world} + " + ("gloo gather (single-GPU rehearsal)" if rehearsal
+                                                                  else "RCCL gather")) if world > 1 else "single GPU",
                        "tree_nodes": int(flat.desc.node_count), "tree_bricks": int(flat.desc.brick_count),
                        "tree_gb": round(flat.nbytes() / 1e9, 3), "build_s": round(build_s, 2),
                        "upload_s": round(upload_s, 2)},
             "roofline": roof, "cpu_baseline": cpu,
         }
+        if mgpu is not None:
+            line["multi_gpu_check"] = mgpu
         if cpu:
             line["gpu_over_cpu"] = round(mrays / cpu["value"], 2)
         print(json.dumps(line), flush=True)
