@@ -170,7 +170,9 @@ int vhx_tree_device_bytes(const vhx_ctx *ctx, uint64_t *bytes);
 
 /* Tracing --------------------------------------------------------------------------------------------------- */
 /* Traces primary rays for every pixel of the square tiles k = tile_start, tile_start+tile_stride, ... (raster order
- * of ceil(W/T) x ceil(H/T) tiles, T = tile_size). tile_size 0 with layout FRAMEBUFFER traces the whole frame. */
+ * of ceil(W/T) x ceil(H/T) tiles, T = tile_size). tile_size 0 with layout FRAMEBUFFER traces the whole frame.
+ * In the TILES layout, entries of pixels past the frame edge are not written (device outputs) or read back as 0
+ * (host outputs). */
 int vhx_trace_primary(vhx_ctx *ctx, const vhx_camera *cam, uint32_t tile_size, uint32_t tile_start,
                       uint32_t tile_stride, uint32_t layout, const vhx_hits *out, int on_device);
 /* Traces n explicit rays; rays = 6 f32 per ray (origin xyz, direction xyz), host or device per on_device. */

@@ -350,3 +350,26 @@ def test_streamed_view_on_device_matches_mirror(gpu, oracle):
     o, d = _rays_in_box(rng, np.array([80.0, 80.0, 70.0]), np.array([120.0, 120.0, 110.0]), 20000)
     assert_same(gpu.trace_rays(o, d, fields=FIELDS), oracle.trace_rays(s.view(), o, d, fields=FIELDS), "after move")
     s.close()
+
+
+def test_tile_layout_padding_reads_zero_and_bytes_add_up(gpu):
+    """Tile layout with host outputs: padding pixels past the frame edge read back as 0, so per-rank byte counts
+    (the bench's roofline for N>1) add up to the whole frame's."""
+    flat = vhx.FlatTree.build_scene(N.VHX_SCENE_LATTICE_CUBE, 64, 4)
+    gpu.upload(flat)
+    W, H, T, R = 200, 136, 64, 3
+    cam = vhx.glass_camera(64, W, H, target=(32.0, 32.0, 32.0))
+    whole = gpu.trace_primary(cam, fields=(), count_bytes=True)["bytes"].astype(np.uint64).sum()
+    total = 0
+    for r in range(R):
+        b = gpu.trace_primary(cam, tile_size=T, tile_start=r, tile_stride=R, layout=N.VHX_LAYOUT_TILES,
+                              fields=("value",), count_bytes=True)
+        total += int(b["bytes"].astype(np.uint64).sum())
+        tiles_x = (W + T - 1) // T
+        v = b["value"].reshape(-1, T, T)
+        for j in range(v.shape[0]):
+            tile = r + j * R
+            w = min(T, W - (tile % tiles_x) * T)
+            h = min(T, H - (tile // tiles_x) * T)
+            assert (v[j, h:, :] == 0).all() and (v[j, :, w:] == 0).all()
+    assert total == int(whole)

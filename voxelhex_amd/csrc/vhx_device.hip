@@ -9,8 +9,6 @@
 //   k_pack_hdr       node type + occupied_bits -> one 16-byte record per node
 //   k_untile_rgba    scatters rank-gathered tile buffers into the framebuffer (multi-GPU screen-tile split)
 #include <hip/hip_runtime.h>
-#include <rocprim/device/device_select.hpp>
-#include <rocprim/iterator/counting_iterator.hpp>
 
 #include <cmath>
 #include <cstdio>
@@ -47,8 +45,10 @@ struct vhx_ctx {
     DevBuf hdr, brick_occ, scratch, rays;
     DevBuf queue[2];  // multi-pass ray queues (ping-pong), output indices of abandoned rays in increasing order
     DevBuf qctl;      // [0..7] queue lengths written after pass p (7: shadow hit list), [8..15] work counters
-    DevBuf flags;     // one byte per output ray: abandoned by the current pass
-    DevBuf seltmp;    // rocPRIM select scratch
+    DevBuf tmp;       // chunk-local lists of abandoned rays (a block's or a queue chunk's, in lane order)
+    DevBuf counts;    // rays listed per chunk
+    DevBuf offsets;   // exclusive scan of counts
+    DevBuf flags;     // primary pass 0: abandoned flag per output index
     uint32_t occ_words = 1;
     bool simple_kernel = true;  // VHX_PERSISTENT=1 selects the persistent wave-refill kernel (A/B)
     // step budgets of the passes before the final (unbounded) one; VHX_BUDGETS="64" / "32,256" style override
@@ -301,17 +301,131 @@ __global__ void __launch_bounds__(256) k_trace_persistent(DevTree t, CamD cam, O
 
 // ------------------------------------------------------------------------------------------- multi-pass scheduling
 // Per-ray work is heavy-tailed (bench frame: mean 14 steps, p99 311, max 2160), and a wave64 runs as long as its
-// longest lane. Pass 0 traces every ray with a small step budget; the rays that exhaust it raise a per-ray flag, a
-// stream compaction (rocPRIM select over the flags) lists their output indices in increasing order, and the next
-// pass traces them again from scratch, 64 long rays per wave, with a larger budget; the last pass is unbounded
-// (VHX_MAX_ITERS). Keeping the queue in output order keeps neighbouring rays together in a wave: the bench frame's
-// long rays take 1.17 ms in frame order and 1.48 ms in completion (atomic-append) order. Every ray's result comes from
-// one uninterrupted, deterministic traversal, so the output is bit-identical to a single pass.
+// longest lane. Pass 0 traces every ray with a small step budget; the rays that exhaust it are listed per chunk (a
+// workgroup's 16x16 pixel block, or a queue pass's chunk) in lane order, a scan over the chunk counts and a gather
+// turn the lists into the next pass's queue, and the next pass traces them again from scratch, 64 long rays per
+// wave, with a larger budget; the last pass is unbounded (VHX_MAX_ITERS). Keeping the queue in spatial order keeps
+// neighbouring rays together in a wave: the bench frame's long rays take 1.17 ms in frame order and 1.48 ms in
+// completion (atomic-append) order. Every ray's result comes from one uninterrupted, deterministic traversal, so the
+// output is bit-identical to a single pass.
 struct PassQ {
     uint32_t budget;   // VHX_MAX_ITERS on the final pass
     uint32_t rpw;      // queue passes: rays per wave (lanes >= rpw idle)
-    uint8_t *flags;    // abandoned-ray flags, indexed by output index (null on the final pass)
+    uint32_t *tmp;     // chunk-local lists of abandoned rays (null on the final pass)
+    uint32_t *counts;  // per chunk
+    uint8_t *flags;    // primary pass 0: abandoned flag per output index (every entry written, no clearing needed)
 };
+
+// Block-level ordered append (all 256 threads of the workgroup call it): the workgroup's rays with push set are
+// listed at tmp[blockIdx * 256 ...] in thread order, their number at counts[blockIdx].
+__device__ __forceinline__ void block_append(bool push, uint32_t idx, uint32_t *tmp, uint32_t *counts) {
+    __shared__ uint32_t s_cnt[4];
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    const uint64_t m = __ballot(push);
+    if (lane == 0) s_cnt[wave] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t before = 0;
+    for (uint32_t w = 0; w < wave; ++w) before += s_cnt[w];
+    if (push) tmp[(uint64_t)blockIdx.x * 256u + before + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = idx;
+    if (threadIdx.x == 0) counts[blockIdx.x] = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+}
+
+// Exclusive scan of the chunk counts in one workgroup of 1024 threads; nchunks = ceil(*n_in / per_chunk) when n_in
+// is given (a queue pass: its input length is only known on the device), else nchunks_host. Writes *total.
+__global__ void __launch_bounds__(1024) k_scan_counts(const uint32_t *__restrict__ counts, uint32_t nchunks_host,
+                                                      const uint32_t *n_in, uint32_t per_chunk,
+                                                      uint32_t *__restrict__ offsets, uint32_t *total) {
+    __shared__ uint32_t s_wave[16];
+    __shared__ uint32_t s_carry;
+    const uint32_t nchunks = n_in ? (*n_in + per_chunk - 1) / per_chunk : nchunks_host;
+    const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
+    constexpr uint32_t K = 16;  // elements per thread per segment; loads issued together
+    if (t == 0) s_carry = 0;
+    __syncthreads();
+    for (uint32_t seg = 0; seg < nchunks; seg += 1024u * K) {
+        const uint32_t b = seg + t * K;
+        uint32_t v[K];
+#pragma unroll
+        for (uint32_t k = 0; k < K; ++k) v[k] = b + k < nchunks ? counts[b + k] : 0u;
+        uint32_t sum = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < K; ++k) sum += v[k];
+        uint32_t inc = sum;  // inclusive scan within the wave
+        for (uint32_t d = 1; d < 64; d <<= 1) {
+            const uint32_t x = __shfl_up(inc, d);
+            if (lane >= d) inc += x;
+        }
+        if (lane == 63) s_wave[wave] = inc;
+        __syncthreads();
+        uint32_t before = s_carry;
+        for (uint32_t w = 0; w < wave; ++w) before += s_wave[w];
+        uint32_t run = before + inc - sum;
+#pragma unroll
+        for (uint32_t k = 0; k < K; ++k) {
+            if (b + k < nchunks) offsets[b + k] = run;
+            run += v[k];
+        }
+        __syncthreads();
+        if (t == 1023) s_carry = before + inc;
+        __syncthreads();
+    }
+    if (t == 0) *total = s_carry;
+}
+
+// Flag compaction in output-index order (primary pass 0): 1024 flags per workgroup, 4 per thread.
+__global__ void __launch_bounds__(256) k_count_flags(const uint8_t *__restrict__ flags, uint64_t n,
+                                                     uint32_t *__restrict__ counts) {
+    __shared__ uint32_t s_cnt[4];
+    const uint64_t i = ((uint64_t)blockIdx.x * 256u + threadIdx.x) * 4u;
+    uint32_t c = 0;
+    if (i + 3 < n) {
+        const uint32_t w = *(const uint32_t *)(flags + i);
+        c = __popc(w & 0x01010101u);
+    } else {
+        for (uint64_t k = i; k < n && k < i + 4; ++k) c += flags[k] ? 1u : 0u;
+    }
+    for (uint32_t d = 32; d > 0; d >>= 1) c += __shfl_down(c, d);
+    if ((threadIdx.x & 63u) == 0) s_cnt[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) counts[blockIdx.x] = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+}
+
+__global__ void __launch_bounds__(256) k_emit_flags(const uint8_t *__restrict__ flags, uint64_t n,
+                                                    const uint32_t *__restrict__ offsets, uint32_t *__restrict__ out) {
+    __shared__ uint32_t s_wave[4];
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint64_t i = ((uint64_t)blockIdx.x * 256u + threadIdx.x) * 4u;
+    uint32_t bits = 0;  // bit k: flag i + k
+    for (uint32_t k = 0; k < 4; ++k)
+        if (i + k < n && flags[i + k]) bits |= 1u << k;
+    const uint32_t c = __popc(bits);
+    uint32_t inc = c;
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t x = __shfl_up(inc, d);
+        if (lane >= d) inc += x;
+    }
+    if (lane == 63) s_wave[wave] = inc;
+    __syncthreads();
+    uint32_t o = offsets[blockIdx.x] + inc - c;
+    for (uint32_t w = 0; w < wave; ++w) o += s_wave[w];
+    for (uint32_t k = 0; k < 4; ++k)
+        if (bits & (1u << k)) out[o++] = (uint32_t)(i + k);
+}
+
+// One wave per chunk: copies the chunk's list to the queue at its offset.
+__global__ void __launch_bounds__(256) k_gather_chunks(const uint32_t *__restrict__ tmp, uint32_t stride,
+                                                       const uint32_t *__restrict__ counts,
+                                                       const uint32_t *__restrict__ offsets, uint32_t nchunks_host,
+                                                       const uint32_t *n_in, uint32_t per_chunk,
+                                                       uint32_t *__restrict__ out) {
+    const uint32_t nchunks = n_in ? (*n_in + per_chunk - 1) / per_chunk : nchunks_host;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t waves = gridDim.x * 4u;
+    for (uint32_t c = blockIdx.x * 4u + (threadIdx.x >> 6); c < nchunks; c += waves) {
+        const uint32_t n = counts[c], o = offsets[c];
+        for (uint32_t k = lane; k < n; k += 64u) out[o + k] = tmp[(uint64_t)c * stride + k];
+    }
+}
 
 // Where a queued output index comes from: a primary-ray frame (framebuffer or tile layout) or an explicit ray batch.
 struct RaySrc {
@@ -370,19 +484,20 @@ __global__ void __launch_bounds__(256) k_trace_primary(DevTree t, CamD cam, OutD
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
     const uint32_t lx = (sb % blocks_per_tile_x) * 16u + (wave & 1u) * 8u + (lane & 7u);
     const uint32_t ly = (sb / blocks_per_tile_x) * 16u + (wave >> 1) * 8u + (lane >> 3);
-    if (lx >= T || ly >= T) return;
     const uint32_t px = (tile % tiles_x) * T + lx, py = (tile / tiles_x) * T + ly;
-    if (px >= cam.width || py >= cam.height) return;
-    F3d o, d;
-    primary_ray(cam, px, py, o, d);
-    HitOut h;
-    const bool done = get_by_ray<COUNT, BD>(t, occ_tab, o, d, h, q.budget);
+    const bool valid = lx < T && ly < T && px < cam.width && py < cam.height;
     const uint64_t idx = layout == VHX_LAYOUT_FRAMEBUFFER ? (uint64_t)py * cam.width + px
                                                           : (uint64_t)j * T * T + (uint64_t)ly * T + lx;
-    if (done)
-        store(t, out, idx, o, h);
-    else
-        q.flags[idx] = 1;
+    bool done = true;
+    if (valid) {
+        F3d o, d;
+        primary_ray(cam, px, py, o, d);
+        HitOut h;
+        done = get_by_ray<COUNT, BD>(t, occ_tab, o, d, h, q.budget);
+        if (done) store(t, out, idx, o, h);
+    }
+    // every in-tile entry (frame padding included) gets its flag, so the flags need no clearing between frames
+    if (q.flags && lx < T && ly < T) q.flags[idx] = done ? 0 : 1;
 }
 
 template <bool COUNT, int BD>
@@ -392,15 +507,22 @@ __global__ void __launch_bounds__(256) k_trace_rays(DevTree t, const float *__re
     fill_occ_tab(occ_tab);
     __syncthreads();
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const F3d o = mk(rays[6 * i], rays[6 * i + 1], rays[6 * i + 2]);
-    const F3d d = mk(rays[6 * i + 3], rays[6 * i + 4], rays[6 * i + 5]);
-    HitOut h;
-    const bool done = get_by_ray<COUNT, BD>(t, occ_tab, o, d, h, q.budget);
-    if (done)
-        store(t, out, i, o, h);
-    else
-        q.flags[i] = 1;
+    bool done = true;
+    if (i < n) {
+        const F3d o = mk(rays[6 * i], rays[6 * i + 1], rays[6 * i + 2]);
+        const F3d d = mk(rays[6 * i + 3], rays[6 * i + 4], rays[6 * i + 5]);
+        HitOut h;
+        done = get_by_ray<COUNT, BD>(t, occ_tab, o, d, h, q.budget);
+        if (done) store(t, out, i, o, h);
+    }
+    if (q.tmp) block_append(!done, (uint32_t)i, q.tmp, q.counts);
+}
+
+// Hit pixels of a previous trace (value != VHX_EMPTY), listed per workgroup: the shadow pass's first queue.
+__global__ void __launch_bounds__(256) k_list_hits(const uint32_t *__restrict__ value, uint64_t n, uint32_t *tmp,
+                                                   uint32_t *counts) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    block_append(i < n && value[i] != VHX_EMPTY, (uint32_t)i, tmp, counts);
 }
 
 // Queue pass: each wave takes 64 consecutive queue entries at a time from a shared counter until the queue written
@@ -412,7 +534,7 @@ __device__ __forceinline__ void store_shadow(const OutD &o, uint64_t i, const Hi
     if (o.bytes) o.bytes[i] = h.bytes;
 }
 
-template <bool COUNT, int BD, bool SHADOW = false>
+template <bool COUNT, int BD>
 __global__ void __launch_bounds__(256) k_trace_queue(DevTree t, CamD cam, RaySrc src, OutD out,
                                                      const uint32_t *__restrict__ in, const uint32_t *in_n,
                                                      uint32_t *grab, PassQ q) {
@@ -427,26 +549,28 @@ __global__ void __launch_bounds__(256) k_trace_queue(DevTree t, CamD cam, RaySrc
         base = __shfl(base, 0);
         if (base >= n) break;  // wave-uniform
         const uint32_t i = base + lane;
+        bool push = false;
+        uint32_t idx = 0;
         if (lane < q.rpw && i < n) {
-            const uint32_t idx = in[i];
+            idx = in[i];
             F3d o, d;
             ray_of(cam, src, idx, o, d);
             HitOut h;
             if (!get_by_ray<COUNT, BD>(t, occ_tab, o, d, h, q.budget))
-                q.flags[idx] = 1;
-            else if (SHADOW)
+                push = true;
+            else if (src.kind == 3u)
                 store_shadow(out, idx, h);
             else
                 store(t, out, idx, o, h);
         }
+        if (q.tmp) {  // this chunk's abandoned rays, in lane order
+            const uint32_t chunk = base / q.rpw;
+            const uint64_t m = __ballot(push);
+            if (push) q.tmp[(uint64_t)chunk * q.rpw + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = idx;
+            if (lane == 0) q.counts[chunk] = (uint32_t)__popcll(m);
+        }
     }
 }
-
-// Hit pixels of a previous trace (value != VHX_EMPTY): the shadow pass's first queue.
-struct IsHit {
-    const uint32_t *value;
-    __device__ bool operator()(uint32_t i) const { return value[i] != VHX_EMPTY; }
-};
 
 __global__ void __launch_bounds__(256) k_untile_rgba(const uint32_t *__restrict__ gathered, uint32_t ranks,
                                                      uint32_t tiles_per_rank, uint32_t T, uint32_t tiles_x,
@@ -572,7 +696,8 @@ struct HostOut {
 };
 
 // Maps the caller's vhx_hits onto device pointers (scratch-backed when the caller passed host memory).
-static int map_out(vhx_ctx *c, const vhx_hits *h, uint64_t n, int on_device, HostOut &ho) {
+// zero_fill: staging is cleared first (tile layout: pixels past the frame edge are never written and read back as 0)
+static int map_out(vhx_ctx *c, const vhx_hits *h, uint64_t n, int on_device, HostOut &ho, bool zero_fill = false) {
     struct F {
         void *user;
         uint64_t per;
@@ -590,6 +715,7 @@ static int map_out(vhx_ctx *c, const vhx_hits *h, uint64_t n, int on_device, Hos
         if (f.user) total += (f.per * n + 255) & ~255ull;
     int rc = ensure(c, c->scratch, total);
     if (rc) return rc;
+    if (zero_fill && total) VHX_HIP(c, hipMemsetAsync(c->scratch.ptr, 0, total, c->stream));
     uint64_t off = 0;
     for (auto &f : fields) {
         if (!f.user) continue;
@@ -608,33 +734,31 @@ static int finish_out(vhx_ctx *c, HostOut &ho) {
     return VHX_OK;
 }
 
-// Multi-pass plumbing: allocates flags, queues, counters and compaction scratch for `nout` rays (may synchronise;
-// called before the trace is timed); returns the number of passes to run.
-static int prepare_passes(vhx_ctx *c, uint64_t nout, uint32_t &npass, bool shadow = false) {
+// Multi-pass plumbing: allocates queues, chunk lists and counters for `nout` rays whose pass 0 runs in `nblocks0`
+// workgroups of 256 (may synchronise; called before the trace is timed). Returns the number of passes to run.
+static int prepare_passes(vhx_ctx *c, uint64_t nout, uint64_t nblocks0, uint32_t &npass, bool shadow = false) {
     npass = nout < 0x7FFFFFFFull ? c->npass : 1u;
     if (npass < 2 && !shadow) return VHX_OK;
+    uint64_t chunks = std::max(nblocks0, (nout + 1023) / 1024), list = nblocks0 * 256;
+    for (uint32_t p = 1; p < npass; ++p) {  // queue passes: chunk = one grab of rpw rays
+        const uint64_t ch = (nout + c->rpw[p] - 1) / c->rpw[p];
+        chunks = std::max(chunks, ch);
+        list = std::max(list, ch * c->rpw[p]);
+    }
     int rc = ensure(c, c->queue[0], nout * 4);
     if (!rc && (npass > 2 || shadow)) rc = ensure(c, c->queue[1], nout * 4);
     if (!rc) rc = ensure(c, c->qctl, 16 * sizeof(uint32_t));
-    if (!rc) rc = ensure(c, c->flags, nout);
-    if (rc) return rc;
-    size_t tmp = 0;
-    VHX_HIP(c, rocprim::select(nullptr, tmp, rocprim::counting_iterator<uint32_t>(0u), (const uint8_t *)nullptr,
-                               (uint32_t *)nullptr, (uint32_t *)nullptr, (size_t)nout, c->stream));
-    if (shadow) {
-        size_t tmp2 = 0;
-        VHX_HIP(c, rocprim::select(nullptr, tmp2, rocprim::counting_iterator<uint32_t>(0u), (uint32_t *)nullptr,
-                                   (uint32_t *)nullptr, (size_t)nout, IsHit{nullptr}, c->stream));
-        tmp = tmp2 > tmp ? tmp2 : tmp;
-    }
-    return ensure(c, c->seltmp, tmp);
+    if (!rc) rc = ensure(c, c->tmp, list * 4);
+    if (!rc) rc = ensure(c, c->counts, chunks * 4);
+    if (!rc) rc = ensure(c, c->offsets, chunks * 4);
+    if (!rc) rc = ensure(c, c->flags, ((nout + 3) & ~3ull));
+    return rc;
 }
 
 // Stream-ordered per-trace reset of the pass state (inside the timed region).
-static int reset_passes(vhx_ctx *c, uint64_t nout, uint32_t npass, bool shadow = false) {
+static int reset_passes(vhx_ctx *c, uint32_t npass, bool shadow = false) {
     if (npass < 2 && !shadow) return VHX_OK;
     VHX_HIP(c, hipMemsetAsync(c->qctl.ptr, 0, 16 * sizeof(uint32_t), c->stream));
-    VHX_HIP(c, hipMemsetAsync(c->flags.ptr, 0, nout, c->stream));
     return VHX_OK;
 }
 
@@ -643,35 +767,72 @@ static PassQ pass_q(const vhx_ctx *c, uint32_t p, uint32_t npass) {
     const bool last = p + 1 >= npass;
     q.budget = last ? VHX_MAX_ITERS : c->budgets[p];
     q.rpw = c->rpw[p];
-    q.flags = last ? nullptr : (uint8_t *)c->flags.ptr;
+    q.tmp = last ? nullptr : (uint32_t *)c->tmp.ptr;
+    q.counts = (uint32_t *)c->counts.ptr;
+    q.flags = nullptr;
     return q;
 }
 
-// After pass p: list the flagged output indices, in increasing order, as the input queue of pass p + 1.
-static int compact_queue(vhx_ctx *c, uint32_t p, uint32_t npass, uint64_t nout) {
-    if (p + 1 >= npass) return VHX_OK;
-    size_t tmp = c->seltmp.bytes;
-    VHX_HIP(c, rocprim::select(c->seltmp.ptr, tmp, rocprim::counting_iterator<uint32_t>(0u),
-                               (const uint8_t *)c->flags.ptr, (uint32_t *)c->queue[p & 1u].ptr,
-                               (uint32_t *)c->qctl.ptr + p, (size_t)nout, c->stream));
-    if (p + 2 < npass) VHX_HIP(c, hipMemsetAsync(c->flags.ptr, 0, nout, c->stream));  // flags of the next pass
+// VHX_DEBUG_PASSES=1: synchronise after every pass step and print the queue counters (diagnostics)
+static void debug_passes(vhx_ctx *c, const char *what) {
+    static const bool on = getenv("VHX_DEBUG_PASSES") != nullptr;
+    if (!on || !c->qctl.ptr) return;
+    uint32_t v[16];
+    (void)hipStreamSynchronize(c->stream);
+    (void)hipMemcpy(v, c->qctl.ptr, sizeof(v), hipMemcpyDeviceToHost);
+    fprintf(stderr, "[vhx passes] %-24s counts %u %u %u %u ... %u  grabs %u %u %u %u\n", what, v[0], v[1], v[2], v[3],
+            v[7], v[8], v[9], v[10], v[11]);
+}
+
+// Chunk lists -> queue `out` with its length at *total: pass-0 style (nchunks_host workgroup chunks of stride 256) or
+// queue-pass style (chunks of per_chunk rays, their number derived from the device-side input length n_in).
+static int compact_chunks(vhx_ctx *c, uint32_t nchunks_host, const uint32_t *n_in, uint32_t per_chunk,
+                          uint32_t stride, uint32_t *out, uint32_t *total, uint64_t max_chunks) {
+    const uint32_t *counts = (const uint32_t *)c->counts.ptr;
+    uint32_t *offsets = (uint32_t *)c->offsets.ptr;
+    k_scan_counts<<<1, 1024, 0, c->stream>>>(counts, nchunks_host, n_in, per_chunk, offsets, total);
+    const uint64_t want = (max_chunks + 3) / 4;
+    const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(want, c->queue_blocks));
+    k_gather_chunks<<<grid, 256, 0, c->stream>>>((const uint32_t *)c->tmp.ptr, stride, counts, offsets,
+                                                 nchunks_host, n_in, per_chunk, out);
+    VHX_HIP(c, hipGetLastError());
+    debug_passes(c, "compacted");
     return VHX_OK;
 }
 
 // Queue passes first..npass-1: pass p re-traces the queue of pass p-1 (pass 0's queue, for first == 0, is the list
-// in queue[1] with its length in qctl[7]), flags what exceeds its budget, and the flags are compacted into the next
-// pass's queue.
-template <bool COUNT, int BD, bool SHADOW = false>
+// in queue[1] with its length in qctl[7]); what exceeds its budget is listed per chunk and compacted into the next
+// pass's queue. For first == 1, pass 0 (a grid kernel of nblocks0 workgroups) has just run and is compacted first.
+template <bool COUNT, int BD>
 static int launch_queue_passes(vhx_ctx *c, const DevTree &t, const CamD &cam, const RaySrc &src, const OutD &o,
-                               uint32_t first, uint32_t npass, uint64_t nout) {
+                               uint32_t first, uint32_t npass, uint64_t nout, uint64_t nblocks0,
+                               bool flags_pass0 = false) {
     uint32_t *ctl = (uint32_t *)c->qctl.ptr;
-    int rc = first > 0 ? compact_queue(c, first - 1, npass, nout) : VHX_OK;
+    int rc = VHX_OK;
+    if (first > 0 && npass > 1) {
+        if (flags_pass0) {  // primary frames: per-ray flags compacted in output-index (frame) order
+            const unsigned nb = (unsigned)((nout + 1023) / 1024);
+            uint32_t *counts = (uint32_t *)c->counts.ptr, *offsets = (uint32_t *)c->offsets.ptr;
+            const uint8_t *flags = (const uint8_t *)c->flags.ptr;
+            k_count_flags<<<nb, 256, 0, c->stream>>>(flags, nout, counts);
+            k_scan_counts<<<1, 1024, 0, c->stream>>>(counts, nb, nullptr, 1, offsets, ctl);
+            k_emit_flags<<<nb, 256, 0, c->stream>>>(flags, nout, offsets, (uint32_t *)c->queue[0].ptr);
+            VHX_HIP(c, hipGetLastError());
+            debug_passes(c, "compacted flags");
+        } else {
+            rc = compact_chunks(c, (uint32_t)nblocks0, nullptr, 256, 256, (uint32_t *)c->queue[0].ptr, ctl, nblocks0);
+        }
+    }
     for (uint32_t p = first; p < npass && !rc; ++p) {
         const uint32_t *in = (const uint32_t *)c->queue[(p - 1) & 1u].ptr;  // p = 0: queue[1]
         const uint32_t *in_n = p > 0 ? ctl + (p - 1) : ctl + 7;
-        k_trace_queue<COUNT, BD, SHADOW><<<c->queue_blocks, 256, 0, c->stream>>>(t, cam, src, o, in, in_n,
-                                                                                 ctl + 8 + p, pass_q(c, p, npass));
-        rc = compact_queue(c, p, npass, nout);
+        const PassQ q = pass_q(c, p, npass);
+        k_trace_queue<COUNT, BD><<<c->queue_blocks, 256, 0, c->stream>>>(t, cam, src, o, in, in_n,
+                                                                                 ctl + 8 + p, q);
+        debug_passes(c, "queue pass");
+        if (p + 1 < npass)
+            rc = compact_chunks(c, 0, in_n, q.rpw, q.rpw, (uint32_t *)c->queue[p & 1u].ptr, ctl + p,
+                                (nout + q.rpw - 1) / q.rpw);
     }
     return rc;
 }
@@ -754,7 +915,7 @@ void vhx_destroy(vhx_ctx *c) {
     for (auto &b : c->raw)
         if (b.ptr) (void)hipFree(b.ptr);
     for (DevBuf *b : {&c->hdr, &c->brick_occ, &c->scratch, &c->rays, &c->queue[0], &c->queue[1], &c->qctl,
-                      &c->flags, &c->seltmp})
+                      &c->tmp, &c->counts, &c->offsets, &c->flags})
         if (b->ptr) (void)hipFree(b->ptr);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -912,7 +1073,7 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
                                                            : (uint64_t)my_tiles * T * T;
     VHX_HIP(c, hipSetDevice(c->device));
     HostOut ho;
-    int rc = map_out(c, out, nout, on_device, ho);
+    int rc = map_out(c, out, nout, on_device, ho, layout == VHX_LAYOUT_TILES);
     if (rc) return rc;
     const DevTree t = dev_tree(c);
     const CamD cd = cam_of(cam);
@@ -938,7 +1099,7 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
     const bool simple = c->simple_kernel;
     uint32_t npass = 1;
     if (simple) {
-        rc = prepare_passes(c, nout, npass);
+        rc = prepare_passes(c, nout, nblocks, npass);
         if (rc) return rc;
     }
     RaySrc src{};
@@ -948,22 +1109,23 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
     src.tile_start = tile_start;
     src.tile_stride = tile_stride;
     VHX_HIP(c, hipEventRecord(c->ev0, c->stream));
-    rc = reset_passes(c, nout, npass);
+    rc = reset_passes(c, npass);
     if (rc) return rc;
     const bool count = ho.dev.bytes != nullptr;
     int qrc = VHX_OK;
     auto launch = [&](auto bd_tag) {
         constexpr int BD = decltype(bd_tag)::value;
-        const PassQ q0 = pass_q(c, 0, npass);
+        PassQ q0 = pass_q(c, 0, npass);
+        if (npass > 1) q0.flags = (uint8_t *)c->flags.ptr;
         if (simple) {
             if (count) {
                 k_trace_primary<true, BD><<<(unsigned)nblocks, 256, 0, c->stream>>>(
                     t, cd, ho.dev, T, tiles_x, tile_start, tile_stride, layout, bpx, bpt, q0);
-                qrc = launch_queue_passes<true, BD>(c, t, cd, src, ho.dev, 1, npass, nout);
+                qrc = launch_queue_passes<true, BD>(c, t, cd, src, ho.dev, 1, npass, nout, nblocks, true);
             } else {
                 k_trace_primary<false, BD><<<(unsigned)nblocks, 256, 0, c->stream>>>(
                     t, cd, ho.dev, T, tiles_x, tile_start, tile_stride, layout, bpx, bpt, q0);
-                qrc = launch_queue_passes<false, BD>(c, t, cd, src, ho.dev, 1, npass, nout);
+                qrc = launch_queue_passes<false, BD>(c, t, cd, src, ho.dev, 1, npass, nout, nblocks, true);
             }
         } else if (count) {
             k_trace_persistent<true, BD, TASK><<<pblocks, 256, 0, c->stream>>>(t, cd, ho.dev, fm);
@@ -999,14 +1161,15 @@ int vhx_trace_rays(vhx_ctx *c, const float *rays, uint64_t n, const vhx_hits *ou
     }
     const DevTree t = dev_tree(c);
     uint32_t npass = 1;
-    rc = prepare_passes(c, n, npass);
+    const uint64_t nb64 = (n + 255) / 256;
+    rc = prepare_passes(c, n, nb64, npass);
     if (rc) return rc;
     RaySrc src{};
     src.kind = 2u;
     src.rays = drays;
     CamD cd{};
     VHX_HIP(c, hipEventRecord(c->ev0, c->stream));
-    rc = reset_passes(c, n, npass);
+    rc = reset_passes(c, npass);
     if (rc) return rc;
     const bool count = ho.dev.bytes != nullptr;
     const unsigned nb = (unsigned)((n + 255) / 256);
@@ -1016,10 +1179,10 @@ int vhx_trace_rays(vhx_ctx *c, const float *rays, uint64_t n, const vhx_hits *ou
         const PassQ q0 = pass_q(c, 0, npass);
         if (count) {
             k_trace_rays<true, BD><<<nb, 256, 0, c->stream>>>(t, drays, n, ho.dev, q0);
-            qrc = launch_queue_passes<true, BD>(c, t, cd, src, ho.dev, 1, npass, n);
+            qrc = launch_queue_passes<true, BD>(c, t, cd, src, ho.dev, 1, npass, n, nb64);
         } else {
             k_trace_rays<false, BD><<<nb, 256, 0, c->stream>>>(t, drays, n, ho.dev, q0);
-            qrc = launch_queue_passes<false, BD>(c, t, cd, src, ho.dev, 1, npass, n);
+            qrc = launch_queue_passes<false, BD>(c, t, cd, src, ho.dev, 1, npass, n, nb64);
         }
     };
     if (!dispatch_bd(c->desc.brick_dim, launch)) return fail(c, VHX_E_INVALID_ARG, "unsupported brick_dim");
@@ -1038,7 +1201,8 @@ int vhx_trace_shadows(vhx_ctx *c, const float light[3], uint64_t n, const uint32
     if (n >= 0x7FFFFFFFull) return fail(c, VHX_E_INVALID_ARG, "too many rays");
     VHX_HIP(c, hipSetDevice(c->device));
     uint32_t npass = 1;
-    int rc = prepare_passes(c, n, npass, true);
+    const uint64_t nb64 = (n + 255) / 256;
+    int rc = prepare_passes(c, n, nb64, npass, true);
     if (rc) return rc;
     const DevTree t = dev_tree(c);
     RaySrc src{};
@@ -1054,22 +1218,22 @@ int vhx_trace_shadows(vhx_ctx *c, const float light[3], uint64_t n, const uint32
     so.bytes = bytes;
     CamD cd{};
     VHX_HIP(c, hipEventRecord(c->ev0, c->stream));
-    rc = reset_passes(c, n, npass, true);
+    rc = reset_passes(c, npass, true);
     if (rc) return rc;
     VHX_HIP(c, hipMemsetAsync(shadowed, 0, n * 4, c->stream));
     if (bytes) VHX_HIP(c, hipMemsetAsync(bytes, 0, n * 4, c->stream));
     // wave-dense secondary rays: the hit pixels, in frame order, are pass 0's queue
-    size_t tmp = c->seltmp.bytes;
-    VHX_HIP(c, rocprim::select(c->seltmp.ptr, tmp, rocprim::counting_iterator<uint32_t>(0u),
-                               (uint32_t *)c->queue[1].ptr, (uint32_t *)c->qctl.ptr + 7, (size_t)n, IsHit{value},
-                               c->stream));
+    k_list_hits<<<(unsigned)nb64, 256, 0, c->stream>>>(value, n, (uint32_t *)c->tmp.ptr, (uint32_t *)c->counts.ptr);
+    rc = compact_chunks(c, (uint32_t)nb64, nullptr, 256, 256, (uint32_t *)c->queue[1].ptr,
+                        (uint32_t *)c->qctl.ptr + 7, nb64);
+    if (rc) return rc;
     int qrc = VHX_OK;
     auto launch = [&](auto bd_tag) {
         constexpr int BD = decltype(bd_tag)::value;
         if (bytes)
-            qrc = launch_queue_passes<true, BD, true>(c, t, cd, src, so, 0, npass, n);
+            qrc = launch_queue_passes<true, BD>(c, t, cd, src, so, 0, npass, n, nb64);
         else
-            qrc = launch_queue_passes<false, BD, true>(c, t, cd, src, so, 0, npass, n);
+            qrc = launch_queue_passes<false, BD>(c, t, cd, src, so, 0, npass, n, nb64);
     };
     if (!dispatch_bd(c->desc.brick_dim, launch)) return fail(c, VHX_E_INVALID_ARG, "unsupported brick_dim");
     if (qrc) return qrc;

@@ -193,7 +193,10 @@ class Raytracer:
             self._h = ctypes.c_void_p(None)
 
     def __del__(self):
-        self.close()
+        try:
+            self.close()
+        except (TypeError, AttributeError):  # interpreter shutdown: module globals already torn down
+            pass
 
     def _check(self, rc):
         return N.check(rc, self._h)

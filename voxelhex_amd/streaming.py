@@ -46,7 +46,10 @@ class StreamingView:
             self._h = ctypes.c_void_p(None)
 
     def __del__(self):
-        self.close()
+        try:
+            self.close()
+        except (TypeError, AttributeError):  # interpreter shutdown
+            pass
 
     def _ctx(self):
         return self.raytracer._h if self.raytracer is not None else None
