@@ -34,6 +34,10 @@ struct DevTree {
     const uint32_t *children;  // 64 per node
     const uint32_t *voxels;    // raw PaletteIndexValues, bd^3 per brick
     const uint64_t *brick_occ; // occ_words per brick; bit = flat cell index
+    // brick_dim <= 4 (one occupancy word per brick): per child entry {children[i] (a UniformLeaf's brick in all 64
+    // entries), occupancy word of that brick (lo, hi; 0 unless a Parted brick of a leaf), 0}, so a node iteration
+    // gets the push target, the brick descriptor and the brick's occupancy with one load
+    const uint4 *child_rec;
     const uint32_t *solid;
     const uint32_t *color;
     uint32_t color_count;
@@ -223,19 +227,21 @@ __device__ __forceinline__ void fill_hit(HitOut &h, uint32_t v, uint32_t cell, F
 }
 
 // probe_brick (cpu.rs:236-292) incl. traverse_brick (cpu.rs:136-232).
-// The cell walk is a single-exit loop: an iteration that stops (hit, or step budget spent) computes its DDA step but
-// does not commit it, which costs four selects instead of the exec-mask bookkeeping of extra loop exits. Per-brick
-// constants: unit * max(signum, 0) (the dda_step term size * signum.max(0)) and signum * unit (the bounds step).
-// st_k = usg_k - sg_k * diff_k is formed with one fma: sg_k is +-1, the product is exact, so fma rounds once exactly
-// where the reference's separate multiply and subtract do.
-// Returns true on a hit; a walk that ran out of budget returns false with iters > budget for the caller to see.
+// The entry cell is tested before the loop; the loop steps from an empty cell and tests the next one, so every
+// iteration commits its step unconditionally and the loop has a single exit (left the brick, or hit). A brick walk
+// is at most 3*BD cells, so the step budget of a pass is checked by the caller once per node iteration; inside the
+// walk only the VHX_MAX_ITERS bound is checked. Per-brick constants: unit * max(signum, 0) (the dda_step term
+// size * signum.max(0)) and signum * unit (the bounds step). st_k = usg_k - sg_k * diff_k is formed with one fma:
+// sg_k is +-1, the product is exact, so fma rounds once exactly where the reference's separate multiply and subtract
+// do. Returns true on a hit, with the hit cell's flat index in `hflat` (-1 for a Solid brick); the hit record itself
+// is filled after the traversal loop (finish_hit), so the loop carries two registers for it instead of a dozen.
 template <bool COUNT, int BD>
-__device__ __forceinline__ bool probe_brick(const DevTree &t, const RayD &r, F3d &p, uint32_t desc, CubeD bb,
-                                            HitOut &h, uint32_t &iters, uint32_t budget) {
+__device__ __forceinline__ bool probe_brick(const DevTree &t, const RayD &r, F3d &p, uint32_t desc, uint64_t cocc,
+                                            CubeD bb, HitOut &h, uint32_t &iters, int32_t &hflat) {
     if (desc == VHX_EMPTY) return false;
     if (desc & VHX_SOLID_BIT) {  // BrickData::Solid, cpu.rs:249-260
         if (COUNT) h.bytes += 4;
-        fill_hit(h, t.solid[desc & 0x7FFFFFFFu], VHX_EMPTY, p, bb);
+        hflat = -1;
         return true;
     }
     using B = Brick<BD>;
@@ -253,46 +259,65 @@ __device__ __forceinline__ bool probe_brick(const DevTree &t, const RayD &r, F3d
     const uint32_t *vox = t.voxels + (uint64_t)desc * (uint64_t)B::N3;
     int32_t flat = ix + iy * BD + iz * (BD * BD);
     int32_t word_idx = flat >> 6;
-    uint64_t word = occw[word_idx];
-    bool hit;
-    for (;;) {
-        flat = ix + iy * BD + iz * (BD * BD);
-        if (B::WORDS > 1) {
-            const int32_t wi = flat >> 6;
-            if (wi != word_idx) {
-                word_idx = wi;
-                word = occw[wi];
+    uint64_t word = B::WORDS == 1 ? cocc : occw[word_idx];  // cocc: the child record's copy of occw[0]
+    bool hit = ((word >> (flat & 63)) & 1ull) != 0ull;
+    if (COUNT) h.bytes += 4 + pal_bytes<COUNT>(vox[flat]);  // the reference reads the palettes of every cell
+    if (!hit) {
+        for (;;) {
+            ++iters;
+            // dda_step_to_next_sibling (cpu.rs:104-132) on the cell bounds {cmin, unit}
+            const F3d diff = vsub(p, cmin);
+            const float stx = __builtin_fmaf(-r.sg.x, diff.x, usg.x), sty = __builtin_fmaf(-r.sg.y, diff.y, usg.y),
+                        stz = __builtin_fmaf(-r.sg.z, diff.z, usg.z);
+            const float dx = __builtin_fabsf(stx * r.sf.x), dy = __builtin_fabsf(sty * r.sf.y),
+                        dz = __builtin_fabsf(stz * r.sf.z);
+            const float m = __builtin_fminf(__builtin_fminf(dx, dy), dz);
+            p = mk(p.x + r.d.x * m, p.y + r.d.y * m, p.z + r.d.z * m);
+            const bool mx = m == dx, my = m == dy, mz = m == dz;
+            cmin = mk(mx ? cmin.x + sgu.x : cmin.x, my ? cmin.y + sgu.y : cmin.y, mz ? cmin.z + sgu.z : cmin.z);
+            ix += mx ? r.isx : 0;
+            iy += my ? r.isy : 0;
+            iz += mz ? r.isz : 0;
+            const bool in = (uint32_t)(ix | iy | iz) < (uint32_t)BD;
+            flat = ix + iy * BD + iz * (BD * BD);
+            if (B::WORDS > 1) {
+                const int32_t wi = flat >> 6;
+                if (in && wi != word_idx) {
+                    word_idx = wi;
+                    word = occw[wi];
+                }
             }
+            const bool occupied = in & (((word >> (flat & 63)) & 1ull) != 0ull);
+            if (COUNT && in) h.bytes += 4 + pal_bytes<COUNT>(vox[flat]);
+            // the bound only ends a ray whose steps make no progress (a zero or NaN direction); at the bound the
+            // oracle tests the cell it stepped into and stops before the next step, like this exit
+            if ((!in) | occupied | (iters >= VHX_MAX_ITERS)) break;
         }
-        hit = ((word >> (flat & 63)) & 1ull) != 0ull;
-        if (COUNT) h.bytes += 4 + pal_bytes<COUNT>(vox[flat]);  // the reference reads the palettes of every cell
-        ++iters;
-        const bool stop = hit || iters > budget;
-        // dda_step_to_next_sibling (cpu.rs:104-132) on the cell bounds {cmin, unit}
-        const F3d diff = vsub(p, cmin);
-        const float stx = __builtin_fmaf(-r.sg.x, diff.x, usg.x), sty = __builtin_fmaf(-r.sg.y, diff.y, usg.y),
-                    stz = __builtin_fmaf(-r.sg.z, diff.z, usg.z);
-        const float dx = __builtin_fabsf(stx * r.sf.x), dy = __builtin_fabsf(sty * r.sf.y),
-                    dz = __builtin_fabsf(stz * r.sf.z);
-        const float m = __builtin_fminf(__builtin_fminf(dx, dy), dz);
-        const float pnx = p.x + r.d.x * m, pny = p.y + r.d.y * m, pnz = p.z + r.d.z * m;
-        const bool mx = !stop && m == dx, my = !stop && m == dy, mz = !stop && m == dz;
-        p.x = stop ? p.x : pnx;  // component-wise: a struct select becomes a pointer select through scratch
-        p.y = stop ? p.y : pny;
-        p.z = stop ? p.z : pnz;
-        cmin = mk(mx ? cmin.x + sgu.x : cmin.x, my ? cmin.y + sgu.y : cmin.y, mz ? cmin.z + sgu.z : cmin.z);
-        ix += mx ? r.isx : 0;
-        iy += my ? r.isy : 0;
-        iz += mz ? r.isz : 0;
-        if (stop || (uint32_t)(ix | iy | iz) >= (uint32_t)BD) break;
+        // hit = the exit test, recomputed once from the final cell instead of carrying the loop's booleans out of it
+        // (opaque copies keep the compiler from reusing the in-loop values, which costs mask bookkeeping per cell)
+        asm volatile("" : "+v"(ix), "+v"(iy), "+v"(iz));
+        flat = ix + iy * BD + iz * (BD * BD);
+        hit = (uint32_t)(ix | iy | iz) < (uint32_t)BD && ((word >> (flat & 63)) & 1ull) != 0ull;
     }
-    if (!hit) return false;
-    const uint32_t v = vox[flat];
+    hflat = flat;
+    return hit;
+}
+
+// The hit record of probe_brick (cpu.rs:249-260 for a Solid brick, cpu.rs:268-289 for a cell of a Parted brick):
+// the voxel value, the cell bounds and the impact normal, computed once after the traversal loop.
+template <int BD>
+__device__ __forceinline__ void finish_hit(const DevTree &t, HitOut &h, uint32_t desc, int32_t hflat, F3d p, CubeD bb) {
+    using B = Brick<BD>;
+    if (hflat < 0) {
+        fill_hit(h, t.solid[desc & 0x7FFFFFFFu], VHX_EMPTY, p, bb);
+        return;
+    }
+    const uint32_t ix = (uint32_t)hflat % BD, iy = ((uint32_t)hflat / BD) % BD, iz = (uint32_t)hflat / (BD * BD);
+    const uint32_t v = t.voxels[(uint64_t)desc * (uint64_t)B::N3 + (uint32_t)hflat];
     CubeD hb;
     hb.size = bb.size * B::INV;
     hb.min = vadd(bb.min, vmul(vmul(mk((float)ix, (float)iy, (float)iz), bb.size), B::INV));
-    fill_hit(h, v, (uint32_t)flat, p, hb);
-    return true;
+    fill_hit(h, v, (uint32_t)hflat, p, hb);
 }
 
 // RAY_TO_NODE_OCCUPANCY_BITMASK_LUT in LDS: occ_tab[s * 8 + o] = occ_lut(s, o); filled by the block before tracing.
@@ -301,7 +326,8 @@ __device__ __forceinline__ void fill_occ_tab(uint64_t *occ_tab) {
 }
 
 // BoxTree::get_by_ray, src/raytracing/cpu.rs:296-458.
-// `budget` bounds the loop iterations (node, advance and brick steps). With budget == VHX_MAX_ITERS this is the full
+// `budget` bounds the loop iterations (node, advance and brick steps; checked at the end of each node iteration, so a
+// pass may overrun it by one brick walk and one advance). With budget == VHX_MAX_ITERS this is the full
 // traversal (a ray exceeding the bound is a miss, as in the oracle) and the return value is always true. A smaller
 // budget makes a pass of the multi-pass scheduler: false = the ray was abandoned after `budget` steps and has to be
 // traced again from scratch with a larger budget (the traversal is deterministic, so the re-trace is bit-identical
@@ -347,12 +373,23 @@ __device__ __forceinline__ bool get_by_ray(const DevTree &t, const uint64_t *occ
     ray_scale_factors(r);
     uint32_t node = 0, s1 = 0, s2 = 0, s3 = 0, count = 1;  // push(ROOT)
     uint32_t iters = 1;  // the first node iteration
-    bool ok = true;
+    bool ok = true, hit = false, huni = false;
+    uint32_t hdesc = 0;
+    int32_t hflat = 0;
     for (;;) {
         const uint4 lh = t.hdr[node];
         // the child slot is read by both the leaf probe and the push: issue it with the header load so the
-        // iteration waits for one memory latency instead of two
-        const uint32_t slot = t.children[(uint64_t)node * 64u + (target & 63u)];
+        // iteration waits for one memory latency instead of two (with brick_dim <= 4 the child record also carries
+        // the brick's occupancy word, so a probe waits for no further load)
+        uint32_t slot;
+        uint64_t cocc = 0;
+        if (Brick<BD>::WORDS == 1) {
+            const uint4 cr = t.child_rec[(uint64_t)node * 64u + (target & 63u)];
+            slot = cr.x;
+            cocc = ((uint64_t)cr.z << 32) | (uint64_t)cr.y;
+        } else {
+            slot = t.children[(uint64_t)node * 64u + (target & 63u)];
+        }
         const uint64_t occ = ((uint64_t)lh.y << 32) | (uint64_t)lh.x;
         const uint32_t ntype = lh.z;
         if (COUNT) h.bytes += 12;
@@ -360,9 +397,11 @@ __device__ __forceinline__ bool get_by_ray(const DevTree &t, const uint64_t *occ
         bool done = false;
         if (target < 64u && (uniform || ntype == VHX_NODE_LEAF)) {
             if (COUNT) h.bytes += 4;
-            const uint32_t desc = uniform ? t.children[(uint64_t)node * 64u] : slot;
-            done = probe_brick<COUNT, BD>(t, r, p, desc, uniform ? cur : child_bounds(cur, target), h, iters, budget);
-            h.hit = done;
+            hdesc = Brick<BD>::WORDS == 1 || !uniform ? slot : t.children[(uint64_t)node * 64u];
+            done = probe_brick<COUNT, BD>(t, r, p, hdesc, cocc, uniform ? cur : child_bounds(cur, target), h, iters,
+                                          hflat);
+            huni = uniform;
+            hit = done;
         }
         if (!done) {
             if (uniform || target >= 64u || occ == 0 || (occ & occ_tab[(target & 63u) * 8u + dir_idx]) == 0) {
@@ -390,9 +429,7 @@ __device__ __forceinline__ bool get_by_ray(const DevTree &t, const uint64_t *occ
                         cur.min = mk(0.0f, 0.0f, 0.0f);
                         cur.size = tsize;
                     } else {
-                        // a brick walk that ran out of budget can end in a pop + restart that leaves the root cube
-                        done = true;
-                        ok = iters <= budget || budget >= VHX_MAX_ITERS;
+                        done = true;  // left the tree: a miss
                     }
                 }
             } else if (ntype == VHX_NODE_INTERNAL && ((occ >> target) & 1ull) != 0) {
@@ -411,18 +448,38 @@ __device__ __forceinline__ bool get_by_ray(const DevTree &t, const uint64_t *occ
                     tb = child_bounds(cur, target);
                 }
             } else {
-                // ADVANCE (cpu.rs:416-437); a step past the budget is harmless: the next check abandons the ray
+                // ADVANCE (cpu.rs:416-437); at most 9 steps across the node, the pass budget is checked after it.
+                // Same shape as the brick walk: the sectant is carried as three coordinates, every step is committed
+                // (tb.min after a step out of the node is dead: the next iteration pops and overwrites it), and the
+                // reference's target (step_sectant) is formed once at the end (>= 64 when the walk left the node).
+                const float usx = tb.size * r.sgmax.x, usy = tb.size * r.sgmax.y, usz = tb.size * r.sgmax.z;
+                const float sgx = r.sg.x * tb.size, sgy = r.sg.y * tb.size, sgz = r.sg.z * tb.size;
+                int32_t ax = (int32_t)(target & 3u), ay = (int32_t)((target >> 2) & 3u), az = (int32_t)(target >> 4);
+                bool in;
                 for (;;) {
                     ++iters;
-                    const uint32_t sel = dda_step(r, p, tb);
-                    target = step_sectant(r, target, sel);
-                    const F3d nmin = vadd(tb.min, vmul(step_vec(r, sel), tb.size));
-                    const bool in = target < 64u;
-                    tb.min.x = in ? nmin.x : tb.min.x;  // component-wise select, no branch
-                    tb.min.y = in ? nmin.y : tb.min.y;
-                    tb.min.z = in ? nmin.z : tb.min.z;
-                    if (iters > budget || !in || ((occ >> target) & 1ull) != 0) break;
+                    // dda_step_to_next_sibling (cpu.rs:104-132) on tb, st_k by one exact-product fma as in the brick walk
+                    const F3d diff = vsub(p, tb.min);
+                    const float stx = __builtin_fmaf(-r.sg.x, diff.x, usx), sty = __builtin_fmaf(-r.sg.y, diff.y, usy),
+                                stz = __builtin_fmaf(-r.sg.z, diff.z, usz);
+                    const float dx = __builtin_fabsf(stx * r.sf.x), dy = __builtin_fabsf(sty * r.sf.y),
+                                dz = __builtin_fabsf(stz * r.sf.z);
+                    const float m = __builtin_fminf(__builtin_fminf(dx, dy), dz);
+                    p = mk(p.x + r.d.x * m, p.y + r.d.y * m, p.z + r.d.z * m);
+                    const bool mx = m == dx, my = m == dy, mz = m == dz;
+                    tb.min = mk(mx ? tb.min.x + sgx : tb.min.x, my ? tb.min.y + sgy : tb.min.y,
+                                mz ? tb.min.z + sgz : tb.min.z);
+                    ax += mx ? r.isx : 0;
+                    ay += my ? r.isy : 0;
+                    az += mz ? r.isz : 0;
+                    in = (uint32_t)(ax | ay | az) < 4u;
+                    const uint32_t tg = (uint32_t)(ax + ay * 4 + az * 16);
+                    const bool occupied = in & (((occ >> (tg & 63u)) & 1ull) != 0ull);
+                    if ((!in) | occupied | (iters > VHX_MAX_ITERS)) break;
                 }
+                asm volatile("" : "+v"(ax), "+v"(ay), "+v"(az));
+                in = (uint32_t)(ax | ay | az) < 4u;
+                target = in ? (uint32_t)(ax + ay * 4 + az * 16) : 64u;
             }
             if (!done && ++iters > budget) {  // the next node iteration
                 done = true;
@@ -430,6 +487,10 @@ __device__ __forceinline__ bool get_by_ray(const DevTree &t, const uint64_t *occ
             }
         }
         if (done) break;
+    }
+    if (hit) {  // the loop left on the hit: cur, target and p are those of the probe
+        h.hit = true;
+        finish_hit<BD>(t, h, hdesc, hflat, p, huni ? cur : child_bounds(cur, target));
     }
     return ok;
 }

@@ -43,6 +43,8 @@ struct vhx_ctx {
     vhx_tree_desc desc{};  // counts of the uploaded tree (pointers unused)
     DevBuf raw[7];         // VHX_BUF_* raw copies
     DevBuf hdr, brick_occ, scratch, rays;
+    DevBuf child_rec;         // brick_dim <= 4: DevTree::child_rec, rebuilt before a trace when stale
+    bool child_rec_stale = false;
     DevBuf queue[2];  // multi-pass ray queues (ping-pong), output indices of abandoned rays in increasing order
     DevBuf qctl;      // [0..7] queue lengths written after pass p (7: shadow hit list), [8..15] work counters
     DevBuf tmp;       // chunk-local lists of abandoned rays (a block's or a queue chunk's, in lane order)
@@ -133,6 +135,21 @@ __global__ void __launch_bounds__(256) k_brick_occ_small(const uint32_t *__restr
     for (uint32_t c = 0; c < n3; ++c)
         if (!cell_empty(vox[(uint64_t)b * n3 + c], color, ncolor, data, ndata)) m |= 1ull << c;
     words[b] = m;
+}
+
+// DevTree::child_rec for brick_dim <= 4: one record per child entry
+__global__ void __launch_bounds__(256) k_child_rec(const uint32_t *__restrict__ type,
+                                                   const uint32_t *__restrict__ children,
+                                                   const uint64_t *__restrict__ words, uint32_t brick_count,
+                                                   uint64_t n, uint4 *__restrict__ rec) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t ty = type[i >> 6];
+    const bool uniform = ty == VHX_NODE_UNIFORM_LEAF;
+    const uint32_t v = children[uniform ? (i & ~63ull) : i];
+    uint64_t o = 0;
+    if ((uniform || ty == VHX_NODE_LEAF) && v != VHX_EMPTY && (v & VHX_SOLID_BIT) == 0 && v < brick_count) o = words[v];
+    rec[i] = make_uint4(v, (uint32_t)o, (uint32_t)(o >> 32), 0u);
 }
 
 __global__ void __launch_bounds__(256) k_pack_hdr(const uint32_t *__restrict__ type, const uint64_t *__restrict__ occ,
@@ -614,6 +631,7 @@ static DevTree dev_tree(const vhx_ctx *c) {
     t.children = (const uint32_t *)c->raw[VHX_BUF_NODE_CHILDREN].ptr;
     t.voxels = (const uint32_t *)c->raw[VHX_BUF_VOXELS].ptr;
     t.brick_occ = (const uint64_t *)c->brick_occ.ptr;
+    t.child_rec = (const uint4 *)c->child_rec.ptr;
     t.solid = (const uint32_t *)c->raw[VHX_BUF_SOLID_VALUES].ptr;
     t.color = (const uint32_t *)c->raw[VHX_BUF_COLOR_PALETTE].ptr;
     t.color_count = c->desc.color_count;
@@ -661,6 +679,24 @@ static int rebuild_hdr(vhx_ctx *c, uint32_t n0, uint32_t n) {
                                                        (const uint64_t *)c->raw[VHX_BUF_NODE_OCBITS].ptr, n0, n,
                                                        (uint4 *)c->hdr.ptr);
     VHX_HIP(c, hipGetLastError());
+    return VHX_OK;
+}
+
+static bool has_child_rec(const vhx_ctx *c) {
+    const uint32_t bd = c->desc.brick_dim;
+    return bd * bd * bd <= 64;
+}
+
+// DevTree::child_rec depends on node types, children and brick occupancy: updates mark it stale and the next trace
+// rebuilds it whole (one pass over the child entries, ~n_nodes * 64 * 24 bytes)
+static int refresh_child_rec(vhx_ctx *c) {
+    if (!has_child_rec(c) || !c->child_rec_stale) return VHX_OK;
+    const uint64_t n = (uint64_t)c->desc.node_count * 64;
+    k_child_rec<<<(unsigned)((n + 255) / 256), 256, 0, c->stream>>>(
+        (const uint32_t *)c->raw[VHX_BUF_NODE_TYPE].ptr, (const uint32_t *)c->raw[VHX_BUF_NODE_CHILDREN].ptr,
+        (const uint64_t *)c->brick_occ.ptr, c->desc.brick_count, n, (uint4 *)c->child_rec.ptr);
+    VHX_HIP(c, hipGetLastError());
+    c->child_rec_stale = false;
     return VHX_OK;
 }
 
@@ -914,7 +950,7 @@ void vhx_destroy(vhx_ctx *c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (auto &b : c->raw)
         if (b.ptr) (void)hipFree(b.ptr);
-    for (DevBuf *b : {&c->hdr, &c->brick_occ, &c->scratch, &c->rays, &c->queue[0], &c->queue[1], &c->qctl,
+    for (DevBuf *b : {&c->hdr, &c->brick_occ, &c->child_rec, &c->scratch, &c->rays, &c->queue[0], &c->queue[1], &c->qctl,
                       &c->tmp, &c->counts, &c->offsets, &c->flags})
         if (b->ptr) (void)hipFree(b->ptr);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -977,6 +1013,11 @@ int vhx_upload_tree(vhx_ctx *c, const vhx_tree_desc *t) {
     if (rc) return rc;
     if ((rc = rebuild_hdr(c, 0, t->node_count))) return rc;
     if ((rc = rebuild_occ(c, 0, t->brick_count))) return rc;
+    if (has_child_rec(c)) {
+        if ((rc = ensure(c, c->child_rec, (uint64_t)t->node_count * 64 * 16))) return rc;
+        c->child_rec_stale = true;
+        if ((rc = refresh_child_rec(c))) return rc;
+    }
     VHX_HIP(c, hipStreamSynchronize(c->stream));
     c->uploaded = true;
     return VHX_OK;
@@ -1000,6 +1041,7 @@ int vhx_update_range(vhx_ctx *c, int id, uint64_t off, uint64_t count, const voi
     } else if (id == VHX_BUF_COLOR_PALETTE || id == VHX_BUF_DATA_PALETTE)
         rc = rebuild_occ(c, 0, c->desc.brick_count);
     if (rc) return rc;
+    if (id != VHX_BUF_NODE_OCBITS && id != VHX_BUF_SOLID_VALUES) c->child_rec_stale = true;
     VHX_HIP(c, hipStreamSynchronize(c->stream));
     return VHX_OK;
 }
@@ -1020,7 +1062,7 @@ int vhx_read_derived(vhx_ctx *c, int which, uint64_t off, uint64_t count, void *
 
 int vhx_tree_device_bytes(const vhx_ctx *c, uint64_t *bytes) {
     if (!c || !bytes) return VHX_E_INVALID_ARG;
-    uint64_t b = c->hdr.bytes + c->brick_occ.bytes;
+    uint64_t b = c->hdr.bytes + c->brick_occ.bytes + c->child_rec.bytes;
     for (auto &r : c->raw) b += r.bytes;
     *bytes = b;
     return VHX_OK;
@@ -1075,6 +1117,7 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
     HostOut ho;
     int rc = map_out(c, out, nout, on_device, ho, layout == VHX_LAYOUT_TILES);
     if (rc) return rc;
+    if ((rc = refresh_child_rec(c))) return rc;
     const DevTree t = dev_tree(c);
     const CamD cd = cam_of(cam);
     FrameMap fm{};
@@ -1159,6 +1202,7 @@ int vhx_trace_rays(vhx_ctx *c, const float *rays, uint64_t n, const vhx_hits *ou
         VHX_HIP(c, hipMemcpyAsync(c->rays.ptr, rays, n * 24, hipMemcpyHostToDevice, c->stream));
         drays = (const float *)c->rays.ptr;
     }
+    if ((rc = refresh_child_rec(c))) return rc;
     const DevTree t = dev_tree(c);
     uint32_t npass = 1;
     const uint64_t nb64 = (n + 255) / 256;
@@ -1204,6 +1248,7 @@ int vhx_trace_shadows(vhx_ctx *c, const float light[3], uint64_t n, const uint32
     const uint64_t nb64 = (n + 255) / 256;
     int rc = prepare_passes(c, n, nb64, npass, true);
     if (rc) return rc;
+    if ((rc = refresh_child_rec(c))) return rc;
     const DevTree t = dev_tree(c);
     RaySrc src{};
     src.kind = 3u;
