@@ -230,11 +230,9 @@ __device__ __forceinline__ void fill_hit(HitOut &h, uint32_t v, uint32_t cell, F
 // The entry cell is tested before the loop; the loop steps from an empty cell and tests the next one, so every
 // iteration commits its step unconditionally and the loop has a single exit (left the brick, or hit). A brick walk
 // is at most 3*BD cells, so the step budget of a pass is checked by the caller once per node iteration; inside the
-// walk only the VHX_MAX_ITERS bound is checked. Per-brick constants: unit * max(signum, 0) (the dda_step term
-// size * signum.max(0)) and signum * unit (the bounds step). st_k = usg_k - sg_k * diff_k is formed with one fma:
-// sg_k is +-1, the product is exact, so fma rounds once exactly where the reference's separate multiply and subtract
-// do. Returns true on a hit, with the hit cell's flat index in `hflat` (-1 for a Solid brick); the hit record itself
-// is filled after the traversal loop (finish_hit), so the loop carries two registers for it instead of a dozen.
+// walk only the VHX_MAX_ITERS bound is checked (the DDA arithmetic is described at the loop). Returns true on a hit,
+// with the hit cell's flat index in `hflat` (-1 for a Solid brick); the hit record itself is filled after the
+// traversal loop (finish_hit), so the loop carries two registers for it instead of a dozen.
 template <bool COUNT, int BD>
 __device__ __forceinline__ bool probe_brick(const DevTree &t, const RayD &r, F3d &p, uint32_t desc, uint64_t cocc,
                                             CubeD bb, HitOut &h, uint32_t &iters, int32_t &hflat) {
@@ -252,9 +250,6 @@ __device__ __forceinline__ bool probe_brick(const DevTree &t, const RayD &r, F3d
     iy = iy < 0 ? 0 : (iy > BD - 1 ? BD - 1 : iy);
     iz = iz < 0 ? 0 : (iz > BD - 1 ? BD - 1 : iz);
     const float unit = bb.size * B::INV;
-    F3d cmin = vadd(bb.min, vmul(mk((float)ix, (float)iy, (float)iz), unit));
-    const F3d usg = mk(unit * r.sgmax.x, unit * r.sgmax.y, unit * r.sgmax.z);
-    const F3d sgu = mk(r.sg.x * unit, r.sg.y * unit, r.sg.z * unit);
     const uint64_t *occw = t.brick_occ + (uint64_t)desc * B::WORDS;
     const uint32_t *vox = t.voxels + (uint64_t)desc * (uint64_t)B::N3;
     int32_t flat = ix + iy * BD + iz * (BD * BD);
@@ -263,41 +258,51 @@ __device__ __forceinline__ bool probe_brick(const DevTree &t, const RayD &r, F3d
     bool hit = ((word >> (flat & 63)) & 1ull) != 0ull;
     if (COUNT) h.bytes += 4 + pal_bytes<COUNT>(vox[flat]);  // the reference reads the palettes of every cell
     if (!hit) {
+        // Cell walk in exit-plane form. The reference's st_k = unit * max(sg_k, 0) - sg_k * (p_k - cmin_k): the
+        // difference p_k - cmin_k is exact (cmin_k is a multiple of unit and p_k lies within a unit of it, so
+        // Sterbenz applies, or cmin_k = 0), hence for sg_k = +1 st_k = unit - (p_k - cmin_k) and (cmin_k + unit) - p_k
+        // are the same real number rounded once, and for sg_k = -1 st_k = p_k - cmin_k exactly. With the exit plane
+        // e_k = cmin_k + unit * max(sg_k, 0) (exact), |st_k * sf_k| = |(e_k - p_k) * sf_k| bit for bit.
+        // Cell indices are carried direction-normalised (j_k = i_k, or BD-1-i_k for a negative direction), so a
+        // step adds 1 and the flat index is j-flat ^ F.
+        F3d e = vadd(vadd(bb.min, vmul(mk((float)ix, (float)iy, (float)iz), unit)),
+                     mk(unit * r.sgmax.x, unit * r.sgmax.y, unit * r.sgmax.z));
+        const F3d sgu = mk(r.sg.x * unit, r.sg.y * unit, r.sg.z * unit);
+        const uint32_t fx = r.isx > 0 ? 0u : BD - 1u, fy = r.isy > 0 ? 0u : BD - 1u, fz = r.isz > 0 ? 0u : BD - 1u;
+        const uint32_t F = fx + fy * BD + fz * (BD * BD);
+        uint32_t jx = (uint32_t)ix ^ fx, jy = (uint32_t)iy ^ fy, jz = (uint32_t)iz ^ fz;
         for (;;) {
             ++iters;
-            // dda_step_to_next_sibling (cpu.rs:104-132) on the cell bounds {cmin, unit}
-            const F3d diff = vsub(p, cmin);
-            const float stx = __builtin_fmaf(-r.sg.x, diff.x, usg.x), sty = __builtin_fmaf(-r.sg.y, diff.y, usg.y),
-                        stz = __builtin_fmaf(-r.sg.z, diff.z, usg.z);
-            const float dx = __builtin_fabsf(stx * r.sf.x), dy = __builtin_fabsf(sty * r.sf.y),
-                        dz = __builtin_fabsf(stz * r.sf.z);
+            // dda_step_to_next_sibling (cpu.rs:104-132) on the cell {cmin, unit}
+            const float dx = __builtin_fabsf((e.x - p.x) * r.sf.x), dy = __builtin_fabsf((e.y - p.y) * r.sf.y),
+                        dz = __builtin_fabsf((e.z - p.z) * r.sf.z);
             const float m = __builtin_fminf(__builtin_fminf(dx, dy), dz);
             p = mk(p.x + r.d.x * m, p.y + r.d.y * m, p.z + r.d.z * m);
             const bool mx = m == dx, my = m == dy, mz = m == dz;
-            cmin = mk(mx ? cmin.x + sgu.x : cmin.x, my ? cmin.y + sgu.y : cmin.y, mz ? cmin.z + sgu.z : cmin.z);
-            ix += mx ? r.isx : 0;
-            iy += my ? r.isy : 0;
-            iz += mz ? r.isz : 0;
-            const bool in = (uint32_t)(ix | iy | iz) < (uint32_t)BD;
-            flat = ix + iy * BD + iz * (BD * BD);
+            e = mk(mx ? e.x + sgu.x : e.x, my ? e.y + sgu.y : e.y, mz ? e.z + sgu.z : e.z);
+            jx += (uint32_t)mx;
+            jy += (uint32_t)my;
+            jz += (uint32_t)mz;
+            const bool in = (jx | jy | jz) < (uint32_t)BD;
+            const uint32_t uflat = (jx + jy * BD + jz * (BD * BD)) ^ F;
             if (B::WORDS > 1) {
-                const int32_t wi = flat >> 6;
+                const int32_t wi = (int32_t)(uflat >> 6);
                 if (in && wi != word_idx) {
                     word_idx = wi;
                     word = occw[wi];
                 }
             }
-            const bool occupied = in & (((word >> (flat & 63)) & 1ull) != 0ull);
-            if (COUNT && in) h.bytes += 4 + pal_bytes<COUNT>(vox[flat]);
+            const bool occupied = in & (((word >> (uflat & 63u)) & 1ull) != 0ull);
+            if (COUNT && in) h.bytes += 4 + pal_bytes<COUNT>(vox[uflat]);
             // the bound only ends a ray whose steps make no progress (a zero or NaN direction); at the bound the
             // oracle tests the cell it stepped into and stops before the next step, like this exit
             if ((!in) | occupied | (iters >= VHX_MAX_ITERS)) break;
         }
         // hit = the exit test, recomputed once from the final cell instead of carrying the loop's booleans out of it
         // (opaque copies keep the compiler from reusing the in-loop values, which costs mask bookkeeping per cell)
-        asm volatile("" : "+v"(ix), "+v"(iy), "+v"(iz));
-        flat = ix + iy * BD + iz * (BD * BD);
-        hit = (uint32_t)(ix | iy | iz) < (uint32_t)BD && ((word >> (flat & 63)) & 1ull) != 0ull;
+        asm volatile("" : "+v"(jx), "+v"(jy), "+v"(jz));
+        flat = (int32_t)((jx + jy * BD + jz * (BD * BD)) ^ F);
+        hit = (jx | jy | jz) < (uint32_t)BD && ((word >> (flat & 63)) & 1ull) != 0ull;
     }
     hflat = flat;
     return hit;
@@ -449,37 +454,34 @@ __device__ __forceinline__ bool get_by_ray(const DevTree &t, const uint64_t *occ
                 }
             } else {
                 // ADVANCE (cpu.rs:416-437); at most 9 steps across the node, the pass budget is checked after it.
-                // Same shape as the brick walk: the sectant is carried as three coordinates, every step is committed
-                // (tb.min after a step out of the node is dead: the next iteration pops and overwrites it), and the
-                // reference's target (step_sectant) is formed once at the end (>= 64 when the walk left the node).
-                const float usx = tb.size * r.sgmax.x, usy = tb.size * r.sgmax.y, usz = tb.size * r.sgmax.z;
-                const float sgx = r.sg.x * tb.size, sgy = r.sg.y * tb.size, sgz = r.sg.z * tb.size;
-                int32_t ax = (int32_t)(target & 3u), ay = (int32_t)((target >> 2) & 3u), az = (int32_t)(target >> 4);
-                bool in;
+                // Same form as the brick walk (exit planes, direction-normalised sectant coordinates). Every step is
+                // committed: tb.min after a step out of the node is dead (the next iteration pops and overwrites it).
+                // The reference's target (step_sectant) is formed once at the end (>= 64 when the walk left the node).
+                const F3d usg = mk(tb.size * r.sgmax.x, tb.size * r.sgmax.y, tb.size * r.sgmax.z);
+                const F3d sgs = mk(r.sg.x * tb.size, r.sg.y * tb.size, r.sg.z * tb.size);
+                const uint32_t fx = r.isx > 0 ? 0u : 3u, fy = r.isy > 0 ? 0u : 3u, fz = r.isz > 0 ? 0u : 3u;
+                const uint32_t F = fx + fy * 4u + fz * 16u;
+                uint32_t jx = (target & 3u) ^ fx, jy = ((target >> 2) & 3u) ^ fy, jz = (target >> 4) ^ fz;
+                F3d e = vadd(tb.min, usg);
                 for (;;) {
                     ++iters;
-                    // dda_step_to_next_sibling (cpu.rs:104-132) on tb, st_k by one exact-product fma as in the brick walk
-                    const F3d diff = vsub(p, tb.min);
-                    const float stx = __builtin_fmaf(-r.sg.x, diff.x, usx), sty = __builtin_fmaf(-r.sg.y, diff.y, usy),
-                                stz = __builtin_fmaf(-r.sg.z, diff.z, usz);
-                    const float dx = __builtin_fabsf(stx * r.sf.x), dy = __builtin_fabsf(sty * r.sf.y),
-                                dz = __builtin_fabsf(stz * r.sf.z);
+                    const float dx = __builtin_fabsf((e.x - p.x) * r.sf.x), dy = __builtin_fabsf((e.y - p.y) * r.sf.y),
+                                dz = __builtin_fabsf((e.z - p.z) * r.sf.z);
                     const float m = __builtin_fminf(__builtin_fminf(dx, dy), dz);
                     p = mk(p.x + r.d.x * m, p.y + r.d.y * m, p.z + r.d.z * m);
                     const bool mx = m == dx, my = m == dy, mz = m == dz;
-                    tb.min = mk(mx ? tb.min.x + sgx : tb.min.x, my ? tb.min.y + sgy : tb.min.y,
-                                mz ? tb.min.z + sgz : tb.min.z);
-                    ax += mx ? r.isx : 0;
-                    ay += my ? r.isy : 0;
-                    az += mz ? r.isz : 0;
-                    in = (uint32_t)(ax | ay | az) < 4u;
-                    const uint32_t tg = (uint32_t)(ax + ay * 4 + az * 16);
+                    e = mk(mx ? e.x + sgs.x : e.x, my ? e.y + sgs.y : e.y, mz ? e.z + sgs.z : e.z);
+                    jx += (uint32_t)mx;
+                    jy += (uint32_t)my;
+                    jz += (uint32_t)mz;
+                    const bool in = (jx | jy | jz) < 4u;
+                    const uint32_t tg = (jx + jy * 4u + jz * 16u) ^ F;
                     const bool occupied = in & (((occ >> (tg & 63u)) & 1ull) != 0ull);
                     if ((!in) | occupied | (iters > VHX_MAX_ITERS)) break;
                 }
-                asm volatile("" : "+v"(ax), "+v"(ay), "+v"(az));
-                in = (uint32_t)(ax | ay | az) < 4u;
-                target = in ? (uint32_t)(ax + ay * 4 + az * 16) : 64u;
+                asm volatile("" : "+v"(jx), "+v"(jy), "+v"(jz));
+                target = (jx | jy | jz) < 4u ? (jx + jy * 4u + jz * 16u) ^ F : 64u;
+                tb.min = vsub(e, usg);  // exact: e - usg undoes the exact e = tb.min + usg
             }
             if (!done && ++iters > budget) {  // the next node iteration
                 done = true;
