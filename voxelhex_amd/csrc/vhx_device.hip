@@ -51,6 +51,7 @@ struct vhx_ctx {
     DevBuf counts;    // rays listed per chunk
     DevBuf offsets;   // exclusive scan of counts
     DevBuf flags;     // primary pass 0: abandoned flag per output index
+    DevBuf qargs;     // QueueArgs of the queue passes
     uint32_t occ_words = 1;
     bool simple_kernel = true;  // VHX_PERSISTENT=1 selects the persistent wave-refill kernel (A/B)
     // step budgets of the passes before the final (unbounded) one; VHX_BUDGETS="64" / "32,256" style override
@@ -551,10 +552,20 @@ __device__ __forceinline__ void store_shadow(const OutD &o, uint64_t i, const Hi
     if (o.bytes) o.bytes[i] = h.bytes;
 }
 
+// Camera, ray source and outputs of a queue pass: read through a pointer where a wave picks up or stores a ray, so
+// they do not occupy scalar registers across the traversal (as kernel arguments they did, and spilled ~100 SGPRs)
+struct QueueArgs {
+    CamD cam;
+    RaySrc src;
+    OutD out;
+};
+__global__ void k_put_queue_args(QueueArgs a, QueueArgs *dst) {
+    if (threadIdx.x == 0) *dst = a;
+}
+
 template <bool COUNT, int BD>
-__global__ void __launch_bounds__(256) k_trace_queue(DevTree t, CamD cam, RaySrc src, OutD out,
-                                                     const uint32_t *__restrict__ in, const uint32_t *in_n,
-                                                     uint32_t *grab, PassQ q) {
+__global__ void __launch_bounds__(256) k_trace_queue(DevTree t, const QueueArgs *qa, const uint32_t *__restrict__ in,
+                                                     const uint32_t *in_n, uint32_t *grab, PassQ q) {
     __shared__ uint64_t occ_tab[512];
     fill_occ_tab(occ_tab);
     __syncthreads();
@@ -571,14 +582,19 @@ __global__ void __launch_bounds__(256) k_trace_queue(DevTree t, CamD cam, RaySrc
         if (lane < q.rpw && i < n) {
             idx = in[i];
             F3d o, d;
-            ray_of(cam, src, idx, o, d);
+            const QueueArgs *a = qa;
+            asm volatile("" : "+s"(a));  // loads through `a` stay here (not hoisted into live registers)
+            ray_of(a->cam, a->src, idx, o, d);
             HitOut h;
-            if (!get_by_ray<COUNT, BD>(t, occ_tab, o, d, h, q.budget))
+            const bool fin = get_by_ray<COUNT, BD>(t, occ_tab, o, d, h, q.budget);
+            const QueueArgs *b = qa;
+            asm volatile("" : "+s"(b));
+            if (!fin)
                 push = true;
-            else if (src.kind == 3u)
-                store_shadow(out, idx, h);
+            else if (b->src.kind == 3u)
+                store_shadow(b->out, idx, h);
             else
-                store(t, out, idx, o, h);
+                store(t, b->out, idx, o, h);
         }
         if (q.tmp) {  // this chunk's abandoned rays, in lane order
             const uint32_t chunk = base / q.rpw;
@@ -784,6 +800,7 @@ static int prepare_passes(vhx_ctx *c, uint64_t nout, uint64_t nblocks0, uint32_t
     int rc = ensure(c, c->queue[0], nout * 4);
     if (!rc && (npass > 2 || shadow)) rc = ensure(c, c->queue[1], nout * 4);
     if (!rc) rc = ensure(c, c->qctl, 16 * sizeof(uint32_t));
+    if (!rc) rc = ensure(c, c->qargs, sizeof(QueueArgs));
     if (!rc) rc = ensure(c, c->tmp, list * 4);
     if (!rc) rc = ensure(c, c->counts, chunks * 4);
     if (!rc) rc = ensure(c, c->offsets, chunks * 4);
@@ -859,12 +876,16 @@ static int launch_queue_passes(vhx_ctx *c, const DevTree &t, const CamD &cam, co
             rc = compact_chunks(c, (uint32_t)nblocks0, nullptr, 256, 256, (uint32_t *)c->queue[0].ptr, ctl, nblocks0);
         }
     }
+    QueueArgs *qa = (QueueArgs *)c->qargs.ptr;
+    if (first < npass) {
+        k_put_queue_args<<<1, 64, 0, c->stream>>>(QueueArgs{cam, src, o}, qa);
+        VHX_HIP(c, hipGetLastError());
+    }
     for (uint32_t p = first; p < npass && !rc; ++p) {
         const uint32_t *in = (const uint32_t *)c->queue[(p - 1) & 1u].ptr;  // p = 0: queue[1]
         const uint32_t *in_n = p > 0 ? ctl + (p - 1) : ctl + 7;
         const PassQ q = pass_q(c, p, npass);
-        k_trace_queue<COUNT, BD><<<c->queue_blocks, 256, 0, c->stream>>>(t, cam, src, o, in, in_n,
-                                                                                 ctl + 8 + p, q);
+        k_trace_queue<COUNT, BD><<<c->queue_blocks, 256, 0, c->stream>>>(t, qa, in, in_n, ctl + 8 + p, q);
         debug_passes(c, "queue pass");
         if (p + 1 < npass)
             rc = compact_chunks(c, 0, in_n, q.rpw, q.rpw, (uint32_t *)c->queue[p & 1u].ptr, ctl + p,
@@ -951,7 +972,7 @@ void vhx_destroy(vhx_ctx *c) {
     for (auto &b : c->raw)
         if (b.ptr) (void)hipFree(b.ptr);
     for (DevBuf *b : {&c->hdr, &c->brick_occ, &c->child_rec, &c->scratch, &c->rays, &c->queue[0], &c->queue[1], &c->qctl,
-                      &c->tmp, &c->counts, &c->offsets, &c->flags})
+                      &c->tmp, &c->counts, &c->offsets, &c->flags, &c->qargs})
         if (b->ptr) (void)hipFree(b->ptr);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
