@@ -23,7 +23,7 @@ def rays(pix):
     return np.repeat(o[None], len(pix), 0), d.astype(np.float32)
 
 rt.set_pass_budgets((1,))
-for name, pix in (("longest", z["top64"][:1]), ("top64", z["top64"]), ("tail>1024", z["tail"][z["steps"] > 1024]),
+for name, pix in (("longest", z["top64"][:1]), ("top64", z["top64"]), ("tail>1024", z["tail"][z["steps"][z["tail"]] > 1024]),
                   ("tail>256", z["tail"])):
     oo, dd = rays(pix)
     ts = []

@@ -25,7 +25,7 @@ def main():
     for sched in ((), (32, 256)):
         rt.set_pass_budgets(sched)
         for name, pix in (("longest", z["top64"][:1]), ("top64", z["top64"]), ("top64x16", np.tile(z["top64"], 16)),
-                          ("tail>256", z["tail"]), ("tail>1024", z["tail"][z["steps"] > 1024]),
+                          ("tail>256", z["tail"]), ("tail>1024", z["tail"][z["steps"][z["tail"]] > 1024]),
                           ("tail>256 shuffled", z["tail_shuf"]), ("tail>64", z["t64"]), ("tail>64 shuffled", z["t64_shuf"])):
             oo, dd = rays(pix)
             ts = []

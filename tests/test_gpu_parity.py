@@ -247,6 +247,34 @@ def test_multipass_schedule_is_bit_identical(gpu, oracle, budgets):
         gpu.set_pass_budgets(DEFAULT_BUDGETS)
 
 
+SCHEDULER_ENVS = [{"VHX_RESUME": "0"},                                   # abandoned rays re-traced from scratch
+                  {"VHX_RPW": "0,0", "VHX_TW": "7"},                      # adaptive rays per wave, few waves
+                  {"VHX_RPW": "0,3", "VHX_TW": "100000", "VHX_QBLOCK": "64"}]  # one ray per wave, 1-wave workgroups
+
+
+@pytest.mark.parametrize("env", SCHEDULER_ENVS, ids=lambda e: "+".join(f"{k}={v}" for k, v in e.items()))
+def test_scheduler_variants_are_bit_identical(oracle, monkeypatch, env):
+    """Scheduler knobs read at context creation (re-trace instead of resume, adaptive rays per wave, queue
+    workgroup size) change only the schedule: results and byte counts stay the oracle's."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    rt = vhx.Raytracer(0)
+    try:
+        flat = vhx.FlatTree.build_scene(N.VHX_SCENE_LATTICE_CUBE, 256, 4)
+        rt.upload(flat)
+        rng = np.random.default_rng(11)
+        o, d = rand_rays(rng, 256, 8000)
+        cam = vhx.glass_camera(256, 160, 96, target=(128.0, 128.0, 128.0))
+        ref_rays = oracle.trace_rays(flat, o, d, count_bytes=True)
+        ref_frame = oracle.trace_primary(flat, cam, 0, 0, 160, 96, count_bytes=True)
+        for budgets in ((2, 9, 30), (16,)):
+            rt.set_pass_budgets(budgets)
+            assert_same(rt.trace_rays(o, d, count_bytes=True), ref_rays, f"rays {env} {budgets}")
+            assert_same(rt.trace_primary(cam, count_bytes=True), ref_frame, f"frame {env} {budgets}")
+    finally:
+        rt.close()
+
+
 def test_pass_budget_validation(gpu):
     for bad in ((0,), (5, 5), (9, 3), (1, 2, 3, 4), (1 << 22,)):
         with pytest.raises(N.VhxError):

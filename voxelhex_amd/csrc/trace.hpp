@@ -330,13 +330,28 @@ __device__ __forceinline__ void fill_occ_tab(uint64_t *occ_tab) {
     for (uint32_t i = threadIdx.x; i < 512u; i += blockDim.x) occ_tab[i] = occ_lut(i >> 3, i & 7u);
 }
 
+// Saved traversal state of a ray abandoned at a pass budget (multi-pass scheduling): everything the loop below
+// carries from one node iteration to the next, 64 bytes. Cube sizes are powers of two (zero mantissa), so the
+// current cube's size word also holds the target sectant (7 bits) and the stack depth (3 bits).
+__device__ __forceinline__ void save_state(uint4 *st, F3d p, uint32_t iters, CubeD cur, CubeD tb, uint32_t target,
+                                           uint32_t count, uint32_t node, uint32_t s1, uint32_t s2, uint32_t s3) {
+    st[0] = make_uint4(__float_as_uint(p.x), __float_as_uint(p.y), __float_as_uint(p.z), iters);
+    st[1] = make_uint4(__float_as_uint(cur.min.x), __float_as_uint(cur.min.y), __float_as_uint(cur.min.z),
+                       __float_as_uint(cur.size) | target | (count << 8));
+    st[2] = make_uint4(__float_as_uint(tb.min.x), __float_as_uint(tb.min.y), __float_as_uint(tb.min.z),
+                       __float_as_uint(tb.size));
+    st[3] = make_uint4(node, s1, s2, s3);
+}
+
 // BoxTree::get_by_ray, src/raytracing/cpu.rs:296-458.
-// `budget` bounds the loop iterations (node, advance and brick steps; checked at the end of each node iteration, so a
-// pass may overrun it by one brick walk and one advance). With budget == VHX_MAX_ITERS this is the full
-// traversal (a ray exceeding the bound is a miss, as in the oracle) and the return value is always true. A smaller
-// budget makes a pass of the multi-pass scheduler: false = the ray was abandoned after `budget` steps and has to be
-// traced again from scratch with a larger budget (the traversal is deterministic, so the re-trace is bit-identical
-// to an uninterrupted one).
+// `budget` bounds the loop iterations (node, advance and brick steps, counted from the ray's start; checked at the end
+// of each node iteration, so a pass may overrun it by one brick walk and one advance). With budget == VHX_MAX_ITERS
+// this is the full traversal (a ray exceeding the bound is a miss, as in the oracle) and the return value is always
+// true. A smaller budget makes a pass of the multi-pass scheduler: false = the ray was abandoned after `budget` steps;
+// with `sbase` given, its state is saved at sbase[4 * sidx] and a later pass continues it (`resume`) exactly where it
+// stopped, otherwise the later pass traces it again from scratch. Either way the result is bit-identical to one
+// uninterrupted traversal (the state is saved whole; the traversal is deterministic). h.bytes is the caller's running byte count
+// (COUNT builds): 0 for a fresh ray, the count at the abandon for a resumed one.
 //
 // Control flow: the reference's two nested loops (restart from the root / walk the NodeStack) are one loop here, and
 // every way out of it sets `done` and leaves through a single exit at the bottom of the iteration. The NodeStack<u32,
@@ -344,9 +359,10 @@ __device__ __forceinline__ void fill_occ_tab(uint64_t *occ_tab) {
 // drops the oldest entry, a pop that empties it ends the walk and restarts from the root.
 template <bool COUNT, int BD>
 __device__ __forceinline__ bool get_by_ray(const DevTree &t, const uint64_t *occ_tab, F3d o, F3d d, HitOut &h,
-                                           uint32_t budget) {
+                                           uint32_t budget, uint4 *sbase = nullptr, uint32_t sidx = 0,
+                                           bool resume = false) {
+    // the state slot is addressed from a uniform base and the ray's index (one VGPR live, not a 64-bit pointer)
     h.hit = false;
-    h.bytes = 0;
     RayD r;
     ray_setup(r, o, d);
     uint32_t dir_idx;
@@ -356,12 +372,28 @@ __device__ __forceinline__ bool get_by_ray(const DevTree &t, const uint64_t *occ
     }
     const float tsize = (float)t.size;
     CubeD cur;
-    cur.min = mk(0.0f, 0.0f, 0.0f);
-    cur.size = tsize;
     F3d p;
     uint32_t target;
     CubeD tb;
-    {
+    uint32_t node, s1, s2, s3, count, iters;
+    if (resume) {
+        const uint4 *st = sbase + 4ull * sidx;
+        const uint4 a = st[0], b = st[1], c = st[2], e = st[3];
+        p = mk(__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(a.z));
+        iters = a.w;
+        cur.min = mk(__uint_as_float(b.x), __uint_as_float(b.y), __uint_as_float(b.z));
+        cur.size = __uint_as_float(b.w & 0xFF800000u);
+        target = b.w & 0x7Fu;
+        count = (b.w >> 8) & 7u;
+        tb.min = mk(__uint_as_float(c.x), __uint_as_float(c.y), __uint_as_float(c.z));
+        tb.size = __uint_as_float(c.w);
+        node = e.x;
+        s1 = e.y;
+        s2 = e.z;
+        s3 = e.w;
+    } else {
+        cur.min = mk(0.0f, 0.0f, 0.0f);
+        cur.size = tsize;
         // Cube::intersect_ray, src/spatial/raytracing/mod.rs:33-62 (root: min 0, max = 0 + size = size)
         const float t1 = (0.0f - o.x) / d.x, t2 = (tsize - o.x) / d.x;
         const float t3 = (0.0f - o.y) / d.y, t4 = (tsize - o.y) / d.y;
@@ -374,10 +406,10 @@ __device__ __forceinline__ bool get_by_ray(const DevTree &t, const uint64_t *occ
         p = vadd(o, vmul(d, tmin < 0.0f ? 0.0f : tmin));
         target = offset_sectant(p, cur.size);
         tb = child_bounds(cur, target);
+        node = 0, s1 = 0, s2 = 0, s3 = 0, count = 1;  // push(ROOT)
+        iters = 1;  // the first node iteration
     }
     ray_scale_factors(r);
-    uint32_t node = 0, s1 = 0, s2 = 0, s3 = 0, count = 1;  // push(ROOT)
-    uint32_t iters = 1;  // the first node iteration
     bool ok = true, hit = false, huni = false;
     uint32_t hdesc = 0;
     int32_t hflat = 0;
@@ -454,9 +486,9 @@ __device__ __forceinline__ bool get_by_ray(const DevTree &t, const uint64_t *occ
                 }
             } else {
                 // ADVANCE (cpu.rs:416-437); at most 9 steps across the node, the pass budget is checked after it.
-                // Same form as the brick walk (exit planes, direction-normalised sectant coordinates). Every step is
-                // committed: tb.min after a step out of the node is dead (the next iteration pops and overwrites it).
-                // The reference's target (step_sectant) is formed once at the end (>= 64 when the walk left the node).
+                // Same form as the brick walk (exit planes, direction-normalised sectant coordinates). Every step
+                // is committed: tb.min after a step out of the node is dead (the next iteration pops and overwrites it).
+                // The reference's target (step_sectant) is formed once at the end (>= 64: the walk left the node).
                 const F3d usg = mk(tb.size * r.sgmax.x, tb.size * r.sgmax.y, tb.size * r.sgmax.z);
                 const F3d sgs = mk(r.sg.x * tb.size, r.sg.y * tb.size, r.sg.z * tb.size);
                 const uint32_t fx = r.isx > 0 ? 0u : 3u, fy = r.isy > 0 ? 0u : 3u, fz = r.isz > 0 ? 0u : 3u;
@@ -465,7 +497,8 @@ __device__ __forceinline__ bool get_by_ray(const DevTree &t, const uint64_t *occ
                 F3d e = vadd(tb.min, usg);
                 for (;;) {
                     ++iters;
-                    const float dx = __builtin_fabsf((e.x - p.x) * r.sf.x), dy = __builtin_fabsf((e.y - p.y) * r.sf.y),
+                    const float dx = __builtin_fabsf((e.x - p.x) * r.sf.x),
+                                dy = __builtin_fabsf((e.y - p.y) * r.sf.y),
                                 dz = __builtin_fabsf((e.z - p.z) * r.sf.z);
                     const float m = __builtin_fminf(__builtin_fminf(dx, dy), dz);
                     p = mk(p.x + r.d.x * m, p.y + r.d.y * m, p.z + r.d.z * m);
@@ -486,6 +519,7 @@ __device__ __forceinline__ bool get_by_ray(const DevTree &t, const uint64_t *occ
             if (!done && ++iters > budget) {  // the next node iteration
                 done = true;
                 ok = budget >= VHX_MAX_ITERS;
+                if (!ok && sbase) save_state(sbase + 4ull * sidx, p, iters, cur, tb, target, count, node, s1, s2, s3);
             }
         }
         if (done) break;

@@ -52,12 +52,16 @@ struct vhx_ctx {
     DevBuf offsets;   // exclusive scan of counts
     DevBuf flags;     // primary pass 0: abandoned flag per output index
     DevBuf qargs;     // QueueArgs of the queue passes
+    DevBuf state;     // saved traversal state per output index (64 B) of rays abandoned at a budget
     uint32_t occ_words = 1;
     bool simple_kernel = true;  // VHX_PERSISTENT=1 selects the persistent wave-refill kernel (A/B)
     // step budgets of the passes before the final (unbounded) one; VHX_BUDGETS="64" / "32,256" style override
     uint32_t budgets[3] = {64u, 0u, 0u};
     uint32_t npass = 2;         // passes including the final one (1 = single pass)
-    uint32_t rpw[4] = {64u, 64u, 64u, 64u};  // rays per wave of each pass (VHX_RPW="64,16" style override)
+    uint32_t rpw[4] = {64u, 64u, 64u, 64u};  // rays per wave of each pass (VHX_RPW="64,16" style override; 0 = adaptive)
+    uint32_t tw = 1024;            // adaptive rays per wave: target waves per queue pass (VHX_TW)
+    bool resume = true;            // abandoned rays continue from saved state (VHX_RESUME=0: re-traced from scratch)
+    uint32_t qblock = 256;         // threads per workgroup of a queue pass (VHX_QBLOCK=64: one wave per workgroup)
     uint32_t queue_blocks = 2048;  // workgroups of a queue pass (CUs x resident workgroups)
 };
 
@@ -328,11 +332,23 @@ __global__ void __launch_bounds__(256) k_trace_persistent(DevTree t, CamD cam, O
 // output is bit-identical to a single pass.
 struct PassQ {
     uint32_t budget;   // VHX_MAX_ITERS on the final pass
-    uint32_t rpw;      // queue passes: rays per wave (lanes >= rpw idle)
+    uint32_t rpw;      // queue passes: rays per wave (lanes >= rpw idle); 0 = adaptive (pass_rpw)
+    uint32_t tw;       // adaptive rays per wave: the pass spreads its rays over about this many waves
+    uint32_t resume;   // queue passes: the input rays continue from their saved state (else traced from scratch)
     uint32_t *tmp;     // chunk-local lists of abandoned rays (null on the final pass)
     uint32_t *counts;  // per chunk
     uint8_t *flags;    // primary pass 0: abandoned flag per output index (every entry written, no clearing needed)
+    uint4 *state;      // per output index, 4 x uint4: saved traversal state of an abandoned ray (null: re-trace)
 };
+
+// Rays per wave of a queue pass over n rays: fixed, or (rpw == 0) as many as spread the pass over about `tw` waves.
+// Long rays traced 64 per wave pay for their divergence (the bench frame's 256 longest: 1.05 ms at 64 per wave,
+// 0.56 ms at one per wave and one wave per workgroup); short queues are better spread thin.
+__device__ __forceinline__ uint32_t pass_rpw(uint32_t rpw, uint32_t tw, uint32_t n) {
+    if (rpw) return rpw;
+    const uint32_t k = (n + tw - 1) / tw;
+    return k < 1u ? 1u : (k > 64u ? 64u : k);
+}
 
 // Block-level ordered append (all 256 threads of the workgroup call it): the workgroup's rays with push set are
 // listed at tmp[blockIdx * 256 ...] in thread order, their number at counts[blockIdx].
@@ -351,11 +367,12 @@ __device__ __forceinline__ void block_append(bool push, uint32_t idx, uint32_t *
 // Exclusive scan of the chunk counts in one workgroup of 1024 threads; nchunks = ceil(*n_in / per_chunk) when n_in
 // is given (a queue pass: its input length is only known on the device), else nchunks_host. Writes *total.
 __global__ void __launch_bounds__(1024) k_scan_counts(const uint32_t *__restrict__ counts, uint32_t nchunks_host,
-                                                      const uint32_t *n_in, uint32_t per_chunk,
+                                                      const uint32_t *n_in, uint32_t per_chunk, uint32_t tw,
                                                       uint32_t *__restrict__ offsets, uint32_t *total) {
     __shared__ uint32_t s_wave[16];
     __shared__ uint32_t s_carry;
-    const uint32_t nchunks = n_in ? (*n_in + per_chunk - 1) / per_chunk : nchunks_host;
+    const uint32_t pc = n_in ? pass_rpw(per_chunk, tw, *n_in) : per_chunk;
+    const uint32_t nchunks = n_in ? (*n_in + pc - 1) / pc : nchunks_host;
     const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
     constexpr uint32_t K = 16;  // elements per thread per segment; loads issued together
     if (t == 0) s_carry = 0;
@@ -434,9 +451,11 @@ __global__ void __launch_bounds__(256) k_emit_flags(const uint8_t *__restrict__ 
 __global__ void __launch_bounds__(256) k_gather_chunks(const uint32_t *__restrict__ tmp, uint32_t stride,
                                                        const uint32_t *__restrict__ counts,
                                                        const uint32_t *__restrict__ offsets, uint32_t nchunks_host,
-                                                       const uint32_t *n_in, uint32_t per_chunk,
+                                                       const uint32_t *n_in, uint32_t per_chunk, uint32_t tw,
                                                        uint32_t *__restrict__ out) {
-    const uint32_t nchunks = n_in ? (*n_in + per_chunk - 1) / per_chunk : nchunks_host;
+    const uint32_t pc = n_in ? pass_rpw(per_chunk, tw, *n_in) : per_chunk;
+    const uint32_t nchunks = n_in ? (*n_in + pc - 1) / pc : nchunks_host;
+    if (n_in) stride = pc;  // a queue pass lists its chunk c at tmp[c * rays per wave]
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t waves = gridDim.x * 4u;
     for (uint32_t c = blockIdx.x * 4u + (threadIdx.x >> 6); c < nchunks; c += waves) {
@@ -511,8 +530,12 @@ __global__ void __launch_bounds__(256) k_trace_primary(DevTree t, CamD cam, OutD
         F3d o, d;
         primary_ray(cam, px, py, o, d);
         HitOut h;
-        done = get_by_ray<COUNT, BD>(t, occ_tab, o, d, h, q.budget);
-        if (done) store(t, out, idx, o, h);
+        h.bytes = 0;
+        done = get_by_ray<COUNT, BD>(t, occ_tab, o, d, h, q.budget, q.state, (uint32_t)idx);
+        if (done)
+            store(t, out, idx, o, h);
+        else if (COUNT && q.state)
+            out.bytes[idx] = h.bytes;  // the running count, continued by the pass that resumes the ray
     }
     // every in-tile entry (frame padding included) gets its flag, so the flags need no clearing between frames
     if (q.flags && lx < T && ly < T) q.flags[idx] = done ? 0 : 1;
@@ -530,8 +553,12 @@ __global__ void __launch_bounds__(256) k_trace_rays(DevTree t, const float *__re
         const F3d o = mk(rays[6 * i], rays[6 * i + 1], rays[6 * i + 2]);
         const F3d d = mk(rays[6 * i + 3], rays[6 * i + 4], rays[6 * i + 5]);
         HitOut h;
-        done = get_by_ray<COUNT, BD>(t, occ_tab, o, d, h, q.budget);
-        if (done) store(t, out, i, o, h);
+        h.bytes = 0;
+        done = get_by_ray<COUNT, BD>(t, occ_tab, o, d, h, q.budget, q.state, (uint32_t)i);
+        if (done)
+            store(t, out, i, o, h);
+        else if (COUNT && q.state)
+            out.bytes[i] = h.bytes;
     }
     if (q.tmp) block_append(!done, (uint32_t)i, q.tmp, q.counts);
 }
@@ -571,35 +598,39 @@ __global__ void __launch_bounds__(256) k_trace_queue(DevTree t, const QueueArgs 
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t n = *in_n;
+    const uint32_t rpw = pass_rpw(q.rpw, q.tw, n);
     for (;;) {
         uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(grab, q.rpw);
+        if (lane == 0) base = atomicAdd(grab, rpw);
         base = __shfl(base, 0);
         if (base >= n) break;  // wave-uniform
         const uint32_t i = base + lane;
         bool push = false;
         uint32_t idx = 0;
-        if (lane < q.rpw && i < n) {
+        if (lane < rpw && i < n) {
             idx = in[i];
             F3d o, d;
             const QueueArgs *a = qa;
             asm volatile("" : "+s"(a));  // loads through `a` stay here (not hoisted into live registers)
             ray_of(a->cam, a->src, idx, o, d);
             HitOut h;
-            const bool fin = get_by_ray<COUNT, BD>(t, occ_tab, o, d, h, q.budget);
+            h.bytes = COUNT && q.resume ? a->out.bytes[idx] : 0u;
+            const bool fin = get_by_ray<COUNT, BD>(t, occ_tab, o, d, h, q.budget, q.state, idx, q.resume != 0);
             const QueueArgs *b = qa;
             asm volatile("" : "+s"(b));
-            if (!fin)
+            if (!fin) {
                 push = true;
-            else if (b->src.kind == 3u)
+                if (COUNT && q.state) b->out.bytes[idx] = h.bytes;
+            } else if (b->src.kind == 3u) {
                 store_shadow(b->out, idx, h);
-            else
+            } else {
                 store(t, b->out, idx, o, h);
+            }
         }
         if (q.tmp) {  // this chunk's abandoned rays, in lane order
-            const uint32_t chunk = base / q.rpw;
+            const uint32_t chunk = base / rpw;
             const uint64_t m = __ballot(push);
-            if (push) q.tmp[(uint64_t)chunk * q.rpw + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = idx;
+            if (push) q.tmp[(uint64_t)chunk * rpw + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = idx;
             if (lane == 0) q.counts[chunk] = (uint32_t)__popcll(m);
         }
     }
@@ -792,10 +823,11 @@ static int prepare_passes(vhx_ctx *c, uint64_t nout, uint64_t nblocks0, uint32_t
     npass = nout < 0x7FFFFFFFull ? c->npass : 1u;
     if (npass < 2 && !shadow) return VHX_OK;
     uint64_t chunks = std::max(nblocks0, (nout + 1023) / 1024), list = nblocks0 * 256;
-    for (uint32_t p = 1; p < npass; ++p) {  // queue passes: chunk = one grab of rpw rays
-        const uint64_t ch = (nout + c->rpw[p] - 1) / c->rpw[p];
+    for (uint32_t p = 1; p < npass; ++p) {  // queue passes: chunk = one grab of rpw rays (adaptive: >= 1)
+        const uint64_t r = c->rpw[p] ? c->rpw[p] : 1u;
+        const uint64_t ch = (nout + r - 1) / r;
         chunks = std::max(chunks, ch);
-        list = std::max(list, ch * c->rpw[p]);
+        list = std::max(list, ch * r + 64u);
     }
     int rc = ensure(c, c->queue[0], nout * 4);
     if (!rc && (npass > 2 || shadow)) rc = ensure(c, c->queue[1], nout * 4);
@@ -805,6 +837,7 @@ static int prepare_passes(vhx_ctx *c, uint64_t nout, uint64_t nblocks0, uint32_t
     if (!rc) rc = ensure(c, c->counts, chunks * 4);
     if (!rc) rc = ensure(c, c->offsets, chunks * 4);
     if (!rc) rc = ensure(c, c->flags, ((nout + 3) & ~3ull));
+    if (!rc && c->resume && npass > 1) rc = ensure(c, c->state, nout * 64);
     return rc;
 }
 
@@ -815,14 +848,20 @@ static int reset_passes(vhx_ctx *c, uint32_t npass, bool shadow = false) {
     return VHX_OK;
 }
 
+// Pass 0 traces fresh rays (the grid kernel of primary and explicit rays, or the shadow path's first queue pass);
+// every later pass resumes the rays its predecessor abandoned.
 static PassQ pass_q(const vhx_ctx *c, uint32_t p, uint32_t npass) {
     PassQ q;
     const bool last = p + 1 >= npass;
     q.budget = last ? VHX_MAX_ITERS : c->budgets[p];
     q.rpw = c->rpw[p];
+    q.tw = c->tw;
     q.tmp = last ? nullptr : (uint32_t *)c->tmp.ptr;
     q.counts = (uint32_t *)c->counts.ptr;
     q.flags = nullptr;
+    // the state buffer is written by every pass that can abandon rays and read by every pass after the first
+    q.state = c->resume && npass > 1 ? (uint4 *)c->state.ptr : nullptr;
+    q.resume = c->resume && p > 0 ? 1u : 0u;
     return q;
 }
 
@@ -843,11 +882,11 @@ static int compact_chunks(vhx_ctx *c, uint32_t nchunks_host, const uint32_t *n_i
                           uint32_t stride, uint32_t *out, uint32_t *total, uint64_t max_chunks) {
     const uint32_t *counts = (const uint32_t *)c->counts.ptr;
     uint32_t *offsets = (uint32_t *)c->offsets.ptr;
-    k_scan_counts<<<1, 1024, 0, c->stream>>>(counts, nchunks_host, n_in, per_chunk, offsets, total);
+    k_scan_counts<<<1, 1024, 0, c->stream>>>(counts, nchunks_host, n_in, per_chunk, c->tw, offsets, total);
     const uint64_t want = (max_chunks + 3) / 4;
     const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(want, c->queue_blocks));
     k_gather_chunks<<<grid, 256, 0, c->stream>>>((const uint32_t *)c->tmp.ptr, stride, counts, offsets,
-                                                 nchunks_host, n_in, per_chunk, out);
+                                                 nchunks_host, n_in, per_chunk, c->tw, out);
     VHX_HIP(c, hipGetLastError());
     debug_passes(c, "compacted");
     return VHX_OK;
@@ -868,7 +907,7 @@ static int launch_queue_passes(vhx_ctx *c, const DevTree &t, const CamD &cam, co
             uint32_t *counts = (uint32_t *)c->counts.ptr, *offsets = (uint32_t *)c->offsets.ptr;
             const uint8_t *flags = (const uint8_t *)c->flags.ptr;
             k_count_flags<<<nb, 256, 0, c->stream>>>(flags, nout, counts);
-            k_scan_counts<<<1, 1024, 0, c->stream>>>(counts, nb, nullptr, 1, offsets, ctl);
+            k_scan_counts<<<1, 1024, 0, c->stream>>>(counts, nb, nullptr, 1, c->tw, offsets, ctl);
             k_emit_flags<<<nb, 256, 0, c->stream>>>(flags, nout, offsets, (uint32_t *)c->queue[0].ptr);
             VHX_HIP(c, hipGetLastError());
             debug_passes(c, "compacted flags");
@@ -885,11 +924,12 @@ static int launch_queue_passes(vhx_ctx *c, const DevTree &t, const CamD &cam, co
         const uint32_t *in = (const uint32_t *)c->queue[(p - 1) & 1u].ptr;  // p = 0: queue[1]
         const uint32_t *in_n = p > 0 ? ctl + (p - 1) : ctl + 7;
         const PassQ q = pass_q(c, p, npass);
-        k_trace_queue<COUNT, BD><<<c->queue_blocks, 256, 0, c->stream>>>(t, qa, in, in_n, ctl + 8 + p, q);
+        k_trace_queue<COUNT, BD><<<c->queue_blocks * (256u / c->qblock), c->qblock, 0, c->stream>>>(t, qa, in, in_n,
+                                                                                                  ctl + 8 + p, q);
         debug_passes(c, "queue pass");
         if (p + 1 < npass)
             rc = compact_chunks(c, 0, in_n, q.rpw, q.rpw, (uint32_t *)c->queue[p & 1u].ptr, ctl + p,
-                                (nout + q.rpw - 1) / q.rpw);
+                                q.rpw ? (nout + q.rpw - 1) / q.rpw : nout);
     }
     return rc;
 }
@@ -947,10 +987,16 @@ int vhx_create(int hip_device, vhx_ctx **out) {
                 char *end = nullptr;
                 const unsigned long v = strtoul(q, &end, 10);
                 if (end == q) break;
-                if (v >= 1 && v <= 64) c->rpw[k++] = (uint32_t)v;
+                if (v <= 64) c->rpw[k++] = (uint32_t)v;  // 0 = adaptive
                 q = *end == ',' ? end + 1 : end;
             }
         }
+        const char *pt = getenv("VHX_TW");
+        if (pt && atoi(pt) > 0) c->tw = (uint32_t)atoi(pt);
+        const char *pz = getenv("VHX_RESUME");
+        if (pz && pz[0] == '0') c->resume = false;
+        const char *pq = getenv("VHX_QBLOCK");
+        if (pq && (atoi(pq) == 64 || atoi(pq) == 128)) c->qblock = (uint32_t)atoi(pq);
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, hip_device) == hipSuccess && prop.multiProcessorCount > 0)
             c->queue_blocks = (uint32_t)prop.multiProcessorCount * 8u;
@@ -972,7 +1018,7 @@ void vhx_destroy(vhx_ctx *c) {
     for (auto &b : c->raw)
         if (b.ptr) (void)hipFree(b.ptr);
     for (DevBuf *b : {&c->hdr, &c->brick_occ, &c->child_rec, &c->scratch, &c->rays, &c->queue[0], &c->queue[1], &c->qctl,
-                      &c->tmp, &c->counts, &c->offsets, &c->flags, &c->qargs})
+                      &c->tmp, &c->counts, &c->offsets, &c->flags, &c->qargs, &c->state})
         if (b->ptr) (void)hipFree(b->ptr);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
