@@ -225,7 +225,8 @@ def main():
                 "traffic": None if tr is None else tr["read_bytes_per_launch"],
                 "traffic_source": None if tr is None else tr["source"],
                 "kernel": "vhx_trace_primary launch = k_trace_primary (pass 0, step budget) + k_trace_queue "
-                          "(re-trace of the rays over budget), timed together with HIP events on the trace stream",
+                          "(the rays over budget, resumed from their saved state), timed together with HIP events "
+                          "on the trace stream",
                 "kernel_ms": round(kernel_ms, 4),
                 "algorithmic_bytes_per_launch": launch_bytes, "tree_bytes_per_ray": round(tree_bytes / max(1, my_rays), 2)}
 

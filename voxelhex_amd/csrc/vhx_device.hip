@@ -63,6 +63,10 @@ struct vhx_ctx {
     bool resume = true;            // abandoned rays continue from saved state (VHX_RESUME=0: re-traced from scratch)
     uint32_t qblock = 256;         // threads per workgroup of a queue pass (VHX_QBLOCK=64: one wave per workgroup)
     uint32_t queue_blocks = 2048;  // workgroups of a queue pass (CUs x resident workgroups)
+    // waves of a queue pass (VHX_QWAVES): 8 per CU. The bench frame's tail pass (148 k rays, 2316 chunks of 64) took
+    // 1.55 ms/frame at 2048 waves against 1.62 at 8192 and 1.82 at 1024 (fewer busy waves per CU at the start of the
+    // pass, while every chunk still starts at once)
+    uint32_t queue_waves = 2048;
 };
 
 #define VHX_HIP(ctx, call)                                                                                         \
@@ -924,8 +928,9 @@ static int launch_queue_passes(vhx_ctx *c, const DevTree &t, const CamD &cam, co
         const uint32_t *in = (const uint32_t *)c->queue[(p - 1) & 1u].ptr;  // p = 0: queue[1]
         const uint32_t *in_n = p > 0 ? ctl + (p - 1) : ctl + 7;
         const PassQ q = pass_q(c, p, npass);
-        k_trace_queue<COUNT, BD><<<c->queue_blocks * (256u / c->qblock), c->qblock, 0, c->stream>>>(t, qa, in, in_n,
-                                                                                                  ctl + 8 + p, q);
+        const uint32_t qwaves = c->queue_waves;
+        k_trace_queue<COUNT, BD><<<(qwaves * 64u + c->qblock - 1) / c->qblock, c->qblock, 0, c->stream>>>(
+            t, qa, in, in_n, ctl + 8 + p, q);
         debug_passes(c, "queue pass");
         if (p + 1 < npass)
             rc = compact_chunks(c, 0, in_n, q.rpw, q.rpw, (uint32_t *)c->queue[p & 1u].ptr, ctl + p,
@@ -998,8 +1003,12 @@ int vhx_create(int hip_device, vhx_ctx **out) {
         const char *pq = getenv("VHX_QBLOCK");
         if (pq && (atoi(pq) == 64 || atoi(pq) == 128)) c->qblock = (uint32_t)atoi(pq);
         hipDeviceProp_t prop;
-        if (hipGetDeviceProperties(&prop, hip_device) == hipSuccess && prop.multiProcessorCount > 0)
+        if (hipGetDeviceProperties(&prop, hip_device) == hipSuccess && prop.multiProcessorCount > 0) {
             c->queue_blocks = (uint32_t)prop.multiProcessorCount * 8u;
+            c->queue_waves = (uint32_t)prop.multiProcessorCount * 8u;
+        }
+        const char *pw = getenv("VHX_QWAVES");  // after the device default
+        if (pw && atoi(pw) > 0) c->queue_waves = (uint32_t)atoi(pw);
     }
     if ((e = hipEventCreate(&c->ev0)) != hipSuccess) return bail("hipEventCreate", e);
     if ((e = hipEventCreate(&c->ev1)) != hipSuccess) return bail("hipEventCreate", e);
