@@ -48,6 +48,8 @@ def parse():
                    help="config 5: each step = primary frame + one hard-shadow ray per hit toward (S,S,S)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-roofline", action="store_true")
+    p.add_argument("--no-overlap", action="store_true",
+                   help="N>1: gather each frame before tracing the next (default: frame k's gather overlaps k+1)")
     return p.parse_args()
 
 
@@ -138,13 +140,22 @@ def main():
                    impact=torch.zeros((n_out, 3), dtype=torch.float32, device=dev),
                    normal=torch.zeros((n_out, 3), dtype=torch.float32, device=dev))
         shadowed = torch.zeros(n_out, dtype=torch.int32, device=dev)
-    if world > 1 and rank == 0:
-        gathered = [torch.zeros(n_out, dtype=torch.int32, device=dev) for _ in range(world)]
-        framebuffer = torch.zeros(W * H, dtype=torch.int32, device=dev)
+    pipe = None
+    if world > 1:
+        framebuffer = torch.zeros(W * H, dtype=torch.int32, device=dev) if rank == 0 else None
+
+        def untile(gathered, slot):
+            rt.untile_rgba(gathered.data_ptr(), world, tiles_per_rank, T, W, H, framebuffer.data_ptr())
+
+        # double-buffered: frame k's RCCL gather to rank 0 (and the untile there) overlaps frame k+1's trace
+        pipe = M.GatherPipeline(n_out, world, rank, dist, dev, untile, overlap=not args.no_overlap,
+                                host_staging=rehearsal)
 
     ev = []
 
     def step(timed):
+        if pipe is not None:
+            out["rgba"] = pipe.out_buffer()
         if timed:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
@@ -154,22 +165,13 @@ def main():
         if timed:
             e1.record(stream)
             ev.append((e0, e1))
-        if world > 1:
-            if rehearsal:
-                host = rgba.cpu()
-                hg = [torch.empty_like(host) for _ in range(world)] if rank == 0 else None
-                dist.gather(host, hg, dst=0)
-                if rank == 0:
-                    for g, h in zip(gathered, hg):
-                        g.copy_(h)
-            else:
-                dist.gather(rgba, gathered if rank == 0 else None, dst=0)
-            if rank == 0:
-                flatg = torch.cat(gathered)
-                rt.untile_rgba(flatg.data_ptr(), world, tiles_per_rank, T, W, H, framebuffer.data_ptr())
+        if pipe is not None:
+            pipe.submit()
 
     for _ in range(args.warmup):
         step(False)
+    if pipe is not None:
+        pipe.drain()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -177,6 +179,8 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step(True)
+    if pipe is not None:
+        pipe.drain()  # the last frame's gather and untile are inside the timed region
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -261,8 +265,10 @@ def main():
                        "shadow_rays_per_frame": n_shadow if args.shadows else None,
                        "tree_size": args.size, "brick_dim": args.brick_dim, "width": W, "height": H,
                        "scene": args.scene, "tile": T if world > 1 else None,
-                       "parallelism": (f"screen-tile split x{world} + " + ("gloo gather (single-GPU rehearsal)" if rehearsal
-                                                                  else "RCCL gather")) if world > 1 else "single GPU",
+                       "parallelism": (f"screen-tile split x{world} + " + (
+                           "gloo gather (single-GPU rehearsal)" if rehearsal else
+                           "RCCL gather" + ("" if args.no_overlap else ", overlapped with the next frame's trace")))
+                       if world > 1 else "single GPU",
                        "tree_nodes": int(flat.desc.node_count), "tree_bricks": int(flat.desc.brick_count),
                        "tree_gb": round(flat.nbytes() / 1e9, 3), "build_s": round(build_s, 2),
                        "upload_s": round(upload_s, 2)},

@@ -64,3 +64,41 @@ def test_two_rank_gloo_gather_matches_single_frame(tmp_path):
     fb, full = np.load(out)
     assert np.array_equal(fb, full)
     assert (full != 0).all()
+
+
+def _pipeline_worker(rank, world, port, out_path, overlap):
+    """Frames with step-dependent content through GatherPipeline (gloo, CPU tensors); rank 0 records every untiled
+    frame, so a buffer mix-up between in-flight frames shows as a wrong frame."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    per = M.tiles_per_rank(W, H, T, world)
+    n_out = per * T * T
+    seen = []
+
+    def untile(gathered, slot):
+        seen.append(M.untile_numpy(gathered.numpy().view(np.uint32), world, per, T, W, H))
+
+    pipe = M.GatherPipeline(n_out, world, rank, dist, "cpu", untile, overlap=overlap)
+    frames = 5
+    for k in range(frames):
+        buf = pipe.out_buffer().numpy().view(np.uint32)
+        for j, tile in enumerate(M.rank_tiles(W, H, T, rank, world)):
+            x0, y0, w, h = M.tile_rect(tile, W, H, T)
+            ys, xs = np.mgrid[y0:y0 + h, x0:x0 + w]
+            buf[j * T * T:(j + 1) * T * T].reshape(T, T)[:h, :w] = (ys * W + xs) * 16 + k
+        pipe.submit()
+    pipe.drain()
+    if rank == 0:
+        np.save(out_path, np.stack(seen))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("overlap", [True, False])
+def test_gather_pipeline_keeps_frames_apart(tmp_path, overlap):
+    out = str(tmp_path / "seen.npy")
+    mp.spawn(_pipeline_worker, args=(2, _free_port(), out, overlap), nprocs=2, join=True)
+    seen = np.load(out)
+    ys, xs = np.mgrid[0:H, 0:W]
+    assert seen.shape[0] == 5
+    for k in range(5):
+        assert np.array_equal(seen[k], ((ys * W + xs) * 16 + k).ravel().astype(np.uint32)), k

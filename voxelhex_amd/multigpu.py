@@ -43,6 +43,71 @@ def untile_numpy(gathered, ranks, per_rank, T, width, height):
     return fb
 
 
+class GatherPipeline:
+    """Per-frame gather of every rank's tile buffer to rank 0 and the untile there, overlapped with the next frame.
+
+    Two output buffers alternate: frame k is traced into `out_buffer()`, then `submit()` first completes frame k-1's
+    gather (the caller's stream waits for it) and untiles it, then starts frame k's gather asynchronously (RCCL runs
+    on its own stream), so frame k+1's trace overlaps frame k's transfer. Buffer reuse is stream-ordered: frame k+2
+    writes frame k's buffer only after submit(k+1) waited for frame k's gather. `drain()` completes the last frame.
+    With overlap=False each submit gathers and untiles its frame before returning to the caller's stream order.
+
+    untile(gathered, slot) scatters rank 0's gathered buffer (world * n_out pixels, rank-major) into the framebuffer.
+    host_staging: the gather runs over host memory (gloo rehearsal of the multi-GPU path on one GPU; synchronous).
+    """
+
+    def __init__(self, n_out, world, rank, dist, device, untile, overlap=True, host_staging=False):
+        import torch
+        self.world, self.rank, self.dist, self.untile = world, rank, dist, untile
+        self.overlap = overlap and not host_staging
+        self.host_staging = host_staging
+        self.bufs = [torch.zeros(n_out, dtype=torch.int32, device=device) for _ in range(2)]
+        self.big = self.parts = None
+        if rank == 0:
+            self.big = [torch.zeros(world * n_out, dtype=torch.int32, device=device) for _ in range(2)]
+            self.parts = [list(b.chunk(world)) for b in self.big]  # views: the gather writes in place, no cat
+        self.k = 0
+        self.pending = None  # (work handle, slot) of the frame whose gather is in flight
+
+    def out_buffer(self):
+        return self.bufs[self.k % 2]
+
+    def _finish(self, work, slot):
+        work.wait()
+        if self.rank == 0:
+            self.untile(self.big[slot], slot)
+
+    def submit(self):
+        slot = self.k % 2
+        self.k += 1
+        if self.pending is not None:
+            self._finish(*self.pending)
+            self.pending = None
+        if self.world == 1:
+            return
+        if self.host_staging:
+            import torch
+            host = self.bufs[slot].cpu()
+            hp = [torch.empty_like(host) for _ in range(self.world)] if self.rank == 0 else None
+            self.dist.gather(host, hp, dst=0)
+            if self.rank == 0:
+                for dst, src in zip(self.parts[slot], hp):
+                    dst.copy_(src)
+                self.untile(self.big[slot], slot)
+            return
+        work = self.dist.gather(self.bufs[slot], self.parts[slot] if self.rank == 0 else None, dst=0,
+                                async_op=True)
+        if self.overlap:
+            self.pending = (work, slot)
+        else:
+            self._finish(work, slot)
+
+    def drain(self):
+        if self.pending is not None:
+            self._finish(*self.pending)
+            self.pending = None
+
+
 def gather_to_root(local, world, rank, dist):
     """torch.distributed.gather of equally sized tile buffers to rank 0; returns the concatenation on rank 0."""
     import torch
