@@ -283,20 +283,23 @@ __device__ __forceinline__ bool probe_brick(const DevTree &t, const RayD &r, F3d
             jx += (uint32_t)mx;
             jy += (uint32_t)my;
             jz += (uint32_t)mz;
-            const bool in = (jx | jy | jz) < (uint32_t)BD;
+            // the exit test is one integer word (left the brick | occupied cell | iteration bound), so the loop's
+            // control costs one compare instead of a chain of mask operations
+            const uint32_t oob = (jx | jy | jz) & ~(uint32_t)(BD - 1);  // non-zero iff the walk left the brick
             const uint32_t uflat = (jx + jy * BD + jz * (BD * BD)) ^ F;
             if (B::WORDS > 1) {
                 const int32_t wi = (int32_t)(uflat >> 6);
-                if (in && wi != word_idx) {
+                if (oob == 0u && wi != word_idx) {
                     word_idx = wi;
                     word = occw[wi];
                 }
             }
-            const bool occupied = in & (((word >> (uflat & 63u)) & 1ull) != 0ull);
-            if (COUNT && in) h.bytes += 4 + pal_bytes<COUNT>(vox[uflat]);
+            const uint32_t bit = (uint32_t)(word >> (uflat & 63u)) & 1u;  // meaningless once oob (exit anyway)
+            if (COUNT && oob == 0u) h.bytes += 4 + pal_bytes<COUNT>(vox[uflat]);
             // the bound only ends a ray whose steps make no progress (a zero or NaN direction); at the bound the
             // oracle tests the cell it stepped into and stops before the next step, like this exit
-            if ((!in) | occupied | (iters >= VHX_MAX_ITERS)) break;
+            static_assert(VHX_MAX_ITERS == (1u << 22), "bound test below");
+            if ((oob | bit | (iters >> 22)) != 0u) break;
         }
         // hit = the exit test, recomputed once from the final cell instead of carrying the loop's booleans out of it
         // (opaque copies keep the compiler from reusing the in-loop values, which costs mask bookkeeping per cell)
@@ -507,10 +510,10 @@ __device__ __forceinline__ bool get_by_ray(const DevTree &t, const uint64_t *occ
                     jx += (uint32_t)mx;
                     jy += (uint32_t)my;
                     jz += (uint32_t)mz;
-                    const bool in = (jx | jy | jz) < 4u;
+                    const uint32_t oob = (jx | jy | jz) & ~3u;  // non-zero iff the walk left the node
                     const uint32_t tg = (jx + jy * 4u + jz * 16u) ^ F;
-                    const bool occupied = in & (((occ >> (tg & 63u)) & 1ull) != 0ull);
-                    if ((!in) | occupied | (iters > VHX_MAX_ITERS)) break;
+                    const uint32_t bit = (uint32_t)(occ >> (tg & 63u)) & 1u;
+                    if ((oob | bit | ((iters - 1u) >> 22)) != 0u) break;  // left | occupied | iters > 2^22
                 }
                 asm volatile("" : "+v"(jx), "+v"(jy), "+v"(jz));
                 target = (jx | jy | jz) < 4u ? (jx + jy * 4u + jz * 16u) ^ F : 64u;
