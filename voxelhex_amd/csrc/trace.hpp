@@ -430,6 +430,10 @@ __device__ __forceinline__ bool get_by_ray(const DevTree &t, const uint64_t *occ
         } else {
             slot = t.children[(uint64_t)node * 64u + (target & 63u)];
         }
+        // the pop test's LUT word, read from LDS while the node loads are in flight (the empty asm keeps the read
+        // here instead of next to its use after the probe, where its latency was exposed)
+        uint64_t omask = occ_tab[(target & 63u) * 8u + dir_idx];
+        asm volatile("" : "+v"(omask));
         const uint64_t occ = ((uint64_t)lh.y << 32) | (uint64_t)lh.x;
         const uint32_t ntype = lh.z;
         if (COUNT) h.bytes += 12;
@@ -444,7 +448,7 @@ __device__ __forceinline__ bool get_by_ray(const DevTree &t, const uint64_t *occ
             hit = done;
         }
         if (!done) {
-            if (uniform || target >= 64u || occ == 0 || (occ & occ_tab[(target & 63u) * 8u + dir_idx]) == 0) {
+            if (uniform || target >= 64u || occ == 0 || (occ & omask) == 0) {
                 // POP (cpu.rs:368-393)
                 count -= 1;
                 node = s1;
