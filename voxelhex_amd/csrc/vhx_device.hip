@@ -61,6 +61,7 @@ struct vhx_ctx {
     uint32_t rpw[4] = {64u, 64u, 64u, 64u};  // rays per wave of each pass (VHX_RPW="64,16" style override; 0 = adaptive)
     uint32_t tw = 1024;            // adaptive rays per wave: target waves per queue pass (VHX_TW)
     bool resume = true;            // abandoned rays continue from saved state (VHX_RESUME=0: re-traced from scratch)
+    uint32_t xcd_group = 0;        // pass-0 XCD-aware block runs (VHX_XCDG; 0 = dispatch order)
     uint32_t qblock = 256;         // threads per workgroup of a queue pass (VHX_QBLOCK=64: one wave per workgroup)
     uint32_t queue_blocks = 2048;  // workgroups of a queue pass (CUs x resident workgroups)
     // waves of a queue pass (VHX_QWAVES): 8 per CU. The bench frame's tail pass (148 k rays, 2316 chunks of 64) took
@@ -343,6 +344,7 @@ struct PassQ {
     uint32_t *counts;  // per chunk
     uint8_t *flags;    // primary pass 0: abandoned flag per output index (every entry written, no clearing needed)
     uint4 *state;      // per output index, 4 x uint4: saved traversal state of an abandoned ray (null: re-trace)
+    uint32_t xcd_group;  // pass 0: XCD-aware block runs (xcd_block), 0 = dispatch order
 };
 
 // Rays per wave of a queue pass over n rays: fixed, or (rpw == 0) as many as spread the pass over about `tw` waves.
@@ -509,6 +511,18 @@ __device__ __forceinline__ void ray_of(const CamD &cam, const RaySrc &src, uint3
     primary_ray(cam, px, py, o, d);
 }
 
+// XCD-aware block order: the dispatcher deals workgroups round-robin over the 8 XCDs (blockIdx % 8 share one XCD and
+// its L2; MI355X_MICROARCH.md, workgroup dispatch), so with G > 0 each XCD's blocks are taken in runs of G
+// consecutive frame blocks (neighbouring pixels walk the same nodes and bricks). A bijection on [0, n) for any n (the
+// last n mod 8G blocks keep their order); only the speed depends on the placement. G = 0: dispatch order.
+__device__ __forceinline__ uint32_t xcd_block(uint32_t bid, uint32_t n, uint32_t G) {
+    if (G == 0u) return bid;
+    const uint32_t full = n / (8u * G) * (8u * G);
+    if (bid >= full) return bid;
+    const uint32_t x = bid & 7u, k = bid >> 3;
+    return ((k / G) * 8u + x) * G + k % G;
+}
+
 // One workgroup = 256 lanes = a 16x16 pixel block made of four 8x8 wave tiles (wave64-coherent ray bundles, the
 // 8x8 footprint of the reference's @workgroup_size(8, 8, 1)). Blocks are dealt tile by tile.
 template <bool COUNT, int BD>
@@ -519,8 +533,9 @@ __global__ void __launch_bounds__(256) k_trace_primary(DevTree t, CamD cam, OutD
     __shared__ uint64_t occ_tab[512];
     fill_occ_tab(occ_tab);
     __syncthreads();
-    const uint32_t j = blockIdx.x / blocks_per_tile;  // j-th tile of this rank
-    const uint32_t sb = blockIdx.x - j * blocks_per_tile;
+    const uint32_t bid = xcd_block(blockIdx.x, gridDim.x, q.xcd_group);
+    const uint32_t j = bid / blocks_per_tile;  // j-th tile of this rank
+    const uint32_t sb = bid - j * blocks_per_tile;
     const uint32_t tile = tile_start + j * tile_stride;
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
     const uint32_t lx = (sb % blocks_per_tile_x) * 16u + (wave & 1u) * 8u + (lane & 7u);
@@ -860,6 +875,7 @@ static PassQ pass_q(const vhx_ctx *c, uint32_t p, uint32_t npass) {
     q.budget = last ? VHX_MAX_ITERS : c->budgets[p];
     q.rpw = c->rpw[p];
     q.tw = c->tw;
+    q.xcd_group = c->xcd_group;
     q.tmp = last ? nullptr : (uint32_t *)c->tmp.ptr;
     q.counts = (uint32_t *)c->counts.ptr;
     q.flags = nullptr;
@@ -998,6 +1014,8 @@ int vhx_create(int hip_device, vhx_ctx **out) {
         }
         const char *pt = getenv("VHX_TW");
         if (pt && atoi(pt) > 0) c->tw = (uint32_t)atoi(pt);
+        const char *pg = getenv("VHX_XCDG");
+        if (pg) c->xcd_group = (uint32_t)atoi(pg);
         const char *pz = getenv("VHX_RESUME");
         if (pz && pz[0] == '0') c->resume = false;
         const char *pq = getenv("VHX_QBLOCK");
