@@ -236,76 +236,80 @@ __device__ __forceinline__ void fill_hit(HitOut &h, uint32_t v, uint32_t cell, F
 template <bool COUNT, int BD>
 __device__ __forceinline__ bool probe_brick(const DevTree &t, const RayD &r, F3d &p, uint32_t desc, uint64_t cocc,
                                             CubeD bb, HitOut &h, uint32_t &iters, int32_t &hflat) {
-    if (desc == VHX_EMPTY) return false;
-    if (desc & VHX_SOLID_BIT) {  // BrickData::Solid, cpu.rs:249-260
-        if (COUNT) h.bytes += 4;
-        hflat = -1;
-        return true;
-    }
-    using B = Brick<BD>;
-    const float rs = rcp_pow2(bb.size);
-    const F3d pib = vmul(vmul(vsub(p, bb.min), (float)BD), rs);
-    int32_t ix = ras_i32(pib.x), iy = ras_i32(pib.y), iz = ras_i32(pib.z);
-    ix = ix < 0 ? 0 : (ix > BD - 1 ? BD - 1 : ix);
-    iy = iy < 0 ? 0 : (iy > BD - 1 ? BD - 1 : iy);
-    iz = iz < 0 ? 0 : (iz > BD - 1 ? BD - 1 : iz);
-    const float unit = bb.size * B::INV;
-    const uint64_t *occw = t.brick_occ + (uint64_t)desc * B::WORDS;
-    const uint32_t *vox = t.voxels + (uint64_t)desc * (uint64_t)B::N3;
-    int32_t flat = ix + iy * BD + iz * (BD * BD);
-    int32_t word_idx = flat >> 6;
-    uint64_t word = B::WORDS == 1 ? cocc : occw[word_idx];  // cocc: the child record's copy of occw[0]
-    bool hit = ((word >> (flat & 63)) & 1ull) != 0ull;
-    if (COUNT) h.bytes += 4 + pal_bytes<COUNT>(vox[flat]);  // the reference reads the palettes of every cell
-    if (!hit) {
-        // Cell walk in exit-plane form. The reference's st_k = unit * max(sg_k, 0) - sg_k * (p_k - cmin_k): the
-        // difference p_k - cmin_k is exact (cmin_k is a multiple of unit and p_k lies within a unit of it, so
-        // Sterbenz applies, or cmin_k = 0), hence for sg_k = +1 st_k = unit - (p_k - cmin_k) and (cmin_k + unit) - p_k
-        // are the same real number rounded once, and for sg_k = -1 st_k = p_k - cmin_k exactly. With the exit plane
-        // e_k = cmin_k + unit * max(sg_k, 0) (exact), |st_k * sf_k| = |(e_k - p_k) * sf_k| bit for bit.
-        // Cell indices are carried direction-normalised (j_k = i_k, or BD-1-i_k for a negative direction), so a
-        // step adds 1 and the flat index is j-flat ^ F.
-        F3d e = vadd(vadd(bb.min, vmul(mk((float)ix, (float)iy, (float)iz), unit)),
-                     mk(unit * r.sgmax.x, unit * r.sgmax.y, unit * r.sgmax.z));
-        const F3d sgu = mk(r.sg.x * unit, r.sg.y * unit, r.sg.z * unit);
-        const uint32_t fx = r.isx > 0 ? 0u : BD - 1u, fy = r.isy > 0 ? 0u : BD - 1u, fz = r.isz > 0 ? 0u : BD - 1u;
-        const uint32_t F = fx + fy * BD + fz * (BD * BD);
-        uint32_t jx = (uint32_t)ix ^ fx, jy = (uint32_t)iy ^ fy, jz = (uint32_t)iz ^ fz;
-        for (;;) {
-            ++iters;
-            // dda_step_to_next_sibling (cpu.rs:104-132) on the cell {cmin, unit}
-            const float dx = __builtin_fabsf((e.x - p.x) * r.sf.x), dy = __builtin_fabsf((e.y - p.y) * r.sf.y),
-                        dz = __builtin_fabsf((e.z - p.z) * r.sf.z);
-            const float m = __builtin_fminf(__builtin_fminf(dx, dy), dz);
-            p = mk(p.x + r.d.x * m, p.y + r.d.y * m, p.z + r.d.z * m);
-            const bool mx = m == dx, my = m == dy, mz = m == dz;
-            e = mk(mx ? e.x + sgu.x : e.x, my ? e.y + sgu.y : e.y, mz ? e.z + sgu.z : e.z);
-            jx += (uint32_t)mx;
-            jy += (uint32_t)my;
-            jz += (uint32_t)mz;
-            // the exit test is one integer word (left the brick | occupied cell | iteration bound), so the loop's
-            // control costs one compare instead of a chain of mask operations
-            const uint32_t oob = (jx | jy | jz) & ~(uint32_t)(BD - 1);  // non-zero iff the walk left the brick
-            const uint32_t uflat = (jx + jy * BD + jz * (BD * BD)) ^ F;
-            if (B::WORDS > 1) {
-                const int32_t wi = (int32_t)(uflat >> 6);
-                if (oob == 0u && wi != word_idx) {
-                    word_idx = wi;
-                    word = occw[wi];
+    // one branch (a Parted brick's walk); Empty and Solid (cpu.rs:249-260) resolve by selects. VHX_EMPTY has the
+    // Solid bit set, so "Parted" is simply the bit clear.
+    const bool solid = (desc & VHX_SOLID_BIT) != 0u && desc != VHX_EMPTY;
+    if (COUNT && solid) h.bytes += 4;
+    bool hit = solid;
+    int32_t flat = -1;  // hflat of a Solid brick
+    if ((desc & VHX_SOLID_BIT) == 0u) {
+        using B = Brick<BD>;
+        const float rs = rcp_pow2(bb.size);
+        const F3d pib = vmul(vmul(vsub(p, bb.min), (float)BD), rs);
+        int32_t ix = ras_i32(pib.x), iy = ras_i32(pib.y), iz = ras_i32(pib.z);
+        ix = ix < 0 ? 0 : (ix > BD - 1 ? BD - 1 : ix);
+        iy = iy < 0 ? 0 : (iy > BD - 1 ? BD - 1 : iy);
+        iz = iz < 0 ? 0 : (iz > BD - 1 ? BD - 1 : iz);
+        const float unit = bb.size * B::INV;
+        const uint64_t *occw = t.brick_occ + (uint64_t)desc * B::WORDS;
+        const uint32_t *vox = t.voxels + (uint64_t)desc * (uint64_t)B::N3;
+        flat = ix + iy * BD + iz * (BD * BD);
+        int32_t word_idx = flat >> 6;
+        uint64_t word = B::WORDS == 1 ? cocc : occw[word_idx];  // cocc: the child record's copy of occw[0]
+        hit = ((word >> (flat & 63)) & 1ull) != 0ull;
+        if (COUNT) h.bytes += 4 + pal_bytes<COUNT>(vox[flat]);  // the reference reads the palettes of every cell
+        if (!hit) {
+            // Cell walk in exit-plane form. The reference's st_k = unit * max(sg_k, 0) - sg_k * (p_k - cmin_k): the
+            // difference p_k - cmin_k is exact (cmin_k is a multiple of unit and p_k lies within a unit of it, so
+            // Sterbenz applies, or cmin_k = 0), hence for sg_k = +1 st_k = unit - (p_k - cmin_k) and
+            // (cmin_k + unit) - p_k are the same real number rounded once, and for sg_k = -1 st_k = p_k - cmin_k
+            // exactly. With the exit plane e_k = cmin_k + unit * max(sg_k, 0) (exact), |st_k * sf_k| =
+            // |(e_k - p_k) * sf_k| bit for bit.
+            // Cell indices are carried direction-normalised (j_k = i_k, or BD-1-i_k for a negative direction), so a
+            // step adds 1 and the flat index is j-flat ^ F.
+            F3d e = vadd(vadd(bb.min, vmul(mk((float)ix, (float)iy, (float)iz), unit)),
+                         mk(unit * r.sgmax.x, unit * r.sgmax.y, unit * r.sgmax.z));
+            const F3d sgu = mk(r.sg.x * unit, r.sg.y * unit, r.sg.z * unit);
+            const uint32_t fx = r.isx > 0 ? 0u : BD - 1u, fy = r.isy > 0 ? 0u : BD - 1u, fz = r.isz > 0 ? 0u : BD - 1u;
+            const uint32_t F = fx + fy * BD + fz * (BD * BD);
+            uint32_t jx = (uint32_t)ix ^ fx, jy = (uint32_t)iy ^ fy, jz = (uint32_t)iz ^ fz;
+            for (;;) {
+                ++iters;
+                // dda_step_to_next_sibling (cpu.rs:104-132) on the cell {cmin, unit}
+                const float dx = __builtin_fabsf((e.x - p.x) * r.sf.x), dy = __builtin_fabsf((e.y - p.y) * r.sf.y),
+                            dz = __builtin_fabsf((e.z - p.z) * r.sf.z);
+                const float m = __builtin_fminf(__builtin_fminf(dx, dy), dz);
+                p = mk(p.x + r.d.x * m, p.y + r.d.y * m, p.z + r.d.z * m);
+                const bool mx = m == dx, my = m == dy, mz = m == dz;
+                e = mk(mx ? e.x + sgu.x : e.x, my ? e.y + sgu.y : e.y, mz ? e.z + sgu.z : e.z);
+                jx += (uint32_t)mx;
+                jy += (uint32_t)my;
+                jz += (uint32_t)mz;
+                // the exit test is one integer word (left the brick | occupied cell | iteration bound), so the loop's
+                // control costs one compare instead of a chain of mask operations
+                const uint32_t oob = (jx | jy | jz) & ~(uint32_t)(BD - 1);  // non-zero iff the walk left the brick
+                const uint32_t uflat = (jx + jy * BD + jz * (BD * BD)) ^ F;
+                if (B::WORDS > 1) {
+                    const int32_t wi = (int32_t)(uflat >> 6);
+                    if (oob == 0u && wi != word_idx) {
+                        word_idx = wi;
+                        word = occw[wi];
+                    }
                 }
+                const uint32_t bit = (uint32_t)(word >> (uflat & 63u)) & 1u;  // meaningless once oob (exit anyway)
+                if (COUNT && oob == 0u) h.bytes += 4 + pal_bytes<COUNT>(vox[uflat]);
+                // the bound only ends a ray whose steps make no progress (a zero or NaN direction); at the bound the
+                // oracle tests the cell it stepped into and stops before the next step, like this exit
+                static_assert(VHX_MAX_ITERS == (1u << 22), "bound test below");
+                if ((oob | bit | (iters >> 22)) != 0u) break;
             }
-            const uint32_t bit = (uint32_t)(word >> (uflat & 63u)) & 1u;  // meaningless once oob (exit anyway)
-            if (COUNT && oob == 0u) h.bytes += 4 + pal_bytes<COUNT>(vox[uflat]);
-            // the bound only ends a ray whose steps make no progress (a zero or NaN direction); at the bound the
-            // oracle tests the cell it stepped into and stops before the next step, like this exit
-            static_assert(VHX_MAX_ITERS == (1u << 22), "bound test below");
-            if ((oob | bit | (iters >> 22)) != 0u) break;
+            // hit = the exit test, recomputed once from the final cell instead of carrying the loop's booleans out of
+            // it (opaque copies keep the compiler from reusing the in-loop values, which costs mask bookkeeping per
+            // cell)
+            asm volatile("" : "+v"(jx), "+v"(jy), "+v"(jz));
+            flat = (int32_t)((jx + jy * BD + jz * (BD * BD)) ^ F);
+            hit = (jx | jy | jz) < (uint32_t)BD && ((word >> (flat & 63)) & 1ull) != 0ull;
         }
-        // hit = the exit test, recomputed once from the final cell instead of carrying the loop's booleans out of it
-        // (opaque copies keep the compiler from reusing the in-loop values, which costs mask bookkeeping per cell)
-        asm volatile("" : "+v"(jx), "+v"(jy), "+v"(jz));
-        flat = (int32_t)((jx + jy * BD + jz * (BD * BD)) ^ F);
-        hit = (jx | jy | jz) < (uint32_t)BD && ((word >> (flat & 63)) & 1ull) != 0ull;
     }
     hflat = flat;
     return hit;
@@ -353,8 +357,8 @@ __device__ __forceinline__ void save_state(uint4 *st, F3d p, uint32_t iters, Cub
 // true. A smaller budget makes a pass of the multi-pass scheduler: false = the ray was abandoned after `budget` steps;
 // with `sbase` given, its state is saved at sbase[4 * sidx] and a later pass continues it (`resume`) exactly where it
 // stopped, otherwise the later pass traces it again from scratch. Either way the result is bit-identical to one
-// uninterrupted traversal (the state is saved whole; the traversal is deterministic). h.bytes is the caller's running byte count
-// (COUNT builds): 0 for a fresh ray, the count at the abandon for a resumed one.
+// uninterrupted traversal (the state is saved whole; the traversal is deterministic). h.bytes is the caller's running
+// byte count (COUNT builds): 0 for a fresh ray, the count at the abandon for a resumed one.
 //
 // Control flow: the reference's two nested loops (restart from the root / walk the NodeStack) are one loop here, and
 // every way out of it sets `done` and leaves through a single exit at the bottom of the iteration. The NodeStack<u32,
@@ -479,22 +483,20 @@ __device__ __forceinline__ bool get_by_ray(const DevTree &t, const uint64_t *occ
             } else if (ntype == VHX_NODE_INTERNAL && ((occ >> target) & 1ull) != 0) {
                 // PUSH (cpu.rs:401-411)
                 if (COUNT) h.bytes += 4;
-                if (slot >= t.node_count) {
-                    done = true;  // the reference would panic on an invalid key
-                } else {
-                    s3 = s2;
-                    s2 = s1;
-                    s1 = node;
-                    node = slot;
-                    count = count + 1 < 4 ? count + 1 : 4;
-                    cur = tb;
-                    target = offset_sectant(vsub(p, tb.min), tb.size);
-                    tb = child_bounds(cur, target);
-                }
+                s3 = s2;
+                s2 = s1;
+                s1 = node;
+                node = slot;
+                count = count + 1 < 4 ? count + 1 : 4;
+                cur = tb;
+                target = offset_sectant(vsub(p, tb.min), tb.size);
+                tb = child_bounds(cur, target);
+                done = slot >= t.node_count;  // the reference would panic on an invalid key: the ray ends, a miss
             } else {
                 // ADVANCE (cpu.rs:416-437); at most 9 steps across the node, the pass budget is checked after it.
                 // Same form as the brick walk (exit planes, direction-normalised sectant coordinates). Every step
-                // is committed: tb.min after a step out of the node is dead (the next iteration pops and overwrites it).
+                // is committed: tb.min after a step out of the node is dead (the next iteration pops and overwrites
+                // it).
                 // The reference's target (step_sectant) is formed once at the end (>= 64: the walk left the node).
                 const F3d usg = mk(tb.size * r.sgmax.x, tb.size * r.sgmax.y, tb.size * r.sgmax.z);
                 const F3d sgs = mk(r.sg.x * tb.size, r.sg.y * tb.size, r.sg.z * tb.size);
