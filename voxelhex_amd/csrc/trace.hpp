@@ -361,9 +361,9 @@ __device__ __forceinline__ void save_state(uint4 *st, F3d p, uint32_t iters, Cub
 // byte count (COUNT builds): 0 for a fresh ray, the count at the abandon for a resumed one.
 //
 // Control flow: the reference's two nested loops (restart from the root / walk the NodeStack) are one loop here, and
-// every way out of it sets `done` and leaves through a single exit at the bottom of the iteration. The NodeStack<u32,
-// 4> ring (cpu.rs:18-76) is a shift register: `node` is its top, s1..s3 the entries below; a push onto a full stack
-// drops the oldest entry, a pop that empties it ends the walk and restarts from the root.
+// every way out of it sets the exit code `ex` and leaves through a single exit at the bottom of the iteration. The
+// NodeStack<u32, 4> ring (cpu.rs:18-76) is a shift register: `node` is its top, s1..s3 the entries below; a push onto
+// a full stack drops the oldest entry, a pop that empties it ends the walk and restarts from the root.
 template <bool COUNT, int BD>
 __device__ __forceinline__ bool get_by_ray(const DevTree &t, const uint64_t *occ_tab, F3d o, F3d d, HitOut &h,
                                            uint32_t budget, uint4 *sbase = nullptr, uint32_t sidx = 0,
@@ -417,7 +417,10 @@ __device__ __forceinline__ bool get_by_ray(const DevTree &t, const uint64_t *occ
         iters = 1;  // the first node iteration
     }
     ray_scale_factors(r);
-    bool ok = true, hit = false, huni = false;
+    // how the loop ended, one integer instead of several booleans (kept in a VGPR; boolean flags set in divergent
+    // branches become 64-bit lane masks merged by scalar instructions at every join): 0 = still running, 1 = hit,
+    // 2 = miss (left the tree, invalid key, or the iteration bound), 3 = abandoned at the pass budget
+    uint32_t ex = 0;
     uint32_t hdesc = 0;
     int32_t hflat = 0;
     for (;;) {
@@ -442,16 +445,15 @@ __device__ __forceinline__ bool get_by_ray(const DevTree &t, const uint64_t *occ
         const uint32_t ntype = lh.z;
         if (COUNT) h.bytes += 12;
         const bool uniform = ntype == VHX_NODE_UNIFORM_LEAF;
-        bool done = false;
         if (target < 64u && (uniform || ntype == VHX_NODE_LEAF)) {
             if (COUNT) h.bytes += 4;
             hdesc = Brick<BD>::WORDS == 1 || !uniform ? slot : t.children[(uint64_t)node * 64u];
-            done = probe_brick<COUNT, BD>(t, r, p, hdesc, cocc, uniform ? cur : child_bounds(cur, target), h, iters,
-                                          hflat);
-            huni = uniform;
-            hit = done;
+            ex = probe_brick<COUNT, BD>(t, r, p, hdesc, cocc, uniform ? cur : child_bounds(cur, target), h, iters,
+                                        hflat)
+                     ? 1u
+                     : 0u;
         }
-        if (!done) {
+        if (ex == 0u) {
             if (uniform || target >= 64u || occ == 0 || (occ & omask) == 0) {
                 // POP (cpu.rs:368-393)
                 count -= 1;
@@ -477,7 +479,7 @@ __device__ __forceinline__ bool get_by_ray(const DevTree &t, const uint64_t *occ
                         cur.min = mk(0.0f, 0.0f, 0.0f);
                         cur.size = tsize;
                     } else {
-                        done = true;  // left the tree: a miss
+                        ex = 2u;  // left the tree: a miss
                     }
                 }
             } else if (ntype == VHX_NODE_INTERNAL && ((occ >> target) & 1ull) != 0) {
@@ -491,7 +493,7 @@ __device__ __forceinline__ bool get_by_ray(const DevTree &t, const uint64_t *occ
                 cur = tb;
                 target = offset_sectant(vsub(p, tb.min), tb.size);
                 tb = child_bounds(cur, target);
-                done = slot >= t.node_count;  // the reference would panic on an invalid key: the ray ends, a miss
+                ex = slot >= t.node_count ? 2u : 0u;  // the reference would panic on an invalid key: a miss here
             } else {
                 // ADVANCE (cpu.rs:416-437); at most 9 steps across the node, the pass budget is checked after it.
                 // Same form as the brick walk (exit planes, direction-normalised sectant coordinates). Every step
@@ -525,19 +527,20 @@ __device__ __forceinline__ bool get_by_ray(const DevTree &t, const uint64_t *occ
                 target = (jx | jy | jz) < 4u ? (jx + jy * 4u + jz * 16u) ^ F : 64u;
                 tb.min = vsub(e, usg);  // exact: e - usg undoes the exact e = tb.min + usg
             }
-            if (!done && ++iters > budget) {  // the next node iteration
-                done = true;
-                ok = budget >= VHX_MAX_ITERS;
-                if (!ok && sbase) save_state(sbase + 4ull * sidx, p, iters, cur, tb, target, count, node, s1, s2, s3);
+            if (ex == 0u && ++iters > budget) {  // the next node iteration
+                ex = budget >= VHX_MAX_ITERS ? 2u : 3u;
+                if (ex == 3u && sbase)
+                    save_state(sbase + 4ull * sidx, p, iters, cur, tb, target, count, node, s1, s2, s3);
             }
         }
-        if (done) break;
+        if (ex != 0u) break;
     }
-    if (hit) {  // the loop left on the hit: cur, target and p are those of the probe
+    if (ex == 1u) {  // the loop left on the hit: node, cur, target and p are those of the probe
         h.hit = true;
+        const bool huni = t.hdr[node].z == VHX_NODE_UNIFORM_LEAF;
         finish_hit<BD>(t, h, hdesc, hflat, p, huni ? cur : child_bounds(cur, target));
     }
-    return ok;
+    return ex != 3u;
 }
 
 }  // namespace vhx
