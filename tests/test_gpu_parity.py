@@ -156,11 +156,12 @@ def test_primary_frame_inverse_vp_vs_oracle(gpu, oracle):
     assert (got["value"] != N.VHX_EMPTY).sum() > 1000
 
 
-def test_tiles_and_untile_match_framebuffer(gpu):
+@pytest.mark.parametrize("T,R", [(64, 3), (20, 2), (13, 4)])  # tile sizes need not be multiples of the 8x8 wave tile
+def test_tiles_and_untile_match_framebuffer(gpu, T, R):
     import torch
     flat = vhx.FlatTree.build_scene(N.VHX_SCENE_LATTICE_CUBE, 64, 4)
     gpu.upload(flat)
-    W, H, T, R = 200, 136, 64, 3
+    W, H = 200, 136
     cam = vhx.glass_camera(64, W, H, target=(32.0, 32.0, 32.0))
     full = gpu.trace_primary(cam, fields=("rgba",))["rgba"]
     ntiles = ((W + T - 1) // T) * ((H + T - 1) // T)

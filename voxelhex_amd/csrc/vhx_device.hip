@@ -54,7 +54,6 @@ struct vhx_ctx {
     DevBuf qargs;     // QueueArgs of the queue passes
     DevBuf state;     // saved traversal state per output index (64 B) of rays abandoned at a budget
     uint32_t occ_words = 1;
-    bool simple_kernel = true;  // VHX_PERSISTENT=1 selects the persistent wave-refill kernel (A/B)
     // step budgets of the passes before the final (unbounded) one; VHX_BUDGETS="64" / "32,256" style override
     uint32_t budgets[3] = {64u, 0u, 0u};
     uint32_t npass = 2;         // passes including the final one (1 = single pass)
@@ -242,87 +241,6 @@ __device__ __forceinline__ void primary_ray(const CamD &c, uint32_t px, uint32_t
         const F3d dd = vsub(fp, np);
         const float rcp = 1.0f / __builtin_sqrtf((dd.x * dd.x + dd.y * dd.y) + dd.z * dd.z);
         d = vmul(dd, rcp);
-    }
-}
-
-#include "persistent.hpp"
-
-// Where the rays of a launch come from: 8x8 micro-tiles either over the whole frame (FRAMEBUFFER layout, raster order of
-// micro-tiles) or over this rank's T x T screen tiles (TILES layout, T % 8 == 0).
-struct FrameMap {
-    uint32_t layout, T, tiles_x, tile_start, tile_stride;
-    uint32_t mtx;          // micro-tiles per row (frame mode) or per tile row (tile mode)
-    uint32_t micro_per_tile;
-    uint32_t n_micro;      // micro-tiles of this launch
-};
-
-__device__ __forceinline__ bool map_ray(const CamD &cam, const FrameMap &fm, uint32_t micro, uint32_t l, uint32_t &px,
-                                        uint32_t &py, uint64_t &idx) {
-    if (fm.layout == VHX_LAYOUT_FRAMEBUFFER) {
-        px = (micro % fm.mtx) * 8u + (l & 7u);
-        py = (micro / fm.mtx) * 8u + (l >> 3);
-        if (px >= cam.width || py >= cam.height) return false;
-        idx = (uint64_t)py * cam.width + px;
-        return true;
-    }
-    const uint32_t j = micro / fm.micro_per_tile, m = micro - j * fm.micro_per_tile;
-    const uint32_t tile = fm.tile_start + j * fm.tile_stride;
-    const uint32_t lx = (m % fm.mtx) * 8u + (l & 7u), ly = (m / fm.mtx) * 8u + (l >> 3);
-    px = (tile % fm.tiles_x) * fm.T + lx;
-    py = (tile / fm.tiles_x) * fm.T + ly;
-    if (px >= cam.width || py >= cam.height) return false;
-    idx = (uint64_t)j * fm.T * fm.T + (uint64_t)ly * fm.T + lx;
-    return true;
-}
-
-// Persistent wave-refill kernel: one task of TASK rays (TASK/64 consecutive micro-tiles) per wave, 4 waves per block.
-template <bool COUNT, int BD, uint32_t TASK>
-__global__ void __launch_bounds__(256) k_trace_persistent(DevTree t, CamD cam, OutD out, FrameMap fm) {
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = blockIdx.x * 4u + (threadIdx.x >> 6);
-    const uint32_t micro0 = wave * (TASK / 64u);
-    if (micro0 >= fm.n_micro) return;  // wave-uniform
-    const uint32_t nrays = min(TASK, (fm.n_micro - micro0) * 64u);
-    const uint64_t below = (1ull << lane) - 1ull;
-    uint32_t next = 0;  // wave-uniform: rays of the task handed out so far
-    bool active = false;
-    uint64_t my_idx = 0;
-    LaneState s;
-    for (;;) {
-        const uint64_t idle = __ballot(!active);
-        if (idle != 0ull) {
-            if (!active) {
-                const uint32_t r = next + (uint32_t)__popcll(idle & below);
-                if (r < nrays) {
-                    uint32_t px, py;
-                    if (map_ray(cam, fm, micro0 + (r >> 6), r & 63u, px, py, my_idx)) {
-                        F3d o, d;
-                        primary_ray(cam, px, py, o, d);
-                        if (ls_begin(t, s, o, d)) {
-                            active = true;
-                        } else {
-                            HitOut h;
-                            h.hit = false;
-                            h.bytes = 0;
-                            store(t, out, my_idx, o, h);
-                        }
-                    }
-                }
-            }
-            next += (uint32_t)__popcll(idle);
-            if (__ballot(active) == 0ull) {
-                if (next >= nrays) break;
-                continue;
-            }
-        }
-        if (active) {
-            HitOut h;
-            if (ls_step<COUNT, BD>(t, s, h)) {
-                h.bytes = s.bytes;
-                store(t, out, my_idx, s.r.o, h);
-                active = false;
-            }
-        }
     }
 }
 
@@ -987,8 +905,6 @@ int vhx_create(int hip_device, vhx_ctx **out) {
         return bail("hipStreamCreate", e);
     c->stream = c->own_stream;
     {
-        const char *pk = getenv("VHX_PERSISTENT");
-        c->simple_kernel = !(pk && pk[0] == '1');
         const char *pb = getenv("VHX_BUDGETS");  // "32,256" = three passes; "" or "0" = one pass
         if (pb) {
             uint32_t b[3], nb = 0;
@@ -1214,31 +1130,9 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
     if ((rc = refresh_child_rec(c))) return rc;
     const DevTree t = dev_tree(c);
     const CamD cd = cam_of(cam);
-    FrameMap fm{};
-    fm.layout = layout;
-    fm.T = T;
-    fm.tiles_x = tiles_x;
-    fm.tile_start = tile_start;
-    fm.tile_stride = tile_stride;
-    if (layout == VHX_LAYOUT_FRAMEBUFFER) {
-        fm.mtx = (cam->width + 7) / 8;
-        fm.micro_per_tile = 0;
-        fm.n_micro = fm.mtx * ((cam->height + 7) / 8);
-    } else {
-        if (T % 8 != 0) return fail(c, VHX_E_INVALID_ARG, "tile_size must be a multiple of 8");
-        fm.mtx = T / 8;
-        fm.micro_per_tile = fm.mtx * fm.mtx;
-        fm.n_micro = my_tiles * fm.micro_per_tile;
-    }
-    constexpr uint32_t TASK = 512;
-    const uint32_t nwaves = (fm.n_micro + TASK / 64 - 1) / (TASK / 64);
-    const uint32_t pblocks = (nwaves + 3) / 4;
-    const bool simple = c->simple_kernel;
     uint32_t npass = 1;
-    if (simple) {
-        rc = prepare_passes(c, nout, nblocks, npass);
-        if (rc) return rc;
-    }
+    rc = prepare_passes(c, nout, nblocks, npass);
+    if (rc) return rc;
     RaySrc src{};
     src.kind = layout == VHX_LAYOUT_FRAMEBUFFER ? 0u : 1u;
     src.T = T;
@@ -1254,20 +1148,14 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
         constexpr int BD = decltype(bd_tag)::value;
         PassQ q0 = pass_q(c, 0, npass);
         if (npass > 1) q0.flags = (uint8_t *)c->flags.ptr;
-        if (simple) {
-            if (count) {
-                k_trace_primary<true, BD><<<(unsigned)nblocks, 256, 0, c->stream>>>(
-                    t, cd, ho.dev, T, tiles_x, tile_start, tile_stride, layout, bpx, bpt, q0);
-                qrc = launch_queue_passes<true, BD>(c, t, cd, src, ho.dev, 1, npass, nout, nblocks, true);
-            } else {
-                k_trace_primary<false, BD><<<(unsigned)nblocks, 256, 0, c->stream>>>(
-                    t, cd, ho.dev, T, tiles_x, tile_start, tile_stride, layout, bpx, bpt, q0);
-                qrc = launch_queue_passes<false, BD>(c, t, cd, src, ho.dev, 1, npass, nout, nblocks, true);
-            }
-        } else if (count) {
-            k_trace_persistent<true, BD, TASK><<<pblocks, 256, 0, c->stream>>>(t, cd, ho.dev, fm);
+        if (count) {
+            k_trace_primary<true, BD><<<(unsigned)nblocks, 256, 0, c->stream>>>(
+                t, cd, ho.dev, T, tiles_x, tile_start, tile_stride, layout, bpx, bpt, q0);
+            qrc = launch_queue_passes<true, BD>(c, t, cd, src, ho.dev, 1, npass, nout, nblocks, true);
         } else {
-            k_trace_persistent<false, BD, TASK><<<pblocks, 256, 0, c->stream>>>(t, cd, ho.dev, fm);
+            k_trace_primary<false, BD><<<(unsigned)nblocks, 256, 0, c->stream>>>(
+                t, cd, ho.dev, T, tiles_x, tile_start, tile_stride, layout, bpx, bpt, q0);
+            qrc = launch_queue_passes<false, BD>(c, t, cd, src, ho.dev, 1, npass, nout, nblocks, true);
         }
     };
     if (!dispatch_bd(c->desc.brick_dim, launch)) return fail(c, VHX_E_INVALID_ARG, "unsupported brick_dim");
