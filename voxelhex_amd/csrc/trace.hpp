@@ -244,8 +244,8 @@ __device__ __forceinline__ bool probe_brick(const DevTree &t, const RayD &r, F3d
     int32_t flat = -1;  // hflat of a Solid brick
     if ((desc & VHX_SOLID_BIT) == 0u) {
         using B = Brick<BD>;
-        const float rs = rcp_pow2(bb.size);
-        const F3d pib = vmul(vmul(vsub(p, bb.min), (float)BD), rs);
+        // (p - min) * dim / size: both scalings are by powers of two, so one multiply by dim/size is the same value
+        const F3d pib = vmul(vsub(p, bb.min), (float)BD * rcp_pow2(bb.size));
         int32_t ix = ras_i32(pib.x), iy = ras_i32(pib.y), iz = ras_i32(pib.z);
         ix = ix < 0 ? 0 : (ix > BD - 1 ? BD - 1 : ix);
         iy = iy < 0 ? 0 : (iy > BD - 1 ? BD - 1 : iy);
@@ -267,8 +267,11 @@ __device__ __forceinline__ bool probe_brick(const DevTree &t, const RayD &r, F3d
             // |(e_k - p_k) * sf_k| bit for bit.
             // Cell indices are carried direction-normalised (j_k = i_k, or BD-1-i_k for a negative direction), so a
             // step adds 1 and the flat index is j-flat ^ F.
-            F3d e = vadd(vadd(bb.min, vmul(mk((float)ix, (float)iy, (float)iz), unit)),
-                         mk(unit * r.sgmax.x, unit * r.sgmax.y, unit * r.sgmax.z));
+            // e_k = min_k + (i_k + max(sg_k, 0)) * unit: every term is an exact multiple of unit below 2^24 * unit,
+            // so the fused form is the value of the reference-order sum (min + i*unit) + unit*max(sg, 0) exactly
+            F3d e = mk(__builtin_fmaf((float)(ix + (int32_t)(r.isx > 0)), unit, bb.min.x),
+                       __builtin_fmaf((float)(iy + (int32_t)(r.isy > 0)), unit, bb.min.y),
+                       __builtin_fmaf((float)(iz + (int32_t)(r.isz > 0)), unit, bb.min.z));
             const F3d sgu = mk(r.sg.x * unit, r.sg.y * unit, r.sg.z * unit);
             const uint32_t fx = r.isx > 0 ? 0u : BD - 1u, fy = r.isy > 0 ? 0u : BD - 1u, fz = r.isz > 0 ? 0u : BD - 1u;
             const uint32_t F = fx + fy * BD + fz * (BD * BD);
@@ -421,6 +424,10 @@ __device__ __forceinline__ bool get_by_ray(const DevTree &t, const uint64_t *occ
     // branches become 64-bit lane masks merged by scalar instructions at every join): 0 = still running, 1 = hit,
     // 2 = miss (left the tree, invalid key, or the iteration bound), 3 = abandoned at the pass budget
     uint32_t ex = 0;
+    // tbok: target_bounds equals child_bounds(current, target) (kept by PUSH, POP and ADVANCE; not after a restart,
+    // which leaves it stale, cpu.rs:317-320), so a leaf probe takes its brick cube from tb instead of recomputing it.
+    // A resumed ray starts with 0 (recompute), which is always correct.
+    uint32_t tbok = resume ? 0u : 1u;
     uint32_t hdesc = 0;
     int32_t hflat = 0;
     for (;;) {
@@ -448,10 +455,9 @@ __device__ __forceinline__ bool get_by_ray(const DevTree &t, const uint64_t *occ
         if (target < 64u && (uniform || ntype == VHX_NODE_LEAF)) {
             if (COUNT) h.bytes += 4;
             hdesc = Brick<BD>::WORDS == 1 || !uniform ? slot : t.children[(uint64_t)node * 64u];
-            ex = probe_brick<COUNT, BD>(t, r, p, hdesc, cocc, uniform ? cur : child_bounds(cur, target), h, iters,
-                                        hflat)
-                     ? 1u
-                     : 0u;
+            CubeD bb = uniform ? cur : tb;
+            if (!uniform && tbok == 0u) bb = child_bounds(cur, target);
+            ex = probe_brick<COUNT, BD>(t, r, p, hdesc, cocc, bb, h, iters, hflat) ? 1u : 0u;
         }
         if (ex == 0u) {
             if (uniform || target >= 64u || occ == 0 || (occ & omask) == 0) {
@@ -469,11 +475,13 @@ __device__ __forceinline__ bool get_by_ray(const DevTree &t, const uint64_t *occ
                 const uint32_t sel = dda_step(r, p, tb);
                 target = step_sectant(r, target, sel);
                 tb.min = vadd(tb.min, vmul(step_vec(r, sel), tb.size));
+                tbok = 1u;
                 if (count == 0) {
                     // the stack ran empty: restart from the root (cpu.rs:441-455); target_bounds stays stale
                     p = vadd(p, vmul(d, 0.1f));
                     if (p.x < tsize && p.y < tsize && p.z < tsize && p.x > 0.0f && p.y > 0.0f && p.z > 0.0f) {
                         target = offset_sectant(p, tsize);
+                        tbok = 0u;  // target_bounds stays stale
                         node = 0;
                         count = 1;
                         cur.min = mk(0.0f, 0.0f, 0.0f);
@@ -493,6 +501,7 @@ __device__ __forceinline__ bool get_by_ray(const DevTree &t, const uint64_t *occ
                 cur = tb;
                 target = offset_sectant(vsub(p, tb.min), tb.size);
                 tb = child_bounds(cur, target);
+                tbok = 1u;
                 ex = slot >= t.node_count ? 2u : 0u;  // the reference would panic on an invalid key: a miss here
             } else {
                 // ADVANCE (cpu.rs:416-437); at most 9 steps across the node, the pass budget is checked after it.
