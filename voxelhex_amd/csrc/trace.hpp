@@ -140,11 +140,13 @@ struct CubeD {
     float size;
 };
 // Cube::child_bounds_for, src/spatial/mod.rs:72-77; SECTANT_OFFSET_LUT[s] = (s&3, (s>>2)&3, s>>4) / 4
+// min + (k * 0.25) * size with k in 0..3: every term is an exact multiple of size / 4 (cube coordinates are such
+// multiples below 2^24 * size / 4), so one fma per axis gives the reference's value bit for bit.
 __device__ __forceinline__ CubeD child_bounds(CubeD c, uint32_t s) {
     CubeD r;
-    r.min = vadd(c.min, vmul(mk((float)(s & 3u) * 0.25f, (float)((s >> 2) & 3u) * 0.25f, (float)(s >> 4) * 0.25f),
-                             c.size));
     r.size = c.size * 0.25f;
+    r.min = mk(__builtin_fmaf((float)(s & 3u), r.size, c.min.x), __builtin_fmaf((float)((s >> 2) & 3u), r.size, c.min.y),
+               __builtin_fmaf((float)(s >> 4), r.size, c.min.z));
     return r;
 }
 // cube_impact_normal, src/spatial/raytracing/mod.rs:97-125
