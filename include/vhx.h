@@ -141,9 +141,9 @@ int vhx_set_stream(vhx_ctx *ctx, void *hip_stream);
 /* Wait for all work of the context; optionally return the device time of the last trace in milliseconds. */
 int vhx_sync(vhx_ctx *ctx, float *last_trace_ms);
 /* Ray scheduling (no reference counterpart; results do not depend on it). A trace runs n+1 passes: pass i abandons
- * rays that need more than budgets[i] loop steps and the next pass re-traces them from scratch with 64 such rays per
- * wave; the last pass is unbounded. n = 0 is a single pass. Budgets strictly increasing, 0 < b < 2^22, n <= 3.
- * Default {64} (environment override VHX_BUDGETS="32,256"). */
+ * rays that need more than budgets[i] loop steps (saving their traversal state) and the next pass resumes them, 64
+ * such rays per wave; the last pass is unbounded. n = 0 is a single pass. Budgets strictly increasing,
+ * 0 < b < 2^22, n <= 3. Default {64} (environment override VHX_BUDGETS="32,256"). */
 int vhx_set_pass_budgets(vhx_ctx *ctx, const uint32_t *budgets, uint32_t n);
 
 /* Tree upload ----------------------------------------------------------------------------------------------- */
