@@ -127,9 +127,11 @@ __device__ __forceinline__ uint32_t step_sectant_i(uint32_t s, int32_t dx, int32
 }
 
 // offset_sectant, src/spatial/math/mod.rs:27-44 ((off * 4) / size with size a power of two)
+// (off * 4) / size: two scalings by powers of two, one multiply by 4/size gives the same value (at most one rounding,
+// on underflow, in either order)
 __device__ __forceinline__ uint32_t offset_sectant(F3d off, float size) {
-    const float rs = rcp_pow2(size);
-    F3d idx = mk((off.x * 4.0f) * rs, (off.y * 4.0f) * rs, (off.z * 4.0f) * rs);
+    const float rs4 = 4.0f * rcp_pow2(size);
+    F3d idx = mk(off.x * rs4, off.y * rs4, off.z * rs4);
     idx = mk(__builtin_floorf(idx.x), __builtin_floorf(idx.y), __builtin_floorf(idx.z));
     idx = mk(__builtin_fminf(idx.x, 3.0f), __builtin_fminf(idx.y, 3.0f), __builtin_fminf(idx.z, 3.0f));
     return ras_u8(idx.x + (idx.y * 4.0f) + (idx.z * 16.0f));
