@@ -52,6 +52,8 @@ struct vhx_ctx {
     DevBuf offsets;   // exclusive scan of counts
     DevBuf flags;     // primary pass 0: abandoned flag per output index
     DevBuf qargs;     // QueueArgs of the queue passes
+    std::vector<uint8_t> qargs_host;  // the QueueArgs last written to qargs (skips the upload when unchanged)
+    void *qargs_host_ptr = nullptr;   // qargs.ptr it was written to
     DevBuf state;     // saved traversal state per output index (64 B) of rays abandoned at a budget
     uint32_t occ_words = 1;
     // step budgets of the passes before the final (unbounded) one; VHX_BUDGETS="64" / "32,256" style override
@@ -855,8 +857,20 @@ static int launch_queue_passes(vhx_ctx *c, const DevTree &t, const CamD &cam, co
     }
     QueueArgs *qa = (QueueArgs *)c->qargs.ptr;
     if (first < npass) {
-        k_put_queue_args<<<1, 64, 0, c->stream>>>(QueueArgs{cam, src, o}, qa);
-        VHX_HIP(c, hipGetLastError());
+        // camera, ray source and outputs rarely change between frames: the device copy is rewritten only when they do
+        QueueArgs a;
+        std::memset(&a, 0, sizeof(a));  // padding included, for the comparison
+        a.cam = cam;
+        a.src = src;
+        a.out = o;
+        const uint8_t *ab = (const uint8_t *)&a;
+        if (c->qargs_host_ptr != c->qargs.ptr || c->qargs_host.size() != sizeof(a) ||
+            std::memcmp(c->qargs_host.data(), ab, sizeof(a)) != 0) {
+            k_put_queue_args<<<1, 64, 0, c->stream>>>(a, qa);
+            VHX_HIP(c, hipGetLastError());
+            c->qargs_host.assign(ab, ab + sizeof(a));
+            c->qargs_host_ptr = c->qargs.ptr;
+        }
     }
     for (uint32_t p = first; p < npass && !rc; ++p) {
         const uint32_t *in = (const uint32_t *)c->queue[(p - 1) & 1u].ptr;  // p = 0: queue[1]
@@ -984,6 +998,7 @@ const char *vhx_last_error(const vhx_ctx *c) { return c ? c->err.c_str() : "null
 int vhx_set_stream(vhx_ctx *c, void *s) {
     if (!c) return VHX_E_INVALID_ARG;
     c->stream = s ? (hipStream_t)s : c->own_stream;
+    c->qargs_host_ptr = nullptr;  // the cached queue arguments were written on the previous stream: rewrite them
     return VHX_OK;
 }
 
