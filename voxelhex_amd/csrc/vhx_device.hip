@@ -333,32 +333,49 @@ __global__ void __launch_bounds__(1024) k_scan_counts(const uint32_t *__restrict
     if (t == 0) *total = s_carry;
 }
 
-// Flag compaction in output-index order (primary pass 0): 1024 flags per workgroup, 4 per thread.
-__global__ void __launch_bounds__(256) k_count_flags(const uint8_t *__restrict__ flags, uint64_t n,
+// Flag compaction in output-index order, 1024 entries per workgroup, 4 per thread. The flag of entry i is flags[i]
+// (primary pass 0: the ray was abandoned) or, with HITS, value[i] != VHX_EMPTY (the hit pixels a shadow pass starts
+// from).
+template <bool HITS>
+__device__ __forceinline__ uint32_t flag_bits(const void *src, uint64_t i, uint64_t n) {
+    uint32_t bits = 0;  // bit k: flag of entry i + k
+    if (i + 3 < n) {
+        if (HITS) {
+            const uint32_t *v = (const uint32_t *)src + i;  // the caller's array: no alignment beyond 4 B assumed
+            bits = (v[0] != VHX_EMPTY ? 1u : 0u) | (v[1] != VHX_EMPTY ? 2u : 0u) | (v[2] != VHX_EMPTY ? 4u : 0u) |
+                   (v[3] != VHX_EMPTY ? 8u : 0u);
+        } else {
+            const uint32_t w = *(const uint32_t *)((const uint8_t *)src + i);
+            bits = (w & 1u) | ((w >> 7) & 2u) | ((w >> 14) & 4u) | ((w >> 21) & 8u);
+        }
+    } else {
+        for (uint64_t k = i; k < n && k < i + 4; ++k) {
+            const bool f = HITS ? ((const uint32_t *)src)[k] != VHX_EMPTY : ((const uint8_t *)src)[k] != 0;
+            if (f) bits |= 1u << (k - i);
+        }
+    }
+    return bits;
+}
+
+template <bool HITS>
+__global__ void __launch_bounds__(256) k_count_flags(const void *__restrict__ src, uint64_t n,
                                                      uint32_t *__restrict__ counts) {
     __shared__ uint32_t s_cnt[4];
     const uint64_t i = ((uint64_t)blockIdx.x * 256u + threadIdx.x) * 4u;
-    uint32_t c = 0;
-    if (i + 3 < n) {
-        const uint32_t w = *(const uint32_t *)(flags + i);
-        c = __popc(w & 0x01010101u);
-    } else {
-        for (uint64_t k = i; k < n && k < i + 4; ++k) c += flags[k] ? 1u : 0u;
-    }
+    uint32_t c = __popc(flag_bits<HITS>(src, i, n));
     for (uint32_t d = 32; d > 0; d >>= 1) c += __shfl_down(c, d);
     if ((threadIdx.x & 63u) == 0) s_cnt[threadIdx.x >> 6] = c;
     __syncthreads();
     if (threadIdx.x == 0) counts[blockIdx.x] = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
 }
 
-__global__ void __launch_bounds__(256) k_emit_flags(const uint8_t *__restrict__ flags, uint64_t n,
+template <bool HITS>
+__global__ void __launch_bounds__(256) k_emit_flags(const void *__restrict__ src, uint64_t n,
                                                     const uint32_t *__restrict__ offsets, uint32_t *__restrict__ out) {
     __shared__ uint32_t s_wave[4];
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     const uint64_t i = ((uint64_t)blockIdx.x * 256u + threadIdx.x) * 4u;
-    uint32_t bits = 0;  // bit k: flag i + k
-    for (uint32_t k = 0; k < 4; ++k)
-        if (i + k < n && flags[i + k]) bits |= 1u << k;
+    const uint32_t bits = flag_bits<HITS>(src, i, n);
     const uint32_t c = __popc(bits);
     uint32_t inc = c;
     for (uint32_t d = 1; d < 64; d <<= 1) {
@@ -502,12 +519,6 @@ __global__ void __launch_bounds__(256) k_trace_rays(DevTree t, const float *__re
     if (q.tmp) block_append(!done, (uint32_t)i, q.tmp, q.counts);
 }
 
-// Hit pixels of a previous trace (value != VHX_EMPTY), listed per workgroup: the shadow pass's first queue.
-__global__ void __launch_bounds__(256) k_list_hits(const uint32_t *__restrict__ value, uint64_t n, uint32_t *tmp,
-                                                   uint32_t *counts) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    block_append(i < n && value[i] != VHX_EMPTY, (uint32_t)i, tmp, counts);
-}
 
 // Queue pass: each wave takes 64 consecutive queue entries at a time from a shared counter until the queue written
 // by the previous pass is drained (its length is read on the device; the host never synchronises between passes).
@@ -846,9 +857,9 @@ static int launch_queue_passes(vhx_ctx *c, const DevTree &t, const CamD &cam, co
             const unsigned nb = (unsigned)((nout + 1023) / 1024);
             uint32_t *counts = (uint32_t *)c->counts.ptr, *offsets = (uint32_t *)c->offsets.ptr;
             const uint8_t *flags = (const uint8_t *)c->flags.ptr;
-            k_count_flags<<<nb, 256, 0, c->stream>>>(flags, nout, counts);
+            k_count_flags<false><<<nb, 256, 0, c->stream>>>(flags, nout, counts);
             k_scan_counts<<<1, 1024, 0, c->stream>>>(counts, nb, nullptr, 1, c->tw, offsets, ctl);
-            k_emit_flags<<<nb, 256, 0, c->stream>>>(flags, nout, offsets, (uint32_t *)c->queue[0].ptr);
+            k_emit_flags<false><<<nb, 256, 0, c->stream>>>(flags, nout, offsets, (uint32_t *)c->queue[0].ptr);
             VHX_HIP(c, hipGetLastError());
             debug_passes(c, "compacted flags");
         } else {
@@ -1265,10 +1276,14 @@ int vhx_trace_shadows(vhx_ctx *c, const float light[3], uint64_t n, const uint32
     VHX_HIP(c, hipMemsetAsync(shadowed, 0, n * 4, c->stream));
     if (bytes) VHX_HIP(c, hipMemsetAsync(bytes, 0, n * 4, c->stream));
     // wave-dense secondary rays: the hit pixels, in frame order, are pass 0's queue
-    k_list_hits<<<(unsigned)nb64, 256, 0, c->stream>>>(value, n, (uint32_t *)c->tmp.ptr, (uint32_t *)c->counts.ptr);
-    rc = compact_chunks(c, (uint32_t)nb64, nullptr, 256, 256, (uint32_t *)c->queue[1].ptr,
-                        (uint32_t *)c->qctl.ptr + 7, nb64);
-    if (rc) return rc;
+    {
+        const unsigned nb = (unsigned)((n + 1023) / 1024);
+        uint32_t *counts = (uint32_t *)c->counts.ptr, *offsets = (uint32_t *)c->offsets.ptr;
+        k_count_flags<true><<<nb, 256, 0, c->stream>>>(value, n, counts);
+        k_scan_counts<<<1, 1024, 0, c->stream>>>(counts, nb, nullptr, 1, c->tw, offsets, (uint32_t *)c->qctl.ptr + 7);
+        k_emit_flags<true><<<nb, 256, 0, c->stream>>>(value, n, offsets, (uint32_t *)c->queue[1].ptr);
+        VHX_HIP(c, hipGetLastError());
+    }
     int qrc = VHX_OK;
     auto launch = [&](auto bd_tag) {
         constexpr int BD = decltype(bd_tag)::value;
