@@ -69,6 +69,7 @@ struct vhx_ctx {
     // 1.55 ms/frame at 2048 waves against 1.62 at 8192 and 1.82 at 1024 (fewer busy waves per CU at the start of the
     // pass, while every chunk still starts at once)
     uint32_t queue_waves = 2048;
+    uint32_t queue_waves0 = 8192;  // waves of a first queue pass over fresh rays (VHX_QWAVES0)
 };
 
 #define VHX_HIP(ctx, call)                                                                                         \
@@ -887,7 +888,8 @@ static int launch_queue_passes(vhx_ctx *c, const DevTree &t, const CamD &cam, co
         const uint32_t *in = (const uint32_t *)c->queue[(p - 1) & 1u].ptr;  // p = 0: queue[1]
         const uint32_t *in_n = p > 0 ? ctl + (p - 1) : ctl + 7;
         const PassQ q = pass_q(c, p, npass);
-        const uint32_t qwaves = c->queue_waves;
+        // a first pass over fresh rays (the shadow path) is throughput-bound like a grid launch: more waves
+        const uint32_t qwaves = p == 0 ? c->queue_waves0 : c->queue_waves;
         k_trace_queue<COUNT, BD><<<(qwaves * 64u + c->qblock - 1) / c->qblock, c->qblock, 0, c->stream>>>(
             t, qa, in, in_n, ctl + 8 + p, q);
         debug_passes(c, "queue pass");
@@ -968,6 +970,8 @@ int vhx_create(int hip_device, vhx_ctx **out) {
         }
         const char *pw = getenv("VHX_QWAVES");  // after the device default
         if (pw && atoi(pw) > 0) c->queue_waves = (uint32_t)atoi(pw);
+        const char *pw0 = getenv("VHX_QWAVES0");
+        if (pw0 && atoi(pw0) > 0) c->queue_waves0 = (uint32_t)atoi(pw0);
     }
     if ((e = hipEventCreate(&c->ev0)) != hipSuccess) return bail("hipEventCreate", e);
     if ((e = hipEventCreate(&c->ev1)) != hipSuccess) return bail("hipEventCreate", e);
