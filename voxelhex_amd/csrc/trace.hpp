@@ -464,7 +464,12 @@ __device__ __forceinline__ bool get_by_ray(const DevTree &t, const uint64_t *occ
             ex = probe_brick<COUNT, BD>(t, r, p, hdesc, cocc, bb, h, iters, hflat) ? 1u : 0u;
         }
         if (ex == 0u) {
-            if (uniform || target >= 64u || occ == 0 || (occ & omask) == 0) {
+            // the three moves are sequential ifs over precomputed conditions rather than an if / else-if chain: each
+            // updates the loop state in place, where the chain's join made the compiler copy every unchanged state
+            // register twice per iteration
+            const bool pop = uniform || target >= 64u || occ == 0 || (occ & omask) == 0;
+            const bool push = !pop && ntype == VHX_NODE_INTERNAL && ((occ >> target) & 1ull) != 0;
+            if (pop) {
                 // POP (cpu.rs:368-393)
                 count -= 1;
                 node = s1;
@@ -494,7 +499,8 @@ __device__ __forceinline__ bool get_by_ray(const DevTree &t, const uint64_t *occ
                         ex = 2u;  // left the tree: a miss
                     }
                 }
-            } else if (ntype == VHX_NODE_INTERNAL && ((occ >> target) & 1ull) != 0) {
+            }
+            if (push) {
                 // PUSH (cpu.rs:401-411)
                 if (COUNT) h.bytes += 4;
                 s3 = s2;
@@ -507,7 +513,8 @@ __device__ __forceinline__ bool get_by_ray(const DevTree &t, const uint64_t *occ
                 tb = child_bounds(cur, target);
                 tbok = 1u;
                 ex = slot >= t.node_count ? 2u : 0u;  // the reference would panic on an invalid key: a miss here
-            } else {
+            }
+            if (!pop && !push) {
                 // ADVANCE (cpu.rs:416-437); at most 9 steps across the node, the pass budget is checked after it.
                 // Same form as the brick walk (exit planes, direction-normalised sectant coordinates). Every step
                 // is committed: tb.min after a step out of the node is dead (the next iteration pops and overwrites
