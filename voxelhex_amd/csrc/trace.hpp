@@ -479,8 +479,17 @@ __device__ __forceinline__ bool get_by_ray(const DevTree &t, const uint64_t *occ
                 cur.size *= 4.0f;
                 cur.min = mk(floor_to_pow2(cur.min.x, cur.size), floor_to_pow2(cur.min.y, cur.size),
                              floor_to_pow2(cur.min.z, cur.size));  // min -= min % size
-                const float hs = tb.size * 0.5f;
-                target = offset_sectant(vsub(vadd(tb.min, mk(hs, hs, hs)), cur.min), cur.size);
+                // offset_sectant(tb.center - cur.min, cur.size) is the popped cube's sectant k in its parent: tb.min =
+                // cur.min + k * tb.size (node cubes are aligned to their size, the parent is the aligned 4x cube), so
+                // center - cur.min = (k + 1/2) * tb.size exactly and floor((k + 1/2) * 4 / cur.size) = k; k is formed
+                // directly from the exact difference tb.min - cur.min
+                {
+                    const float rs = rcp_pow2(tb.size);
+                    const uint32_t kx = (uint32_t)((tb.min.x - cur.min.x) * rs),
+                                   ky = (uint32_t)((tb.min.y - cur.min.y) * rs),
+                                   kz = (uint32_t)((tb.min.z - cur.min.z) * rs);
+                    target = kx + ky * 4u + kz * 16u;
+                }
                 const uint32_t sel = dda_step(r, p, tb);
                 target = step_sectant(r, target, sel);
                 tb.min = vadd(tb.min, vmul(step_vec(r, sel), tb.size));
