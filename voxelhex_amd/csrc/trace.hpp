@@ -556,14 +556,12 @@ __device__ __forceinline__ bool get_by_ray(const DevTree &t, const uint64_t *occ
                 target = (jx | jy | jz) < 4u ? (jx + jy * 4u + jz * 16u) ^ F : 64u;
                 tb.min = vsub(e, usg);  // exact: e - usg undoes the exact e = tb.min + usg
             }
-            if (ex == 0u && ++iters > budget) {  // the next node iteration
-                ex = budget >= VHX_MAX_ITERS ? 2u : 3u;
-                if (ex == 3u && sbase)
-                    save_state(sbase + 4ull * sidx, p, iters, cur, tb, target, count, node, s1, s2, s3);
-            }
+            if (ex == 0u && ++iters > budget) ex = budget >= VHX_MAX_ITERS ? 2u : 3u;  // the next node iteration
         }
         if (ex != 0u) break;
     }
+    // an abandoned ray's state is the loop state at its exit (saved here, outside the hot loop)
+    if (ex == 3u && sbase) save_state(sbase + 4ull * sidx, p, iters, cur, tb, target, count, node, s1, s2, s3);
     if (ex == 1u) {  // the loop left on the hit: node, cur, target and p are those of the probe
         h.hit = true;
         const bool huni = t.hdr[node].z == VHX_NODE_UNIFORM_LEAF;
