@@ -56,6 +56,10 @@ struct HitOut {
 struct F3d {
     float x, y, z;
 };
+// (x, y) pairs for the walk loops: arithmetic on this type issues v_pk_add_f32 / v_pk_mul_f32 (two IEEE f32 ops per
+// lane per instruction, each rounded exactly like the scalar op), z stays scalar
+typedef float F2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ F2 mk2(float x, float y) { return F2{x, y}; }
 
 __device__ __forceinline__ F3d mk(float x, float y, float z) { return F3d{x, y, z}; }
 __device__ __forceinline__ F3d vadd(F3d a, F3d b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
@@ -273,22 +277,30 @@ __device__ __forceinline__ bool probe_brick(const DevTree &t, const RayD &r, F3d
             // step adds 1 and the flat index is j-flat ^ F.
             // e_k = min_k + (i_k + max(sg_k, 0)) * unit: every term is an exact multiple of unit below 2^24 * unit,
             // so the fused form is the value of the reference-order sum (min + i*unit) + unit*max(sg, 0) exactly
-            F3d e = mk(__builtin_fmaf((float)(ix + (int32_t)(r.isx > 0)), unit, bb.min.x),
-                       __builtin_fmaf((float)(iy + (int32_t)(r.isy > 0)), unit, bb.min.y),
-                       __builtin_fmaf((float)(iz + (int32_t)(r.isz > 0)), unit, bb.min.z));
-            const F3d sgu = mk(r.sg.x * unit, r.sg.y * unit, r.sg.z * unit);
+            F2 exy = mk2(__builtin_fmaf((float)(ix + (int32_t)(r.isx > 0)), unit, bb.min.x),
+                         __builtin_fmaf((float)(iy + (int32_t)(r.isy > 0)), unit, bb.min.y));
+            float ez = __builtin_fmaf((float)(iz + (int32_t)(r.isz > 0)), unit, bb.min.z);
+            const F2 sguxy = mk2(r.sg.x * unit, r.sg.y * unit);
+            const float sguz = r.sg.z * unit;
+            const F2 sfxy = mk2(r.sf.x, r.sf.y), dxy = mk2(r.d.x, r.d.y);
+            F2 pxy = mk2(p.x, p.y);
+            float pz = p.z;
             const uint32_t fx = r.isx > 0 ? 0u : BD - 1u, fy = r.isy > 0 ? 0u : BD - 1u, fz = r.isz > 0 ? 0u : BD - 1u;
             const uint32_t F = fx + fy * BD + fz * (BD * BD);
             uint32_t jx = (uint32_t)ix ^ fx, jy = (uint32_t)iy ^ fy, jz = (uint32_t)iz ^ fz;
             for (;;) {
                 ++iters;
                 // dda_step_to_next_sibling (cpu.rs:104-132) on the cell {cmin, unit}
-                const float dx = __builtin_fabsf((e.x - p.x) * r.sf.x), dy = __builtin_fabsf((e.y - p.y) * r.sf.y),
-                            dz = __builtin_fabsf((e.z - p.z) * r.sf.z);
+                const F2 sxy = (exy - pxy) * sfxy;
+                const float dx = __builtin_fabsf(sxy.x), dy = __builtin_fabsf(sxy.y),
+                            dz = __builtin_fabsf((ez - pz) * r.sf.z);
                 const float m = __builtin_fminf(__builtin_fminf(dx, dy), dz);
-                p = mk(p.x + r.d.x * m, p.y + r.d.y * m, p.z + r.d.z * m);
+                pxy = pxy + dxy * m;
+                pz = pz + r.d.z * m;
                 const bool mx = m == dx, my = m == dy, mz = m == dz;
-                e = mk(mx ? e.x + sgu.x : e.x, my ? e.y + sgu.y : e.y, mz ? e.z + sgu.z : e.z);
+                const F2 en = exy + sguxy;
+                exy = mk2(mx ? en.x : exy.x, my ? en.y : exy.y);
+                ez = mz ? ez + sguz : ez;
                 jx += (uint32_t)mx;
                 jy += (uint32_t)my;
                 jz += (uint32_t)mz;
@@ -313,6 +325,7 @@ __device__ __forceinline__ bool probe_brick(const DevTree &t, const RayD &r, F3d
             // hit = the exit test, recomputed once from the final cell instead of carrying the loop's booleans out of
             // it (opaque copies keep the compiler from reusing the in-loop values, which costs mask bookkeeping per
             // cell)
+            p = mk(pxy.x, pxy.y, pz);
             asm volatile("" : "+v"(jx), "+v"(jy), "+v"(jz));
             flat = (int32_t)((jx + jy * BD + jz * (BD * BD)) ^ F);
             hit = (jx | jy | jz) < (uint32_t)BD && ((word >> (flat & 63)) & 1ull) != 0ull;
@@ -534,16 +547,23 @@ __device__ __forceinline__ bool get_by_ray(const DevTree &t, const uint64_t *occ
                 const uint32_t fx = r.isx > 0 ? 0u : 3u, fy = r.isy > 0 ? 0u : 3u, fz = r.isz > 0 ? 0u : 3u;
                 const uint32_t F = fx + fy * 4u + fz * 16u;
                 uint32_t jx = (target & 3u) ^ fx, jy = ((target >> 2) & 3u) ^ fy, jz = (target >> 4) ^ fz;
-                F3d e = vadd(tb.min, usg);
+                F2 exy = mk2(tb.min.x + usg.x, tb.min.y + usg.y);
+                float ez = tb.min.z + usg.z;
+                const F2 sgsxy = mk2(sgs.x, sgs.y), sfxy = mk2(r.sf.x, r.sf.y), dxy = mk2(r.d.x, r.d.y);
+                F2 pxy = mk2(p.x, p.y);
+                float pz = p.z;
                 for (;;) {
                     ++iters;
-                    const float dx = __builtin_fabsf((e.x - p.x) * r.sf.x),
-                                dy = __builtin_fabsf((e.y - p.y) * r.sf.y),
-                                dz = __builtin_fabsf((e.z - p.z) * r.sf.z);
+                    const F2 sxy = (exy - pxy) * sfxy;
+                    const float dx = __builtin_fabsf(sxy.x), dy = __builtin_fabsf(sxy.y),
+                                dz = __builtin_fabsf((ez - pz) * r.sf.z);
                     const float m = __builtin_fminf(__builtin_fminf(dx, dy), dz);
-                    p = mk(p.x + r.d.x * m, p.y + r.d.y * m, p.z + r.d.z * m);
+                    pxy = pxy + dxy * m;
+                    pz = pz + r.d.z * m;
                     const bool mx = m == dx, my = m == dy, mz = m == dz;
-                    e = mk(mx ? e.x + sgs.x : e.x, my ? e.y + sgs.y : e.y, mz ? e.z + sgs.z : e.z);
+                    const F2 en = exy + sgsxy;
+                    exy = mk2(mx ? en.x : exy.x, my ? en.y : exy.y);
+                    ez = mz ? ez + sgs.z : ez;
                     jx += (uint32_t)mx;
                     jy += (uint32_t)my;
                     jz += (uint32_t)mz;
@@ -552,9 +572,10 @@ __device__ __forceinline__ bool get_by_ray(const DevTree &t, const uint64_t *occ
                     const uint32_t bit = (uint32_t)(occ >> (tg & 63u)) & 1u;
                     if ((oob | bit | ((iters - 1u) >> 22)) != 0u) break;  // left | occupied | iters > 2^22
                 }
+                p = mk(pxy.x, pxy.y, pz);
                 asm volatile("" : "+v"(jx), "+v"(jy), "+v"(jz));
                 target = (jx | jy | jz) < 4u ? (jx + jy * 4u + jz * 16u) ^ F : 64u;
-                tb.min = vsub(e, usg);  // exact: e - usg undoes the exact e = tb.min + usg
+                tb.min = mk(exy.x - usg.x, exy.y - usg.y, ez - usg.z);  // exact: undoes the exact e = tb.min + usg
             }
             if (ex == 0u && ++iters > budget) ex = budget >= VHX_MAX_ITERS ? 2u : 3u;  // the next node iteration
         }
