@@ -197,21 +197,41 @@ def test_update_range(gpu, oracle):
         gpu.update_range(N.VHX_BUF_VOXELS, vox.size - 4, np.zeros(8, np.uint32))
 
 
-def test_full_size_frame_crops(gpu, oracle):
-    """BASELINE config 3 geometry (1024^3, brick_dim 4, 3840x2160): GPU frame checked on oracle crops, plus
-    run-to-run idempotence of the whole frame."""
+def test_full_size_frame_vs_oracle(gpu, oracle):
+    """The bench frame (BASELINE config 3 geometry: 1024^3, brick_dim 4, 3840x2160, default schedule): every pixel of
+    the GPU frame equals the oracle's in every field, byte counts included, and the frame is identical run to run."""
     flat = vhx.FlatTree.build_scene(N.VHX_SCENE_LATTICE_CUBE, 1024, 4)
     gpu.upload(flat)
     W, H = 3840, 2160
     cam = vhx.glass_camera(1024, W, H, target=(512.0, 512.0, 512.0))
-    a = gpu.trace_primary(cam, fields=("value", "cell", "voxel", "depth", "rgba"))
-    b = gpu.trace_primary(cam, fields=("value", "cell", "voxel", "depth", "rgba"))
-    assert_same(a, b, "idempotence")
-    for (x0, y0) in ((0, 0), (1888, 1048), (3776, 2096), (1000, 300)):
-        ref = oracle.trace_primary(flat, cam, x0, y0, 64, 64, fields=("value", "cell", "voxel", "depth", "rgba"))
-        idx = (np.arange(y0, y0 + 64)[:, None] * W + np.arange(x0, x0 + 64)[None, :]).reshape(-1)
-        assert_same({k: v[idx] for k, v in a.items()}, ref, f"crop {x0},{y0}")
+    fields = ("value", "cell", "voxel", "impact", "normal", "depth", "rgba")
+    ref = oracle.trace_primary(flat, cam, 0, 0, W, H, fields=fields, count_bytes=True)
+    a = gpu.trace_primary(cam, fields=fields)  # the kernels bench.py times (no byte counting)
+    assert_same(a, {k: ref[k] for k in fields}, "full frame")
+    assert_same(gpu.trace_primary(cam, fields=fields), a, "idempotence")
+    counted = gpu.trace_primary(cam, fields=(), count_bytes=True)
+    assert np.array_equal(counted["bytes"], ref["bytes"]), "byte counts differ"
     assert (a["value"] != N.VHX_EMPTY).mean() > 0.2
+
+
+def test_full_size_shadows_vs_oracle(gpu, oracle):
+    """BASELINE config 5 at full size: shadow flags, darkened rgba and byte counts of the bench frame's 2.5 M shadow
+    rays equal the oracle's."""
+    flat = vhx.FlatTree.build_scene(N.VHX_SCENE_LATTICE_CUBE, 1024, 4)
+    gpu.upload(flat)
+    W, H = 3840, 2160
+    cam = vhx.glass_camera(1024, W, H, target=(512.0, 512.0, 512.0))
+    light = (1024.0,) * 3
+    hits = gpu.trace_primary(cam, out=_device_hits(W * H))
+    res = gpu.trace_shadows(light, hits, count_bytes=True)
+    gpu.sync()
+    ref_primary = oracle.trace_primary(flat, cam, 0, 0, W, H, fields=("value", "impact", "normal", "rgba"))
+    ref = oracle.trace_shadows(flat, light, ref_primary)
+    sh = res["shadowed"].cpu().numpy().view(np.uint32)
+    assert np.array_equal(sh, ref["shadowed"]), f"shadow flags differ at {np.count_nonzero(sh != ref['shadowed'])}"
+    assert np.array_equal(hits["rgba"].cpu().numpy().view(np.uint32), ref["rgba"])
+    assert np.array_equal(res["bytes"].cpu().numpy().view(np.uint32), ref["bytes"])
+    assert sh.sum() > 100000
 
 
 DEFAULT_BUDGETS = (64,)
