@@ -197,10 +197,13 @@ def test_update_range(gpu, oracle):
         gpu.update_range(N.VHX_BUF_VOXELS, vox.size - 4, np.zeros(8, np.uint32))
 
 
-def test_full_size_frame_vs_oracle(gpu, oracle):
-    """The bench frame (BASELINE config 3 geometry: 1024^3, brick_dim 4, 3840x2160, default schedule): every pixel of
-    the GPU frame equals the oracle's in every field, byte counts included, and the frame is identical run to run."""
-    flat = vhx.FlatTree.build_scene(N.VHX_SCENE_LATTICE_CUBE, 1024, 4)
+@pytest.mark.parametrize("scene,bd", [(N.VHX_SCENE_LATTICE_CUBE, 4), (N.VHX_SCENE_LATTICE_CUBE, 16),
+                                      (N.VHX_SCENE_HEIGHTFIELD, 4)])
+def test_full_size_frame_vs_oracle(gpu, oracle, scene, bd):
+    """The bench frame (BASELINE config 3 geometry: 1024^3, 3840x2160, default schedule; scene S at brick_dim 4 is
+    the bench workload): every pixel of the GPU frame equals the oracle's in every field, byte counts included, and
+    the frame is identical run to run."""
+    flat = vhx.FlatTree.build_scene(scene, 1024, bd)
     gpu.upload(flat)
     W, H = 3840, 2160
     cam = vhx.glass_camera(1024, W, H, target=(512.0, 512.0, 512.0))
@@ -211,7 +214,7 @@ def test_full_size_frame_vs_oracle(gpu, oracle):
     assert_same(gpu.trace_primary(cam, fields=fields), a, "idempotence")
     counted = gpu.trace_primary(cam, fields=(), count_bytes=True)
     assert np.array_equal(counted["bytes"], ref["bytes"]), "byte counts differ"
-    assert (a["value"] != N.VHX_EMPTY).mean() > 0.2
+    assert (a["value"] != N.VHX_EMPTY).mean() > 0.1
 
 
 def test_full_size_shadows_vs_oracle(gpu, oracle):
