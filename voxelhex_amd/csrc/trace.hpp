@@ -370,12 +370,14 @@ __device__ __forceinline__ void save_state(uint4 *st, F3d p, uint32_t iters, Cub
     st[3] = make_uint4(node, s1, s2, s3);
 }
 
-// BoxTree::get_by_ray, src/raytracing/cpu.rs:296-458.
+// BoxTree::get_by_ray, src/raytracing/cpu.rs:296-458, as a traversal state with three steps: begin (ray setup and the
+// root intersection, or a resumed state), step (one iteration of the node loop) and end (save an abandoned ray's
+// state, or fill the hit record). get_by_ray runs them back to back; a caller may also interleave rays per lane.
 // `budget` bounds the loop iterations (node, advance and brick steps, counted from the ray's start; checked at the end
 // of each node iteration, so a pass may overrun it by one brick walk and one advance). With budget == VHX_MAX_ITERS
-// this is the full traversal (a ray exceeding the bound is a miss, as in the oracle) and the return value is always
-// true. A smaller budget makes a pass of the multi-pass scheduler: false = the ray was abandoned after `budget` steps;
-// with `sbase` given, its state is saved at sbase[4 * sidx] and a later pass continues it (`resume`) exactly where it
+// this is the full traversal (a ray exceeding the bound is a miss, as in the oracle) and end() always returns true.
+// A smaller budget makes a pass of the multi-pass scheduler: false = the ray was abandoned after `budget` steps; with
+// `sbase` given, its state is saved at sbase[4 * sidx] and a later pass continues it (`resume`) exactly where it
 // stopped, otherwise the later pass traces it again from scratch. Either way the result is bit-identical to one
 // uninterrupted traversal (the state is saved whole; the traversal is deterministic). h.bytes is the caller's running
 // byte count (COUNT builds): 0 for a fresh ray, the count at the abandon for a resumed one.
@@ -385,69 +387,81 @@ __device__ __forceinline__ void save_state(uint4 *st, F3d p, uint32_t iters, Cub
 // NodeStack<u32, 4> ring (cpu.rs:18-76) is a shift register: `node` is its top, s1..s3 the entries below; a push onto
 // a full stack drops the oldest entry, a pop that empties it ends the walk and restarts from the root.
 template <bool COUNT, int BD>
-__device__ __forceinline__ bool get_by_ray(const DevTree &t, const uint64_t *occ_tab, F3d o, F3d d, HitOut &h,
-                                           uint32_t budget, uint4 *sbase = nullptr, uint32_t sidx = 0,
-                                           bool resume = false) {
-    // the state slot is addressed from a uniform base and the ray's index (one VGPR live, not a 64-bit pointer)
-    h.hit = false;
+struct Trav {
     RayD r;
-    ray_setup(r, o, d);
     uint32_t dir_idx;
-    {
-        const F3d od = vadd(mk(1.0f, 1.0f, 1.0f), d);
-        dir_idx = (uint32_t)(od.x >= 1.0f) + (uint32_t)(od.z >= 1.0f) * 2u + (uint32_t)(od.y >= 1.0f) * 4u;
-    }
-    const float tsize = (float)t.size;
+    float tsize;
     CubeD cur;
     F3d p;
     uint32_t target;
     CubeD tb;
     uint32_t node, s1, s2, s3, count, iters;
-    if (resume) {
-        const uint4 *st = sbase + 4ull * sidx;
-        const uint4 a = st[0], b = st[1], c = st[2], e = st[3];
-        p = mk(__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(a.z));
-        iters = a.w;
-        cur.min = mk(__uint_as_float(b.x), __uint_as_float(b.y), __uint_as_float(b.z));
-        cur.size = __uint_as_float(b.w & 0xFF800000u);
-        target = b.w & 0x7Fu;
-        count = (b.w >> 8) & 7u;
-        tb.min = mk(__uint_as_float(c.x), __uint_as_float(c.y), __uint_as_float(c.z));
-        tb.size = __uint_as_float(c.w);
-        node = e.x;
-        s1 = e.y;
-        s2 = e.z;
-        s3 = e.w;
-    } else {
-        cur.min = mk(0.0f, 0.0f, 0.0f);
-        cur.size = tsize;
-        // Cube::intersect_ray, src/spatial/raytracing/mod.rs:33-62 (root: min 0, max = 0 + size = size)
-        const float t1 = (0.0f - o.x) / d.x, t2 = (tsize - o.x) / d.x;
-        const float t3 = (0.0f - o.y) / d.y, t4 = (tsize - o.y) / d.y;
-        const float t5 = (0.0f - o.z) / d.z, t6 = (tsize - o.z) / d.z;
-        const float tmin = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(t1, t2), __builtin_fminf(t3, t4)),
-                                           __builtin_fminf(t5, t6));
-        const float tmax = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(t1, t2), __builtin_fmaxf(t3, t4)),
-                                           __builtin_fmaxf(t5, t6));
-        if (tmax < 0.0f || tmin > tmax) return true;  // target = 64: the outer loop never runs
-        p = vadd(o, vmul(d, tmin < 0.0f ? 0.0f : tmin));
-        target = offset_sectant(p, cur.size);
-        tb = child_bounds(cur, target);
-        node = 0, s1 = 0, s2 = 0, s3 = 0, count = 1;  // push(ROOT)
-        iters = 1;  // the first node iteration
-    }
-    ray_scale_factors(r);
     // how the loop ended, one integer instead of several booleans (kept in a VGPR; boolean flags set in divergent
     // branches become 64-bit lane masks merged by scalar instructions at every join): 0 = still running, 1 = hit,
     // 2 = miss (left the tree, invalid key, or the iteration bound), 3 = abandoned at the pass budget
-    uint32_t ex = 0;
+    uint32_t ex;
     // tbok: target_bounds equals child_bounds(current, target) (kept by PUSH, POP and ADVANCE; not after a restart,
     // which leaves it stale, cpu.rs:317-320), so a leaf probe takes its brick cube from tb instead of recomputing it.
     // A resumed ray starts with 0 (recompute), which is always correct.
-    uint32_t tbok = resume ? 0u : 1u;
-    uint32_t hdesc = 0;
-    int32_t hflat = 0;
-    for (;;) {
+    uint32_t tbok;
+    uint32_t hdesc;
+    int32_t hflat;
+
+    // false: the ray misses the root cube (a miss, nothing more to do)
+    __device__ __forceinline__ bool begin(const DevTree &t, F3d o, F3d d, HitOut &h, const uint4 *sbase, uint32_t sidx,
+                                          bool resume) {
+        h.hit = false;
+        ray_setup(r, o, d);
+        {
+            const F3d od = vadd(mk(1.0f, 1.0f, 1.0f), d);
+            dir_idx = (uint32_t)(od.x >= 1.0f) + (uint32_t)(od.z >= 1.0f) * 2u + (uint32_t)(od.y >= 1.0f) * 4u;
+        }
+        tsize = (float)t.size;
+        ex = 0;
+        hdesc = 0;
+        hflat = 0;
+        if (resume) {
+            const uint4 *st = sbase + 4ull * sidx;
+            const uint4 a = st[0], b = st[1], c = st[2], e = st[3];
+            p = mk(__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(a.z));
+            iters = a.w;
+            cur.min = mk(__uint_as_float(b.x), __uint_as_float(b.y), __uint_as_float(b.z));
+            cur.size = __uint_as_float(b.w & 0xFF800000u);
+            target = b.w & 0x7Fu;
+            count = (b.w >> 8) & 7u;
+            tb.min = mk(__uint_as_float(c.x), __uint_as_float(c.y), __uint_as_float(c.z));
+            tb.size = __uint_as_float(c.w);
+            node = e.x;
+            s1 = e.y;
+            s2 = e.z;
+            s3 = e.w;
+        } else {
+            cur.min = mk(0.0f, 0.0f, 0.0f);
+            cur.size = tsize;
+            // Cube::intersect_ray, src/spatial/raytracing/mod.rs:33-62 (root: min 0, max = 0 + size = size)
+            const float t1 = (0.0f - o.x) / d.x, t2 = (tsize - o.x) / d.x;
+            const float t3 = (0.0f - o.y) / d.y, t4 = (tsize - o.y) / d.y;
+            const float t5 = (0.0f - o.z) / d.z, t6 = (tsize - o.z) / d.z;
+            const float tmin = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(t1, t2), __builtin_fminf(t3, t4)),
+                                               __builtin_fminf(t5, t6));
+            const float tmax = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(t1, t2), __builtin_fmaxf(t3, t4)),
+                                               __builtin_fmaxf(t5, t6));
+            if (tmax < 0.0f || tmin > tmax) {  // the outer loop never runs: a miss
+                ex = 2u;
+                return false;
+            }
+            p = vadd(o, vmul(d, tmin < 0.0f ? 0.0f : tmin));
+            target = offset_sectant(p, cur.size);
+            tb = child_bounds(cur, target);
+            node = 0, s1 = 0, s2 = 0, s3 = 0, count = 1;  // push(ROOT)
+            iters = 1;  // the first node iteration
+        }
+        ray_scale_factors(r);
+        tbok = resume ? 0u : 1u;
+        return true;
+    }
+
+    __device__ __forceinline__ void step(const DevTree &t, const uint64_t *occ_tab, HitOut &h, uint32_t budget) {
         const uint4 lh = t.hdr[node];
         // the child slot is read by both the leaf probe and the push: issue it with the header load so the
         // iteration waits for one memory latency instead of two (with brick_dim <= 4 the child record also carries
@@ -509,7 +523,7 @@ __device__ __forceinline__ bool get_by_ray(const DevTree &t, const uint64_t *occ
                 tbok = 1u;
                 if (count == 0) {
                     // the stack ran empty: restart from the root (cpu.rs:441-455); target_bounds stays stale
-                    p = vadd(p, vmul(d, 0.1f));
+                    p = vadd(p, vmul(r.d, 0.1f));
                     if (p.x < tsize && p.y < tsize && p.z < tsize && p.x > 0.0f && p.y > 0.0f && p.z > 0.0f) {
                         target = offset_sectant(p, tsize);
                         tbok = 0u;  // target_bounds stays stale
@@ -579,16 +593,31 @@ __device__ __forceinline__ bool get_by_ray(const DevTree &t, const uint64_t *occ
             }
             if (ex == 0u && ++iters > budget) ex = budget >= VHX_MAX_ITERS ? 2u : 3u;  // the next node iteration
         }
-        if (ex != 0u) break;
     }
-    // an abandoned ray's state is the loop state at its exit (saved here, outside the hot loop)
-    if (ex == 3u && sbase) save_state(sbase + 4ull * sidx, p, iters, cur, tb, target, count, node, s1, s2, s3);
-    if (ex == 1u) {  // the loop left on the hit: node, cur, target and p are those of the probe
-        h.hit = true;
-        const bool huni = t.hdr[node].z == VHX_NODE_UNIFORM_LEAF;
-        finish_hit<BD>(t, h, hdesc, hflat, p, huni ? cur : child_bounds(cur, target));
+
+    __device__ __forceinline__ bool end(const DevTree &t, HitOut &h, uint4 *sbase, uint32_t sidx) {
+        // an abandoned ray's state is the loop state at its exit (saved here, outside the hot loop)
+        if (ex == 3u && sbase) save_state(sbase + 4ull * sidx, p, iters, cur, tb, target, count, node, s1, s2, s3);
+        if (ex == 1u) {  // the loop left on the hit: node, cur, target and p are those of the probe
+            h.hit = true;
+            const bool huni = t.hdr[node].z == VHX_NODE_UNIFORM_LEAF;
+            finish_hit<BD>(t, h, hdesc, hflat, p, huni ? cur : child_bounds(cur, target));
+        }
+        return ex != 3u;
     }
-    return ex != 3u;
+};
+
+template <bool COUNT, int BD>
+__device__ __forceinline__ bool get_by_ray(const DevTree &t, const uint64_t *occ_tab, F3d o, F3d d, HitOut &h,
+                                           uint32_t budget, uint4 *sbase = nullptr, uint32_t sidx = 0,
+                                           bool resume = false) {
+    Trav<COUNT, BD> tr;
+    if (!tr.begin(t, o, d, h, sbase, sidx, resume)) return true;
+    for (;;) {
+        tr.step(t, occ_tab, h, budget);
+        if (tr.ex != 0u) break;
+    }
+    return tr.end(t, h, sbase, sidx);
 }
 
 }  // namespace vhx
