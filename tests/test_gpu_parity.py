@@ -291,10 +291,21 @@ def test_scheduler_variants_are_bit_identical(oracle, monkeypatch, env):
         cam = vhx.glass_camera(256, 160, 96, target=(128.0, 128.0, 128.0))
         ref_rays = oracle.trace_rays(flat, o, d, count_bytes=True)
         ref_frame = oracle.trace_primary(flat, cam, 0, 0, 160, 96, count_bytes=True)
-        for budgets in ((2, 9, 30), (16,)):
+        for budgets in ((2, 9, 30), (16,), ()):
             rt.set_pass_budgets(budgets)
             assert_same(rt.trace_rays(o, d, count_bytes=True), ref_rays, f"rays {env} {budgets}")
             assert_same(rt.trace_primary(cam, count_bytes=True), ref_frame, f"frame {env} {budgets}")
+            full = ref_frame["rgba"].reshape(96, 160)
+            for T, R in ((64, 2), (24, 3)):  # tile layout: the pixel stream maps back through the tile numbering
+                tiles_x = (160 + T - 1) // T
+                for r in range(R):
+                    part = rt.trace_primary(cam, tile_size=T, tile_start=r, tile_stride=R, layout=N.VHX_LAYOUT_TILES,
+                                            fields=("rgba",))["rgba"].reshape(-1, T, T)
+                    for j in range(part.shape[0]):
+                        tile = r + j * R
+                        tx, ty = (tile % tiles_x) * T, (tile // tiles_x) * T
+                        want = full[ty:ty + T, tx:tx + T]
+                        assert np.array_equal(part[j, :want.shape[0], :want.shape[1]], want), (env, budgets, T, tile)
     finally:
         rt.close()
 
