@@ -241,11 +241,15 @@ def main():
         orc = Oracle()
         cores = max(1, min(16, len(os.sched_getaffinity(0))))
         orc.trace_primary(flat, cam, 0, 0, W, 16, threads=cores, fields=("rgba",))  # warm
-        t0 = time.perf_counter()
-        orc.trace_primary(flat, cam, 0, 0, W, H, threads=cores, fields=("rgba", "depth"))
-        cpu_s = time.perf_counter() - t0
+        ts = []
+        for _ in range(3):  # three full frames (about 15 s of CPU work on 16 cores), the median reported
+            t0 = time.perf_counter()
+            orc.trace_primary(flat, cam, 0, 0, W, H, threads=cores, fields=("rgba", "depth"))
+            ts.append(time.perf_counter() - t0)
+        cpu_s = sorted(ts)[1]
         cpu = {"value": round(W * H / cpu_s / 1e6, 4), "unit": "Mrays/s", "cores": cores, "kind": "port",
-               "sample": f"full {W}x{H} frame, same tree and camera, OpenMP dynamic over pixels, {cpu_s:.2f} s"}
+               "sample": f"median of 3 full {W}x{H} frames, same tree and camera, OpenMP dynamic over pixels, "
+                         f"{cpu_s:.2f} s per frame"}
 
     if rank == 0:
         metric = BASELINE["metric"]
