@@ -108,7 +108,7 @@ __device__ __forceinline__ float floor_to_pow2(float x, float s) {
 
 // RAY_TO_NODE_OCCUPANCY_BITMASK_LUT[s][o] (src/spatial/lut.rs:96-161): sectants t with t_k on the ray's side of
 // s_k on every axis; o = (dx>=0) + 2(dz>=0) + 4(dy>=0).
-__device__ __forceinline__ uint64_t occ_lut(uint32_t s, uint32_t o) {
+__host__ __device__ constexpr uint64_t occ_lut(uint32_t s, uint32_t o) {
     const uint32_t sx = s & 3u, sy = (s >> 2) & 3u, sz = s >> 4;
     const uint32_t mx = (o & 1u) ? (0xFu << sx) & 0xFu : (0xFu >> (3u - sx));
     const uint32_t my = (o & 4u) ? (0xFu << sy) & 0xFu : (0xFu >> (3u - sy));
@@ -352,9 +352,19 @@ __device__ __forceinline__ void finish_hit(const DevTree &t, HitOut &h, uint32_t
     fill_hit(h, v, (uint32_t)hflat, p, hb);
 }
 
-// RAY_TO_NODE_OCCUPANCY_BITMASK_LUT in LDS: occ_tab[s * 8 + o] = occ_lut(s, o); filled by the block before tracing.
+// RAY_TO_NODE_OCCUPANCY_BITMASK_LUT, tabulated at compile time (occ_tab[s * 8 + o] = occ_lut(s, o), 4 KB in constant
+// memory) and copied into LDS by every block before tracing (a copy instead of 512 evaluations per block).
+struct OccTab {
+    uint64_t v[512];
+};
+constexpr OccTab make_occ_tab() {
+    OccTab t{};
+    for (uint32_t i = 0; i < 512u; ++i) t.v[i] = occ_lut(i >> 3, i & 7u);
+    return t;
+}
+__constant__ OccTab g_occ_tab = make_occ_tab();
 __device__ __forceinline__ void fill_occ_tab(uint64_t *occ_tab) {
-    for (uint32_t i = threadIdx.x; i < 512u; i += blockDim.x) occ_tab[i] = occ_lut(i >> 3, i & 7u);
+    for (uint32_t i = threadIdx.x; i < 512u; i += blockDim.x) occ_tab[i] = g_occ_tab.v[i];
 }
 
 // Saved traversal state of a ray abandoned at a pass budget (multi-pass scheduling): everything the loop below
