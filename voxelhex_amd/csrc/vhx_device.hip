@@ -51,9 +51,9 @@ struct vhx_ctx {
     DevBuf counts;    // rays listed per chunk
     DevBuf offsets;   // exclusive scan of counts
     DevBuf flags;     // primary pass 0: abandoned flag per output index
-    DevBuf qargs;     // QueueArgs of the queue passes
-    std::vector<uint8_t> qargs_host;  // the QueueArgs last written to qargs (skips the upload when unchanged)
-    void *qargs_host_ptr = nullptr;   // qargs.ptr it was written to
+    DevBuf qargs;     // QueueArgs of the queue passes: slot 0 primary rays / ray batches, slot 1 shadow rays
+    std::vector<uint8_t> qargs_host[2];  // the QueueArgs last written to each slot (skips the upload when unchanged)
+    void *qargs_host_ptr[2] = {nullptr, nullptr};  // qargs.ptr they were written to
     DevBuf state;     // saved traversal state per output index (64 B) of rays abandoned at a budget
     uint32_t occ_words = 1;
     // step budgets of the passes before the final (unbounded) one; VHX_BUDGETS="64" / "32,256" style override
@@ -293,6 +293,15 @@ __device__ __forceinline__ void block_append(bool push, uint32_t idx, uint32_t *
 
 // Exclusive scan of the chunk counts in one workgroup of 1024 threads; nchunks = ceil(*n_in / per_chunk) when n_in
 // is given (a queue pass: its input length is only known on the device), else nchunks_host. Writes *total.
+// Each wave scans 1024 consecutive counts per segment as 16 coalesced rows of 64 (a wave-wide scan per row), the
+// waves' totals are combined through LDS.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, uint32_t lane) {
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t x = __shfl_up(v, d);
+        if (lane >= d) v += x;
+    }
+    return v;
+}
 __global__ void __launch_bounds__(1024) k_scan_counts(const uint32_t *__restrict__ counts, uint32_t nchunks_host,
                                                       const uint32_t *n_in, uint32_t per_chunk, uint32_t tw,
                                                       uint32_t *__restrict__ offsets, uint32_t *total) {
@@ -301,34 +310,35 @@ __global__ void __launch_bounds__(1024) k_scan_counts(const uint32_t *__restrict
     const uint32_t pc = n_in ? pass_rpw(per_chunk, tw, *n_in) : per_chunk;
     const uint32_t nchunks = n_in ? (*n_in + pc - 1) / pc : nchunks_host;
     const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
-    constexpr uint32_t K = 16;  // elements per thread per segment; loads issued together
+    constexpr uint32_t K = 16;  // rows of 64 per wave per segment; loads issued together
     if (t == 0) s_carry = 0;
     __syncthreads();
     for (uint32_t seg = 0; seg < nchunks; seg += 1024u * K) {
-        const uint32_t b = seg + t * K;
+        const uint32_t b = seg + wave * (64u * K) + lane;
         uint32_t v[K];
 #pragma unroll
-        for (uint32_t k = 0; k < K; ++k) v[k] = b + k < nchunks ? counts[b + k] : 0u;
-        uint32_t sum = 0;
+        for (uint32_t k = 0; k < K; ++k) v[k] = b + 64u * k < nchunks ? counts[b + 64u * k] : 0u;
+        uint32_t run = 0;  // the wave's sum of the rows before row k
 #pragma unroll
-        for (uint32_t k = 0; k < K; ++k) sum += v[k];
-        uint32_t inc = sum;  // inclusive scan within the wave
-        for (uint32_t d = 1; d < 64; d <<= 1) {
-            const uint32_t x = __shfl_up(inc, d);
-            if (lane >= d) inc += x;
+        for (uint32_t k = 0; k < K; ++k) {
+            const uint32_t inc = wave_incl_scan(v[k], lane);
+            const uint32_t row = __shfl(inc, 63);
+            v[k] = run + inc - v[k];  // exclusive within the wave's 1024 counts
+            run += row;
         }
-        if (lane == 63) s_wave[wave] = inc;
+        if (lane == 0) s_wave[wave] = run;
         __syncthreads();
         uint32_t before = s_carry;
         for (uint32_t w = 0; w < wave; ++w) before += s_wave[w];
-        uint32_t run = before + inc - sum;
 #pragma unroll
-        for (uint32_t k = 0; k < K; ++k) {
-            if (b + k < nchunks) offsets[b + k] = run;
-            run += v[k];
-        }
+        for (uint32_t k = 0; k < K; ++k)
+            if (b + 64u * k < nchunks) offsets[b + 64u * k] = before + v[k];
         __syncthreads();
-        if (t == 1023) s_carry = before + inc;
+        if (t == 0) {
+            uint32_t sum = s_carry;
+            for (uint32_t w = 0; w < 16u; ++w) sum += s_wave[w];
+            s_carry = sum;
+        }
         __syncthreads();
     }
     if (t == 0) *total = s_carry;
@@ -783,7 +793,7 @@ static int prepare_passes(vhx_ctx *c, uint64_t nout, uint64_t nblocks0, uint32_t
     int rc = ensure(c, c->queue[0], nout * 4);
     if (!rc && (npass > 2 || shadow)) rc = ensure(c, c->queue[1], nout * 4);
     if (!rc) rc = ensure(c, c->qctl, 16 * sizeof(uint32_t));
-    if (!rc) rc = ensure(c, c->qargs, sizeof(QueueArgs));
+    if (!rc) rc = ensure(c, c->qargs, 2 * sizeof(QueueArgs));
     if (!rc) rc = ensure(c, c->tmp, list * 4);
     if (!rc) rc = ensure(c, c->counts, chunks * 4);
     if (!rc) rc = ensure(c, c->offsets, chunks * 4);
@@ -867,7 +877,8 @@ static int launch_queue_passes(vhx_ctx *c, const DevTree &t, const CamD &cam, co
             rc = compact_chunks(c, (uint32_t)nblocks0, nullptr, 256, 256, (uint32_t *)c->queue[0].ptr, ctl, nblocks0);
         }
     }
-    QueueArgs *qa = (QueueArgs *)c->qargs.ptr;
+    const uint32_t slot = src.kind == 3u ? 1u : 0u;  // a shadow frame alternates with its primary frame
+    QueueArgs *qa = (QueueArgs *)c->qargs.ptr + slot;
     if (first < npass) {
         // camera, ray source and outputs rarely change between frames: the device copy is rewritten only when they do
         QueueArgs a;
@@ -876,12 +887,12 @@ static int launch_queue_passes(vhx_ctx *c, const DevTree &t, const CamD &cam, co
         a.src = src;
         a.out = o;
         const uint8_t *ab = (const uint8_t *)&a;
-        if (c->qargs_host_ptr != c->qargs.ptr || c->qargs_host.size() != sizeof(a) ||
-            std::memcmp(c->qargs_host.data(), ab, sizeof(a)) != 0) {
+        if (c->qargs_host_ptr[slot] != c->qargs.ptr || c->qargs_host[slot].size() != sizeof(a) ||
+            std::memcmp(c->qargs_host[slot].data(), ab, sizeof(a)) != 0) {
             k_put_queue_args<<<1, 64, 0, c->stream>>>(a, qa);
             VHX_HIP(c, hipGetLastError());
-            c->qargs_host.assign(ab, ab + sizeof(a));
-            c->qargs_host_ptr = c->qargs.ptr;
+            c->qargs_host[slot].assign(ab, ab + sizeof(a));
+            c->qargs_host_ptr[slot] = c->qargs.ptr;
         }
     }
     for (uint32_t p = first; p < npass && !rc; ++p) {
@@ -1013,7 +1024,7 @@ const char *vhx_last_error(const vhx_ctx *c) { return c ? c->err.c_str() : "null
 int vhx_set_stream(vhx_ctx *c, void *s) {
     if (!c) return VHX_E_INVALID_ARG;
     c->stream = s ? (hipStream_t)s : c->own_stream;
-    c->qargs_host_ptr = nullptr;  // the cached queue arguments were written on the previous stream: rewrite them
+    c->qargs_host_ptr[0] = c->qargs_host_ptr[1] = nullptr;  // written on the previous stream: rewrite them
     return VHX_OK;
 }
 
