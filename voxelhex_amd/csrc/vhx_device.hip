@@ -368,10 +368,12 @@ __device__ __forceinline__ uint32_t flag_bits(const void *src, uint64_t i, uint6
     return bits;
 }
 
+// zero8: the queue passes' work counters (qctl[8..15]), zeroed here instead of by a separate memset launch
 template <bool HITS>
 __global__ void __launch_bounds__(256) k_count_flags(const void *__restrict__ src, uint64_t n,
-                                                     uint32_t *__restrict__ counts) {
+                                                     uint32_t *__restrict__ counts, uint32_t *zero8) {
     __shared__ uint32_t s_cnt[4];
+    if (blockIdx.x == 0 && threadIdx.x < 8u) zero8[threadIdx.x] = 0u;
     const uint64_t i = ((uint64_t)blockIdx.x * 256u + threadIdx.x) * 4u;
     uint32_t c = __popc(flag_bits<HITS>(src, i, n));
     for (uint32_t d = 32; d > 0; d >>= 1) c += __shfl_down(c, d);
@@ -802,9 +804,10 @@ static int prepare_passes(vhx_ctx *c, uint64_t nout, uint64_t nblocks0, uint32_t
     return rc;
 }
 
-// Stream-ordered per-trace reset of the pass state (inside the timed region).
-static int reset_passes(vhx_ctx *c, uint32_t npass, bool shadow = false) {
-    if (npass < 2 && !shadow) return VHX_OK;
+// Stream-ordered per-trace reset of the pass state (inside the timed region) for ray batches; primary and shadow
+// frames zero the counters in their first compaction kernel instead.
+static int reset_passes(vhx_ctx *c, uint32_t npass) {
+    if (npass < 2) return VHX_OK;
     VHX_HIP(c, hipMemsetAsync(c->qctl.ptr, 0, 16 * sizeof(uint32_t), c->stream));
     return VHX_OK;
 }
@@ -868,7 +871,7 @@ static int launch_queue_passes(vhx_ctx *c, const DevTree &t, const CamD &cam, co
             const unsigned nb = (unsigned)((nout + 1023) / 1024);
             uint32_t *counts = (uint32_t *)c->counts.ptr, *offsets = (uint32_t *)c->offsets.ptr;
             const uint8_t *flags = (const uint8_t *)c->flags.ptr;
-            k_count_flags<false><<<nb, 256, 0, c->stream>>>(flags, nout, counts);
+            k_count_flags<false><<<nb, 256, 0, c->stream>>>(flags, nout, counts, ctl + 8);
             k_scan_counts<<<1, 1024, 0, c->stream>>>(counts, nb, nullptr, 1, c->tw, offsets, ctl);
             k_emit_flags<false><<<nb, 256, 0, c->stream>>>(flags, nout, offsets, (uint32_t *)c->queue[0].ptr);
             VHX_HIP(c, hipGetLastError());
@@ -1181,8 +1184,7 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
     src.tile_start = tile_start;
     src.tile_stride = tile_stride;
     VHX_HIP(c, hipEventRecord(c->ev0, c->stream));
-    rc = reset_passes(c, npass);
-    if (rc) return rc;
+    // no reset_passes: the flag compaction after pass 0 zeroes the queue passes' counters
     const bool count = ho.dev.bytes != nullptr;
     int qrc = VHX_OK;
     auto launch = [&](auto bd_tag) {
@@ -1286,15 +1288,14 @@ int vhx_trace_shadows(vhx_ctx *c, const float light[3], uint64_t n, const uint32
     so.bytes = bytes;
     CamD cd{};
     VHX_HIP(c, hipEventRecord(c->ev0, c->stream));
-    rc = reset_passes(c, npass, true);
-    if (rc) return rc;
+    // no reset_passes: the hit compaction (k_count_flags) zeroes the queue passes' counters
     VHX_HIP(c, hipMemsetAsync(shadowed, 0, n * 4, c->stream));
     if (bytes) VHX_HIP(c, hipMemsetAsync(bytes, 0, n * 4, c->stream));
     // wave-dense secondary rays: the hit pixels, in frame order, are pass 0's queue
     {
         const unsigned nb = (unsigned)((n + 1023) / 1024);
         uint32_t *counts = (uint32_t *)c->counts.ptr, *offsets = (uint32_t *)c->offsets.ptr;
-        k_count_flags<true><<<nb, 256, 0, c->stream>>>(value, n, counts);
+        k_count_flags<true><<<nb, 256, 0, c->stream>>>(value, n, counts, (uint32_t *)c->qctl.ptr + 8);
         k_scan_counts<<<1, 1024, 0, c->stream>>>(counts, nb, nullptr, 1, c->tw, offsets, (uint32_t *)c->qctl.ptr + 7);
         k_emit_flags<true><<<nb, 256, 0, c->stream>>>(value, n, offsets, (uint32_t *)c->queue[1].ptr);
         VHX_HIP(c, hipGetLastError());
