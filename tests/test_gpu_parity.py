@@ -436,3 +436,25 @@ def test_tile_layout_padding_reads_zero_and_bytes_add_up(gpu):
             h = min(T, H - (tile // tiles_x) * T)
             assert (v[j, h:, :] == 0).all() and (v[j, :, w:] == 0).all()
     assert total == int(whole)
+
+
+def test_host_out_arrays_match_device_outputs(gpu):
+    """trace_primary(out=...) with host arrays (copied back over PCIe into the caller's reused buffers) gives the
+    device-output frame; undersized or mixed host/device out= dicts are refused before anything is written."""
+    import torch
+    flat = vhx.FlatTree.build_scene(N.VHX_SCENE_LATTICE_CUBE, 64, 4)
+    gpu.upload(flat)
+    W, H = 96, 64
+    cam = vhx.glass_camera(64, W, H, target=(32.0, 32.0, 32.0))
+    dev = gpu.trace_primary(cam, out={"rgba": torch.zeros(W * H, dtype=torch.int32, device="cuda"),
+                                      "depth": torch.zeros(W * H, dtype=torch.float32, device="cuda")})
+    gpu.sync()
+    host = {"rgba": np.zeros(W * H, np.uint32), "depth": np.zeros(W * H, np.float32)}
+    for _ in range(2):  # reused buffers
+        gpu.trace_primary(cam, out=host)
+        assert np.array_equal(host["rgba"], dev["rgba"].cpu().numpy().view(np.uint32))
+        assert np.array_equal(host["depth"].view(np.uint32), dev["depth"].cpu().numpy().view(np.uint32))
+    with pytest.raises(ValueError):
+        gpu.trace_primary(cam, out={"rgba": np.zeros(W * H - 1, np.uint32)})
+    with pytest.raises(ValueError):
+        gpu.trace_primary(cam, out={"rgba": np.zeros(W * H, np.uint32), "depth": dev["depth"]})

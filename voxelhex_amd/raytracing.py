@@ -166,6 +166,14 @@ def _hits_struct(arrays):
     return h
 
 
+def _on_device(arrays):
+    """1 when every array of an out= dict is a GPU tensor, 0 when every one is host memory (numpy / CPU tensor)."""
+    dev = {bool(getattr(a, "is_cuda", False)) for a in arrays.values() if a is not None}
+    if len(dev) > 1:
+        raise ValueError("out= mixes device and host arrays")
+    return 1 if dev == {True} else 0
+
+
 def _ptr(a):
     if hasattr(a, "data_ptr"):  # torch tensor (device or host)
         return a.data_ptr()
@@ -252,18 +260,24 @@ class Raytracer:
     def trace_primary(self, cam, tile_size=0, tile_start=0, tile_stride=1, layout=N.VHX_LAYOUT_FRAMEBUFFER,
                       fields=("value", "cell", "voxel", "impact", "normal", "depth", "rgba"), count_bytes=False,
                       out=None):
-        """Traces one frame (or this rank's tiles). With out=dict of device tensors nothing is copied back."""
-        if out is not None:
-            hs = _hits_struct(out)
-            self._check(N.lib().vhx_trace_primary(self._h, ctypes.byref(cam), tile_size, tile_start, tile_stride,
-                                                  layout, ctypes.byref(hs), 1))
-            return out
+        """Traces one frame (or this rank's tiles). With out=dict of device tensors nothing is copied back; with
+        out=dict of host arrays (numpy or CPU tensors, reused across frames) the results are copied into them."""
         if layout == N.VHX_LAYOUT_FRAMEBUFFER:
             n = cam.width * cam.height
         else:
             T = tile_size
             ntiles = ((cam.width + T - 1) // T) * ((cam.height + T - 1) // T)
             n = max(0, (ntiles - tile_start + tile_stride - 1) // tile_stride) * T * T
+        if out is not None:
+            for name, dt, k in HIT_FIELDS:
+                a = out.get(name)
+                nbytes = None if a is None else (a.numel() * a.element_size() if hasattr(a, "numel") else a.nbytes)
+                if nbytes is not None and nbytes < n * k * 4:
+                    raise ValueError(f"out[{name!r}] holds {nbytes} bytes, the trace writes {n * k * 4}")
+            hs = _hits_struct(out)
+            self._check(N.lib().vhx_trace_primary(self._h, ctypes.byref(cam), tile_size, tile_start, tile_stride,
+                                                  layout, ctypes.byref(hs), _on_device(out)))
+            return out
         fields = tuple(fields) + (("bytes",) if count_bytes else ())
         alloc = np.empty if layout == N.VHX_LAYOUT_FRAMEBUFFER else np.zeros  # tiles past the frame edge stay 0
         res = {name: alloc((n, k) if k > 1 else (n,), dt) for name, dt, k in HIT_FIELDS if name in fields}
