@@ -46,7 +46,7 @@ struct vhx_ctx {
     DevBuf child_rec;         // brick_dim <= 4: DevTree::child_rec, rebuilt before a trace when stale
     bool child_rec_stale = false;
     DevBuf queue[2];  // multi-pass ray queues (ping-pong), output indices of abandoned rays in increasing order
-    DevBuf qctl;      // [0..7] queue lengths written after pass p (7: shadow hit list), [8..15] work counters
+    DevBuf qctl;      // QCTL_WORDS: [0..7] queue lengths after pass p (7: shadow hit list), [16 + 16p ..] counters
     DevBuf tmp;       // chunk-local lists of abandoned rays (a block's or a queue chunk's, in lane order)
     DevBuf counts;    // rays listed per chunk
     DevBuf offsets;   // exclusive scan of counts
@@ -70,6 +70,7 @@ struct vhx_ctx {
     // pass, while every chunk still starts at once)
     uint32_t queue_waves = 2048;
     uint32_t queue_waves0 = 8192;  // waves of a first queue pass over fresh rays (VHX_QWAVES0)
+    uint32_t qxcd = 16;            // queue passes: XCD-dealt chunk runs (VHX_QXCD = run length, 0 = one counter)
 };
 
 #define VHX_HIP(ctx, call)                                                                                         \
@@ -266,6 +267,7 @@ struct PassQ {
     uint8_t *flags;    // primary pass 0: abandoned flag per output index (every entry written, no clearing needed)
     uint4 *state;      // per output index, 4 x uint4: saved traversal state of an abandoned ray (null: re-trace)
     uint32_t xcd_group;  // pass 0: XCD-aware block runs (xcd_block), 0 = dispatch order
+    uint32_t qxcd;       // queue passes: runs of this many chunks dealt over the 8 XCDs, one counter each (0 = off)
 };
 
 // Rays per wave of a queue pass over n rays: fixed, or (rpw == 0) as many as spread the pass over about `tw` waves.
@@ -368,12 +370,14 @@ __device__ __forceinline__ uint32_t flag_bits(const void *src, uint64_t i, uint6
     return bits;
 }
 
-// zero8: the queue passes' work counters (qctl[8..15]), zeroed here instead of by a separate memset launch
+// qctl: [0..7] queue lengths written after pass p (7: shadow hit list), [16 + 16p ..] pass p's work counters
+#define QCTL_WORDS 80u
+// zero: the queue passes' work counters (qctl[16..79]), zeroed here instead of by a separate memset launch
 template <bool HITS>
 __global__ void __launch_bounds__(256) k_count_flags(const void *__restrict__ src, uint64_t n,
-                                                     uint32_t *__restrict__ counts, uint32_t *zero8) {
+                                                     uint32_t *__restrict__ counts, uint32_t *zero) {
     __shared__ uint32_t s_cnt[4];
-    if (blockIdx.x == 0 && threadIdx.x < 8u) zero8[threadIdx.x] = 0u;
+    if (blockIdx.x == 0 && threadIdx.x < QCTL_WORDS - 16u) zero[threadIdx.x] = 0u;
     const uint64_t i = ((uint64_t)blockIdx.x * 256u + threadIdx.x) * 4u;
     uint32_t c = __popc(flag_bits<HITS>(src, i, n));
     for (uint32_t d = 32; d > 0; d >>= 1) c += __shfl_down(c, d);
@@ -562,11 +566,34 @@ __global__ void __launch_bounds__(256) k_trace_queue(DevTree t, const QueueArgs 
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t n = *in_n;
     const uint32_t rpw = pass_rpw(q.rpw, q.tw, n);
+    // q.qxcd = G > 0: chunk runs of G are dealt round-robin over the XCDs (blockIdx % 8 runs on one XCD and shares
+    // its L2), each XCD's waves take its runs in order from their own counter (grab[8 + x]) and move on to the next
+    // XCD's runs once theirs are taken
+    uint32_t xcd = blockIdx.x & 7u, tries = 0;
     for (;;) {
         uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(grab, rpw);
-        base = __shfl(base, 0);
-        if (base >= n) break;  // wave-uniform
+        if (q.qxcd == 0u) {
+            if (lane == 0) base = atomicAdd(grab, rpw);
+            base = __shfl(base, 0);
+            if (base >= n) break;  // wave-uniform
+        } else {
+            const uint32_t G = q.qxcd;
+            uint32_t chunk = 0xFFFFFFFFu;
+            while (tries < 8u) {
+                uint32_t k = 0;
+                if (lane == 0) k = atomicAdd(grab + 8u + xcd, 1u);
+                k = __builtin_amdgcn_readfirstlane(__shfl(k, 0));
+                const uint64_t cc = ((uint64_t)(k / G) * 8u + xcd) * G + k % G;
+                if (cc * rpw < n) {
+                    chunk = (uint32_t)cc;
+                    break;
+                }
+                xcd = (xcd + 1u) & 7u;
+                ++tries;
+            }
+            if (chunk == 0xFFFFFFFFu) break;
+            base = chunk * rpw;
+        }
         const uint32_t i = base + lane;
         bool push = false;
         uint32_t idx = 0;
@@ -794,7 +821,7 @@ static int prepare_passes(vhx_ctx *c, uint64_t nout, uint64_t nblocks0, uint32_t
     }
     int rc = ensure(c, c->queue[0], nout * 4);
     if (!rc && (npass > 2 || shadow)) rc = ensure(c, c->queue[1], nout * 4);
-    if (!rc) rc = ensure(c, c->qctl, 16 * sizeof(uint32_t));
+    if (!rc) rc = ensure(c, c->qctl, QCTL_WORDS * sizeof(uint32_t));
     if (!rc) rc = ensure(c, c->qargs, 2 * sizeof(QueueArgs));
     if (!rc) rc = ensure(c, c->tmp, list * 4);
     if (!rc) rc = ensure(c, c->counts, chunks * 4);
@@ -808,7 +835,7 @@ static int prepare_passes(vhx_ctx *c, uint64_t nout, uint64_t nblocks0, uint32_t
 // frames zero the counters in their first compaction kernel instead.
 static int reset_passes(vhx_ctx *c, uint32_t npass) {
     if (npass < 2) return VHX_OK;
-    VHX_HIP(c, hipMemsetAsync(c->qctl.ptr, 0, 16 * sizeof(uint32_t), c->stream));
+    VHX_HIP(c, hipMemsetAsync(c->qctl.ptr, 0, QCTL_WORDS * sizeof(uint32_t), c->stream));
     return VHX_OK;
 }
 
@@ -821,6 +848,7 @@ static PassQ pass_q(const vhx_ctx *c, uint32_t p, uint32_t npass) {
     q.rpw = c->rpw[p];
     q.tw = c->tw;
     q.xcd_group = c->xcd_group;
+    q.qxcd = last ? c->qxcd : 0u;  // the unbounded last pass only (a budgeted pass over many short chunks: 2x slower)
     q.tmp = last ? nullptr : (uint32_t *)c->tmp.ptr;
     q.counts = (uint32_t *)c->counts.ptr;
     q.flags = nullptr;
@@ -871,7 +899,7 @@ static int launch_queue_passes(vhx_ctx *c, const DevTree &t, const CamD &cam, co
             const unsigned nb = (unsigned)((nout + 1023) / 1024);
             uint32_t *counts = (uint32_t *)c->counts.ptr, *offsets = (uint32_t *)c->offsets.ptr;
             const uint8_t *flags = (const uint8_t *)c->flags.ptr;
-            k_count_flags<false><<<nb, 256, 0, c->stream>>>(flags, nout, counts, ctl + 8);
+            k_count_flags<false><<<nb, 256, 0, c->stream>>>(flags, nout, counts, ctl + 16);
             k_scan_counts<<<1, 1024, 0, c->stream>>>(counts, nb, nullptr, 1, c->tw, offsets, ctl);
             k_emit_flags<false><<<nb, 256, 0, c->stream>>>(flags, nout, offsets, (uint32_t *)c->queue[0].ptr);
             VHX_HIP(c, hipGetLastError());
@@ -905,7 +933,7 @@ static int launch_queue_passes(vhx_ctx *c, const DevTree &t, const CamD &cam, co
         // a first pass over fresh rays (the shadow path) is throughput-bound like a grid launch: more waves
         const uint32_t qwaves = p == 0 ? c->queue_waves0 : c->queue_waves;
         k_trace_queue<COUNT, BD><<<(qwaves * 64u + c->qblock - 1) / c->qblock, c->qblock, 0, c->stream>>>(
-            t, qa, in, in_n, ctl + 8 + p, q);
+            t, qa, in, in_n, ctl + 16u + 16u * p, q);
         debug_passes(c, "queue pass");
         if (p + 1 < npass)
             rc = compact_chunks(c, 0, in_n, q.rpw, q.rpw, (uint32_t *)c->queue[p & 1u].ptr, ctl + p,
@@ -986,6 +1014,8 @@ int vhx_create(int hip_device, vhx_ctx **out) {
         if (pw && atoi(pw) > 0) c->queue_waves = (uint32_t)atoi(pw);
         const char *pw0 = getenv("VHX_QWAVES0");
         if (pw0 && atoi(pw0) > 0) c->queue_waves0 = (uint32_t)atoi(pw0);
+        const char *pqx = getenv("VHX_QXCD");
+        if (pqx && atoi(pqx) >= 0) c->qxcd = (uint32_t)atoi(pqx);
     }
     if ((e = hipEventCreate(&c->ev0)) != hipSuccess) return bail("hipEventCreate", e);
     if ((e = hipEventCreate(&c->ev1)) != hipSuccess) return bail("hipEventCreate", e);
@@ -1295,7 +1325,7 @@ int vhx_trace_shadows(vhx_ctx *c, const float light[3], uint64_t n, const uint32
     {
         const unsigned nb = (unsigned)((n + 1023) / 1024);
         uint32_t *counts = (uint32_t *)c->counts.ptr, *offsets = (uint32_t *)c->offsets.ptr;
-        k_count_flags<true><<<nb, 256, 0, c->stream>>>(value, n, counts, (uint32_t *)c->qctl.ptr + 8);
+        k_count_flags<true><<<nb, 256, 0, c->stream>>>(value, n, counts, (uint32_t *)c->qctl.ptr + 16);
         k_scan_counts<<<1, 1024, 0, c->stream>>>(counts, nb, nullptr, 1, c->tw, offsets, (uint32_t *)c->qctl.ptr + 7);
         k_emit_flags<true><<<nb, 256, 0, c->stream>>>(value, n, offsets, (uint32_t *)c->queue[1].ptr);
         VHX_HIP(c, hipGetLastError());
