@@ -274,7 +274,8 @@ def test_multipass_schedule_is_bit_identical(gpu, oracle, budgets):
 SCHEDULER_ENVS = [{"VHX_RESUME": "0"},                                   # abandoned rays re-traced from scratch
                   {"VHX_RPW": "0,0", "VHX_TW": "7"},                      # adaptive rays per wave, few waves
                   {"VHX_RPW": "0,3", "VHX_TW": "100000", "VHX_QBLOCK": "64"},  # one ray per wave, 1-wave workgroups
-                  {"VHX_QXCD": "0"},                                     # one counter instead of XCD-dealt runs
+                  {"VHX_QXCD": "0", "VHX_XCDG": "0"},                    # one counter, pass-0 blocks in dispatch order
+                  {"VHX_XCDG": "3"},                                     # odd pass-0 XCD block runs
                   {"VHX_QXCD": "4"},                                     # shorter runs dealt over the XCDs
                   {"VHX_QXCD": "1", "VHX_RPW": "0,0", "VHX_TW": "7"}]    # ... single chunks, few adaptive waves
 
