@@ -570,22 +570,30 @@ __global__ void __launch_bounds__(256) k_trace_queue(DevTree t, const QueueArgs 
     // its L2), each XCD's waves take its runs in order from their own counter (grab[8 + x]) and move on to the next
     // XCD's runs once theirs are taken
     uint32_t xcd = blockIdx.x & 7u, tries = 0;
+    // only a queue with more chunks than waves is dealt over the XCDs (a smaller one starts every chunk at once
+    // anyway and measured slower dealt)
+    const uint32_t qxcd = (n + rpw - 1) / rpw > gridDim.x * (blockDim.x / 64u) ? q.qxcd : 0u;
     for (;;) {
         uint32_t base = 0;
-        if (q.qxcd == 0u) {
+        if (qxcd == 0u) {
             if (lane == 0) base = atomicAdd(grab, rpw);
             base = __shfl(base, 0);
             if (base >= n) break;  // wave-uniform
         } else {
-            const uint32_t G = q.qxcd;
+            const uint32_t G = qxcd;
+            const uint32_t nch = (n + rpw - 1) / rpw, nfull = nch / G, rem = nch % G;
             uint32_t chunk = 0xFFFFFFFFu;
             while (tries < 8u) {
-                uint32_t k = 0;
-                if (lane == 0) k = atomicAdd(grab + 8u + xcd, 1u);
+                // XCD xcd owns runs xcd, xcd + 8, ...: kmax of its takes are valid (the last run may be partial); an
+                // exhausted counter is recognised by a plain load, so finished waves do not queue atomics on it
+                const uint32_t kmax = (nfull > xcd ? (nfull - xcd + 7u) / 8u : 0u) * G +
+                                      (rem > 0u && nfull % 8u == xcd ? rem : 0u);
+                uint32_t k = 0xFFFFFFFFu;
+                if (lane == 0 && __atomic_load_n(grab + 8u + xcd, __ATOMIC_RELAXED) < kmax)
+                    k = atomicAdd(grab + 8u + xcd, 1u);
                 k = __builtin_amdgcn_readfirstlane(__shfl(k, 0));
-                const uint64_t cc = ((uint64_t)(k / G) * 8u + xcd) * G + k % G;
-                if (cc * rpw < n) {
-                    chunk = (uint32_t)cc;
+                if (k < kmax) {
+                    chunk = ((k / G) * 8u + xcd) * G + k % G;
                     break;
                 }
                 xcd = (xcd + 1u) & 7u;
