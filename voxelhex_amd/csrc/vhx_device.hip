@@ -372,13 +372,17 @@ __device__ __forceinline__ uint32_t flag_bits(const void *src, uint64_t i, uint6
 
 // qctl: [0..7] queue lengths written after pass p (7: shadow hit list), [16 + 16p ..] pass p's work counters
 #define QCTL_WORDS 80u
-// zero: the queue passes' work counters (qctl[16..79]), zeroed here instead of by a separate memset launch
+// zero: the queue passes' work counters (qctl[16..79]), zeroed here instead of by a separate memset launch;
+// clear (optional, n entries): an output array zeroed alongside (the shadow flags of a shadow frame)
 template <bool HITS>
 __global__ void __launch_bounds__(256) k_count_flags(const void *__restrict__ src, uint64_t n,
-                                                     uint32_t *__restrict__ counts, uint32_t *zero) {
+                                                     uint32_t *__restrict__ counts, uint32_t *zero,
+                                                     uint32_t *__restrict__ clear = nullptr) {
     __shared__ uint32_t s_cnt[4];
     if (blockIdx.x == 0 && threadIdx.x < QCTL_WORDS - 16u) zero[threadIdx.x] = 0u;
     const uint64_t i = ((uint64_t)blockIdx.x * 256u + threadIdx.x) * 4u;
+    if (clear)
+        for (uint64_t k = i; k < n && k < i + 4u; ++k) clear[k] = 0u;
     uint32_t c = __popc(flag_bits<HITS>(src, i, n));
     for (uint32_t d = 32; d > 0; d >>= 1) c += __shfl_down(c, d);
     if ((threadIdx.x & 63u) == 0) s_cnt[threadIdx.x >> 6] = c;
@@ -1327,13 +1331,12 @@ int vhx_trace_shadows(vhx_ctx *c, const float light[3], uint64_t n, const uint32
     CamD cd{};
     VHX_HIP(c, hipEventRecord(c->ev0, c->stream));
     // no reset_passes: the hit compaction (k_count_flags) zeroes the queue passes' counters
-    VHX_HIP(c, hipMemsetAsync(shadowed, 0, n * 4, c->stream));
     if (bytes) VHX_HIP(c, hipMemsetAsync(bytes, 0, n * 4, c->stream));
     // wave-dense secondary rays: the hit pixels, in frame order, are pass 0's queue
     {
         const unsigned nb = (unsigned)((n + 1023) / 1024);
         uint32_t *counts = (uint32_t *)c->counts.ptr, *offsets = (uint32_t *)c->offsets.ptr;
-        k_count_flags<true><<<nb, 256, 0, c->stream>>>(value, n, counts, (uint32_t *)c->qctl.ptr + 16);
+        k_count_flags<true><<<nb, 256, 0, c->stream>>>(value, n, counts, (uint32_t *)c->qctl.ptr + 16, shadowed);
         k_scan_counts<<<1, 1024, 0, c->stream>>>(counts, nb, nullptr, 1, c->tw, offsets, (uint32_t *)c->qctl.ptr + 7);
         k_emit_flags<true><<<nb, 256, 0, c->stream>>>(value, n, offsets, (uint32_t *)c->queue[1].ptr);
         VHX_HIP(c, hipGetLastError());
