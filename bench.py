@@ -1,11 +1,18 @@
 """Headline benchmark: primary Mrays/s at 3840x2160 on a 1024^3 brick tree (BASELINE.json `metric`).
 
 One step = one frame: every pixel's primary ray traced with get_by_ray semantics (src/raytracing/cpu.rs:296-458)
-through the HIP kernel, shaded to RGBA8 + f32 depth in HBM. With N GPUs (torchrun, one process per GPU, RCCL) the
-frame is split into 64x64 screen tiles dealt round-robin over the ranks; each rank traces its tiles into a
-contiguous buffer, rank 0 gathers the RGBA tiles over RCCL and scatters them into the framebuffer. Weak scaling:
-the camera's field of view is fixed and the resolution grows with N so every rank keeps 3840x2160 rays
-(N=4 is config 4's 7680x4320 frame; N=2 5432x3056, N=8 10864x6112).
+through the HIP kernel, shaded to RGBA8 + f32 depth in HBM.
+
+Multi-GPU (torchrun, one process per GPU): the split lives behind the C ABI (vhx_mgpu_*, include/vhx.h): libvhx owns
+an RCCL communicator (its id travels over a gloo process group, which also carries the barriers and the max-over-ranks
+timing), rank 0 builds the tree and ncclBroadcasts it to the other GPUs, and every frame each rank traces its 64x64
+screen tiles (dealt round-robin), one ncclGather brings RGBA8 + f32 depth to rank 0, rank 0 untiles them into its
+framebuffers; frame k's gather overlaps frame k+1's trace. Scaling modes (--scaling):
+  auto   (default) N = 1: the headline 3840x2160 frame; N > 1: BASELINE config 4, a fixed 7680x4320 frame (strong)
+  strong the 7680x4320 config-4 frame at every N (N = 1 included)
+  weak   the field of view fixed, W*H grown with N so that every rank keeps 3840x2160 rays
+--mgpu torch keeps the previous torch.distributed gather (and VHX_BENCH_REHEARSAL=1 rehearses it with two ranks on
+one GPU over gloo; RCCL needs one GPU per rank).
 
 Workload: the reference's lattice+cube scene S (examples/gpu_render.rs:57-82) at 1024^3
 with brick_dim 4 (1024 is not a valid size for brick_dim 8, src/boxtree/mod.rs:188-202; the 1024^3 .vox model is not
@@ -14,7 +21,7 @@ in the reference checkout), glass camera of benches/performance.rs on radius 2S 
 Also printed: roofline (algorithmic bytes per launch, counted by the instrumented kernel, / measured kernel time vs
 8 TB/s; `traffic` = the PMC-measured memory-side read bytes of the same launch from profiles/, see
 scripts/pmc_traffic.py), and cpu_baseline: the CPU restatement of the reference raytracer (oracle/) on the host
-cores over the same frame.
+cores over the same frame (all cores available to the process and 1 core, 1 warm-up + median of 5).
 """
 import argparse
 import json
@@ -38,8 +45,13 @@ def parse():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--size", type=int, default=1024)
     p.add_argument("--brick-dim", type=int, default=4)
-    p.add_argument("--width", type=int, default=3840, help="per-rank-equivalent frame width (N=1 frame)")
-    p.add_argument("--height", type=int, default=2160)
+    p.add_argument("--width", type=int, default=None, help="frame width (default: by --scaling)")
+    p.add_argument("--height", type=int, default=None)
+    p.add_argument("--scaling", choices=("auto", "weak", "strong"), default="auto",
+                   help="auto: N=1 3840x2160, N>1 config 4 (7680x4320 fixed); strong: 7680x4320 at every N; weak: "
+                        "3840x2160 rays per rank")
+    p.add_argument("--mgpu", choices=("vhx", "torch"), default="vhx",
+                   help="N>1 data path: vhx = RCCL behind the C ABI (vhx_mgpu_*), torch = torch.distributed gather")
     p.add_argument("--scene", type=int, default=1, help="VHX_SCENE_* (1 = lattice+cube scene S)")
     p.add_argument("--vox", default=None, help="trace a MagicaVoxel model instead (BoxTree::load_vox_file, bd = "
                                               "--brick-dim; tree size from the model)")
@@ -53,12 +65,51 @@ def parse():
     return p.parse_args()
 
 
-def frame_size(w, h, world):
-    """Weak scaling: same field of view, w*h rays per rank (dimensions rounded to multiples of 8)."""
+CONFIG4 = (7680, 4320)  # BASELINE config 4 frame
+HEADLINE = (3840, 2160)  # BASELINE metric / config 3 frame
+
+
+def frame_size(args, world):
+    """(W, H, scaling label). Weak scaling keeps the field of view and W*H/N = 3840*2160 (dimensions rounded to
+    multiples of 8); strong scaling keeps the frame."""
+    mode = args.scaling
+    if mode == "auto":
+        mode = "strong" if world > 1 else "single"
+    if args.width and args.height:
+        return args.width, args.height, ("weak" if mode == "weak" else "strong")
+    if mode == "single":
+        return HEADLINE[0], HEADLINE[1], "weak"
+    if mode == "strong":
+        return CONFIG4[0], CONFIG4[1], "strong"
+    w, h = HEADLINE
     if world == 1:
-        return w, h
+        return w, h, "weak"
     f = world ** 0.5
-    return int(round(w * f / 8.0)) * 8, int(round(h * f / 8.0)) * 8
+    return int(round(w * f / 8.0)) * 8, int(round(h * f / 8.0)) * 8, "weak"
+
+
+def cpu_cores():
+    """Cores this process may run on: the affinity set, capped by a cgroup CPU quota when there is one (a GPU box
+    shows the whole machine's CPUs but grants each job a share)."""
+    n = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = max(1, int(-(-int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    return (min(n, quota) if quota else n), n, quota
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
 
 
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic.json")
@@ -74,6 +125,31 @@ def pmc_traffic(workload):
     return None if e is None else e
 
 
+def cpu_baseline(flat, cam, W, H, threads_all):
+    """The oracle (reference semantics, oracle/) on the host cores over the bench frame: all cores available to the
+    process (OpenMP, dynamic over pixels), 1 warm-up + median of 5 full frames; and 1 core, 1 warm-up + median of 5
+    frames of the same view at a quarter of the resolution per axis (a uniform 1/16 sample of the frame's rays, about
+    0.4 s each, so that the default bench still finishes in minutes)."""
+    from tests._oracle import Oracle
+    orc = Oracle()
+
+    def timed(w, h, c, threads):
+        orc.trace_primary(flat, c, 0, 0, w, h, threads=threads, fields=("rgba", "depth"))  # warm-up
+        ts = []
+        for _ in range(5):
+            t0 = time.perf_counter()
+            orc.trace_primary(flat, c, 0, 0, w, h, threads=threads, fields=("rgba", "depth"))
+            ts.append(time.perf_counter() - t0)
+        return sorted(ts)[2]
+
+    import voxelhex_amd as vhx
+    t_all = timed(W, H, cam, threads_all)
+    w1, h1 = max(1, W // 4), max(1, H // 4)
+    c1 = vhx.glass_camera(int(flat.desc.boxtree_size), w1, h1, target=(flat.desc.boxtree_size / 2.0,) * 3)
+    t_one = timed(w1, h1, c1, 1)
+    return t_all, t_one, (w1, h1)
+
+
 def main():
     args = parse()
     import torch
@@ -86,42 +162,67 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # rehearsal of the multi-GPU path on a single GPU: VHX_BENCH_REHEARSAL=1 puts every rank on cuda:0 and gathers
-    # over gloo through host memory (RCCL needs one GPU per rank); timings from such a run are not scaling numbers
+    # rehearsal of the torch multi-GPU path on a single GPU: VHX_BENCH_REHEARSAL=1 puts every rank on cuda:0 and
+    # gathers over gloo through host memory (RCCL needs one GPU per rank); timings from such a run are not scaling
     rehearsal = world > 1 and os.environ.get("VHX_BENCH_REHEARSAL") == "1"
+    use_vhx_mgpu = world > 1 and args.mgpu == "vhx" and not rehearsal
     if rehearsal:
         local = 0
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(local)
-        if rehearsal:
+        if rehearsal or use_vhx_mgpu:
+            # gloo: barriers, the max-over-ranks timing and the RCCL id exchange; the frame data moves over RCCL
+            # inside libvhx (vhx_mgpu) or, in the rehearsal, over gloo through host memory
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-
-    t0 = time.time()
-    if args.vox:
-        flat = vhx.BoxTree.load_vox_file(args.vox, args.brick_dim).flatten()
-        args.size = int(flat.desc.boxtree_size)
-    else:
-        flat = vhx.FlatTree.build_scene(args.scene, args.size, args.brick_dim, threads=min(16, os.cpu_count() or 1))
-    build_s = time.time() - t0
     rt = vhx.Raytracer(local)
-    # one dedicated (non-null) stream shared by libvhx and torch: the kernel, the torch events that time it and
-    # the RCCL gather are ordered on it
+    # one dedicated (non-null) stream shared by libvhx and torch: the kernels and the events that time them are ordered
+    # on it
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     rt.set_stream(stream.cuda_stream)
-    t0 = time.time()
-    rt.upload(flat)
-    upload_s = time.time() - t0
 
-    (W, H), T = frame_size(args.width, args.height, world), args.tile
+    mg = None
+    if use_vhx_mgpu:
+        obj = [M.mgpu_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        mg = M.MgpuRenderer(rt, obj[0], world, rank, tile_size=args.tile, overlap=not args.no_overlap)
+
+    # the tree: built on the host (rank 0 only when it is broadcast over RCCL), uploaded to HBM
+    t0 = time.time()
+    flat = None
+    if args.vox:
+        if mg is None or rank == 0:
+            flat = vhx.BoxTree.load_vox_file(args.vox, args.brick_dim).flatten()
+    elif mg is None or rank == 0:
+        flat = vhx.FlatTree.build_scene(args.scene, args.size, args.brick_dim, threads=min(16, os.cpu_count() or 1))
+    build_s = time.time() - t0
+    t0 = time.time()
+    if mg is not None:
+        mg.broadcast_tree(flat if rank == 0 else None)
+    else:
+        rt.upload(flat)
+    upload_s = time.time() - t0
+    tree_info = None
+    if rank == 0:
+        tree_info = dict(tree_nodes=int(flat.desc.node_count), tree_bricks=int(flat.desc.brick_count),
+                         tree_gb=round(flat.nbytes() / 1e9, 3), size=int(flat.desc.boxtree_size))
+    if args.vox:
+        obj = [tree_info["size"] if rank == 0 else None]
+        if world > 1:
+            dist.broadcast_object_list(obj, src=0)
+        args.size = obj[0]
+
+    W, H, scaling = frame_size(args, world)
+    T = args.tile
     c = args.size / 2.0
     cam = vhx.glass_camera(args.size, W, H, target=(c, c, c))
+    light = (float(args.size),) * 3  # ambient_light_position, src/raytracing/bevy/view.rs:81-85
     if world == 1:
         n_out = W * H
         trace_kw = dict(tile_size=0, tile_start=0, tile_stride=1, layout=N.VHX_LAYOUT_FRAMEBUFFER)
@@ -130,10 +231,14 @@ def main():
         tiles_per_rank = M.tiles_per_rank(W, H, T, world)
         n_out = tiles_per_rank * T * T
         trace_kw = dict(tile_size=T, tile_start=rank, tile_stride=world, layout=N.VHX_LAYOUT_TILES)
-    rgba = torch.zeros(n_out, dtype=torch.int32, device=dev)
-    depth = torch.zeros(n_out, dtype=torch.float32, device=dev)
-    out = {"rgba": rgba, "depth": depth}
-    light = (float(args.size),) * 3  # ambient_light_position, src/raytracing/bevy/view.rs:81-85
+    if args.shadows and mg is not None:
+        raise SystemExit("--shadows with N > 1 needs --mgpu torch")
+    fb_rgba = fb_depth = None
+    if mg is not None and rank == 0:
+        fb_rgba = torch.zeros(W * H, dtype=torch.int32, device=dev)
+        fb_depth = torch.zeros(W * H, dtype=torch.float32, device=dev)
+    out = {"rgba": torch.zeros(n_out, dtype=torch.int32, device=dev),
+           "depth": torch.zeros(n_out, dtype=torch.float32, device=dev)}
     if args.shadows:
         # -1 = VHX_EMPTY: tile padding past the frame edge is never written and casts no shadow ray
         out.update(value=torch.full((n_out,), -1, dtype=torch.int32, device=dev),
@@ -141,53 +246,62 @@ def main():
                    normal=torch.zeros((n_out, 3), dtype=torch.float32, device=dev))
         shadowed = torch.zeros(n_out, dtype=torch.int32, device=dev)
     pipe = None
-    if world > 1:
+    framebuffer = None
+    if world > 1 and mg is None:
         framebuffer = torch.zeros(W * H, dtype=torch.int32, device=dev) if rank == 0 else None
 
         def untile(gathered, slot):
             rt.untile_rgba(gathered.data_ptr(), world, tiles_per_rank, T, W, H, framebuffer.data_ptr())
 
-        # double-buffered: frame k's RCCL gather to rank 0 (and the untile there) overlaps frame k+1's trace
+        # double-buffered: frame k's gather to rank 0 (and the untile there) overlaps frame k+1's trace
         pipe = M.GatherPipeline(n_out, world, rank, dist, dev, untile, overlap=not args.no_overlap,
                                 host_staging=rehearsal)
 
     ev = []
 
     def step(timed):
-        if pipe is not None:
-            out["rgba"] = pipe.out_buffer()
         if timed:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-        rt.trace_primary(cam, out=out, **trace_kw)
-        if args.shadows:
-            rt.trace_shadows(light, out, shadowed=shadowed)
+        if mg is not None:
+            mg.render(cam, fb_rgba, fb_depth)  # this rank's tiles -> ncclGather -> untile on rank 0
+        else:
+            if pipe is not None:
+                out["rgba"] = pipe.out_buffer()
+            rt.trace_primary(cam, out=out, **trace_kw)
+            if args.shadows:
+                rt.trace_shadows(light, out, shadowed=shadowed)
         if timed:
-            e1.record(stream)
+            e1.record(stream)  # the trace (the gather runs on the communication stream)
             ev.append((e0, e1))
         if pipe is not None:
             pipe.submit()
 
+    def drain():
+        if pipe is not None:
+            pipe.drain()
+        if mg is not None:
+            mg.sync()
+        torch.cuda.synchronize(dev)
+
     for _ in range(args.warmup):
         step(False)
-    if pipe is not None:
-        pipe.drain()
-    torch.cuda.synchronize(dev)
+    drain()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step(True)
-    if pipe is not None:
-        pipe.drain()  # the last frame's gather and untile are inside the timed region
-    torch.cuda.synchronize(dev)
+    drain()  # the last frame's gather and untile are inside the timed region
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if rehearsal else dev)
+        tt = torch.tensor([elapsed], dtype=torch.float64)
+        if not (rehearsal or use_vhx_mgpu):
+            tt = tt.to(dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
@@ -200,7 +314,9 @@ def main():
         workload += " +shadows"
         n_shadow = int((out["value"] != -1).sum().item())  # shadow rays this rank traced per frame
         if world > 1:
-            ts = torch.tensor([n_shadow], dtype=torch.int64, device="cpu" if rehearsal else dev)
+            ts = torch.tensor([n_shadow], dtype=torch.int64)
+            if not rehearsal:
+                ts = ts.to(dev)
             dist.all_reduce(ts)
             n_shadow = int(ts.item())
         total_rays += n_shadow
@@ -210,9 +326,13 @@ def main():
     # ---- multi-GPU check (untimed): the gathered, untiled frame equals rank 0 tracing the whole frame alone -------
     mgpu = None
     if world > 1 and rank == 0:
-        whole = rt.trace_primary(cam, fields=("rgba",))["rgba"]
-        got = framebuffer.cpu().numpy().view(np.uint32)
-        mgpu = {"frame_equal": bool(np.array_equal(got, whole)), "pixels": int(whole.size)}
+        fields = ("rgba", "depth") if mg is not None else ("rgba",)
+        whole = rt.trace_primary(cam, fields=fields)
+        got = (fb_rgba if mg is not None else framebuffer).cpu().numpy().view(np.uint32)
+        eq = bool(np.array_equal(got, whole["rgba"]))
+        if mg is not None:
+            eq = eq and bool(np.array_equal(fb_depth.cpu().numpy().view(np.uint32), whole["depth"].view(np.uint32)))
+        mgpu = {"frame_equal": eq, "fields": list(fields), "pixels": int(W * H)}
 
     # ---- roofline: algorithmic bytes of this rank's launch (instrumented kernel, untimed) -------------------------
     roof = None
@@ -230,52 +350,54 @@ def main():
                 "traffic_source": None if tr is None else tr["source"],
                 "kernel": "vhx_trace_primary launch = k_trace_primary (pass 0, step budget) + k_trace_queue "
                           "(the rays over budget, resumed from their saved state), timed together with HIP events "
-                          "on the trace stream",
+                          "on the trace stream" + (" (N>1: rank 0's tile set; the gather runs on the communication "
+                                                   "stream)" if world > 1 else ""),
                 "kernel_ms": round(kernel_ms, 4),
                 "algorithmic_bytes_per_launch": launch_bytes, "tree_bytes_per_ray": round(tree_bytes / max(1, my_rays), 2)}
+        if tr is not None and "issue" in tr:
+            roof["issue"] = tr["issue"]
 
     # ---- CPU baseline: the oracle (reference semantics) on the host cores, rank 0 at N=1 only ----------------------
     cpu = None
     if world == 1 and rank == 0 and not args.no_cpu_baseline and not args.shadows:
-        from tests._oracle import Oracle
-        orc = Oracle()
-        cores = max(1, min(16, len(os.sched_getaffinity(0))))
-        orc.trace_primary(flat, cam, 0, 0, W, 16, threads=cores, fields=("rgba",))  # warm
-        ts = []
-        for _ in range(3):  # three full frames (about 15 s of CPU work on 16 cores), the median reported
-            t0 = time.perf_counter()
-            orc.trace_primary(flat, cam, 0, 0, W, H, threads=cores, fields=("rgba", "depth"))
-            ts.append(time.perf_counter() - t0)
-        cpu_s = sorted(ts)[1]
-        cpu = {"value": round(W * H / cpu_s / 1e6, 4), "unit": "Mrays/s", "cores": cores, "kind": "port",
-               "sample": f"median of 3 full {W}x{H} frames, same tree and camera, OpenMP dynamic over pixels, "
-                         f"{cpu_s:.2f} s per frame"}
+        cores, affinity, quota = cpu_cores()
+        t_all, t_one, (w1, h1) = cpu_baseline(flat, cam, W, H, cores)
+        cpu = {"value": round(W * H / t_all / 1e6, 4), "unit": "Mrays/s", "cores": cores, "kind": "port",
+               "value_1core": round(w1 * h1 / t_one / 1e6, 4),
+               "nproc": os.cpu_count(), "affinity_cpus": affinity, "cgroup_cpu_quota": quota,
+               "cpu_model": cpu_model(),
+               "sample": f"all {cores} cores: 1 warm-up + median of 5 full {W}x{H} frames ({t_all:.2f} s per frame); "
+                         f"1 core: 1 warm-up + median of 5 {w1}x{h1} frames of the same view ({t_one:.2f} s each); "
+                         f"same tree and camera, OpenMP dynamic over pixels"}
 
     if rank == 0:
         metric = BASELINE["metric"]
         if args.shadows:
             metric = "primary + hard-shadow Mrays/s (BASELINE config 5)"
+        if world > 1:
+            par = f"screen-tile split x{world} + " + (
+                "gloo gather (single-GPU rehearsal)" if rehearsal else
+                ("RCCL ncclGather of RGBA8 + depth behind the C ABI (vhx_mgpu), tree ncclBroadcast from rank 0"
+                 if mg is not None else "RCCL gather via torch.distributed")
+                + ("" if args.no_overlap else ", overlapped with the next frame's trace"))
+        else:
+            par = "single GPU"
+        cfg4 = (W, H) == CONFIG4
         line = {
             "metric": metric, "value": round(mrays, 3), "unit": "Mrays/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": "f32",
             "data": "model file" if args.vox else "synthetic",
-            "config": {"workload": f"primary rays {W}x{H}, {args.size}^3 "
+            "config": {"workload": ("BASELINE config 4: " if cfg4 else "") + f"primary rays {W}x{H}, {args.size}^3 "
                                    + (f".vox model {os.path.basename(args.vox)}" if args.vox
                                       else "procedural scene S (lattice+cube)")
                                    + f", brick_dim {args.brick_dim}, glass camera"
-                                   + (f", {W * H // world} rays per rank" if world > 1 else ""),
+                                   + (f", {T}x{T} tiles round-robin over {world} ranks" if world > 1 else ""),
                        "workload_key": workload,
                        "shadow_rays_per_frame": n_shadow if args.shadows else None,
                        "tree_size": args.size, "brick_dim": args.brick_dim, "width": W, "height": H,
-                       "scene": args.scene, "tile": T if world > 1 else None,
-                       "parallelism": (f"screen-tile split x{world} + " + (
-                           "gloo gather (single-GPU rehearsal)" if rehearsal else
-                           "RCCL gather" + ("" if args.no_overlap else ", overlapped with the next frame's trace")))
-                       if world > 1 else "single GPU",
-                       "tree_nodes": int(flat.desc.node_count), "tree_bricks": int(flat.desc.brick_count),
-                       "tree_gb": round(flat.nbytes() / 1e9, 3), "build_s": round(build_s, 2),
-                       "upload_s": round(upload_s, 2)},
+                       "scene": args.scene, "tile": T if world > 1 else None, "parallelism": par,
+                       **{k: v for k, v in tree_info.items() if k != "size"}, "build_s": round(build_s, 2), "upload_s": round(upload_s, 2)},
             "roofline": roof, "cpu_baseline": cpu,
         }
         if mgpu is not None:
@@ -283,6 +405,8 @@ def main():
         if cpu:
             line["gpu_over_cpu"] = round(mrays / cpu["value"], 2)
         print(json.dumps(line), flush=True)
+    if mg is not None:
+        mg.close()
     if world > 1:
         dist.destroy_process_group()
     rt.close()

@@ -43,6 +43,7 @@ extern "C" {
                                   view.resize / re_evaluate_view_size (src/raytracing/bevy/streaming/mod.rs:292-340) */
 #define VHX_E_NO_DEVICE (-4)   /* no HIP device available                                                       */
 #define VHX_E_STATE (-5)       /* call order violated (e.g. trace before upload)                                */
+#define VHX_E_RCCL (-6)        /* RCCL missing or an RCCL call failed (message in vhx_last_error)               */
 
 /* ---- node types (NodeContent, src/boxtree/types.rs:57-73) ------------------------------------------------- */
 #define VHX_NODE_NOTHING 0u
@@ -183,7 +184,8 @@ int vhx_trace_rays(vhx_ctx *ctx, const float *rays, uint64_t n, const vhx_hits *
  * src/raytracing/bevy/view.rs:81-85) is traced with get_by_ray semantics; shadowed[i] = 1 if it hits a voxel, else 0
  * (0 for primary misses). rgba (optional) is darkened in place (rgb >> 1) where shadowed; bytes (optional) receives
  * the algorithmic bytes of each shadow ray. All pointers are device memory (the on_device output of
- * vhx_trace_primary / vhx_trace_rays); hit pixels are compacted first so waves trace only shadow rays. */
+ * vhx_trace_primary / vhx_trace_rays); hit pixels are compacted first so waves trace only shadow rays. The outputs
+ * (shadowed, rgba, bytes) must not overlap the hit records (value, impact, normal) or each other: VHX_E_INVALID_ARG. */
 int vhx_trace_shadows(vhx_ctx *ctx, const float light[3], uint64_t n, const uint32_t *value, const float *impact,
                       const float *normal, uint32_t *shadowed, uint32_t *rgba, uint32_t *bytes);
 
@@ -191,6 +193,48 @@ int vhx_trace_shadows(vhx_ctx *ctx, const float light[3], uint64_t n, const uint
  * buffer holds tiles_per_rank*T*T pixels, concatenated by rank) into a width x height framebuffer.       */
 int vhx_untile_rgba(vhx_ctx *ctx, const uint32_t *gathered, uint32_t ranks, uint32_t tiles_per_rank,
                     uint32_t tile_size, uint32_t width, uint32_t height, uint32_t *framebuffer, int on_device);
+
+/* Scatters rank-gathered tile buffers into device framebuffers (the general form of vhx_untile_rgba). Rank r's part
+ * of `gathered` (rank-major) holds `planes` planes of tiles_per_rank*T*T 32-bit words each — plane 0 the RGBA8 of its
+ * tiles, plane 1 (planes = 2) their f32 depth — in the VHX_LAYOUT_TILES order of tiles r, r+ranks, ... Either
+ * framebuffer may be NULL to skip its plane (fb_depth must be NULL when planes = 1). Device pointers only.           */
+int vhx_untile_frame(vhx_ctx *ctx, const void *gathered, uint32_t planes, uint32_t ranks, uint32_t tiles_per_rank,
+                     uint32_t tile_size, uint32_t width, uint32_t height, uint32_t *fb_rgba, float *fb_depth);
+
+/* ---- multi-GPU: screen-tile split over RCCL ------------------------------------------------------
+ * One context per GPU and process (the reference renders one view per Bevy render world, VhxRenderNode::run,
+ * src/raytracing/bevy/pipeline/mod.rs:96-155; these calls spread that view over the GPUs of a node). The frame is cut
+ * into tile_size^2 screen tiles dealt round-robin over the ranks (rank r traces tiles r, r+N, ...); each frame every
+ * rank traces its tiles into a contiguous RGBA8 + f32-depth buffer, one ncclGather (RCCL over xGMI) brings the
+ * buffers to rank 0, and rank 0 untiles them into its framebuffers. The tree is replicated: vhx_mgpu_broadcast_tree
+ * uploads it on rank 0 and ncclBroadcasts the device buffers to the other ranks (no host copy of the tree there).
+ * RCCL is loaded at run time (dlopen of librccl.so.1, or the path in VHX_RCCL_LIB), so libvhx itself has no link-time
+ * RCCL dependency; without it these calls return VHX_E_RCCL. Errors are reported through vhx_last_error(ctx).      */
+#define VHX_MGPU_ID_BYTES 128 /* = NCCL_UNIQUE_ID_BYTES */
+typedef struct vhx_mgpu vhx_mgpu;
+/* Rank 0 creates the communicator id; the caller sends its bytes to every rank out of band (e.g. a TCP store). */
+int vhx_mgpu_unique_id(uint8_t id[VHX_MGPU_ID_BYTES]);
+/* Collective over the N ranks (ncclCommInitRank): joins the communicator `id` as `rank` of `nranks`. */
+int vhx_mgpu_create(vhx_ctx *ctx, const uint8_t id[VHX_MGPU_ID_BYTES], int nranks, int rank, uint32_t tile_size,
+                    vhx_mgpu **out);
+/* Same on a communicator the caller already owns (an ncclComm_t passed as void*; borrowed, never destroyed). */
+int vhx_mgpu_create_from_comm(vhx_ctx *ctx, void *nccl_comm, uint32_t tile_size, vhx_mgpu **out);
+/* Collective: rank 0 passes the tree (uploaded to its context like vhx_upload_tree), every other rank NULL; returns
+ * once every rank holds the tree and its derived device layout. */
+int vhx_mgpu_broadcast_tree(vhx_mgpu *m, const vhx_tree_desc *tree);
+/* overlap = 1 (default): frame k's gather and untile run on a communication stream while frame k+1 is traced (two
+ * tile buffers alternate); 0: each render completes its gather and untile in the context's stream order. */
+int vhx_mgpu_set_overlap(vhx_mgpu *m, int overlap);
+/* Collective: renders one frame. On rank 0, fb_rgba (width*height u32, RGBA8) and fb_depth (width*height f32, may be
+ * NULL) are device framebuffers receiving the whole frame; other ranks pass NULL. Outputs are complete after
+ * vhx_mgpu_sync. */
+int vhx_mgpu_render(vhx_mgpu *m, const vhx_camera *cam, uint32_t *fb_rgba, float *fb_depth);
+/* Waits for every frame submitted on this rank (trace, gather and untile); optionally returns the device time of the
+ * last frame's trace on this rank in milliseconds. */
+int vhx_mgpu_sync(vhx_mgpu *m, float *last_trace_ms);
+/* nranks, rank, and the rays this rank traces for a width x height frame (any pointer may be NULL). */
+int vhx_mgpu_info(const vhx_mgpu *m, uint32_t width, uint32_t height, int *nranks, int *rank, uint64_t *rays);
+void vhx_mgpu_destroy(vhx_mgpu *m);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,97 @@
+"""BASELINE config 4 (8 x MI355X screen-tile split + gather, 7680x4320, 1024^3) on one GPU, and the multi-GPU C ABI.
+
+* The 7680x4320 frame of the bench tree is traced as the 8 rank tile sets of config 4 (64x64 tiles dealt round-robin,
+  VHX_LAYOUT_TILES), concatenated rank-major as the gather delivers them ([RGBA plane | depth plane] per rank),
+  scattered with vhx_untile_frame and compared with the oracle's whole 7680x4320 frame (RGBA and depth bit-exact).
+* vhx_mgpu_* (RCCL behind the C ABI) with a one-rank communicator: the tree broadcast, the per-frame ncclGather and
+  the untile on rank 0 reproduce the same frame, with and without overlapped frames. (RCCL refuses two ranks on one
+  GPU, so N > 1 runs first on the driver's 8-GPU node; the code path is the same apart from RCCL's own transport.)
+"""
+import numpy as np
+import pytest
+
+import voxelhex_amd as vhx
+from voxelhex_amd import _native as N
+from voxelhex_amd import multigpu as M
+
+pytestmark = pytest.mark.gpu
+
+W4, H4, T4, R4 = 7680, 4320, 64, 8
+
+
+@pytest.fixture(scope="module")
+def config4(oracle):
+    flat = vhx.FlatTree.build_scene(N.VHX_SCENE_LATTICE_CUBE, 1024, 4)
+    cam = vhx.glass_camera(1024, W4, H4, target=(512.0, 512.0, 512.0))
+    ref = oracle.trace_primary(flat, cam, 0, 0, W4, H4, fields=("rgba", "depth"))
+    return flat, cam, ref
+
+
+def _check_frame(rgba, depth, ref, what):
+    got_rgba = rgba.cpu().numpy().view(np.uint32)
+    got_depth = depth.cpu().numpy().view(np.uint32)
+    bad = np.count_nonzero(got_rgba != ref["rgba"])
+    assert bad == 0, f"{what}: rgba differs at {bad} pixels"
+    bad = np.count_nonzero(got_depth != ref["depth"].view(np.uint32))
+    assert bad == 0, f"{what}: depth differs at {bad} pixels"
+
+
+def test_config4_eight_rank_tile_sets_vs_oracle(gpu, config4):
+    import torch
+    flat, cam, ref = config4
+    gpu.upload(flat)
+    per = M.tiles_per_rank(W4, H4, T4, R4)
+    n_out = per * T4 * T4
+    gathered = torch.zeros(R4 * 2 * n_out, dtype=torch.int32, device="cuda")
+    for r in range(R4):
+        part = gathered[r * 2 * n_out:(r + 1) * 2 * n_out]
+        gpu.trace_primary(cam, tile_size=T4, tile_start=r, tile_stride=R4, layout=N.VHX_LAYOUT_TILES,
+                          out={"rgba": part[:n_out], "depth": part[n_out:].view(torch.float32)})
+    rgba = torch.zeros(W4 * H4, dtype=torch.int32, device="cuda")
+    depth = torch.zeros(W4 * H4, dtype=torch.float32, device="cuda")
+    gpu.untile_frame(gathered.data_ptr(), 2, R4, per, T4, W4, H4, rgba.data_ptr(), depth.data_ptr())
+    gpu.sync()
+    _check_frame(rgba, depth, ref, "config 4, 8 rank tile sets")
+    assert (ref["rgba"] != 0xFF808080).mean() > 0.1  # a frame with geometry, not the background
+
+
+@pytest.mark.parametrize("overlap", [True, False])
+def test_mgpu_one_rank_rccl_frame_vs_oracle(config4, overlap):
+    import torch
+    flat, cam, ref = config4
+    rt = vhx.Raytracer(0)
+    try:
+        m = M.MgpuRenderer(rt, M.mgpu_unique_id(), 1, 0, tile_size=T4, overlap=overlap)
+        m.broadcast_tree(flat)
+        assert m.rays(W4, H4) == W4 * H4
+        fbs = [(torch.zeros(W4 * H4, dtype=torch.int32, device="cuda"),
+                torch.zeros(W4 * H4, dtype=torch.float32, device="cuda")) for _ in range(3)]
+        for rgba, depth in fbs:  # three frames in flight through the two alternating tile buffers
+            m.render(cam, rgba, depth)
+        m.sync()
+        for k, (rgba, depth) in enumerate(fbs):
+            _check_frame(rgba, depth, ref, f"vhx_mgpu frame {k} (overlap={overlap})")
+        m.close()
+    finally:
+        rt.close()
+
+
+def test_mgpu_argument_errors(gpu):
+    import ctypes
+    flat = vhx.FlatTree.build_scene(N.VHX_SCENE_LATTICE_CUBE, 64, 4)
+    uid = M.mgpu_unique_id()
+    rt = vhx.Raytracer(0)
+    try:
+        idbuf = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
+        h = ctypes.c_void_p()
+        assert N.lib().vhx_mgpu_create(rt._h, idbuf, 1, 1, 64, ctypes.byref(h)) == N.VHX_E_INVALID_ARG  # rank >= N
+        assert N.lib().vhx_mgpu_create(rt._h, idbuf, 1, 0, 0, ctypes.byref(h)) == N.VHX_E_INVALID_ARG  # tile 0
+        m = M.MgpuRenderer(rt, uid, 1, 0, tile_size=32)
+        with pytest.raises(N.VhxError):
+            m.broadcast_tree(None)  # rank 0 must pass the tree
+        with pytest.raises(N.VhxError):
+            m.render(vhx.glass_camera(64, 64, 64))  # rank 0 without a framebuffer (and no tree yet)
+        m.broadcast_tree(flat)
+        m.close()
+    finally:
+        rt.close()

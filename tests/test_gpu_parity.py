@@ -462,3 +462,77 @@ def test_host_out_arrays_match_device_outputs(gpu):
         gpu.trace_primary(cam, out={"rgba": np.zeros(W * H - 1, np.uint32)})
     with pytest.raises(ValueError):
         gpu.trace_primary(cam, out={"rgba": np.zeros(W * H, np.uint32), "depth": dev["depth"]})
+
+
+def test_pass0_flags_at_ragged_frame_edges(oracle):
+    """A frame whose width and height are not multiples of the 16x16 workgroup block, traced with a 1-step first
+    budget (nearly every ray is abandoned and queued) on a fresh context (flags buffer sized exactly): lanes past the
+    right and bottom frame edges must not write flags (they would alias the next row's left-edge pixels or run past
+    the buffer), so every pixel, the left column included, equals the oracle."""
+    flat = vhx.FlatTree.build_scene(N.VHX_SCENE_LATTICE_CUBE, 64, 4)
+    W, H = 200, 136
+    # zoomed onto the solid cube: every pixel, the left column included, hits geometry
+    cam = vhx.glass_camera(64, W, H, target=(48.0, 48.0, 48.0), glass_width=0.6)
+    ref = oracle.trace_primary(flat, cam, 0, 0, W, H, count_bytes=True)
+    left = ref["value"].reshape(H, W)[:, :8]
+    assert (left != N.VHX_EMPTY).mean() > 0.9
+    for budgets in ((1,), (1, 2, 3)):
+        rt = vhx.Raytracer(0)
+        try:
+            rt.upload(flat)
+            rt.set_pass_budgets(budgets)
+            assert_same(rt.trace_primary(cam, count_bytes=True), ref, f"ragged frame {budgets}")
+        finally:
+            rt.close()
+
+
+@pytest.mark.parametrize("budgets", [(1,), DEFAULT_BUDGETS])
+def test_sharded_framebuffer_multipass(gpu, oracle, budgets):
+    """Framebuffer layout with a rank's tile subset (tile_start / tile_stride) under a multi-pass schedule: the rank
+    writes exactly its own pixels (equal to the oracle's) and leaves every other pixel untouched, also after a
+    whole-frame trace left its flags behind."""
+    import torch
+    flat = vhx.FlatTree.build_scene(N.VHX_SCENE_LATTICE_CUBE, 256, 4)
+    gpu.upload(flat)
+    W, H, T, R = 200, 136, 32, 3
+    cam = vhx.glass_camera(256, W, H, target=(128.0, 128.0, 128.0))
+    ref = oracle.trace_primary(flat, cam, 0, 0, W, H)
+    try:
+        gpu.set_pass_budgets(budgets)
+        gpu.trace_primary(cam, fields=("value",))  # leaves this frame's pass-0 flags in the context
+        tiles_x = (W + T - 1) // T
+        for r in range(R):
+            out = {"value": torch.full((W * H,), 0x5A5A5A5A, dtype=torch.int32, device="cuda"),
+                   "rgba": torch.full((W * H,), 0x5A5A5A5A, dtype=torch.int32, device="cuda")}
+            gpu.trace_primary(cam, tile_size=T, tile_start=r, tile_stride=R, out=out)
+            gpu.sync()
+            mine = np.zeros((H, W), bool)
+            for tile in range(r, tiles_x * ((H + T - 1) // T), R):
+                tx, ty = (tile % tiles_x) * T, (tile // tiles_x) * T
+                mine[ty:ty + T, tx:tx + T] = True
+            mine = mine.reshape(-1)
+            for k in ("value", "rgba"):
+                got = out[k].cpu().numpy().view(np.uint32)
+                assert np.array_equal(got[mine], ref[k][mine]), (k, r, budgets)
+                assert (got[~mine] == 0x5A5A5A5A).all(), (k, r, budgets, "foreign pixels written")
+    finally:
+        gpu.set_pass_budgets(DEFAULT_BUDGETS)
+
+
+def test_shadow_outputs_must_not_alias_hits(gpu):
+    """vhx_trace_shadows refuses outputs that overlap the hit records it reads (or each other)."""
+    import torch
+    flat = vhx.FlatTree.build_scene(N.VHX_SCENE_LATTICE_CUBE, 64, 4)
+    gpu.upload(flat)
+    W, H = 64, 48
+    cam = vhx.glass_camera(64, W, H, target=(32.0, 32.0, 32.0))
+    hits = gpu.trace_primary(cam, out=_device_hits(W * H))
+    with pytest.raises(N.VhxError):
+        gpu.trace_shadows((64.0,) * 3, hits, shadowed=hits["value"])
+    with pytest.raises(N.VhxError):
+        gpu.trace_shadows((64.0,) * 3, hits, shadowed=hits["rgba"])  # rgba is darkened in place: an output too
+    with pytest.raises(N.VhxError):
+        gpu.trace_shadows((64.0,) * 3, hits, shadowed=hits["impact"].view(-1)[5:5 + W * H].view(torch.int32))
+    res = gpu.trace_shadows((64.0,) * 3, hits)
+    gpu.sync()
+    assert res["shadowed"].numel() == W * H

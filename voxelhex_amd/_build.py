@@ -17,8 +17,8 @@ LIB = os.path.join(LIBDIR, "libvhx.so")
 ARCH = os.environ.get("VHX_OFFLOAD_ARCH", "gfx950")
 
 HOST_SRCS = ["boxtree.cpp", "flatten.cpp", "vox.cpp", "stream.cpp"]
-DEV_SRCS = ["vhx_device.hip"]
-HEADERS = ["boxtree.hpp", "trace.hpp"]
+DEV_SRCS = ["vhx_device.hip", "vhx_mgpu.hip"]
+HEADERS = ["boxtree.hpp", "trace.hpp", "ctx.hpp"]
 
 
 def _hipcc():
@@ -62,7 +62,8 @@ def build(verbose=False, force=False):
                   "-fno-fast-math", "-Wall", "-I", inc, "-c", s, "-o", o], verbose)
         objs.append(o)
     if force or _stale(LIB, objs):
-        _run([_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-pthread", "-o", LIB] + objs, verbose)
+        # -ldl: RCCL is dlopen()ed by vhx_mgpu.hip (no link-time RCCL dependency)
+        _run([_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-pthread", "-o", LIB] + objs + ["-ldl"], verbose)
     return LIB
 
 

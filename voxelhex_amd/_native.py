@@ -22,6 +22,8 @@ VHX_E_HIP = -2
 VHX_E_CAPACITY = -3
 VHX_E_NO_DEVICE = -4
 VHX_E_STATE = -5
+VHX_E_RCCL = -6
+VHX_MGPU_ID_BYTES = 128
 VHX_E_TREE_INVALID_SIZE = -10
 VHX_E_TREE_INVALID_BRICK_DIMENSION = -11
 VHX_E_TREE_INVALID_STRUCTURE = -12
@@ -86,6 +88,16 @@ SIGNATURES = [
     ("vhx_trace_shadows", c_int, [c_void_p, P(c_f32), c_u64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                   c_void_p]),
     ("vhx_untile_rgba", c_int, [c_void_p, c_void_p, c_u32, c_u32, c_u32, c_u32, c_u32, c_void_p, c_int]),
+    ("vhx_untile_frame", c_int, [c_void_p, c_void_p, c_u32, c_u32, c_u32, c_u32, c_u32, c_u32, c_void_p, c_void_p]),
+    ("vhx_mgpu_unique_id", c_int, [c_void_p]),
+    ("vhx_mgpu_create", c_int, [c_void_p, c_void_p, c_int, c_int, c_u32, P(c_void_p)]),
+    ("vhx_mgpu_create_from_comm", c_int, [c_void_p, c_void_p, c_u32, P(c_void_p)]),
+    ("vhx_mgpu_broadcast_tree", c_int, [c_void_p, P(TreeDesc)]),
+    ("vhx_mgpu_set_overlap", c_int, [c_void_p, c_int]),
+    ("vhx_mgpu_render", c_int, [c_void_p, P(Camera), c_void_p, c_void_p]),
+    ("vhx_mgpu_sync", c_int, [c_void_p, P(c_f32)]),
+    ("vhx_mgpu_info", c_int, [c_void_p, c_u32, c_u32, P(c_int), P(c_int), P(c_u64)]),
+    ("vhx_mgpu_destroy", None, [c_void_p]),
     ("vhx_boxtree_new", c_int, [c_u32, c_u32, P(c_void_p)]),
     ("vhx_boxtree_free", None, [c_void_p]),
     ("vhx_boxtree_set_auto_simplify", c_int, [c_void_p, c_int]),

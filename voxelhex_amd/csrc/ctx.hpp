@@ -1,0 +1,87 @@
+// Internal context of libvhx (shared by the translation units of the device side: vhx_device.hip, vhx_mgpu.hip).
+// Not part of the ABI: callers see vhx_ctx only as an opaque pointer (include/vhx.h).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/vhx.h"
+
+struct DevBuf {
+    void *ptr = nullptr;
+    uint64_t bytes = 0;
+};
+
+struct vhx_ctx {
+    int device = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    bool timed = false;
+    std::string err;
+    bool uploaded = false;
+    vhx_tree_desc desc{};  // counts of the uploaded tree (pointers unused)
+    DevBuf raw[7];         // VHX_BUF_* raw copies
+    DevBuf hdr, brick_occ, scratch, rays;
+    DevBuf child_rec;         // brick_dim <= 4: DevTree::child_rec, rebuilt before a trace when stale
+    bool child_rec_stale = false;
+    DevBuf queue[2];  // multi-pass ray queues (ping-pong), output indices of abandoned rays in increasing order
+    DevBuf qctl;      // QCTL_WORDS: [0..7] queue lengths after pass p (7: shadow hit list), [16 + 16p ..] counters
+    DevBuf tmp;       // chunk-local lists of abandoned rays (a block's or a queue chunk's, in lane order)
+    DevBuf counts;    // rays listed per chunk
+    DevBuf offsets;   // exclusive scan of counts
+    DevBuf flags;     // primary pass 0: abandoned flag per output index
+    DevBuf qargs;     // QueueArgs of the queue passes: slot 0 primary rays / ray batches, slot 1 shadow rays
+    std::vector<uint8_t> qargs_host[2];  // the QueueArgs last written to each slot (skips the upload when unchanged)
+    void *qargs_host_ptr[2] = {nullptr, nullptr};  // qargs.ptr they were written to
+    DevBuf state;     // saved traversal state per output index (64 B) of rays abandoned at a budget
+    uint32_t occ_words = 1;
+    // step budgets of the passes before the final (unbounded) one; VHX_BUDGETS="64" / "32,256" style override
+    uint32_t budgets[3] = {64u, 0u, 0u};
+    uint32_t npass = 2;         // passes including the final one (1 = single pass)
+    uint32_t rpw[4] = {64u, 64u, 64u, 64u};  // rays per wave of each pass (VHX_RPW="64,16" style override; 0 = adaptive)
+    uint32_t tw = 1024;            // adaptive rays per wave: target waves per queue pass (VHX_TW)
+    bool resume = true;            // abandoned rays continue from saved state (VHX_RESUME=0: re-traced from scratch)
+    uint32_t xcd_group = 16;       // pass-0 XCD-aware block runs (VHX_XCDG; 0 = dispatch order)
+    uint32_t qblock = 256;         // threads per workgroup of a queue pass (VHX_QBLOCK=64: one wave per workgroup)
+    uint32_t queue_blocks = 2048;  // workgroups of a queue pass (CUs x resident workgroups)
+    // waves of a queue pass (VHX_QWAVES): 8 per CU. The bench frame's tail pass (148 k rays, 2316 chunks of 64) took
+    // 1.55 ms/frame at 2048 waves against 1.62 at 8192 and 1.82 at 1024 (fewer busy waves per CU at the start of the
+    // pass, while every chunk still starts at once)
+    uint32_t queue_waves = 2048;
+    uint32_t queue_waves0 = 8192;  // waves of a first queue pass over fresh rays (VHX_QWAVES0)
+    uint32_t qxcd = 16;            // queue passes: XCD-dealt chunk runs (VHX_QXCD = run length, 0 = one counter)
+};
+
+#define VHX_HIP(ctx, call)                                                                                         \
+    do {                                                                                                           \
+        hipError_t e_ = (call);                                                                                    \
+        if (e_ != hipSuccess) {                                                                                    \
+            (ctx)->err = std::string(#call) + ": " + hipGetErrorString(e_);                                        \
+            return VHX_E_HIP;                                                                                      \
+        }                                                                                                          \
+    } while (0)
+
+static inline int fail(vhx_ctx *ctx, int code, const char *msg) {
+    if (ctx) ctx->err = msg;
+    return code;
+}
+
+namespace vhx {
+// device buffer of at least `bytes` (contents not kept when it grows)
+int ensure(vhx_ctx *c, DevBuf &b, uint64_t bytes);
+// element size / count of the VHX_BUF_* raw buffers of a tree
+uint64_t elem_size(int id);
+uint64_t elem_count(const vhx_tree_desc &d, int id);
+// allocates the raw buffers for the counts of *t (t's pointers unused) and records the counts
+int alloc_tree(vhx_ctx *c, const vhx_tree_desc *t);
+// derives the device-side layout (node headers, brick bitmaps, child records) from the raw buffers, synchronously
+int finish_upload(vhx_ctx *c);
+// k_untile_planes on `stream` (arguments as vhx_untile_frame, already validated)
+int launch_untile(vhx_ctx *c, hipStream_t stream, const void *gathered, uint32_t planes, uint32_t ranks,
+                  uint32_t tiles_per_rank, uint32_t T, uint32_t width, uint32_t height, uint32_t *fb_rgba,
+                  float *fb_depth);
+}  // namespace vhx
+

@@ -26,66 +26,7 @@ __constant__ uint8_t c_step_lut[64 * 27];
 
 using namespace vhx;
 
-// ------------------------------------------------------------------------------------------------ device context
-struct DevBuf {
-    void *ptr = nullptr;
-    uint64_t bytes = 0;
-};
-
-struct vhx_ctx {
-    int device = 0;
-    hipStream_t own_stream = nullptr;
-    hipStream_t stream = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    bool timed = false;
-    std::string err;
-    bool uploaded = false;
-    vhx_tree_desc desc{};  // counts of the uploaded tree (pointers unused)
-    DevBuf raw[7];         // VHX_BUF_* raw copies
-    DevBuf hdr, brick_occ, scratch, rays;
-    DevBuf child_rec;         // brick_dim <= 4: DevTree::child_rec, rebuilt before a trace when stale
-    bool child_rec_stale = false;
-    DevBuf queue[2];  // multi-pass ray queues (ping-pong), output indices of abandoned rays in increasing order
-    DevBuf qctl;      // QCTL_WORDS: [0..7] queue lengths after pass p (7: shadow hit list), [16 + 16p ..] counters
-    DevBuf tmp;       // chunk-local lists of abandoned rays (a block's or a queue chunk's, in lane order)
-    DevBuf counts;    // rays listed per chunk
-    DevBuf offsets;   // exclusive scan of counts
-    DevBuf flags;     // primary pass 0: abandoned flag per output index
-    DevBuf qargs;     // QueueArgs of the queue passes: slot 0 primary rays / ray batches, slot 1 shadow rays
-    std::vector<uint8_t> qargs_host[2];  // the QueueArgs last written to each slot (skips the upload when unchanged)
-    void *qargs_host_ptr[2] = {nullptr, nullptr};  // qargs.ptr they were written to
-    DevBuf state;     // saved traversal state per output index (64 B) of rays abandoned at a budget
-    uint32_t occ_words = 1;
-    // step budgets of the passes before the final (unbounded) one; VHX_BUDGETS="64" / "32,256" style override
-    uint32_t budgets[3] = {64u, 0u, 0u};
-    uint32_t npass = 2;         // passes including the final one (1 = single pass)
-    uint32_t rpw[4] = {64u, 64u, 64u, 64u};  // rays per wave of each pass (VHX_RPW="64,16" style override; 0 = adaptive)
-    uint32_t tw = 1024;            // adaptive rays per wave: target waves per queue pass (VHX_TW)
-    bool resume = true;            // abandoned rays continue from saved state (VHX_RESUME=0: re-traced from scratch)
-    uint32_t xcd_group = 16;       // pass-0 XCD-aware block runs (VHX_XCDG; 0 = dispatch order)
-    uint32_t qblock = 256;         // threads per workgroup of a queue pass (VHX_QBLOCK=64: one wave per workgroup)
-    uint32_t queue_blocks = 2048;  // workgroups of a queue pass (CUs x resident workgroups)
-    // waves of a queue pass (VHX_QWAVES): 8 per CU. The bench frame's tail pass (148 k rays, 2316 chunks of 64) took
-    // 1.55 ms/frame at 2048 waves against 1.62 at 8192 and 1.82 at 1024 (fewer busy waves per CU at the start of the
-    // pass, while every chunk still starts at once)
-    uint32_t queue_waves = 2048;
-    uint32_t queue_waves0 = 8192;  // waves of a first queue pass over fresh rays (VHX_QWAVES0)
-    uint32_t qxcd = 16;            // queue passes: XCD-dealt chunk runs (VHX_QXCD = run length, 0 = one counter)
-};
-
-#define VHX_HIP(ctx, call)                                                                                         \
-    do {                                                                                                           \
-        hipError_t e_ = (call);                                                                                    \
-        if (e_ != hipSuccess) {                                                                                    \
-            (ctx)->err = std::string(#call) + ": " + hipGetErrorString(e_);                                        \
-            return VHX_E_HIP;                                                                                      \
-        }                                                                                                          \
-    } while (0)
-
-static int fail(vhx_ctx *ctx, int code, const char *msg) {
-    if (ctx) ctx->err = msg;
-    return code;
-}
+#include "ctx.hpp"
 
 // SECTANT_STEP_RESULT_LUT generator (src/bin/sectant_step_result_lut.rs:48-114), host side
 static void make_step_lut(uint8_t *lut) {
@@ -514,8 +455,10 @@ __global__ void __launch_bounds__(256) k_trace_primary(DevTree t, CamD cam, OutD
         else if (COUNT && q.state)
             out.bytes[idx] = h.bytes;  // the running count, continued by the pass that resumes the ray
     }
-    // every in-tile entry (frame padding included) gets its flag, so the flags need no clearing between frames
-    if (q.flags && lx < T && ly < T) q.flags[idx] = done ? 0 : 1;
+    // every entry of the output gets its flag, so the flags need no clearing between frames: in the tile layout
+    // every in-tile entry (frame padding included, done = true there); in the framebuffer layout only pixels of the
+    // frame (a lane past the frame edge has no entry of its own: its idx aliases the next row or runs past the end)
+    if (q.flags && (layout == VHX_LAYOUT_FRAMEBUFFER ? valid : (lx < T && ly < T))) q.flags[idx] = done ? 0 : 1;
 }
 
 template <bool COUNT, int BD>
@@ -638,15 +581,22 @@ __global__ void __launch_bounds__(256) k_trace_queue(DevTree t, const QueueArgs 
     }
 }
 
-__global__ void __launch_bounds__(256) k_untile_rgba(const uint32_t *__restrict__ gathered, uint32_t ranks,
-                                                     uint32_t tiles_per_rank, uint32_t T, uint32_t tiles_x,
-                                                     uint32_t ntiles, uint32_t width, uint32_t height,
-                                                     uint32_t *__restrict__ fb) {
+// Scatters rank-gathered tile buffers into framebuffers. Rank r's part of `gathered` holds `planes` planes of
+// tiles_per_rank*T*T words each (plane 0 RGBA8, plane 1 f32 depth bits), rank r traced tiles r, r + ranks, ...
+__global__ void __launch_bounds__(256) k_untile_planes(const uint32_t *__restrict__ gathered, uint32_t planes,
+                                                       uint32_t ranks, uint32_t tiles_per_rank, uint32_t T,
+                                                       uint32_t tiles_x, uint32_t ntiles, uint32_t width,
+                                                       uint32_t height, uint32_t *__restrict__ fb0,
+                                                       uint32_t *__restrict__ fb1) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint64_t per_rank = (uint64_t)tiles_per_rank * T * T;
+    const uint64_t per_plane = (uint64_t)tiles_per_rank * T * T, per_rank = per_plane * planes;
     if (i >= per_rank * ranks) return;
     const uint32_t r = (uint32_t)(i / per_rank);
-    const uint64_t k = i - (uint64_t)r * per_rank;
+    const uint64_t w = i - (uint64_t)r * per_rank;
+    const uint32_t plane = (uint32_t)(w / per_plane);
+    const uint64_t k = w - (uint64_t)plane * per_plane;
+    uint32_t *fb = plane ? fb1 : fb0;
+    if (!fb) return;
     const uint32_t j = (uint32_t)(k / ((uint64_t)T * T));
     const uint32_t local = (uint32_t)(k - (uint64_t)j * T * T);
     const uint32_t tile = r + j * ranks;
@@ -691,7 +641,7 @@ static DevTree dev_tree(const vhx_ctx *c) {
     return t;
 }
 
-static int ensure(vhx_ctx *c, DevBuf &b, uint64_t bytes) {
+int vhx::ensure(vhx_ctx *c, DevBuf &b, uint64_t bytes) {
     if (b.bytes >= bytes && b.ptr) return VHX_OK;
     if (b.ptr) VHX_HIP(c, hipFree(b.ptr));
     b.ptr = nullptr;
@@ -702,13 +652,13 @@ static int ensure(vhx_ctx *c, DevBuf &b, uint64_t bytes) {
     return VHX_OK;
 }
 
-static uint64_t elem_size(int id) {
+uint64_t vhx::elem_size(int id) {
     switch (id) {
         case VHX_BUF_NODE_OCBITS: return 8;
         default: return 4;
     }
 }
-static uint64_t elem_count(const vhx_tree_desc &d, int id) {
+uint64_t vhx::elem_count(const vhx_tree_desc &d, int id) {
     const uint64_t n3 = (uint64_t)d.brick_dim * d.brick_dim * d.brick_dim;
     switch (id) {
         case VHX_BUF_NODE_TYPE: return d.node_count;
@@ -1084,24 +1034,44 @@ int vhx_sync(vhx_ctx *c, float *ms) {
     return VHX_OK;
 }
 
-int vhx_upload_tree(vhx_ctx *c, const vhx_tree_desc *t) {
-    if (!c || !t) return VHX_E_INVALID_ARG;
+}  // extern "C"
+
+int vhx::launch_untile(vhx_ctx *c, hipStream_t stream, const void *gathered, uint32_t planes, uint32_t ranks,
+                       uint32_t tiles_per_rank, uint32_t T, uint32_t width, uint32_t height, uint32_t *fb_rgba,
+                       float *fb_depth) {
+    const uint32_t tiles_x = (width + T - 1) / T, tiles_y = (height + T - 1) / T;
+    const uint64_t n = (uint64_t)ranks * planes * tiles_per_rank * T * T;
+    if (n == 0) return VHX_OK;
+    k_untile_planes<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>((const uint32_t *)gathered, planes, ranks,
+                                                                     tiles_per_rank, T, tiles_x, tiles_x * tiles_y,
+                                                                     width, height, fb_rgba, (uint32_t *)fb_depth);
+    VHX_HIP(c, hipGetLastError());
+    return VHX_OK;
+}
+
+int vhx::alloc_tree(vhx_ctx *c, const vhx_tree_desc *t) {
     const uint32_t bd = t->brick_dim;
     if (t->node_count == 0 || bd == 0 || t->boxtree_size == 0 || (bd & (bd - 1)) != 0 || bd > 32 ||
         (t->boxtree_size & (t->boxtree_size - 1)) != 0 || t->boxtree_size > (1u << 24))
         return fail(c, VHX_E_INVALID_ARG, "vhx_upload_tree: invalid sizes");
-    const void *src[7] = {t->node_type, t->node_ocbits, t->node_children, t->voxels,
-                          t->solid_values, t->color_palette, t->data_palette};
     VHX_HIP(c, hipSetDevice(c->device));
+    c->uploaded = false;
     for (int id = 0; id < 7; ++id) {
-        const uint64_t n = elem_count(*t, id), bytes = n * elem_size(id);
-        if (n && !src[id]) return fail(c, VHX_E_INVALID_ARG, "vhx_upload_tree: null array with non-zero count");
-        int rc = ensure(c, c->raw[id], bytes);
+        int rc = ensure(c, c->raw[id], elem_count(*t, id) * elem_size(id));
         if (rc) return rc;
-        if (bytes) VHX_HIP(c, hipMemcpyAsync(c->raw[id].ptr, src[id], bytes, hipMemcpyHostToDevice, c->stream));
     }
     c->desc = *t;
-    const uint64_t n3 = (uint64_t)bd * bd * bd;
+    for (const void **q : {(const void **)&c->desc.node_type, (const void **)&c->desc.node_ocbits,
+                           (const void **)&c->desc.node_children, (const void **)&c->desc.voxels,
+                           (const void **)&c->desc.solid_values, (const void **)&c->desc.color_palette,
+                           (const void **)&c->desc.data_palette})
+        *q = nullptr;  // only the counts are kept
+    return VHX_OK;
+}
+
+int vhx::finish_upload(vhx_ctx *c) {
+    const vhx_tree_desc *t = &c->desc;
+    const uint64_t bd = t->brick_dim, n3 = bd * bd * bd;
     c->occ_words = n3 >= 64 ? (uint32_t)(n3 / 64) : 1u;
     int rc = ensure(c, c->hdr, (uint64_t)t->node_count * 16);
     if (rc) return rc;
@@ -1117,6 +1087,24 @@ int vhx_upload_tree(vhx_ctx *c, const vhx_tree_desc *t) {
     VHX_HIP(c, hipStreamSynchronize(c->stream));
     c->uploaded = true;
     return VHX_OK;
+}
+
+extern "C" {
+
+int vhx_upload_tree(vhx_ctx *c, const vhx_tree_desc *t) {
+    if (!c || !t) return VHX_E_INVALID_ARG;
+    const void *src[7] = {t->node_type, t->node_ocbits, t->node_children, t->voxels,
+                          t->solid_values, t->color_palette, t->data_palette};
+    for (int id = 0; id < 7; ++id)
+        if (elem_count(*t, id) && !src[id])
+            return fail(c, VHX_E_INVALID_ARG, "vhx_upload_tree: null array with non-zero count");
+    int rc = alloc_tree(c, t);
+    if (rc) return rc;
+    for (int id = 0; id < 7; ++id) {
+        const uint64_t bytes = elem_count(*t, id) * elem_size(id);
+        if (bytes) VHX_HIP(c, hipMemcpyAsync(c->raw[id].ptr, src[id], bytes, hipMemcpyHostToDevice, c->stream));
+    }
+    return finish_upload(c);
 }
 
 int vhx_update_range(vhx_ctx *c, int id, uint64_t off, uint64_t count, const void *src) {
@@ -1226,7 +1214,11 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
     src.tile_start = tile_start;
     src.tile_stride = tile_stride;
     VHX_HIP(c, hipEventRecord(c->ev0, c->stream));
-    // no reset_passes: the flag compaction after pass 0 zeroes the queue passes' counters
+    // no reset_passes: the flag compaction after pass 0 zeroes the queue passes' counters.
+    // A rank-sharded framebuffer (tile_start > 0 or tile_stride > 1) leaves the flags of other ranks' pixels unwritten,
+    // while the compaction scans every pixel: they are cleared first (stale flags would queue foreign pixels)
+    if (npass > 1 && layout == VHX_LAYOUT_FRAMEBUFFER && (tile_start > 0 || tile_stride > 1))
+        VHX_HIP(c, hipMemsetAsync(c->flags.ptr, 0, nout, c->stream));
     const bool count = ho.dev.bytes != nullptr;
     int qrc = VHX_OK;
     auto launch = [&](auto bd_tag) {
@@ -1310,6 +1302,27 @@ int vhx_trace_shadows(vhx_ctx *c, const float light[3], uint64_t n, const uint32
     if (!c->uploaded) return fail(c, VHX_E_STATE, "vhx_trace_shadows before vhx_upload_tree");
     if (n == 0) return VHX_OK;
     if (n >= 0x7FFFFFFFull) return fail(c, VHX_E_INVALID_ARG, "too many rays");
+    // the outputs are written while the hit records are still being read (the flags are cleared by the compaction
+    // kernel that reads value[]): they must not overlap them or each other
+    {
+        struct R {
+            const void *p;
+            uint64_t bytes;
+        } outs[] = {{shadowed, n * 4}, {rgba, n * 4}, {bytes, n * 4}},
+          ins[] = {{value, n * 4}, {impact, n * 12}, {normal, n * 12}};
+        auto overlap = [](const R &a, const R &b) {
+            return a.p && b.p && (const char *)a.p < (const char *)b.p + b.bytes &&
+                   (const char *)b.p < (const char *)a.p + a.bytes;
+        };
+        for (int i = 0; i < 3; ++i) {
+            for (int j = 0; j < 3; ++j)
+                if (overlap(outs[i], ins[j]))
+                    return fail(c, VHX_E_INVALID_ARG, "vhx_trace_shadows: an output overlaps the hit records");
+            for (int j = i + 1; j < 3; ++j)
+                if (overlap(outs[i], outs[j]))
+                    return fail(c, VHX_E_INVALID_ARG, "vhx_trace_shadows: outputs overlap each other");
+        }
+    }
     VHX_HIP(c, hipSetDevice(c->device));
     uint32_t npass = 1;
     const uint64_t nb64 = (n + 255) / 256;
@@ -1357,18 +1370,26 @@ int vhx_trace_shadows(vhx_ctx *c, const float light[3], uint64_t n, const uint32
     return VHX_OK;
 }
 
+int vhx_untile_frame(vhx_ctx *c, const void *gathered, uint32_t planes, uint32_t ranks, uint32_t tiles_per_rank,
+                     uint32_t T, uint32_t width, uint32_t height, uint32_t *fb_rgba, float *fb_depth) {
+    if (!c || !gathered || (!fb_rgba && !fb_depth) || planes < 1 || planes > 2 || (planes == 1 && fb_depth) ||
+        ranks == 0 || T == 0 || width == 0 || height == 0)
+        return fail(c, VHX_E_INVALID_ARG, "vhx_untile_frame: bad arguments");
+    const uint32_t tiles_x = (width + T - 1) / T, tiles_y = (height + T - 1) / T;
+    const uint64_t ntiles = (uint64_t)tiles_x * tiles_y;
+    if (ntiles > 0xFFFFFFFFull || (uint64_t)tiles_per_rank * ranks < ntiles)
+        return fail(c, VHX_E_INVALID_ARG, "vhx_untile_frame: tiles_per_rank * ranks does not cover the frame");
+    const uint64_t n = (uint64_t)ranks * planes * tiles_per_rank * T * T;
+    if ((n + 255) / 256 > 0x7FFFFFFFull) return fail(c, VHX_E_INVALID_ARG, "too many pixels");
+    VHX_HIP(c, hipSetDevice(c->device));
+    return launch_untile(c, c->stream, gathered, planes, ranks, tiles_per_rank, T, width, height, fb_rgba, fb_depth);
+}
+
 int vhx_untile_rgba(vhx_ctx *c, const uint32_t *gathered, uint32_t ranks, uint32_t tiles_per_rank, uint32_t T,
                     uint32_t width, uint32_t height, uint32_t *fb, int on_device) {
     if (!c || !gathered || !fb || ranks == 0 || T == 0 || width == 0 || height == 0) return VHX_E_INVALID_ARG;
     if (!on_device) return fail(c, VHX_E_INVALID_ARG, "vhx_untile_rgba works on device buffers");
-    const uint32_t tiles_x = (width + T - 1) / T, tiles_y = (height + T - 1) / T;
-    const uint64_t n = (uint64_t)ranks * tiles_per_rank * T * T;
-    if ((n + 255) / 256 > 0x7FFFFFFFull) return fail(c, VHX_E_INVALID_ARG, "too many pixels");
-    VHX_HIP(c, hipSetDevice(c->device));
-    k_untile_rgba<<<(unsigned)((n + 255) / 256), 256, 0, c->stream>>>(gathered, ranks, tiles_per_rank, T, tiles_x,
-                                                                      tiles_x * tiles_y, width, height, fb);
-    VHX_HIP(c, hipGetLastError());
-    return VHX_OK;
+    return vhx_untile_frame(c, gathered, 1, ranks, tiles_per_rank, T, width, height, fb, nullptr);
 }
 
 }  // extern "C"

@@ -43,6 +43,15 @@ def untile_numpy(gathered, ranks, per_rank, T, width, height):
     return fb
 
 
+def untile_planes_numpy(gathered, planes, ranks, per_rank, T, width, height):
+    """Host restatement of k_untile_planes (vhx_untile_frame): rank r's part of `gathered` holds `planes` planes of
+    per_rank*T*T words ([RGBA | depth] for planes = 2); returns one framebuffer per plane."""
+    n = per_rank * T * T
+    g = np.asarray(gathered).reshape(ranks, planes, n)
+    return [untile_numpy(np.ascontiguousarray(g[:, p, :]).reshape(-1), ranks, per_rank, T, width, height)
+            for p in range(planes)]
+
+
 class GatherPipeline:
     """Per-frame gather of every rank's tile buffer to rank 0 and the untile there, overlapped with the next frame.
 
@@ -116,3 +125,71 @@ def gather_to_root(local, world, rank, dist):
     bufs = [torch.empty_like(local) for _ in range(world)] if rank == 0 else None
     dist.gather(local, bufs, dst=0)
     return torch.cat(bufs) if rank == 0 else None
+
+
+def mgpu_unique_id():
+    """vhx_mgpu_unique_id: rank 0's RCCL communicator id (128 bytes) to send to every rank out of band."""
+    import ctypes
+    from . import _native as N
+    buf = (ctypes.c_uint8 * N.VHX_MGPU_ID_BYTES)()
+    N.check(N.lib().vhx_mgpu_unique_id(buf))
+    return bytes(buf)
+
+
+class MgpuRenderer:
+    """The multi-GPU split behind the C ABI (vhx_mgpu_*): one libvhx context per process and GPU, an RCCL
+    communicator owned by libvhx, the tree broadcast from rank 0 over RCCL, and per frame the rank's tiles traced,
+    ncclGather'ed to rank 0 (RGBA8 + f32 depth) and untiled there. `uid` = the bytes of mgpu_unique_id() created on
+    rank 0 (exchange them with e.g. torch.distributed.broadcast_object_list over gloo)."""
+
+    def __init__(self, raytracer, uid, world, rank, tile_size=64, overlap=True):
+        import ctypes
+        from . import _native as N
+        self.rt, self.world, self.rank, self.T = raytracer, world, rank, tile_size
+        idbuf = (ctypes.c_uint8 * N.VHX_MGPU_ID_BYTES).from_buffer_copy(uid)
+        h = ctypes.c_void_p()
+        raytracer._check(N.lib().vhx_mgpu_create(raytracer._h, idbuf, world, rank, tile_size, ctypes.byref(h)))
+        self._h = h
+        self.set_overlap(overlap)
+
+    def _check(self, rc):
+        return self.rt._check(rc)
+
+    def set_overlap(self, on):
+        from . import _native as N
+        self._check(N.lib().vhx_mgpu_set_overlap(self._h, 1 if on else 0))
+
+    def broadcast_tree(self, flat=None):
+        """Rank 0 passes the FlatTree, the other ranks None (collective)."""
+        import ctypes
+        from . import _native as N
+        desc = ctypes.byref(flat.desc) if flat is not None else None
+        self._check(N.lib().vhx_mgpu_broadcast_tree(self._h, desc))
+        self.rt._tree = flat
+
+    def render(self, cam, fb_rgba=None, fb_depth=None):
+        """Collective; rank 0 passes device framebuffers (torch tensors of width*height int32 / float32)."""
+        import ctypes
+        from . import _native as N
+        p = lambda t: ctypes.c_void_p(None if t is None else t.data_ptr())
+        self._check(N.lib().vhx_mgpu_render(self._h, ctypes.byref(cam), p(fb_rgba), p(fb_depth)))
+
+    def sync(self):
+        import ctypes
+        from . import _native as N
+        ms = ctypes.c_float()
+        self._check(N.lib().vhx_mgpu_sync(self._h, ctypes.byref(ms)))
+        return ms.value
+
+    def rays(self, width, height):
+        import ctypes
+        from . import _native as N
+        n = ctypes.c_uint64()
+        self._check(N.lib().vhx_mgpu_info(self._h, width, height, None, None, ctypes.byref(n)))
+        return n.value
+
+    def close(self):
+        from . import _native as N
+        if getattr(self, "_h", None) and self._h.value:
+            N.lib().vhx_mgpu_destroy(self._h)
+            self._h = None

@@ -306,6 +306,13 @@ class Raytracer:
             ctypes.c_void_p(_ptr(res["bytes"]) if count_bytes else None)))
         return res
 
+    def untile_frame(self, gathered_dev_ptr, planes, ranks, tiles_per_rank, tile_size, width, height, rgba_dev_ptr,
+                     depth_dev_ptr=None):
+        """vhx_untile_frame: rank-major [RGBA plane | depth plane] tile buffers -> device framebuffers."""
+        self._check(N.lib().vhx_untile_frame(self._h, ctypes.c_void_p(gathered_dev_ptr), planes, ranks,
+                                             tiles_per_rank, tile_size, width, height, ctypes.c_void_p(rgba_dev_ptr),
+                                             ctypes.c_void_p(depth_dev_ptr)))
+
     def untile_rgba(self, gathered_dev_ptr, ranks, tiles_per_rank, tile_size, width, height, fb_dev_ptr):
         self._check(N.lib().vhx_untile_rgba(self._h, ctypes.c_void_p(gathered_dev_ptr), ranks, tiles_per_rank,
                                             tile_size, width, height, ctypes.c_void_p(fb_dev_ptr), 1))
