@@ -60,6 +60,10 @@ def parse():
                    help="config 5: each step = primary frame + one hard-shadow ray per hit toward (S,S,S)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-roofline", action="store_true")
+    p.add_argument("--inflight", type=int, default=3,
+                   help="frames in flight per GPU: F contexts sharing the tree (vhx_create_shared), each on its own "
+                        "stream, frame i traced by context i %% F, so a frame's latency-bound long-ray tail overlaps the "
+                        "next frame's pass 0 (1 = one frame at a time)")
     p.add_argument("--no-overlap", action="store_true",
                    help="N>1: gather each frame before tracing the next (default: frame k's gather overlaps k+1)")
     return p.parse_args()
@@ -186,12 +190,16 @@ def main():
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     rt.set_stream(stream.cuda_stream)
+    F = max(1, args.inflight)
+    if world > 1 and not use_vhx_mgpu:
+        F = 1  # the torch gather pipeline keeps one frame per rank in flight
 
     mg = None
     if use_vhx_mgpu:
         obj = [M.mgpu_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         mg = M.MgpuRenderer(rt, obj[0], world, rank, tile_size=args.tile, overlap=not args.no_overlap)
+        mg.set_frames_in_flight(F)
 
     # the tree: built on the host (rank 0 only when it is broadcast over RCCL), uploaded to HBM
     t0 = time.time()
@@ -237,14 +245,27 @@ def main():
     if mg is not None and rank == 0:
         fb_rgba = torch.zeros(W * H, dtype=torch.int32, device=dev)
         fb_depth = torch.zeros(W * H, dtype=torch.float32, device=dev)
-    out = {"rgba": torch.zeros(n_out, dtype=torch.int32, device=dev),
-           "depth": torch.zeros(n_out, dtype=torch.float32, device=dev)}
-    if args.shadows:
-        # -1 = VHX_EMPTY: tile padding past the frame edge is never written and casts no shadow ray
-        out.update(value=torch.full((n_out,), -1, dtype=torch.int32, device=dev),
-                   impact=torch.zeros((n_out, 3), dtype=torch.float32, device=dev),
-                   normal=torch.zeros((n_out, 3), dtype=torch.float32, device=dev))
-        shadowed = torch.zeros(n_out, dtype=torch.int32, device=dev)
+    # frames in flight (single-GPU and torch paths; vhx_mgpu keeps its own): F contexts sharing the tree, F streams,
+    # F output sets
+    rts, streams, outs = [rt], [stream], []
+    if mg is None:
+        for _ in range(F - 1):
+            r = rt.shared()
+            s_ = torch.cuda.Stream(dev)
+            r.set_stream(s_.cuda_stream)
+            rts.append(r)
+            streams.append(s_)
+    for _ in range(len(rts)):
+        o = {"rgba": torch.zeros(n_out, dtype=torch.int32, device=dev),
+             "depth": torch.zeros(n_out, dtype=torch.float32, device=dev)}
+        if args.shadows:
+            # -1 = VHX_EMPTY: tile padding past the frame edge is never written and casts no shadow ray
+            o.update(value=torch.full((n_out,), -1, dtype=torch.int32, device=dev),
+                     impact=torch.zeros((n_out, 3), dtype=torch.float32, device=dev),
+                     normal=torch.zeros((n_out, 3), dtype=torch.float32, device=dev),
+                     shadowed=torch.zeros(n_out, dtype=torch.int32, device=dev))
+        outs.append(o)
+    out = outs[0]
     pipe = None
     framebuffer = None
     if world > 1 and mg is None:
@@ -258,21 +279,25 @@ def main():
                                 host_staging=rehearsal)
 
     ev = []
+    frame = [0]
 
     def step(timed):
-        if timed:
+        f = frame[0] % len(rts)
+        frame[0] += 1
+        r, s_, o = rts[f], streams[f], outs[f]
+        if timed and mg is None:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
+            e0.record(s_)
         if mg is not None:
             mg.render(cam, fb_rgba, fb_depth)  # this rank's tiles -> ncclGather -> untile on rank 0
         else:
             if pipe is not None:
-                out["rgba"] = pipe.out_buffer()
-            rt.trace_primary(cam, out=out, **trace_kw)
+                o["rgba"] = pipe.out_buffer()
+            r.trace_primary(cam, out=o, **trace_kw)
             if args.shadows:
-                rt.trace_shadows(light, out, shadowed=shadowed)
-        if timed:
-            e1.record(stream)  # the trace (the gather runs on the communication stream)
+                r.trace_shadows(light, o, shadowed=o["shadowed"])
+        if timed and mg is None:
+            e1.record(s_)  # the launch on its own stream (the gather runs on the communication stream)
             ev.append((e0, e1))
         if pipe is not None:
             pipe.submit()
@@ -304,7 +329,26 @@ def main():
             tt = tt.to(dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    # per-launch duration: with frames in flight (HIP events on each launch's stream, over the timed region); the
+    # isolated launch (one frame at a time, libvhx's own events) after it
+    if ev:
+        kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    iso = []
+    for _ in range(5):
+        if mg is not None:
+            mg.render(cam, fb_rgba, fb_depth)
+            iso.append(mg.sync())
+        else:
+            rt.trace_primary(cam, out=out, **trace_kw)
+            if args.shadows:
+                rt.trace_shadows(light, out, shadowed=out["shadowed"])
+                rt.sync()
+                iso = None
+                break
+            iso.append(rt.sync())
+    kernel_ms_isolated = float(np.median(iso)) if iso else None
+    if not ev:
+        kernel_ms = kernel_ms_isolated
 
     scene_tag = f"vox:{os.path.basename(args.vox)}" if args.vox else f"S{args.scene}"
     workload = f"primary {W}x{H} {scene_tag} {args.size}^3 bd{args.brick_dim} ranks{world}"
@@ -312,7 +356,7 @@ def main():
     n_shadow = 0
     if args.shadows:
         workload += " +shadows"
-        n_shadow = int((out["value"] != -1).sum().item())  # shadow rays this rank traced per frame
+        n_shadow = int((outs[0]["value"] != -1).sum().item())  # shadow rays this rank traced per frame
         if world > 1:
             ts = torch.tensor([n_shadow], dtype=torch.int64)
             if not rehearsal:
@@ -342,10 +386,19 @@ def main():
         my_rays = W * H if world == 1 else M.rank_rays(W, H, T, rank, world)
         out_bytes = 8.0 * my_rays  # rgba8 + f32 depth per ray
         launch_bytes = tree_bytes + out_bytes
-        achieved = launch_bytes / (kernel_ms * 1e-3) / 1e9
+        # chip-level: a launch's bytes per frame period (F frames in flight overlap: each launch's own duration
+        # includes the time it shares the GPU with its neighbours)
+        period_ms = ms_per_step if world == 1 else (kernel_ms_isolated or kernel_ms)
+        achieved = launch_bytes / (period_ms * 1e-3) / 1e9
         tr = pmc_traffic(workload)
         roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5),
+                "basis": ("algorithmic bytes of one frame's launch / the frame period (wall time per frame with "
+                          f"{F} frames in flight)") if world == 1 else
+                         "algorithmic bytes of rank 0's launch / its isolated launch duration",
+                "achieved_per_launch": round(launch_bytes / (kernel_ms * 1e-3) / 1e9, 2),
+                "achieved_isolated_launch": None if not kernel_ms_isolated else
+                round(launch_bytes / (kernel_ms_isolated * 1e-3) / 1e9, 2),
                 "traffic": None if tr is None else tr["read_bytes_per_launch"],
                 "traffic_source": None if tr is None else tr["source"],
                 "kernel": "vhx_trace_primary launch = k_trace_primary (pass 0, step budget) + k_trace_queue "
@@ -353,6 +406,8 @@ def main():
                           "on the trace stream" + (" (N>1: rank 0's tile set; the gather runs on the communication "
                                                    "stream)" if world > 1 else ""),
                 "kernel_ms": round(kernel_ms, 4),
+                "kernel_ms_isolated": None if kernel_ms_isolated is None else round(kernel_ms_isolated, 4),
+                "frames_in_flight": F,
                 "algorithmic_bytes_per_launch": launch_bytes, "tree_bytes_per_ray": round(tree_bytes / max(1, my_rays), 2)}
         if tr is not None and "issue" in tr:
             roof["issue"] = tr["issue"]
@@ -387,6 +442,7 @@ def main():
             "metric": metric, "value": round(mrays, 3), "unit": "Mrays/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": "f32",
+            "frames_in_flight": F,
             "data": "model file" if args.vox else "synthetic",
             "config": {"workload": ("BASELINE config 4: " if cfg4 else "") + f"primary rays {W}x{H}, {args.size}^3 "
                                    + (f".vox model {os.path.basename(args.vox)}" if args.vox
@@ -409,6 +465,8 @@ def main():
         mg.close()
     if world > 1:
         dist.destroy_process_group()
+    for r in rts[1:]:
+        r.close()
     rt.close()
 
 

@@ -135,6 +135,12 @@ typedef struct vhx_ctx vhx_ctx;
 uint32_t vhx_abi_version(void);
 int vhx_device_count(int *count);
 int vhx_create(int hip_device, vhx_ctx **out);
+/* A further context on the owner's device that traces the owner's uploaded tree (no second copy in HBM): one context
+ * per frame in flight. Each context has its own stream, ray queues and outputs, so frame k+1's trace runs while frame
+ * k's long-ray tail still occupies a few SIMDs (the frames of a renderer are independent of each other). Uploads and updates go through the owner (a shared context returns
+ * VHX_E_STATE for them) and need every context of the tree idle (vhx_sync). The tree lives until its last context is
+ * destroyed, in any order. */
+int vhx_create_shared(const vhx_ctx *owner, vhx_ctx **out);
 void vhx_destroy(vhx_ctx *ctx);
 const char *vhx_last_error(const vhx_ctx *ctx);
 /* Use an external HIP stream (hipStream_t passed as void*; NULL = the context's own stream). */
@@ -232,6 +238,11 @@ int vhx_mgpu_render(vhx_mgpu *m, const vhx_camera *cam, uint32_t *fb_rgba, float
 /* Waits for every frame submitted on this rank (trace, gather and untile); optionally returns the device time of the
  * last frame's trace on this rank in milliseconds. */
 int vhx_mgpu_sync(vhx_mgpu *m, float *last_trace_ms);
+/* Frames in flight on this rank (1..VHX_MGPU_MAX_INFLIGHT, default 1): frame k is traced by the k % F-th of F contexts
+ * sharing the tree (vhx_create_shared), each on its own stream, so frame k+1's trace overlaps frame k's long-ray tail;
+ * gathers stay in frame order on the communication stream. Waits for the frames in flight before it changes them. */
+#define VHX_MGPU_MAX_INFLIGHT 4
+int vhx_mgpu_set_frames_in_flight(vhx_mgpu *m, uint32_t frames);
 /* nranks, rank, and the rays this rank traces for a width x height frame (any pointer may be NULL). */
 int vhx_mgpu_info(const vhx_mgpu *m, uint32_t width, uint32_t height, int *nranks, int *rank, uint64_t *rays);
 void vhx_mgpu_destroy(vhx_mgpu *m);

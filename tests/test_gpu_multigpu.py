@@ -55,18 +55,19 @@ def test_config4_eight_rank_tile_sets_vs_oracle(gpu, config4):
     assert (ref["rgba"] != 0xFF808080).mean() > 0.1  # a frame with geometry, not the background
 
 
-@pytest.mark.parametrize("overlap", [True, False])
-def test_mgpu_one_rank_rccl_frame_vs_oracle(config4, overlap):
+@pytest.mark.parametrize("overlap,inflight", [(True, 1), (False, 1), (True, 3)])
+def test_mgpu_one_rank_rccl_frame_vs_oracle(config4, overlap, inflight):
     import torch
     flat, cam, ref = config4
     rt = vhx.Raytracer(0)
     try:
         m = M.MgpuRenderer(rt, M.mgpu_unique_id(), 1, 0, tile_size=T4, overlap=overlap)
+        m.set_frames_in_flight(inflight)
         m.broadcast_tree(flat)
         assert m.rays(W4, H4) == W4 * H4
         fbs = [(torch.zeros(W4 * H4, dtype=torch.int32, device="cuda"),
-                torch.zeros(W4 * H4, dtype=torch.float32, device="cuda")) for _ in range(3)]
-        for rgba, depth in fbs:  # three frames in flight through the two alternating tile buffers
+                torch.zeros(W4 * H4, dtype=torch.float32, device="cuda")) for _ in range(4)]
+        for rgba, depth in fbs:  # frames in flight through the alternating tile buffers (and contexts)
             m.render(cam, rgba, depth)
         m.sync()
         for k, (rgba, depth) in enumerate(fbs):
@@ -95,3 +96,37 @@ def test_mgpu_argument_errors(gpu):
         m.close()
     finally:
         rt.close()
+
+
+def test_shared_contexts_frames_in_flight(oracle):
+    """vhx_create_shared: contexts tracing one uploaded tree on their own streams, frames in flight, each frame equal to
+    the oracle's; uploads and updates through a shared context are refused; the tree outlives its owner."""
+    import torch
+    flat = vhx.FlatTree.build_scene(N.VHX_SCENE_LATTICE_CUBE, 256, 4)
+    W, H = 320, 200
+    cams = [vhx.glass_camera(256, W, H, angle=40.0 + 0.05 * k, target=(128.0, 128.0, 128.0)) for k in range(6)]
+    refs = [oracle.trace_primary(flat, c, 0, 0, W, H, fields=("rgba", "depth", "value")) for c in cams]
+    owner = vhx.Raytracer(0)
+    owner.upload(flat)
+    ctxs = [owner] + [owner.shared() for _ in range(2)]
+    streams = [torch.cuda.Stream() for _ in ctxs]
+    for r, s in zip(ctxs, streams):
+        r.set_stream(s.cuda_stream)
+    outs = [{"rgba": torch.zeros(W * H, dtype=torch.int32, device="cuda"),
+             "depth": torch.zeros(W * H, dtype=torch.float32, device="cuda"),
+             "value": torch.zeros(W * H, dtype=torch.int32, device="cuda")} for _ in cams]
+    for k, (c, o) in enumerate(zip(cams, outs)):  # six frames, three in flight
+        ctxs[k % 3].trace_primary(c, out=o)
+    torch.cuda.synchronize()
+    for k, (o, ref) in enumerate(zip(outs, refs)):
+        for f in ("rgba", "depth", "value"):
+            assert np.array_equal(o[f].cpu().numpy().view(np.uint32), ref[f].view(np.uint32)), (k, f)
+    with pytest.raises(N.VhxError):
+        ctxs[1].update_range(N.VHX_BUF_VOXELS, 0, flat.voxels[:4])
+    with pytest.raises(N.VhxError):
+        N.check(N.lib().vhx_upload_tree(ctxs[2]._h, __import__("ctypes").byref(flat.desc)), ctxs[2]._h)
+    owner.close()  # the shared contexts keep the tree alive
+    got = ctxs[2].trace_primary(cams[0], fields=("rgba",))
+    assert np.array_equal(got["rgba"], refs[0]["rgba"])
+    for r in ctxs[1:]:
+        r.close()

@@ -74,6 +74,7 @@ SIGNATURES = [
     ("vhx_abi_version", c_u32, []),
     ("vhx_device_count", c_int, [P(c_int)]),
     ("vhx_create", c_int, [c_int, P(c_void_p)]),
+    ("vhx_create_shared", c_int, [c_void_p, P(c_void_p)]),
     ("vhx_destroy", None, [c_void_p]),
     ("vhx_last_error", ctypes.c_char_p, [c_void_p]),
     ("vhx_set_stream", c_int, [c_void_p, c_void_p]),
@@ -94,6 +95,7 @@ SIGNATURES = [
     ("vhx_mgpu_create_from_comm", c_int, [c_void_p, c_void_p, c_u32, P(c_void_p)]),
     ("vhx_mgpu_broadcast_tree", c_int, [c_void_p, P(TreeDesc)]),
     ("vhx_mgpu_set_overlap", c_int, [c_void_p, c_int]),
+    ("vhx_mgpu_set_frames_in_flight", c_int, [c_void_p, c_u32]),
     ("vhx_mgpu_render", c_int, [c_void_p, P(Camera), c_void_p, c_void_p]),
     ("vhx_mgpu_sync", c_int, [c_void_p, P(c_f32)]),
     ("vhx_mgpu_info", c_int, [c_void_p, c_u32, c_u32, P(c_int), P(c_int), P(c_u64)]),

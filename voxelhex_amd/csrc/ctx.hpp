@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -14,6 +15,20 @@ struct DevBuf {
     uint64_t bytes = 0;
 };
 
+// The device copy of a tree and its derived layout. Held by every context that traces it (vhx_create_shared gives
+// further contexts — one per frame in flight — the same store), freed with the last of them.
+struct TreeStore {
+    int device = 0;
+    bool uploaded = false;
+    vhx_tree_desc desc{};  // counts of the uploaded tree (pointers unused)
+    DevBuf raw[7];         // VHX_BUF_* raw copies
+    DevBuf hdr, brick_occ;
+    DevBuf child_rec;      // brick_dim <= 4: DevTree::child_rec, rebuilt before a trace when stale
+    bool child_rec_stale = false;
+    uint32_t occ_words = 1;
+    ~TreeStore();
+};
+
 struct vhx_ctx {
     int device = 0;
     hipStream_t own_stream = nullptr;
@@ -21,12 +36,9 @@ struct vhx_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
     std::string err;
-    bool uploaded = false;
-    vhx_tree_desc desc{};  // counts of the uploaded tree (pointers unused)
-    DevBuf raw[7];         // VHX_BUF_* raw copies
-    DevBuf hdr, brick_occ, scratch, rays;
-    DevBuf child_rec;         // brick_dim <= 4: DevTree::child_rec, rebuilt before a trace when stale
-    bool child_rec_stale = false;
+    std::shared_ptr<TreeStore> tree;  // shared by the contexts of one tree
+    bool shared = false;              // made by vhx_create_shared: traces only (uploads and updates go to the owner)
+    DevBuf scratch, rays;
     DevBuf queue[2];  // multi-pass ray queues (ping-pong), output indices of abandoned rays in increasing order
     DevBuf qctl;      // QCTL_WORDS: [0..7] queue lengths after pass p (7: shadow hit list), [16 + 16p ..] counters
     DevBuf tmp;       // chunk-local lists of abandoned rays (a block's or a queue chunk's, in lane order)
@@ -37,7 +49,6 @@ struct vhx_ctx {
     std::vector<uint8_t> qargs_host[2];  // the QueueArgs last written to each slot (skips the upload when unchanged)
     void *qargs_host_ptr[2] = {nullptr, nullptr};  // qargs.ptr they were written to
     DevBuf state;     // saved traversal state per output index (64 B) of rays abandoned at a budget
-    uint32_t occ_words = 1;
     // step budgets of the passes before the final (unbounded) one; VHX_BUDGETS="64" / "32,256" style override
     uint32_t budgets[3] = {64u, 0u, 0u};
     uint32_t npass = 2;         // passes including the final one (1 = single pass)

@@ -626,19 +626,27 @@ static bool dispatch_bd(uint32_t bd, F &&f) {
 }
 static DevTree dev_tree(const vhx_ctx *c) {
     DevTree t;
-    t.hdr = (const uint4 *)c->hdr.ptr;
-    t.children = (const uint32_t *)c->raw[VHX_BUF_NODE_CHILDREN].ptr;
-    t.voxels = (const uint32_t *)c->raw[VHX_BUF_VOXELS].ptr;
-    t.brick_occ = (const uint64_t *)c->brick_occ.ptr;
-    t.child_rec = (const uint4 *)c->child_rec.ptr;
-    t.solid = (const uint32_t *)c->raw[VHX_BUF_SOLID_VALUES].ptr;
-    t.color = (const uint32_t *)c->raw[VHX_BUF_COLOR_PALETTE].ptr;
-    t.color_count = c->desc.color_count;
-    t.node_count = c->desc.node_count;
-    t.size = c->desc.boxtree_size;
-    t.bd = c->desc.brick_dim;
-    t.occ_words = c->occ_words;
+    t.hdr = (const uint4 *)c->tree->hdr.ptr;
+    t.children = (const uint32_t *)c->tree->raw[VHX_BUF_NODE_CHILDREN].ptr;
+    t.voxels = (const uint32_t *)c->tree->raw[VHX_BUF_VOXELS].ptr;
+    t.brick_occ = (const uint64_t *)c->tree->brick_occ.ptr;
+    t.child_rec = (const uint4 *)c->tree->child_rec.ptr;
+    t.solid = (const uint32_t *)c->tree->raw[VHX_BUF_SOLID_VALUES].ptr;
+    t.color = (const uint32_t *)c->tree->raw[VHX_BUF_COLOR_PALETTE].ptr;
+    t.color_count = c->tree->desc.color_count;
+    t.node_count = c->tree->desc.node_count;
+    t.size = c->tree->desc.boxtree_size;
+    t.bd = c->tree->desc.brick_dim;
+    t.occ_words = c->tree->occ_words;
     return t;
+}
+
+TreeStore::~TreeStore() {
+    (void)hipSetDevice(device);
+    for (auto &b : raw)
+        if (b.ptr) (void)hipFree(b.ptr);
+    for (DevBuf *b : {&hdr, &brick_occ, &child_rec})
+        if (b->ptr) (void)hipFree(b->ptr);
 }
 
 int vhx::ensure(vhx_ctx *c, DevBuf &b, uint64_t bytes) {
@@ -674,38 +682,38 @@ uint64_t vhx::elem_count(const vhx_tree_desc &d, int id) {
 
 static int rebuild_hdr(vhx_ctx *c, uint32_t n0, uint32_t n) {
     if (n == 0) return VHX_OK;
-    k_pack_hdr<<<(n + 255) / 256, 256, 0, c->stream>>>((const uint32_t *)c->raw[VHX_BUF_NODE_TYPE].ptr,
-                                                       (const uint64_t *)c->raw[VHX_BUF_NODE_OCBITS].ptr, n0, n,
-                                                       (uint4 *)c->hdr.ptr);
+    k_pack_hdr<<<(n + 255) / 256, 256, 0, c->stream>>>((const uint32_t *)c->tree->raw[VHX_BUF_NODE_TYPE].ptr,
+                                                       (const uint64_t *)c->tree->raw[VHX_BUF_NODE_OCBITS].ptr, n0, n,
+                                                       (uint4 *)c->tree->hdr.ptr);
     VHX_HIP(c, hipGetLastError());
     return VHX_OK;
 }
 
 static bool has_child_rec(const vhx_ctx *c) {
-    const uint32_t bd = c->desc.brick_dim;
+    const uint32_t bd = c->tree->desc.brick_dim;
     return bd * bd * bd <= 64;
 }
 
 // DevTree::child_rec depends on node types, children and brick occupancy: updates mark it stale and the next trace
 // rebuilds it whole (one pass over the child entries, ~n_nodes * 64 * 24 bytes)
 static int refresh_child_rec(vhx_ctx *c) {
-    if (!has_child_rec(c) || !c->child_rec_stale) return VHX_OK;
-    const uint64_t n = (uint64_t)c->desc.node_count * 64;
+    if (!has_child_rec(c) || !c->tree->child_rec_stale) return VHX_OK;
+    const uint64_t n = (uint64_t)c->tree->desc.node_count * 64;
     k_child_rec<<<(unsigned)((n + 255) / 256), 256, 0, c->stream>>>(
-        (const uint32_t *)c->raw[VHX_BUF_NODE_TYPE].ptr, (const uint32_t *)c->raw[VHX_BUF_NODE_CHILDREN].ptr,
-        (const uint64_t *)c->brick_occ.ptr, c->desc.brick_count, n, (uint4 *)c->child_rec.ptr);
+        (const uint32_t *)c->tree->raw[VHX_BUF_NODE_TYPE].ptr, (const uint32_t *)c->tree->raw[VHX_BUF_NODE_CHILDREN].ptr,
+        (const uint64_t *)c->tree->brick_occ.ptr, c->tree->desc.brick_count, n, (uint4 *)c->tree->child_rec.ptr);
     VHX_HIP(c, hipGetLastError());
-    c->child_rec_stale = false;
+    c->tree->child_rec_stale = false;
     return VHX_OK;
 }
 
 static int rebuild_occ(vhx_ctx *c, uint32_t brick0, uint32_t nbricks) {
     if (nbricks == 0) return VHX_OK;
-    const uint32_t bd = c->desc.brick_dim;
+    const uint32_t bd = c->tree->desc.brick_dim;
     const uint32_t n3 = bd * bd * bd;
-    const uint32_t *vox = (const uint32_t *)c->raw[VHX_BUF_VOXELS].ptr;
-    const uint32_t *col = (const uint32_t *)c->raw[VHX_BUF_COLOR_PALETTE].ptr;
-    const uint32_t *dat = (const uint32_t *)c->raw[VHX_BUF_DATA_PALETTE].ptr;
+    const uint32_t *vox = (const uint32_t *)c->tree->raw[VHX_BUF_VOXELS].ptr;
+    const uint32_t *col = (const uint32_t *)c->tree->raw[VHX_BUF_COLOR_PALETTE].ptr;
+    const uint32_t *dat = (const uint32_t *)c->tree->raw[VHX_BUF_DATA_PALETTE].ptr;
     if (n3 >= 64) {
         const uint64_t cell0 = (uint64_t)brick0 * n3, ncells = (uint64_t)nbricks * n3;
         // grid-stride chunks keep gridDim.x within range for multi-GB voxel buffers
@@ -713,13 +721,13 @@ static int rebuild_occ(vhx_ctx *c, uint32_t brick0, uint32_t nbricks) {
         for (uint64_t s = 0; s < ncells; s += chunk) {
             const uint64_t n = std::min(chunk, ncells - s);
             k_brick_occ_ballot<<<(unsigned)((n + 255) / 256), 256, 0, c->stream>>>(
-                vox, n, cell0 + s, col, c->desc.color_count, dat, c->desc.data_count, (uint64_t *)c->brick_occ.ptr);
+                vox, n, cell0 + s, col, c->tree->desc.color_count, dat, c->tree->desc.data_count, (uint64_t *)c->tree->brick_occ.ptr);
             VHX_HIP(c, hipGetLastError());
         }
     } else {
         k_brick_occ_small<<<(nbricks + 255) / 256, 256, 0, c->stream>>>(vox, nbricks, brick0, n3, col,
-                                                                         c->desc.color_count, dat, c->desc.data_count,
-                                                                         (uint64_t *)c->brick_occ.ptr);
+                                                                         c->tree->desc.color_count, dat, c->tree->desc.data_count,
+                                                                         (uint64_t *)c->tree->brick_occ.ptr);
         VHX_HIP(c, hipGetLastError());
     }
     return VHX_OK;
@@ -925,6 +933,8 @@ int vhx_create(int hip_device, vhx_ctx **out) {
     if (hip_device < 0 || hip_device >= n) return VHX_E_INVALID_ARG;
     vhx_ctx *c = new vhx_ctx();
     c->device = hip_device;
+    c->tree = std::make_shared<TreeStore>();
+    c->tree->device = hip_device;
     auto bail = [&](const char *what, hipError_t e) {
         fprintf(stderr, "vhx_create: %s: %s\n", what, hipGetErrorString(e));
         delete c;
@@ -989,14 +999,37 @@ int vhx_create(int hip_device, vhx_ctx **out) {
     return VHX_OK;
 }
 
+int vhx_create_shared(const vhx_ctx *owner, vhx_ctx **out) {
+    if (!owner || !out) return VHX_E_INVALID_ARG;
+    *out = nullptr;
+    vhx_ctx *c = nullptr;
+    int rc = vhx_create(owner->device, &c);
+    if (rc) return rc;
+    c->tree = owner->tree;  // the same device tree (reference-counted)
+    c->shared = true;
+    // the owner's scheduling settings
+    std::memcpy(c->budgets, owner->budgets, sizeof(c->budgets));
+    std::memcpy(c->rpw, owner->rpw, sizeof(c->rpw));
+    c->npass = owner->npass;
+    c->tw = owner->tw;
+    c->resume = owner->resume;
+    c->xcd_group = owner->xcd_group;
+    c->qblock = owner->qblock;
+    c->queue_blocks = owner->queue_blocks;
+    c->queue_waves = owner->queue_waves;
+    c->queue_waves0 = owner->queue_waves0;
+    c->qxcd = owner->qxcd;
+    *out = c;
+    return VHX_OK;
+}
+
 void vhx_destroy(vhx_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    for (auto &b : c->raw)
-        if (b.ptr) (void)hipFree(b.ptr);
-    for (DevBuf *b : {&c->hdr, &c->brick_occ, &c->child_rec, &c->scratch, &c->rays, &c->queue[0], &c->queue[1], &c->qctl,
-                      &c->tmp, &c->counts, &c->offsets, &c->flags, &c->qargs, &c->state})
+    c->tree.reset();  // frees the device tree with its last context
+    for (DevBuf *b : {&c->scratch, &c->rays, &c->queue[0], &c->queue[1], &c->qctl, &c->tmp, &c->counts, &c->offsets,
+                      &c->flags, &c->qargs, &c->state})
         if (b->ptr) (void)hipFree(b->ptr);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -1055,37 +1088,37 @@ int vhx::alloc_tree(vhx_ctx *c, const vhx_tree_desc *t) {
         (t->boxtree_size & (t->boxtree_size - 1)) != 0 || t->boxtree_size > (1u << 24))
         return fail(c, VHX_E_INVALID_ARG, "vhx_upload_tree: invalid sizes");
     VHX_HIP(c, hipSetDevice(c->device));
-    c->uploaded = false;
+    c->tree->uploaded = false;
     for (int id = 0; id < 7; ++id) {
-        int rc = ensure(c, c->raw[id], elem_count(*t, id) * elem_size(id));
+        int rc = ensure(c, c->tree->raw[id], elem_count(*t, id) * elem_size(id));
         if (rc) return rc;
     }
-    c->desc = *t;
-    for (const void **q : {(const void **)&c->desc.node_type, (const void **)&c->desc.node_ocbits,
-                           (const void **)&c->desc.node_children, (const void **)&c->desc.voxels,
-                           (const void **)&c->desc.solid_values, (const void **)&c->desc.color_palette,
-                           (const void **)&c->desc.data_palette})
+    c->tree->desc = *t;
+    for (const void **q : {(const void **)&c->tree->desc.node_type, (const void **)&c->tree->desc.node_ocbits,
+                           (const void **)&c->tree->desc.node_children, (const void **)&c->tree->desc.voxels,
+                           (const void **)&c->tree->desc.solid_values, (const void **)&c->tree->desc.color_palette,
+                           (const void **)&c->tree->desc.data_palette})
         *q = nullptr;  // only the counts are kept
     return VHX_OK;
 }
 
 int vhx::finish_upload(vhx_ctx *c) {
-    const vhx_tree_desc *t = &c->desc;
+    const vhx_tree_desc *t = &c->tree->desc;
     const uint64_t bd = t->brick_dim, n3 = bd * bd * bd;
-    c->occ_words = n3 >= 64 ? (uint32_t)(n3 / 64) : 1u;
-    int rc = ensure(c, c->hdr, (uint64_t)t->node_count * 16);
+    c->tree->occ_words = n3 >= 64 ? (uint32_t)(n3 / 64) : 1u;
+    int rc = ensure(c, c->tree->hdr, (uint64_t)t->node_count * 16);
     if (rc) return rc;
-    rc = ensure(c, c->brick_occ, (uint64_t)t->brick_count * c->occ_words * 8);
+    rc = ensure(c, c->tree->brick_occ, (uint64_t)t->brick_count * c->tree->occ_words * 8);
     if (rc) return rc;
     if ((rc = rebuild_hdr(c, 0, t->node_count))) return rc;
     if ((rc = rebuild_occ(c, 0, t->brick_count))) return rc;
     if (has_child_rec(c)) {
-        if ((rc = ensure(c, c->child_rec, (uint64_t)t->node_count * 64 * 16))) return rc;
-        c->child_rec_stale = true;
+        if ((rc = ensure(c, c->tree->child_rec, (uint64_t)t->node_count * 64 * 16))) return rc;
+        c->tree->child_rec_stale = true;
         if ((rc = refresh_child_rec(c))) return rc;
     }
     VHX_HIP(c, hipStreamSynchronize(c->stream));
-    c->uploaded = true;
+    c->tree->uploaded = true;
     return VHX_OK;
 }
 
@@ -1093,6 +1126,7 @@ extern "C" {
 
 int vhx_upload_tree(vhx_ctx *c, const vhx_tree_desc *t) {
     if (!c || !t) return VHX_E_INVALID_ARG;
+    if (c->shared) return fail(c, VHX_E_STATE, "vhx_upload_tree on a shared context: upload through the owner");
     const void *src[7] = {t->node_type, t->node_ocbits, t->node_children, t->voxels,
                           t->solid_values, t->color_palette, t->data_palette};
     for (int id = 0; id < 7; ++id)
@@ -1102,42 +1136,43 @@ int vhx_upload_tree(vhx_ctx *c, const vhx_tree_desc *t) {
     if (rc) return rc;
     for (int id = 0; id < 7; ++id) {
         const uint64_t bytes = elem_count(*t, id) * elem_size(id);
-        if (bytes) VHX_HIP(c, hipMemcpyAsync(c->raw[id].ptr, src[id], bytes, hipMemcpyHostToDevice, c->stream));
+        if (bytes) VHX_HIP(c, hipMemcpyAsync(c->tree->raw[id].ptr, src[id], bytes, hipMemcpyHostToDevice, c->stream));
     }
     return finish_upload(c);
 }
 
 int vhx_update_range(vhx_ctx *c, int id, uint64_t off, uint64_t count, const void *src) {
     if (!c || id < 0 || id > 6 || (!src && count)) return VHX_E_INVALID_ARG;
-    if (!c->uploaded) return fail(c, VHX_E_STATE, "vhx_update_range before vhx_upload_tree");
-    const uint64_t cap = elem_count(c->desc, id);
+    if (c->shared) return fail(c, VHX_E_STATE, "vhx_update_range on a shared context: update through the owner");
+    if (!c->tree->uploaded) return fail(c, VHX_E_STATE, "vhx_update_range before vhx_upload_tree");
+    const uint64_t cap = elem_count(c->tree->desc, id);
     if (off + count > cap) return fail(c, VHX_E_CAPACITY, "vhx_update_range: range beyond the uploaded buffer");
     if (count == 0) return VHX_OK;
     VHX_HIP(c, hipSetDevice(c->device));
     const uint64_t es = elem_size(id);
-    VHX_HIP(c, hipMemcpyAsync((char *)c->raw[id].ptr + off * es, src, count * es, hipMemcpyHostToDevice, c->stream));
+    VHX_HIP(c, hipMemcpyAsync((char *)c->tree->raw[id].ptr + off * es, src, count * es, hipMemcpyHostToDevice, c->stream));
     int rc = VHX_OK;
-    const uint64_t n3 = (uint64_t)c->desc.brick_dim * c->desc.brick_dim * c->desc.brick_dim;
+    const uint64_t n3 = (uint64_t)c->tree->desc.brick_dim * c->tree->desc.brick_dim * c->tree->desc.brick_dim;
     if (id == VHX_BUF_NODE_TYPE || id == VHX_BUF_NODE_OCBITS) rc = rebuild_hdr(c, (uint32_t)off, (uint32_t)count);
     else if (id == VHX_BUF_VOXELS) {
         const uint64_t b0 = off / n3, b1 = (off + count + n3 - 1) / n3;
         rc = rebuild_occ(c, (uint32_t)b0, (uint32_t)(b1 - b0));
     } else if (id == VHX_BUF_COLOR_PALETTE || id == VHX_BUF_DATA_PALETTE)
-        rc = rebuild_occ(c, 0, c->desc.brick_count);
+        rc = rebuild_occ(c, 0, c->tree->desc.brick_count);
     if (rc) return rc;
-    if (id != VHX_BUF_NODE_OCBITS && id != VHX_BUF_SOLID_VALUES) c->child_rec_stale = true;
+    if (id != VHX_BUF_NODE_OCBITS && id != VHX_BUF_SOLID_VALUES) c->tree->child_rec_stale = true;
     VHX_HIP(c, hipStreamSynchronize(c->stream));
     return VHX_OK;
 }
 
 int vhx_read_derived(vhx_ctx *c, int which, uint64_t off, uint64_t count, void *dst) {
     if (!c || (!dst && count) || which < 0 || which > 1) return VHX_E_INVALID_ARG;
-    if (!c->uploaded) return fail(c, VHX_E_STATE, "vhx_read_derived before vhx_upload_tree");
+    if (!c->tree->uploaded) return fail(c, VHX_E_STATE, "vhx_read_derived before vhx_upload_tree");
     const uint64_t es = which == VHX_DERIVED_NODE_HDR ? 16 : 8;
-    const uint64_t cap = which == VHX_DERIVED_NODE_HDR ? c->desc.node_count
-                                                       : (uint64_t)c->desc.brick_count * c->occ_words;
+    const uint64_t cap = which == VHX_DERIVED_NODE_HDR ? c->tree->desc.node_count
+                                                       : (uint64_t)c->tree->desc.brick_count * c->tree->occ_words;
     if (off + count > cap) return fail(c, VHX_E_CAPACITY, "vhx_read_derived: range beyond the buffer");
-    const DevBuf &b = which == VHX_DERIVED_NODE_HDR ? c->hdr : c->brick_occ;
+    const DevBuf &b = which == VHX_DERIVED_NODE_HDR ? c->tree->hdr : c->tree->brick_occ;
     VHX_HIP(c, hipSetDevice(c->device));
     VHX_HIP(c, hipMemcpyAsync(dst, (const char *)b.ptr + off * es, count * es, hipMemcpyDeviceToHost, c->stream));
     VHX_HIP(c, hipStreamSynchronize(c->stream));
@@ -1146,8 +1181,8 @@ int vhx_read_derived(vhx_ctx *c, int which, uint64_t off, uint64_t count, void *
 
 int vhx_tree_device_bytes(const vhx_ctx *c, uint64_t *bytes) {
     if (!c || !bytes) return VHX_E_INVALID_ARG;
-    uint64_t b = c->hdr.bytes + c->brick_occ.bytes + c->child_rec.bytes;
-    for (auto &r : c->raw) b += r.bytes;
+    uint64_t b = c->tree->hdr.bytes + c->tree->brick_occ.bytes + c->tree->child_rec.bytes;
+    for (auto &r : c->tree->raw) b += r.bytes;
     *bytes = b;
     return VHX_OK;
 }
@@ -1178,7 +1213,7 @@ static CamD cam_of(const vhx_camera *cam) {
 int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t tile_start, uint32_t tile_stride,
                       uint32_t layout, const vhx_hits *out, int on_device) {
     if (!c || !cam || !out) return VHX_E_INVALID_ARG;
-    if (!c->uploaded) return fail(c, VHX_E_STATE, "vhx_trace_primary before vhx_upload_tree");
+    if (!c->tree->uploaded) return fail(c, VHX_E_STATE, "vhx_trace_primary before vhx_upload_tree");
     if (cam->width == 0 || cam->height == 0 || cam->ray_model > VHX_RAY_GLASS || layout > VHX_LAYOUT_TILES)
         return fail(c, VHX_E_INVALID_ARG, "vhx_trace_primary: bad camera or layout");
     if (T == 0) {
@@ -1235,7 +1270,7 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
             qrc = launch_queue_passes<false, BD>(c, t, cd, src, ho.dev, 1, npass, nout, nblocks, true);
         }
     };
-    if (!dispatch_bd(c->desc.brick_dim, launch)) return fail(c, VHX_E_INVALID_ARG, "unsupported brick_dim");
+    if (!dispatch_bd(c->tree->desc.brick_dim, launch)) return fail(c, VHX_E_INVALID_ARG, "unsupported brick_dim");
     if (qrc) return qrc;
     VHX_HIP(c, hipGetLastError());
     VHX_HIP(c, hipEventRecord(c->ev1, c->stream));
@@ -1245,7 +1280,7 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
 
 int vhx_trace_rays(vhx_ctx *c, const float *rays, uint64_t n, const vhx_hits *out, int on_device) {
     if (!c || !out || (!rays && n)) return VHX_E_INVALID_ARG;
-    if (!c->uploaded) return fail(c, VHX_E_STATE, "vhx_trace_rays before vhx_upload_tree");
+    if (!c->tree->uploaded) return fail(c, VHX_E_STATE, "vhx_trace_rays before vhx_upload_tree");
     if (n == 0) return VHX_OK;
     if ((n + 255) / 256 > 0x7FFFFFFFull) return fail(c, VHX_E_INVALID_ARG, "too many rays");
     VHX_HIP(c, hipSetDevice(c->device));
@@ -1288,7 +1323,7 @@ int vhx_trace_rays(vhx_ctx *c, const float *rays, uint64_t n, const vhx_hits *ou
             qrc = launch_queue_passes<false, BD>(c, t, cd, src, ho.dev, 1, npass, n, nb64);
         }
     };
-    if (!dispatch_bd(c->desc.brick_dim, launch)) return fail(c, VHX_E_INVALID_ARG, "unsupported brick_dim");
+    if (!dispatch_bd(c->tree->desc.brick_dim, launch)) return fail(c, VHX_E_INVALID_ARG, "unsupported brick_dim");
     if (qrc) return qrc;
     VHX_HIP(c, hipGetLastError());
     VHX_HIP(c, hipEventRecord(c->ev1, c->stream));
@@ -1299,7 +1334,7 @@ int vhx_trace_rays(vhx_ctx *c, const float *rays, uint64_t n, const vhx_hits *ou
 int vhx_trace_shadows(vhx_ctx *c, const float light[3], uint64_t n, const uint32_t *value, const float *impact,
                       const float *normal, uint32_t *shadowed, uint32_t *rgba, uint32_t *bytes) {
     if (!c || !light || (n && (!value || !impact || !normal || !shadowed))) return VHX_E_INVALID_ARG;
-    if (!c->uploaded) return fail(c, VHX_E_STATE, "vhx_trace_shadows before vhx_upload_tree");
+    if (!c->tree->uploaded) return fail(c, VHX_E_STATE, "vhx_trace_shadows before vhx_upload_tree");
     if (n == 0) return VHX_OK;
     if (n >= 0x7FFFFFFFull) return fail(c, VHX_E_INVALID_ARG, "too many rays");
     // the outputs are written while the hit records are still being read (the flags are cleared by the compaction
@@ -1362,7 +1397,7 @@ int vhx_trace_shadows(vhx_ctx *c, const float light[3], uint64_t n, const uint32
         else
             qrc = launch_queue_passes<false, BD>(c, t, cd, src, so, 0, npass, n, nb64);
     };
-    if (!dispatch_bd(c->desc.brick_dim, launch)) return fail(c, VHX_E_INVALID_ARG, "unsupported brick_dim");
+    if (!dispatch_bd(c->tree->desc.brick_dim, launch)) return fail(c, VHX_E_INVALID_ARG, "unsupported brick_dim");
     if (qrc) return qrc;
     VHX_HIP(c, hipGetLastError());
     VHX_HIP(c, hipEventRecord(c->ev1, c->stream));

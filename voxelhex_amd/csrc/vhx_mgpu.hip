@@ -88,9 +88,14 @@ struct vhx_mgpu {
     uint32_t T = 64;
     bool overlap = true;
     hipStream_t cstream = nullptr;     // gather + untile
-    hipEvent_t ready[2] = {}, free_[2] = {};  // slot traced (context stream) / slot gathered (comm stream)
-    bool used[2] = {false, false};
-    DevBuf send[2], gathered[2];
+    // frames in flight: frame k is traced by context k % F (ctx, then the shared contexts extra[0..F-2], each on its
+    // own stream) into the tile buffers of slot k % S, S = max(2, F)
+    uint32_t F = 1, S = 2;
+    vhx_ctx *extra[VHX_MGPU_MAX_INFLIGHT - 1] = {};
+    hipEvent_t ready[VHX_MGPU_MAX_INFLIGHT] = {}, free_[VHX_MGPU_MAX_INFLIGHT] = {};  // slot traced / slot gathered
+    bool used[VHX_MGPU_MAX_INFLIGHT] = {};
+    DevBuf send[VHX_MGPU_MAX_INFLIGHT], gathered[VHX_MGPU_MAX_INFLIGHT];
+    vhx_ctx *last = nullptr;  // the context of the last frame submitted
     DevBuf hdr;  // tree counts during the broadcast
     uint64_t k = 0;  // frames submitted
 };
@@ -108,7 +113,7 @@ static int mgpu_init(vhx_mgpu *m) {
     vhx_ctx *c = m->ctx;
     VHX_HIP(c, hipSetDevice(c->device));
     VHX_HIP(c, hipStreamCreateWithFlags(&m->cstream, hipStreamNonBlocking));
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < VHX_MGPU_MAX_INFLIGHT; ++s) {
         VHX_HIP(c, hipEventCreateWithFlags(&m->ready[s], hipEventDisableTiming));
         VHX_HIP(c, hipEventCreateWithFlags(&m->free_[s], hipEventDisableTiming));
     }
@@ -192,10 +197,13 @@ void vhx_mgpu_destroy(vhx_mgpu *m) {
     (void)hipSetDevice(c->device);
     if (m->cstream) (void)hipStreamSynchronize(m->cstream);
     (void)hipStreamSynchronize(c->stream);
+    for (vhx_ctx *x : m->extra) vhx_destroy(x);
     if (m->comm && m->own_comm) rccl().CommDestroy(m->comm);
-    for (DevBuf *b : {&m->send[0], &m->send[1], &m->gathered[0], &m->gathered[1], &m->hdr})
-        if (b->ptr) (void)hipFree(b->ptr);
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < VHX_MGPU_MAX_INFLIGHT; ++s)
+        for (DevBuf *b : {&m->send[s], &m->gathered[s]})
+            if (b->ptr) (void)hipFree(b->ptr);
+    if (m->hdr.ptr) (void)hipFree(m->hdr.ptr);
+    for (int s = 0; s < VHX_MGPU_MAX_INFLIGHT; ++s) {
         if (m->ready[s]) (void)hipEventDestroy(m->ready[s]);
         if (m->free_[s]) (void)hipEventDestroy(m->free_[s]);
     }
@@ -206,6 +214,28 @@ void vhx_mgpu_destroy(vhx_mgpu *m) {
 int vhx_mgpu_set_overlap(vhx_mgpu *m, int on) {
     if (!m) return VHX_E_INVALID_ARG;
     m->overlap = on != 0;
+    return VHX_OK;
+}
+
+int vhx_mgpu_set_frames_in_flight(vhx_mgpu *m, uint32_t frames) {
+    if (!m) return VHX_E_INVALID_ARG;
+    vhx_ctx *c = m->ctx;
+    if (frames < 1 || frames > VHX_MGPU_MAX_INFLIGHT)
+        return fail(c, VHX_E_INVALID_ARG, "vhx_mgpu_set_frames_in_flight: 1..VHX_MGPU_MAX_INFLIGHT");
+    int rc = vhx_mgpu_sync(m, nullptr);  // no frame may be in flight while the slots change
+    if (rc) return rc;
+    for (uint32_t i = 0; i + 1 < VHX_MGPU_MAX_INFLIGHT; ++i) {
+        const bool want = i + 1 < frames;
+        if (want && !m->extra[i] && (rc = vhx_create_shared(c, &m->extra[i]))) return fail(c, rc, "vhx_create_shared");
+        if (!want && m->extra[i]) {
+            vhx_destroy(m->extra[i]);
+            m->extra[i] = nullptr;
+        }
+    }
+    m->F = frames;
+    m->S = frames < 2 ? 2u : frames;
+    m->k = 0;
+    for (bool &u : m->used) u = false;
     return VHX_OK;
 }
 
@@ -233,6 +263,7 @@ int vhx_mgpu_broadcast_tree(vhx_mgpu *m, const vhx_tree_desc *t) {
     if ((m->rank == 0) != (t != nullptr)) return fail(c, VHX_E_INVALID_ARG, "vhx_mgpu_broadcast_tree: rank 0 passes the tree, the others NULL");
     const Rccl &r = rccl();
     VHX_HIP(c, hipSetDevice(c->device));
+    if (c->shared) return fail(c, VHX_E_STATE, "vhx_mgpu_broadcast_tree on a shared context");
     if (m->rank == 0) {
         int rc = vhx_upload_tree(c, t);  // host -> HBM of rank 0, derived layout included
         if (rc) return rc;
@@ -242,7 +273,7 @@ int vhx_mgpu_broadcast_tree(vhx_mgpu *m, const vhx_tree_desc *t) {
     if (rc) return rc;
     uint32_t counts[8] = {0};
     if (m->rank == 0) {
-        const vhx_tree_desc &d = c->desc;
+        const vhx_tree_desc &d = c->tree->desc;
         const uint32_t v[8] = {d.boxtree_size, d.brick_dim, d.node_count, d.brick_count,
                                d.solid_count, d.color_count, d.data_count, 0};
         std::memcpy(counts, v, sizeof(v));
@@ -265,10 +296,10 @@ int vhx_mgpu_broadcast_tree(vhx_mgpu *m, const vhx_tree_desc *t) {
     // the raw buffers, device to device over xGMI, in chunks of at most 1 GiB per call
     VHX_NCCL(m, r.GroupStart());
     for (int id = 0; id < 7; ++id) {
-        const uint64_t bytes = elem_count(c->desc, id) * elem_size(id);
+        const uint64_t bytes = elem_count(c->tree->desc, id) * elem_size(id);
         for (uint64_t off = 0; off < bytes; off += 1ull << 30) {
             const uint64_t n = std::min<uint64_t>(1ull << 30, bytes - off);
-            char *p = (char *)c->raw[id].ptr + off;
+            char *p = (char *)c->tree->raw[id].ptr + off;
             const ncclResult_t e = r.Broadcast(p, p, n, ncclUint8, 0, m->comm, c->stream);
             if (e != ncclSuccess) {
                 r.GroupEnd();
@@ -287,20 +318,21 @@ int vhx_mgpu_render(vhx_mgpu *m, const vhx_camera *cam, uint32_t *fb_rgba, float
     if (!m || !cam) return VHX_E_INVALID_ARG;
     vhx_ctx *c = m->ctx;
     if (m->rank == 0 && !fb_rgba && !fb_depth) return fail(c, VHX_E_INVALID_ARG, "vhx_mgpu_render: rank 0 needs a framebuffer");
-    if (!c->uploaded) return fail(c, VHX_E_STATE, "vhx_mgpu_render before the tree is uploaded");
+    if (!c->tree->uploaded) return fail(c, VHX_E_STATE, "vhx_mgpu_render before the tree is uploaded");
     if (cam->width == 0 || cam->height == 0) return fail(c, VHX_E_INVALID_ARG, "vhx_mgpu_render: empty frame");
     const Rccl &r = rccl();
     VHX_HIP(c, hipSetDevice(c->device));
     uint32_t ntiles, per;
     tiles_of(m, cam->width, cam->height, ntiles, per);
     const uint64_t n_out = (uint64_t)per * m->T * m->T;  // words per plane of one rank
-    const int slot = (int)(m->k & 1u);
-    // a slot's buffers are rewritten only after the gather that read them (stream order on the context stream)
-    if (m->used[slot]) VHX_HIP(c, hipStreamWaitEvent(c->stream, m->free_[slot], 0));
+    const uint32_t slot = (uint32_t)(m->k % m->S);
+    vhx_ctx *tc = m->k % m->F == 0 ? c : m->extra[m->k % m->F - 1];  // the context tracing this frame
+    // a slot's buffers are rewritten only after the gather that read them (stream order on the tracing stream)
+    if (m->used[slot]) VHX_HIP(c, hipStreamWaitEvent(tc->stream, m->free_[slot], 0));
     if (m->send[slot].bytes < n_out * 8 || (m->rank == 0 && m->gathered[slot].bytes < n_out * 8 * m->nranks)) {
         // (re)allocation: no frame may still use the old buffers
-        VHX_HIP(c, hipStreamSynchronize(m->cstream));
-        VHX_HIP(c, hipStreamSynchronize(c->stream));
+        int rc = vhx_mgpu_sync(m, nullptr);
+        if (rc) return rc;
     }
     int rc = ensure(c, m->send[slot], n_out * 8);
     if (!rc && m->rank == 0) rc = ensure(c, m->gathered[slot], n_out * 8 * (uint64_t)m->nranks);
@@ -310,10 +342,11 @@ int vhx_mgpu_render(vhx_mgpu *m, const vhx_camera *cam, uint32_t *fb_rgba, float
     h.rgba = send;
     h.depth = (float *)(send + n_out);
     if ((uint32_t)m->rank < ntiles) {
-        rc = vhx_trace_primary(c, cam, m->T, (uint32_t)m->rank, (uint32_t)m->nranks, VHX_LAYOUT_TILES, &h, 1);
-        if (rc) return rc;
+        rc = vhx_trace_primary(tc, cam, m->T, (uint32_t)m->rank, (uint32_t)m->nranks, VHX_LAYOUT_TILES, &h, 1);
+        if (rc) return tc == c ? rc : fail(c, rc, tc->err.c_str());
     }
-    VHX_HIP(c, hipEventRecord(m->ready[slot], c->stream));
+    m->last = tc;
+    VHX_HIP(c, hipEventRecord(m->ready[slot], tc->stream));
     VHX_HIP(c, hipStreamWaitEvent(m->cstream, m->ready[slot], 0));
     void *recv = m->rank == 0 ? m->gathered[slot].ptr : nullptr;
     VHX_NCCL(m, r.Gather(send, recv, n_out * 2, ncclUint32, 0, m->comm, m->cstream));  // a local copy at N = 1
@@ -324,7 +357,7 @@ int vhx_mgpu_render(vhx_mgpu *m, const vhx_camera *cam, uint32_t *fb_rgba, float
     VHX_HIP(c, hipEventRecord(m->free_[slot], m->cstream));
     m->used[slot] = true;
     ++m->k;
-    if (!m->overlap) VHX_HIP(c, hipStreamWaitEvent(c->stream, m->free_[slot], 0));
+    if (!m->overlap) VHX_HIP(c, hipStreamWaitEvent(tc->stream, m->free_[slot], 0));
     return VHX_OK;
 }
 
@@ -333,7 +366,11 @@ int vhx_mgpu_sync(vhx_mgpu *m, float *ms) {
     vhx_ctx *c = m->ctx;
     VHX_HIP(c, hipSetDevice(c->device));
     VHX_HIP(c, hipStreamSynchronize(m->cstream));
-    return vhx_sync(c, ms);
+    for (vhx_ctx *x : m->extra)
+        if (x) VHX_HIP(c, hipStreamSynchronize(x->stream));
+    int rc = vhx_sync(c, ms);
+    if (!rc && ms && m->last && m->last != c) rc = vhx_sync(m->last, ms);
+    return rc;
 }
 
 }  // extern "C"

@@ -159,6 +159,10 @@ class MgpuRenderer:
         from . import _native as N
         self._check(N.lib().vhx_mgpu_set_overlap(self._h, 1 if on else 0))
 
+    def set_frames_in_flight(self, frames):
+        from . import _native as N
+        self._check(N.lib().vhx_mgpu_set_frames_in_flight(self._h, frames))
+
     def broadcast_tree(self, flat=None):
         """Rank 0 passes the FlatTree, the other ranks None (collective)."""
         import ctypes

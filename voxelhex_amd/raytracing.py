@@ -195,6 +195,16 @@ class Raytracer:
         self.device = device
         self._tree = None
 
+    def shared(self):
+        """vhx_create_shared: another context (its own stream, queues and outputs) tracing this context's tree."""
+        if self._tree is None:
+            raise RuntimeError("upload a tree before sharing it")
+        rt = Raytracer.__new__(Raytracer)
+        h = ctypes.c_void_p()
+        self._check(N.lib().vhx_create_shared(self._h, ctypes.byref(h)))
+        rt._h, rt.device, rt._tree = h, self.device, self._tree
+        return rt
+
     def close(self):
         if getattr(self, "_h", None) and self._h.value:
             N.lib().vhx_destroy(self._h)
