@@ -234,10 +234,12 @@ __device__ __forceinline__ void block_append(bool push, uint32_t idx, uint32_t *
     if (threadIdx.x == 0) counts[blockIdx.x] = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
 }
 
-// Exclusive scan of the chunk counts in one workgroup of 1024 threads; nchunks = ceil(*n_in / per_chunk) when n_in
-// is given (a queue pass: its input length is only known on the device), else nchunks_host. Writes *total.
+// Exclusive scan of the chunk counts in one workgroup of SCAN_THREADS threads; nchunks = ceil(*n_in / per_chunk) when
+// n_in is given (a queue pass: its input length is only known on the device), else nchunks_host. Writes *total.
 // Each wave scans 1024 consecutive counts per segment as 16 coalesced rows of 64 (a wave-wide scan per row), the
-// waves' totals are combined through LDS.
+// waves' totals are combined through LDS. Four waves, not sixteen: with other frames in flight the GPU is full, and a
+// 1024-thread workgroup waited up to 0.25 ms for a CU with room for it (kernel trace of three frames in flight).
+#define SCAN_THREADS 256u
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, uint32_t lane) {
     for (uint32_t d = 1; d < 64; d <<= 1) {
         const uint32_t x = __shfl_up(v, d);
@@ -245,10 +247,12 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, uint32_t lane) {
     }
     return v;
 }
-__global__ void __launch_bounds__(1024) k_scan_counts(const uint32_t *__restrict__ counts, uint32_t nchunks_host,
-                                                      const uint32_t *n_in, uint32_t per_chunk, uint32_t tw,
-                                                      uint32_t *__restrict__ offsets, uint32_t *total) {
-    __shared__ uint32_t s_wave[16];
+__global__ void __launch_bounds__(SCAN_THREADS) k_scan_counts(const uint32_t *__restrict__ counts,
+                                                              uint32_t nchunks_host, const uint32_t *n_in,
+                                                              uint32_t per_chunk, uint32_t tw,
+                                                              uint32_t *__restrict__ offsets, uint32_t *total) {
+    constexpr uint32_t NW = SCAN_THREADS / 64u;
+    __shared__ uint32_t s_wave[NW];
     __shared__ uint32_t s_carry;
     const uint32_t pc = n_in ? pass_rpw(per_chunk, tw, *n_in) : per_chunk;
     const uint32_t nchunks = n_in ? (*n_in + pc - 1) / pc : nchunks_host;
@@ -256,7 +260,7 @@ __global__ void __launch_bounds__(1024) k_scan_counts(const uint32_t *__restrict
     constexpr uint32_t K = 16;  // rows of 64 per wave per segment; loads issued together
     if (t == 0) s_carry = 0;
     __syncthreads();
-    for (uint32_t seg = 0; seg < nchunks; seg += 1024u * K) {
+    for (uint32_t seg = 0; seg < nchunks; seg += SCAN_THREADS * K) {
         const uint32_t b = seg + wave * (64u * K) + lane;
         uint32_t v[K];
 #pragma unroll
@@ -279,7 +283,7 @@ __global__ void __launch_bounds__(1024) k_scan_counts(const uint32_t *__restrict
         __syncthreads();
         if (t == 0) {
             uint32_t sum = s_carry;
-            for (uint32_t w = 0; w < 16u; ++w) sum += s_wave[w];
+            for (uint32_t w = 0; w < NW; ++w) sum += s_wave[w];
             s_carry = sum;
         }
         __syncthreads();
@@ -845,7 +849,7 @@ static int compact_chunks(vhx_ctx *c, uint32_t nchunks_host, const uint32_t *n_i
                           uint32_t stride, uint32_t *out, uint32_t *total, uint64_t max_chunks) {
     const uint32_t *counts = (const uint32_t *)c->counts.ptr;
     uint32_t *offsets = (uint32_t *)c->offsets.ptr;
-    k_scan_counts<<<1, 1024, 0, c->stream>>>(counts, nchunks_host, n_in, per_chunk, c->tw, offsets, total);
+    k_scan_counts<<<1, SCAN_THREADS, 0, c->stream>>>(counts, nchunks_host, n_in, per_chunk, c->tw, offsets, total);
     const uint64_t want = (max_chunks + 3) / 4;
     const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(want, c->queue_blocks));
     k_gather_chunks<<<grid, 256, 0, c->stream>>>((const uint32_t *)c->tmp.ptr, stride, counts, offsets,
@@ -870,7 +874,7 @@ static int launch_queue_passes(vhx_ctx *c, const DevTree &t, const CamD &cam, co
             uint32_t *counts = (uint32_t *)c->counts.ptr, *offsets = (uint32_t *)c->offsets.ptr;
             const uint8_t *flags = (const uint8_t *)c->flags.ptr;
             k_count_flags<false><<<nb, 256, 0, c->stream>>>(flags, nout, counts, ctl + 16);
-            k_scan_counts<<<1, 1024, 0, c->stream>>>(counts, nb, nullptr, 1, c->tw, offsets, ctl);
+            k_scan_counts<<<1, SCAN_THREADS, 0, c->stream>>>(counts, nb, nullptr, 1, c->tw, offsets, ctl);
             k_emit_flags<false><<<nb, 256, 0, c->stream>>>(flags, nout, offsets, (uint32_t *)c->queue[0].ptr);
             VHX_HIP(c, hipGetLastError());
             debug_passes(c, "compacted flags");
@@ -902,8 +906,8 @@ static int launch_queue_passes(vhx_ctx *c, const DevTree &t, const CamD &cam, co
         const PassQ q = pass_q(c, p, npass);
         // a first pass over fresh rays (the shadow path) is throughput-bound like a grid launch: more waves
         const uint32_t qwaves = p == 0 ? c->queue_waves0 : c->queue_waves;
-        k_trace_queue<COUNT, BD><<<(qwaves * 64u + c->qblock - 1) / c->qblock, c->qblock, 0, c->stream>>>(
-            t, qa, in, in_n, ctl + 16u + 16u * p, q);
+        const unsigned qgrid = (qwaves * 64u + c->qblock - 1) / c->qblock;
+        k_trace_queue<COUNT, BD><<<qgrid, c->qblock, 0, c->stream>>>(t, qa, in, in_n, ctl + 16u + 16u * p, q);
         debug_passes(c, "queue pass");
         if (p + 1 < npass)
             rc = compact_chunks(c, 0, in_n, q.rpw, q.rpw, (uint32_t *)c->queue[p & 1u].ptr, ctl + p,
@@ -991,6 +995,7 @@ int vhx_create(int hip_device, vhx_ctx **out) {
     }
     if ((e = hipEventCreate(&c->ev0)) != hipSuccess) return bail("hipEventCreate", e);
     if ((e = hipEventCreate(&c->ev1)) != hipSuccess) return bail("hipEventCreate", e);
+
     uint8_t lut[64 * 27];
     make_step_lut(lut);
     if ((e = hipMemcpyToSymbol(HIP_SYMBOL(vhx::c_step_lut), lut, sizeof(lut))) != hipSuccess)
@@ -1254,6 +1259,7 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
     // while the compaction scans every pixel: they are cleared first (stale flags would queue foreign pixels)
     if (npass > 1 && layout == VHX_LAYOUT_FRAMEBUFFER && (tile_start > 0 || tile_stride > 1))
         VHX_HIP(c, hipMemsetAsync(c->flags.ptr, 0, nout, c->stream));
+
     const bool count = ho.dev.bytes != nullptr;
     int qrc = VHX_OK;
     auto launch = [&](auto bd_tag) {
@@ -1385,7 +1391,7 @@ int vhx_trace_shadows(vhx_ctx *c, const float light[3], uint64_t n, const uint32
         const unsigned nb = (unsigned)((n + 1023) / 1024);
         uint32_t *counts = (uint32_t *)c->counts.ptr, *offsets = (uint32_t *)c->offsets.ptr;
         k_count_flags<true><<<nb, 256, 0, c->stream>>>(value, n, counts, (uint32_t *)c->qctl.ptr + 16, shadowed);
-        k_scan_counts<<<1, 1024, 0, c->stream>>>(counts, nb, nullptr, 1, c->tw, offsets, (uint32_t *)c->qctl.ptr + 7);
+        k_scan_counts<<<1, SCAN_THREADS, 0, c->stream>>>(counts, nb, nullptr, 1, c->tw, offsets, (uint32_t *)c->qctl.ptr + 7);
         k_emit_flags<true><<<nb, 256, 0, c->stream>>>(value, n, offsets, (uint32_t *)c->queue[1].ptr);
         VHX_HIP(c, hipGetLastError());
     }
