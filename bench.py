@@ -60,10 +60,15 @@ def parse():
                    help="config 5: each step = primary frame + one hard-shadow ray per hit toward (S,S,S)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-roofline", action="store_true")
-    p.add_argument("--inflight", type=int, default=3,
+    p.add_argument("--inflight", type=int, default=8,
                    help="frames in flight per GPU: F contexts sharing the tree (vhx_create_shared), each on its own "
                         "stream, frame i traced by context i %% F, so a frame's latency-bound long-ray tail overlaps the "
-                        "next frame's pass 0 (1 = one frame at a time)")
+                        "next frame's pass 0 (1 = one frame at a time); GPU_MAX_HW_QUEUES is raised to F + 4 so that every "
+                        "frame's stream has a hardware queue of its own")
+    p.add_argument("--orbit", type=float, default=0.0,
+                   help="moving camera: frame k (warm-up included) views from angle 40 + k*ORBIT rad on the glass "
+                        "camera's circle (0 = the reference bench's static camera); the roofline bytes are then the "
+                        "mean of the first, middle and last timed views")
     p.add_argument("--no-overlap", action="store_true",
                    help="N>1: gather each frame before tracing the next (default: frame k's gather overlaps k+1)")
     return p.parse_args()
@@ -154,8 +159,25 @@ def cpu_baseline(flat, cam, W, H, threads_all):
     return t_all, t_one, (w1, h1)
 
 
+def hw_queues(frames):
+    """Hardware queues for F frames in flight: HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues per process (4
+    by default) round-robin, and the default stream holds one, so with the default four frames in flight two frames
+    share a queue and run one after the other (bench frame: 0.93 ms per frame at F = 4 against 0.70 with five queues;
+    0.66 at F = 8 with nine or more). Read by the HIP runtime at initialisation: set before torch is imported. The
+    frames' streams, the gather stream (N > 1) and the default stream each get their own queue (at most 32)."""
+    want = min(32, frames + 4)
+    try:
+        cur = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
+    except ValueError:
+        cur = 4
+    if cur < want:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(want)
+    return int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
+
+
 def main():
     args = parse()
+    queues = hw_queues(max(1, args.inflight))
     import torch
     import torch.distributed as dist
 
@@ -185,11 +207,12 @@ def main():
         torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     rt = vhx.Raytracer(local)
-    # one dedicated (non-null) stream shared by libvhx and torch: the kernels and the events that time them are ordered
-    # on it
-    stream = torch.cuda.Stream(dev)
+    # the context's own stream, shared with torch (ExternalStream): the kernels and the events that time them are
+    # ordered on it. Every frame in flight traces on its context's own stream; those streams are created back to back
+    # so that each gets a hardware queue of its own (GPU_MAX_HW_QUEUES = 4; streams share queues round-robin in
+    # creation order, and extra streams created in between made two frames share a queue: 0.91 against 0.70 ms/frame)
+    stream = torch.cuda.ExternalStream(rt.stream(), device=dev)
     torch.cuda.set_stream(stream)
-    rt.set_stream(stream.cuda_stream)
     F = max(1, args.inflight)
     if world > 1 and not use_vhx_mgpu:
         F = 1  # the torch gather pipeline keeps one frame per rank in flight
@@ -230,6 +253,10 @@ def main():
     T = args.tile
     c = args.size / 2.0
     cam = vhx.glass_camera(args.size, W, H, target=(c, c, c))
+    cams = [cam]
+    if args.orbit:
+        cams = [vhx.glass_camera(args.size, W, H, angle=40.0 + k * args.orbit, target=(c, c, c))
+                for k in range(args.warmup + args.steps)]
     light = (float(args.size),) * 3  # ambient_light_position, src/raytracing/bevy/view.rs:81-85
     if world == 1:
         n_out = W * H
@@ -251,10 +278,8 @@ def main():
     if mg is None:
         for _ in range(F - 1):
             r = rt.shared()
-            s_ = torch.cuda.Stream(dev)
-            r.set_stream(s_.cuda_stream)
             rts.append(r)
-            streams.append(s_)
+            streams.append(torch.cuda.ExternalStream(r.stream(), device=dev))
     for _ in range(len(rts)):
         o = {"rgba": torch.zeros(n_out, dtype=torch.int32, device=dev),
              "depth": torch.zeros(n_out, dtype=torch.float32, device=dev)}
@@ -280,23 +305,25 @@ def main():
 
     ev = []
     frame = [0]
+    NOEV = os.environ.get("VHX_BENCH_NOEV") == "1"
 
     def step(timed):
         f = frame[0] % len(rts)
+        cam_k = cams[frame[0] % len(cams)]
         frame[0] += 1
         r, s_, o = rts[f], streams[f], outs[f]
-        if timed and mg is None:
+        if timed and mg is None and not NOEV:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(s_)
         if mg is not None:
-            mg.render(cam, fb_rgba, fb_depth)  # this rank's tiles -> ncclGather -> untile on rank 0
+            mg.render(cam_k, fb_rgba, fb_depth)  # this rank's tiles -> ncclGather -> untile on rank 0
         else:
             if pipe is not None:
                 o["rgba"] = pipe.out_buffer()
-            r.trace_primary(cam, out=o, **trace_kw)
+            r.trace_primary(cam_k, out=o, **trace_kw)
             if args.shadows:
                 r.trace_shadows(light, o, shadowed=o["shadowed"])
-        if timed and mg is None:
+        if timed and mg is None and not NOEV:
             e1.record(s_)  # the launch on its own stream (the gather runs on the communication stream)
             ev.append((e0, e1))
         if pipe is not None:
@@ -309,6 +336,12 @@ def main():
             mg.sync()
         torch.cuda.synchronize(dev)
 
+    # setup (not a step): one untimed frame per context allocates its queues and state buffers, so that no
+    # allocation (hipMalloc synchronises the device) falls into the timed region when F exceeds the warm-up count
+    for _ in range(len(rts) if mg is None else 1):
+        step(False)
+    drain()
+    frame[0] = 0
     for _ in range(args.warmup):
         step(False)
     drain()
@@ -351,7 +384,8 @@ def main():
         kernel_ms = kernel_ms_isolated
 
     scene_tag = f"vox:{os.path.basename(args.vox)}" if args.vox else f"S{args.scene}"
-    workload = f"primary {W}x{H} {scene_tag} {args.size}^3 bd{args.brick_dim} ranks{world}"
+    workload = f"primary {W}x{H} {scene_tag} {args.size}^3 bd{args.brick_dim} ranks{world}" + (
+        f" orbit{args.orbit}" if args.orbit else "")
     total_rays = W * H
     n_shadow = 0
     if args.shadows:
@@ -381,8 +415,9 @@ def main():
     # ---- roofline: algorithmic bytes of this rank's launch (instrumented kernel, untimed) -------------------------
     roof = None
     if not args.no_roofline and not args.shadows:
-        res = rt.trace_primary(cam, fields=(), count_bytes=True, **trace_kw)
-        tree_bytes = float(res["bytes"].astype(np.float64).sum())
+        views = [cam] if len(cams) == 1 else [cams[args.warmup], cams[args.warmup + args.steps // 2], cams[-1]]
+        tree_bytes = float(np.mean([rt.trace_primary(v, fields=(), count_bytes=True, **trace_kw)["bytes"]
+                                    .astype(np.float64).sum() for v in views]))
         my_rays = W * H if world == 1 else M.rank_rays(W, H, T, rank, world)
         out_bytes = 8.0 * my_rays  # rgba8 + f32 depth per ray
         launch_bytes = tree_bytes + out_bytes
@@ -442,16 +477,17 @@ def main():
             "metric": metric, "value": round(mrays, 3), "unit": "Mrays/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": "f32",
-            "frames_in_flight": F,
+            "frames_in_flight": F, "gpu_max_hw_queues": queues,
             "data": "model file" if args.vox else "synthetic",
             "config": {"workload": ("BASELINE config 4: " if cfg4 else "") + f"primary rays {W}x{H}, {args.size}^3 "
                                    + (f".vox model {os.path.basename(args.vox)}" if args.vox
                                       else "procedural scene S (lattice+cube)")
                                    + f", brick_dim {args.brick_dim}, glass camera"
+                                   + (f" orbiting {args.orbit} rad per frame" if args.orbit else "")
                                    + (f", {T}x{T} tiles round-robin over {world} ranks" if world > 1 else ""),
                        "workload_key": workload,
                        "shadow_rays_per_frame": n_shadow if args.shadows else None,
-                       "tree_size": args.size, "brick_dim": args.brick_dim, "width": W, "height": H,
+                       "camera_orbit_rad_per_frame": args.orbit, "tree_size": args.size, "brick_dim": args.brick_dim, "width": W, "height": H,
                        "scene": args.scene, "tile": T if world > 1 else None, "parallelism": par,
                        **{k: v for k, v in tree_info.items() if k != "size"}, "build_s": round(build_s, 2), "upload_s": round(upload_s, 2)},
             "roofline": roof, "cpu_baseline": cpu,

@@ -145,12 +145,18 @@ void vhx_destroy(vhx_ctx *ctx);
 const char *vhx_last_error(const vhx_ctx *ctx);
 /* Use an external HIP stream (hipStream_t passed as void*; NULL = the context's own stream). */
 int vhx_set_stream(vhx_ctx *ctx, void *hip_stream);
+/* The context's stream (hipStream_t as void*): the one set by vhx_set_stream, else the context's own, created at its
+ * first use (a context given a stream before its first call creates none: streams share the device's few hardware
+ * queues round-robin, so frames in flight want one stream each and no idle ones). */
+int vhx_get_stream(vhx_ctx *ctx, void **hip_stream);
 /* Wait for all work of the context; optionally return the device time of the last trace in milliseconds. */
 int vhx_sync(vhx_ctx *ctx, float *last_trace_ms);
 /* Ray scheduling (no reference counterpart; results do not depend on it). A trace runs n+1 passes: pass i abandons
  * rays that need more than budgets[i] loop steps (saving their traversal state) and the next pass resumes them, 64
  * such rays per wave; the last pass is unbounded. n = 0 is a single pass. Budgets strictly increasing,
- * 0 < b < 2^22, n <= 3. Default {64} (environment override VHX_BUDGETS="32,256"). */
+ * 0 < b < 2^22, n <= VHX_MAX_BUDGETS. Default {24, 96, 768}, tuned for frames in flight (vhx_create_shared);
+ * {64} gives the shortest latency of a lone frame (environment override VHX_BUDGETS="64"). */
+#define VHX_MAX_BUDGETS 4
 int vhx_set_pass_budgets(vhx_ctx *ctx, const uint32_t *budgets, uint32_t n);
 
 /* Tree upload ----------------------------------------------------------------------------------------------- */
@@ -241,7 +247,7 @@ int vhx_mgpu_sync(vhx_mgpu *m, float *last_trace_ms);
 /* Frames in flight on this rank (1..VHX_MGPU_MAX_INFLIGHT, default 1): frame k is traced by the k % F-th of F contexts
  * sharing the tree (vhx_create_shared), each on its own stream, so frame k+1's trace overlaps frame k's long-ray tail;
  * gathers stay in frame order on the communication stream. Waits for the frames in flight before it changes them. */
-#define VHX_MGPU_MAX_INFLIGHT 4
+#define VHX_MGPU_MAX_INFLIGHT 16
 int vhx_mgpu_set_frames_in_flight(vhx_mgpu *m, uint32_t frames);
 /* nranks, rank, and the rays this rank traces for a width x height frame (any pointer may be NULL). */
 int vhx_mgpu_info(const vhx_mgpu *m, uint32_t width, uint32_t height, int *nranks, int *rank, uint64_t *rays);

@@ -10,10 +10,10 @@ flat = vhx.FlatTree.build_scene(N.VHX_SCENE_LATTICE_CUBE, 1024, 4, threads=16)
 W, H = 3840, 2160
 cam = vhx.glass_camera(1024, W, H, target=(512.0,) * 3)
 owner = vhx.Raytracer(0); owner.upload(flat)
-ctxs = [owner] + [owner.shared() for _ in range(3)]
-streams = [torch.cuda.Stream() for _ in ctxs]
-for r, s in zip(ctxs, streams):
-    r.set_stream(s.cuda_stream)
+FS = [int(x) for x in os.environ.get("VHX_PROBE_F", "1,3").split(",")]
+ctxs = [owner] + [owner.shared() for _ in range(max(FS) - 1)]
+# each context on its own stream (created back to back: one hardware queue each)
+streams = [torch.cuda.ExternalStream(r.stream()) for r in ctxs]
 outs = [{"rgba": torch.zeros(W * H, dtype=torch.int32, device="cuda"),
          "depth": torch.zeros(W * H, dtype=torch.float32, device="cuda")} for _ in ctxs]
 ref = None
@@ -21,7 +21,7 @@ for spec in sys.argv[1:] or ["64"]:
     b = tuple(int(x) for x in spec.split(",") if x)
     for r in ctxs:
         r.set_pass_budgets(b)
-    for F in (1, 3):
+    for F in FS:
         K = 40
         for i in range(6):
             ctxs[i % F].trace_primary(cam, out=outs[i % F])

@@ -237,10 +237,11 @@ def test_full_size_shadows_vs_oracle(gpu, oracle):
     assert sh.sum() > 100000
 
 
-DEFAULT_BUDGETS = (64,)
+DEFAULT_BUDGETS = (24, 96, 768)
 
 
-@pytest.mark.parametrize("budgets", [(), (1,), (1, 2, 3), (4, 40), (8, 64, 512), DEFAULT_BUDGETS])
+@pytest.mark.parametrize("budgets", [(), (1,), (1, 2, 3), (1, 2, 3, 4), (4, 40), (8, 64, 512), (64,),
+                                     (16, 64, 256, 1024), DEFAULT_BUDGETS])
 def test_multipass_schedule_is_bit_identical(gpu, oracle, budgets):
     """The multi-pass scheduler (vhx_set_pass_budgets) abandons and re-traces rays; every schedule, down to a
     1-step first budget that requeues nearly every ray, must give the oracle's results (incl. byte counts)."""
@@ -315,7 +316,7 @@ def test_scheduler_variants_are_bit_identical(oracle, monkeypatch, env):
 
 
 def test_pass_budget_validation(gpu):
-    for bad in ((0,), (5, 5), (9, 3), (1, 2, 3, 4), (1 << 22,)):
+    for bad in ((0,), (5, 5), (9, 3), (1, 2, 3, 4, 5), (1 << 22,)):
         with pytest.raises(N.VhxError):
             gpu.set_pass_budgets(bad)
     gpu.set_pass_budgets(DEFAULT_BUDGETS)

@@ -41,30 +41,34 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(verbose=False, force=False):
-    os.makedirs(LIBDIR, exist_ok=True)
-    os.makedirs(BUILD, exist_ok=True)
+def build(verbose=False, force=False, lib=None, build_dir=None, defines=()):
+    """lib / build_dir / defines: a variant build (probes), e.g. defines=("VHX_QUEUE_WPE=5",)."""
+    lib = lib or LIB
+    bdir = build_dir or BUILD
+    os.makedirs(os.path.dirname(lib), exist_ok=True)
+    os.makedirs(bdir, exist_ok=True)
+    dflags = [f"-D{d}" for d in defines]
     inc = os.path.join(ROOT, "include")
     common_deps = [os.path.join(inc, h) for h in ("vhx.h", "vhx_boxtree.h")] + [os.path.join(CSRC, h) for h in HEADERS]
     objs = []
     for src in HOST_SRCS:
         s = os.path.join(CSRC, src)
-        o = os.path.join(BUILD, src + ".o")
+        o = os.path.join(bdir, src + ".o")
         if force or _stale(o, [s] + common_deps):
             _run(["g++", "-O3", "-std=c++17", "-fPIC", "-pthread", "-ffp-contract=off", "-fno-fast-math",
                   "-Wall", "-Wextra", "-I", inc, "-c", s, "-o", o], verbose)
         objs.append(o)
     for src in DEV_SRCS:
         s = os.path.join(CSRC, src)
-        o = os.path.join(BUILD, src + ".o")
+        o = os.path.join(bdir, src + ".o")
         if force or _stale(o, [s] + common_deps):
             _run([_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
-                  "-fno-fast-math", "-Wall", "-I", inc, "-c", s, "-o", o], verbose)
+                  "-fno-fast-math", "-Wall", "-I", inc] + dflags + ["-c", s, "-o", o], verbose)
         objs.append(o)
-    if force or _stale(LIB, objs):
+    if force or _stale(lib, objs):
         # -ldl: RCCL is dlopen()ed by vhx_mgpu.hip (no link-time RCCL dependency)
-        _run([_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-pthread", "-o", LIB] + objs + ["-ldl"], verbose)
-    return LIB
+        _run([_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-pthread", "-o", lib] + objs + ["-ldl"], verbose)
+    return lib
 
 
 if __name__ == "__main__":

@@ -7,7 +7,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_lib", "libvhx.so")
+# VHX_LIB: an alternative build of libvhx (A/B probes of kernel variants); the in-tree build by default
+LIB_PATH = os.environ.get("VHX_LIB") or os.path.join(_HERE, "_lib", "libvhx.so")
 
 c_u32 = ctypes.c_uint32
 c_u64 = ctypes.c_uint64
@@ -78,6 +79,7 @@ SIGNATURES = [
     ("vhx_destroy", None, [c_void_p]),
     ("vhx_last_error", ctypes.c_char_p, [c_void_p]),
     ("vhx_set_stream", c_int, [c_void_p, c_void_p]),
+    ("vhx_get_stream", c_int, [c_void_p, P(c_void_p)]),
     ("vhx_sync", c_int, [c_void_p, P(c_f32)]),
     ("vhx_set_pass_budgets", c_int, [c_void_p, P(c_u32), c_u32]),
     ("vhx_upload_tree", c_int, [c_void_p, P(TreeDesc)]),

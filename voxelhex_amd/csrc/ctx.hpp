@@ -49,10 +49,14 @@ struct vhx_ctx {
     std::vector<uint8_t> qargs_host[2];  // the QueueArgs last written to each slot (skips the upload when unchanged)
     void *qargs_host_ptr[2] = {nullptr, nullptr};  // qargs.ptr they were written to
     DevBuf state;     // saved traversal state per output index (64 B) of rays abandoned at a budget
-    // step budgets of the passes before the final (unbounded) one; VHX_BUDGETS="64" / "32,256" style override
-    uint32_t budgets[3] = {64u, 0u, 0u};
-    uint32_t npass = 2;         // passes including the final one (1 = single pass)
-    uint32_t rpw[4] = {64u, 64u, 64u, 64u};  // rays per wave of each pass (VHX_RPW="64,16" style override; 0 = adaptive)
+    // step budgets of the passes before the final (unbounded) one; VHX_BUDGETS="64" / "32,256" style override.
+    // {24, 96, 768}: with four frames in flight (bench frame) 0.697 ms per frame against 0.847 for {64}, 0.715 for
+    // {32, 128, 1024} and 0.740 for four budgets {16, 64, 256, 1024}: each pass re-packs the surviving rays into full
+    // waves, and the other frames fill the SIMDs a pass leaves idle. One frame at a time, {64} is faster (1.295 against
+    // 1.390 ms): the extra passes lengthen a lone frame's critical path (profiles/r02/sched_sweep_*.log).
+    uint32_t budgets[VHX_MAX_BUDGETS] = {24u, 96u, 768u, 0u};
+    uint32_t npass = 4;         // passes including the final one (1 = single pass)
+    uint32_t rpw[VHX_MAX_BUDGETS + 1] = {64u, 64u, 64u, 64u, 64u};  // rays per wave of each pass (VHX_RPW="64,16" style override; 0 = adaptive)
     uint32_t tw = 1024;            // adaptive rays per wave: target waves per queue pass (VHX_TW)
     bool resume = true;            // abandoned rays continue from saved state (VHX_RESUME=0: re-traced from scratch)
     uint32_t xcd_group = 16;       // pass-0 XCD-aware block runs (VHX_XCDG; 0 = dispatch order)
@@ -63,6 +67,7 @@ struct vhx_ctx {
     // pass, while every chunk still starts at once)
     uint32_t queue_waves = 2048;
     uint32_t queue_waves0 = 8192;  // waves of a first queue pass over fresh rays (VHX_QWAVES0)
+    uint32_t queue_waves_mid = 0;  // waves of a budgeted queue pass after the first (VHX_QWAVESM; 0 = queue_waves)
     uint32_t qxcd = 16;            // queue passes: XCD-dealt chunk runs (VHX_QXCD = run length, 0 = one counter)
 };
 
@@ -72,6 +77,18 @@ struct vhx_ctx {
         if (e_ != hipSuccess) {                                                                                    \
             (ctx)->err = std::string(#call) + ": " + hipGetErrorString(e_);                                        \
             return VHX_E_HIP;                                                                                      \
+        }                                                                                                          \
+    } while (0)
+
+// The context's stream: the caller's (vhx_set_stream), else its own, created at first use. A context given a stream
+// before its first call never creates one: the device has few hardware queues (GPU_MAX_HW_QUEUES, 4 by default) and
+// streams share them round-robin in creation order, so an unused stream per context made frames in flight share
+// queues (bench frame, four frames in flight: 0.91 against 0.70 ms per frame).
+#define VHX_STREAM(ctx)                                                                                            \
+    do {                                                                                                           \
+        if (!(ctx)->stream) {                                                                                      \
+            if (!(ctx)->own_stream) VHX_HIP(ctx, hipStreamCreateWithFlags(&(ctx)->own_stream, hipStreamNonBlocking)); \
+            (ctx)->stream = (ctx)->own_stream;                                                                     \
         }                                                                                                          \
     } while (0)
 

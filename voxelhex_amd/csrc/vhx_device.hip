@@ -316,7 +316,7 @@ __device__ __forceinline__ uint32_t flag_bits(const void *src, uint64_t i, uint6
 }
 
 // qctl: [0..7] queue lengths written after pass p (7: shadow hit list), [16 + 16p ..] pass p's work counters
-#define QCTL_WORDS 80u
+#define QCTL_WORDS (16u + 16u * (VHX_MAX_BUDGETS + 1u))
 // zero: the queue passes' work counters (qctl[16..79]), zeroed here instead of by a separate memset launch;
 // clear (optional, n entries): an output array zeroed alongside (the shadow flags of a shadow frame)
 template <bool HITS>
@@ -426,10 +426,28 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t bid, uint32_t n, uint32_t
     return ((k / G) * 8u + x) * G + k % G;
 }
 
+// occupancy of the traversal kernels (waves per SIMD the register allocation must allow; 0 = the compiler's choice)
+#ifndef VHX_QUEUE_WPE
+#define VHX_QUEUE_WPE 0
+#endif
+#ifndef VHX_PRIMARY_WPE
+#define VHX_PRIMARY_WPE 0
+#endif
+#if VHX_QUEUE_WPE > 0
+#define VHX_QUEUE_ATTR __attribute__((amdgpu_waves_per_eu(VHX_QUEUE_WPE)))
+#else
+#define VHX_QUEUE_ATTR
+#endif
+#if VHX_PRIMARY_WPE > 0
+#define VHX_PRIMARY_ATTR __attribute__((amdgpu_waves_per_eu(VHX_PRIMARY_WPE)))
+#else
+#define VHX_PRIMARY_ATTR
+#endif
+
 // One workgroup = 256 lanes = a 16x16 pixel block made of four 8x8 wave tiles (wave64-coherent ray bundles, the
 // 8x8 footprint of the reference's @workgroup_size(8, 8, 1)). Blocks are dealt tile by tile.
 template <bool COUNT, int BD>
-__global__ void __launch_bounds__(256) k_trace_primary(DevTree t, CamD cam, OutD out, uint32_t T, uint32_t tiles_x,
+__global__ void __launch_bounds__(256) VHX_PRIMARY_ATTR k_trace_primary(DevTree t, CamD cam, OutD out, uint32_t T, uint32_t tiles_x,
                                                        uint32_t tile_start, uint32_t tile_stride, uint32_t layout,
                                                        uint32_t blocks_per_tile_x, uint32_t blocks_per_tile,
                                                        PassQ q) {
@@ -509,7 +527,7 @@ __global__ void k_put_queue_args(QueueArgs a, QueueArgs *dst) {
 }
 
 template <bool COUNT, int BD>
-__global__ void __launch_bounds__(256) k_trace_queue(DevTree t, const QueueArgs *qa, const uint32_t *__restrict__ in,
+__global__ void __launch_bounds__(256) VHX_QUEUE_ATTR k_trace_queue(DevTree t, const QueueArgs *qa, const uint32_t *__restrict__ in,
                                                      const uint32_t *in_n, uint32_t *grab, PassQ q) {
     __shared__ uint64_t occ_tab[512];
     fill_occ_tab(occ_tab);
@@ -905,7 +923,8 @@ static int launch_queue_passes(vhx_ctx *c, const DevTree &t, const CamD &cam, co
         const uint32_t *in_n = p > 0 ? ctl + (p - 1) : ctl + 7;
         const PassQ q = pass_q(c, p, npass);
         // a first pass over fresh rays (the shadow path) is throughput-bound like a grid launch: more waves
-        const uint32_t qwaves = p == 0 ? c->queue_waves0 : c->queue_waves;
+        const uint32_t qwaves = p == 0 ? c->queue_waves0
+                                : (p + 1 < npass && c->queue_waves_mid ? c->queue_waves_mid : c->queue_waves);
         const unsigned qgrid = (qwaves * 64u + c->qblock - 1) / c->qblock;
         k_trace_queue<COUNT, BD><<<qgrid, c->qblock, 0, c->stream>>>(t, qa, in, in_n, ctl + 16u + 16u * p, q);
         debug_passes(c, "queue pass");
@@ -946,14 +965,12 @@ int vhx_create(int hip_device, vhx_ctx **out) {
     };
     hipError_t e;
     if ((e = hipSetDevice(hip_device)) != hipSuccess) return bail("hipSetDevice", e);
-    if ((e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking)) != hipSuccess)
-        return bail("hipStreamCreate", e);
-    c->stream = c->own_stream;
+    // no stream yet: the caller's (vhx_set_stream) or the context's own, created at first use (VHX_STREAM)
     {
         const char *pb = getenv("VHX_BUDGETS");  // "32,256" = three passes; "" or "0" = one pass
         if (pb) {
-            uint32_t b[3], nb = 0;
-            for (const char *q = pb; *q && nb < 3;) {
+            uint32_t b[VHX_MAX_BUDGETS], nb = 0;
+            for (const char *q = pb; *q && nb < VHX_MAX_BUDGETS;) {
                 char *end = nullptr;
                 const unsigned long v = strtoul(q, &end, 10);
                 if (end == q) break;
@@ -965,7 +982,7 @@ int vhx_create(int hip_device, vhx_ctx **out) {
         const char *pr = getenv("VHX_RPW");  // rays per wave of the queue passes 1.., e.g. "64,16"
         if (pr) {
             uint32_t k = 1;
-            for (const char *q = pr; *q && k < 4;) {
+            for (const char *q = pr; *q && k < VHX_MAX_BUDGETS + 1;) {
                 char *end = nullptr;
                 const unsigned long v = strtoul(q, &end, 10);
                 if (end == q) break;
@@ -988,6 +1005,8 @@ int vhx_create(int hip_device, vhx_ctx **out) {
         }
         const char *pw = getenv("VHX_QWAVES");  // after the device default
         if (pw && atoi(pw) > 0) c->queue_waves = (uint32_t)atoi(pw);
+        const char *pwm = getenv("VHX_QWAVESM");
+        if (pwm && atoi(pwm) > 0) c->queue_waves_mid = (uint32_t)atoi(pwm);
         const char *pw0 = getenv("VHX_QWAVES0");
         if (pw0 && atoi(pw0) > 0) c->queue_waves0 = (uint32_t)atoi(pw0);
         const char *pqx = getenv("VHX_QXCD");
@@ -1023,6 +1042,7 @@ int vhx_create_shared(const vhx_ctx *owner, vhx_ctx **out) {
     c->queue_blocks = owner->queue_blocks;
     c->queue_waves = owner->queue_waves;
     c->queue_waves0 = owner->queue_waves0;
+    c->queue_waves_mid = owner->queue_waves_mid;
     c->qxcd = owner->qxcd;
     *out = c;
     return VHX_OK;
@@ -1043,11 +1063,11 @@ void vhx_destroy(vhx_ctx *c) {
 }
 
 int vhx_set_pass_budgets(vhx_ctx *c, const uint32_t *budgets, uint32_t n) {
-    if (!c || n > 3 || (n && !budgets)) return VHX_E_INVALID_ARG;
+    if (!c || n > VHX_MAX_BUDGETS || (n && !budgets)) return VHX_E_INVALID_ARG;
     for (uint32_t i = 0; i < n; ++i)
         if (budgets[i] == 0 || budgets[i] >= VHX_MAX_ITERS || (i && budgets[i] <= budgets[i - 1]))
             return fail(c, VHX_E_INVALID_ARG, "pass budgets must be increasing, > 0 and < 2^22");
-    for (uint32_t i = 0; i < 3; ++i) c->budgets[i] = i < n ? budgets[i] : 0u;
+    for (uint32_t i = 0; i < VHX_MAX_BUDGETS; ++i) c->budgets[i] = i < n ? budgets[i] : 0u;
     c->npass = n + 1;
     return VHX_OK;
 }
@@ -1056,15 +1076,23 @@ const char *vhx_last_error(const vhx_ctx *c) { return c ? c->err.c_str() : "null
 
 int vhx_set_stream(vhx_ctx *c, void *s) {
     if (!c) return VHX_E_INVALID_ARG;
-    c->stream = s ? (hipStream_t)s : c->own_stream;
+    c->stream = s ? (hipStream_t)s : c->own_stream;  // null own stream: created at the next use
     c->qargs_host_ptr[0] = c->qargs_host_ptr[1] = nullptr;  // written on the previous stream: rewrite them
+    return VHX_OK;
+}
+
+int vhx_get_stream(vhx_ctx *c, void **s) {
+    if (!c || !s) return VHX_E_INVALID_ARG;
+    VHX_HIP(c, hipSetDevice(c->device));
+    VHX_STREAM(c);
+    *s = (void *)c->stream;
     return VHX_OK;
 }
 
 int vhx_sync(vhx_ctx *c, float *ms) {
     if (!c) return VHX_E_INVALID_ARG;
     VHX_HIP(c, hipSetDevice(c->device));
-    VHX_HIP(c, hipStreamSynchronize(c->stream));
+    if (c->stream) VHX_HIP(c, hipStreamSynchronize(c->stream));
     if (ms) {
         *ms = 0.f;
         if (c->timed) VHX_HIP(c, hipEventElapsedTime(ms, c->ev0, c->ev1));
@@ -1139,6 +1167,7 @@ int vhx_upload_tree(vhx_ctx *c, const vhx_tree_desc *t) {
             return fail(c, VHX_E_INVALID_ARG, "vhx_upload_tree: null array with non-zero count");
     int rc = alloc_tree(c, t);
     if (rc) return rc;
+    VHX_STREAM(c);
     for (int id = 0; id < 7; ++id) {
         const uint64_t bytes = elem_count(*t, id) * elem_size(id);
         if (bytes) VHX_HIP(c, hipMemcpyAsync(c->tree->raw[id].ptr, src[id], bytes, hipMemcpyHostToDevice, c->stream));
@@ -1154,6 +1183,7 @@ int vhx_update_range(vhx_ctx *c, int id, uint64_t off, uint64_t count, const voi
     if (off + count > cap) return fail(c, VHX_E_CAPACITY, "vhx_update_range: range beyond the uploaded buffer");
     if (count == 0) return VHX_OK;
     VHX_HIP(c, hipSetDevice(c->device));
+    VHX_STREAM(c);
     const uint64_t es = elem_size(id);
     VHX_HIP(c, hipMemcpyAsync((char *)c->tree->raw[id].ptr + off * es, src, count * es, hipMemcpyHostToDevice, c->stream));
     int rc = VHX_OK;
@@ -1179,6 +1209,7 @@ int vhx_read_derived(vhx_ctx *c, int which, uint64_t off, uint64_t count, void *
     if (off + count > cap) return fail(c, VHX_E_CAPACITY, "vhx_read_derived: range beyond the buffer");
     const DevBuf &b = which == VHX_DERIVED_NODE_HDR ? c->tree->hdr : c->tree->brick_occ;
     VHX_HIP(c, hipSetDevice(c->device));
+    VHX_STREAM(c);
     VHX_HIP(c, hipMemcpyAsync(dst, (const char *)b.ptr + off * es, count * es, hipMemcpyDeviceToHost, c->stream));
     VHX_HIP(c, hipStreamSynchronize(c->stream));
     return VHX_OK;
@@ -1238,6 +1269,7 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
     const uint64_t nout = layout == VHX_LAYOUT_FRAMEBUFFER ? (uint64_t)cam->width * cam->height
                                                            : (uint64_t)my_tiles * T * T;
     VHX_HIP(c, hipSetDevice(c->device));
+    VHX_STREAM(c);
     HostOut ho;
     int rc = map_out(c, out, nout, on_device, ho, layout == VHX_LAYOUT_TILES);
     if (rc) return rc;
@@ -1290,6 +1322,7 @@ int vhx_trace_rays(vhx_ctx *c, const float *rays, uint64_t n, const vhx_hits *ou
     if (n == 0) return VHX_OK;
     if ((n + 255) / 256 > 0x7FFFFFFFull) return fail(c, VHX_E_INVALID_ARG, "too many rays");
     VHX_HIP(c, hipSetDevice(c->device));
+    VHX_STREAM(c);
     HostOut ho;
     int rc = map_out(c, out, n, on_device, ho);
     if (rc) return rc;
@@ -1365,6 +1398,7 @@ int vhx_trace_shadows(vhx_ctx *c, const float light[3], uint64_t n, const uint32
         }
     }
     VHX_HIP(c, hipSetDevice(c->device));
+    VHX_STREAM(c);
     uint32_t npass = 1;
     const uint64_t nb64 = (n + 255) / 256;
     int rc = prepare_passes(c, n, nb64, npass, true);
@@ -1423,6 +1457,7 @@ int vhx_untile_frame(vhx_ctx *c, const void *gathered, uint32_t planes, uint32_t
     const uint64_t n = (uint64_t)ranks * planes * tiles_per_rank * T * T;
     if ((n + 255) / 256 > 0x7FFFFFFFull) return fail(c, VHX_E_INVALID_ARG, "too many pixels");
     VHX_HIP(c, hipSetDevice(c->device));
+    VHX_STREAM(c);
     return launch_untile(c, c->stream, gathered, planes, ranks, tiles_per_rank, T, width, height, fb_rgba, fb_depth);
 }
 

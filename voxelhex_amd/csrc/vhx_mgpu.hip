@@ -196,7 +196,7 @@ void vhx_mgpu_destroy(vhx_mgpu *m) {
     vhx_ctx *c = m->ctx;
     (void)hipSetDevice(c->device);
     if (m->cstream) (void)hipStreamSynchronize(m->cstream);
-    (void)hipStreamSynchronize(c->stream);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (vhx_ctx *x : m->extra) vhx_destroy(x);
     if (m->comm && m->own_comm) rccl().CommDestroy(m->comm);
     for (int s = 0; s < VHX_MGPU_MAX_INFLIGHT; ++s)
@@ -264,6 +264,7 @@ int vhx_mgpu_broadcast_tree(vhx_mgpu *m, const vhx_tree_desc *t) {
     const Rccl &r = rccl();
     VHX_HIP(c, hipSetDevice(c->device));
     if (c->shared) return fail(c, VHX_E_STATE, "vhx_mgpu_broadcast_tree on a shared context");
+    VHX_STREAM(c);
     if (m->rank == 0) {
         int rc = vhx_upload_tree(c, t);  // host -> HBM of rank 0, derived layout included
         if (rc) return rc;
@@ -327,6 +328,7 @@ int vhx_mgpu_render(vhx_mgpu *m, const vhx_camera *cam, uint32_t *fb_rgba, float
     const uint64_t n_out = (uint64_t)per * m->T * m->T;  // words per plane of one rank
     const uint32_t slot = (uint32_t)(m->k % m->S);
     vhx_ctx *tc = m->k % m->F == 0 ? c : m->extra[m->k % m->F - 1];  // the context tracing this frame
+    VHX_STREAM(tc);
     // a slot's buffers are rewritten only after the gather that read them (stream order on the tracing stream)
     if (m->used[slot]) VHX_HIP(c, hipStreamWaitEvent(tc->stream, m->free_[slot], 0));
     if (m->send[slot].bytes < n_out * 8 || (m->rank == 0 && m->gathered[slot].bytes < n_out * 8 * m->nranks)) {
@@ -367,7 +369,7 @@ int vhx_mgpu_sync(vhx_mgpu *m, float *ms) {
     VHX_HIP(c, hipSetDevice(c->device));
     VHX_HIP(c, hipStreamSynchronize(m->cstream));
     for (vhx_ctx *x : m->extra)
-        if (x) VHX_HIP(c, hipStreamSynchronize(x->stream));
+        if (x && x->stream) VHX_HIP(c, hipStreamSynchronize(x->stream));
     int rc = vhx_sync(c, ms);
     if (!rc && ms && m->last && m->last != c) rc = vhx_sync(m->last, ms);
     return rc;

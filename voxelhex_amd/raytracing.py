@@ -244,6 +244,13 @@ class Raytracer:
     def set_stream(self, stream_ptr):
         self._check(N.lib().vhx_set_stream(self._h, ctypes.c_void_p(stream_ptr)))
 
+    def stream(self):
+        """The context's hipStream_t (vhx_get_stream): the one set by set_stream, else its own (created now if
+        needed); wrap it with torch.cuda.ExternalStream to order torch work and events with the traces."""
+        s = ctypes.c_void_p()
+        self._check(N.lib().vhx_get_stream(self._h, ctypes.byref(s)))
+        return s.value
+
     def set_pass_budgets(self, budgets):
         """Step budgets of the multi-pass ray scheduler (vhx_set_pass_budgets); () = one unbounded pass."""
         b = (ctypes.c_uint32 * max(1, len(budgets)))(*budgets)
