@@ -445,7 +445,19 @@ def main():
                 "frames_in_flight": F,
                 "algorithmic_bytes_per_launch": launch_bytes, "tree_bytes_per_ray": round(tree_bytes / max(1, my_rays), 2)}
         if tr is not None and "issue" in tr:
-            roof["issue"] = tr["issue"]
+            # issue side (the traversal is bound by SIMD issue and divergence, not bytes): VALU wave-instructions of
+            # a frame (PMC, profiles/traffic.json) per frame period against 1024 SIMDs x 2.4 GHz / 2 cycles, and the
+            # share of those slots' lanes doing useful work
+            iss = tr["issue"]
+            valu_rate = iss["valu_wave_instructions_per_frame"] / (period_ms * 1e-3) / 1e9
+            peak_rate = iss["peak_valu_wave_instructions_per_s"] / 1e9
+            roof["issue"] = {"bound": "valu issue", "achieved": round(valu_rate, 1), "peak": round(peak_rate, 1),
+                             "unit": "G wave64 VALU instr/s", "frac": round(valu_rate / peak_rate, 4),
+                             "useful_lane_frac": iss["useful_lane_frac"],
+                             "useful_lane_ops_frac": round(valu_rate / peak_rate * iss["useful_lane_frac"], 4),
+                             "active_lanes_per_valu": iss["active_lanes_per_valu"],
+                             "valu_wave_instructions_per_frame": iss["valu_wave_instructions_per_frame"],
+                             "source": iss["source"]}
 
     # ---- CPU baseline: the oracle (reference semantics) on the host cores, rank 0 at N=1 only ----------------------
     cpu = None

@@ -1,0 +1,26 @@
+"""Frame timing from a rocprofv3 kernel trace of bench.py (gpu_profile.sh ks_kernel_trace.csv): for the timed frames
+(the pass-0 dispatches after the setup and warm-up ones), the span from the first timed pass-0 start to the last
+frame-kernel end divided by the frame count (the frame period, to compare with bench's ms_per_step), and the mean
+per-frame sum of kernel durations by kernel (with frames in flight the kernels of different frames overlap, so these
+sums exceed the period). usage: trace_frames.py KERNEL_TRACE_CSV SKIP STEPS"""
+import csv
+import sys
+from collections import defaultdict
+
+rows = list(csv.DictReader(open(sys.argv[1])))
+skip, steps = int(sys.argv[2]), int(sys.argv[3])
+frame_k = ("k_trace_primary<false", "k_trace_queue<false", "k_count_flags", "k_scan_counts", "k_emit_flags",
+           "k_gather_chunks", "k_put_queue_args")
+ks = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"].replace("void ", ""))
+            for r in rows)
+p0 = [k for k in ks if k[2].startswith("k_trace_primary<false")]
+t0 = p0[skip][0]
+t_last_start = p0[skip + steps][0] if len(p0) > skip + steps else None
+sel = [k for k in ks if k[2].startswith(frame_k) and k[0] >= t0 and (t_last_start is None or k[0] < t_last_start)]
+end = max(k[1] for k in sel)
+print(f"timed frames {steps}: span {(end - t0) / 1e6:.4f} ms, period {(end - t0) / 1e6 / steps:.4f} ms/frame")
+dur = defaultdict(float)
+for s, e, n in sel:
+    dur[n.split("(")[0]] += (e - s) / 1e6
+for n, v in sorted(dur.items(), key=lambda x: -x[1]):
+    print(f"  {n:32s} {v / steps:.4f} ms per frame (summed over its dispatches)")
