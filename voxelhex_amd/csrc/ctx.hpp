@@ -69,6 +69,7 @@ struct vhx_ctx {
     uint32_t queue_waves0 = 8192;  // waves of a first queue pass over fresh rays (VHX_QWAVES0)
     uint32_t queue_waves_mid = 0;  // waves of a budgeted queue pass after the first (VHX_QWAVESM; 0 = queue_waves)
     uint32_t qxcd = 16;            // queue passes: XCD-dealt chunk runs (VHX_QXCD = run length, 0 = one counter)
+    bool qxcd_all = false;         // deal every queue pass, not only the last (VHX_QXCD_ALL=1, diagnostics)
 };
 
 #define VHX_HIP(ctx, call)                                                                                         \

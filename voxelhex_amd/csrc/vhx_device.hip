@@ -315,8 +315,12 @@ __device__ __forceinline__ uint32_t flag_bits(const void *src, uint64_t i, uint6
     return bits;
 }
 
-// qctl: [0..7] queue lengths written after pass p (7: shadow hit list), [16 + 16p ..] pass p's work counters
-#define QCTL_WORDS (16u + 16u * (VHX_MAX_BUDGETS + 1u))
+// qctl: [0..7] queue lengths written after pass p (7: shadow hit list), [16 + QCTL_PASS_WORDS p ..] pass p's work
+// counters: the single counter, then the 8 XCD counters, each on a 256-byte line of its own (with the XCD counters in
+// one line, the drain of a budgeted pass over many short chunks, every wave probing every exhausted counter, took 2.5 -
+// 3.6 times as long as with one counter: DESIGN.md §3)
+#define QCTL_PASS_WORDS (9u * 64u)
+#define QCTL_WORDS (16u + QCTL_PASS_WORDS * (VHX_MAX_BUDGETS + 1u))
 // zero: the queue passes' work counters (qctl[16..79]), zeroed here instead of by a separate memset launch;
 // clear (optional, n entries): an output array zeroed alongside (the shadow flags of a shadow frame)
 template <bool HITS>
@@ -324,7 +328,8 @@ __global__ void __launch_bounds__(256) k_count_flags(const void *__restrict__ sr
                                                      uint32_t *__restrict__ counts, uint32_t *zero,
                                                      uint32_t *__restrict__ clear = nullptr) {
     __shared__ uint32_t s_cnt[4];
-    if (blockIdx.x == 0 && threadIdx.x < QCTL_WORDS - 16u) zero[threadIdx.x] = 0u;
+    if (blockIdx.x == 0)
+        for (uint32_t w = threadIdx.x; w < QCTL_WORDS - 16u; w += blockDim.x) zero[w] = 0u;
     const uint64_t i = ((uint64_t)blockIdx.x * 256u + threadIdx.x) * 4u;
     if (clear)
         for (uint64_t k = i; k < n && k < i + 4u; ++k) clear[k] = 0u;
@@ -536,7 +541,7 @@ __global__ void __launch_bounds__(256) VHX_QUEUE_ATTR k_trace_queue(DevTree t, c
     const uint32_t n = *in_n;
     const uint32_t rpw = pass_rpw(q.rpw, q.tw, n);
     // q.qxcd = G > 0: chunk runs of G are dealt round-robin over the XCDs (blockIdx % 8 runs on one XCD and shares
-    // its L2), each XCD's waves take its runs in order from their own counter (grab[8 + x]) and move on to the next
+    // its L2), each XCD's waves take its runs in order from their own counter (grab[64 (x + 1)]) and move on to the next
     // XCD's runs once theirs are taken
     uint32_t xcd = blockIdx.x & 7u, tries = 0;
     // only a queue with more chunks than waves is dealt over the XCDs (a smaller one starts every chunk at once
@@ -558,8 +563,8 @@ __global__ void __launch_bounds__(256) VHX_QUEUE_ATTR k_trace_queue(DevTree t, c
                 const uint32_t kmax = (nfull > xcd ? (nfull - xcd + 7u) / 8u : 0u) * G +
                                       (rem > 0u && nfull % 8u == xcd ? rem : 0u);
                 uint32_t k = 0xFFFFFFFFu;
-                if (lane == 0 && __atomic_load_n(grab + 8u + xcd, __ATOMIC_RELAXED) < kmax)
-                    k = atomicAdd(grab + 8u + xcd, 1u);
+                uint32_t *ctr = grab + 64u * (xcd + 1u);
+                if (lane == 0 && __atomic_load_n(ctr, __ATOMIC_RELAXED) < kmax) k = atomicAdd(ctr, 1u);
                 k = __builtin_amdgcn_readfirstlane(__shfl(k, 0));
                 if (k < kmax) {
                     chunk = ((k / G) * 8u + xcd) * G + k % G;
@@ -840,7 +845,10 @@ static PassQ pass_q(const vhx_ctx *c, uint32_t p, uint32_t npass) {
     q.rpw = c->rpw[p];
     q.tw = c->tw;
     q.xcd_group = c->xcd_group;
-    q.qxcd = last ? c->qxcd : 0u;  // the unbounded last pass only (a budgeted pass over many short chunks: 2x slower)
+    // the unbounded last pass only: dealing the budgeted passes too measured the same (shadow frames 2.90 against
+    // 2.87 ms, primary frames equal) once the XCD counters had cache lines of their own; VHX_QXCD_ALL=1 deals every
+    // queue pass (diagnostics)
+    q.qxcd = last || c->qxcd_all ? c->qxcd : 0u;
     q.tmp = last ? nullptr : (uint32_t *)c->tmp.ptr;
     q.counts = (uint32_t *)c->counts.ptr;
     q.flags = nullptr;
@@ -926,7 +934,8 @@ static int launch_queue_passes(vhx_ctx *c, const DevTree &t, const CamD &cam, co
         const uint32_t qwaves = p == 0 ? c->queue_waves0
                                 : (p + 1 < npass && c->queue_waves_mid ? c->queue_waves_mid : c->queue_waves);
         const unsigned qgrid = (qwaves * 64u + c->qblock - 1) / c->qblock;
-        k_trace_queue<COUNT, BD><<<qgrid, c->qblock, 0, c->stream>>>(t, qa, in, in_n, ctl + 16u + 16u * p, q);
+        k_trace_queue<COUNT, BD><<<qgrid, c->qblock, 0, c->stream>>>(t, qa, in, in_n, ctl + 16u + QCTL_PASS_WORDS * p,
+                                                                    q);
         debug_passes(c, "queue pass");
         if (p + 1 < npass)
             rc = compact_chunks(c, 0, in_n, q.rpw, q.rpw, (uint32_t *)c->queue[p & 1u].ptr, ctl + p,
@@ -1011,6 +1020,8 @@ int vhx_create(int hip_device, vhx_ctx **out) {
         if (pw0 && atoi(pw0) > 0) c->queue_waves0 = (uint32_t)atoi(pw0);
         const char *pqx = getenv("VHX_QXCD");
         if (pqx && atoi(pqx) >= 0) c->qxcd = (uint32_t)atoi(pqx);
+        const char *pqa = getenv("VHX_QXCD_ALL");
+        if (pqa && pqa[0] == '1') c->qxcd_all = true;
     }
     if ((e = hipEventCreate(&c->ev0)) != hipSuccess) return bail("hipEventCreate", e);
     if ((e = hipEventCreate(&c->ev1)) != hipSuccess) return bail("hipEventCreate", e);
@@ -1044,6 +1055,7 @@ int vhx_create_shared(const vhx_ctx *owner, vhx_ctx **out) {
     c->queue_waves0 = owner->queue_waves0;
     c->queue_waves_mid = owner->queue_waves_mid;
     c->qxcd = owner->qxcd;
+    c->qxcd_all = owner->qxcd_all;
     *out = c;
     return VHX_OK;
 }
