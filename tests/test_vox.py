@@ -329,3 +329,20 @@ def test_reference_models(path):
         p = keys[i]
         e = t.get(p)
         assert e.kind == "Visual" and e.albedo().packed() == want[p], (p, e)
+
+
+def test_gingerbread_fixture_is_the_imported_asset():
+    """tests/golden/gingerbread_bd8.npz (the GPU tests' copy of the reference's gingerbread model) equals what
+    vhx_boxtree_load_vox builds from the asset, where the reference checkout exists."""
+    import hashlib
+    import os
+    from tests._arraytree import ArrayTree, FIELDS
+    from tests.golden.make_vox_fixture import SRC, build
+    fx = ArrayTree(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "gingerbread_bd8.npz"))
+    assert fx.brick_dim == 8 and fx.boxtree_size == 2048 and fx.desc.node_count > 0
+    if not os.path.exists(SRC):
+        pytest.skip("reference checkout not present (the GPU box): fixture checked for shape only")
+    assert hashlib.sha256(open(SRC, "rb").read()).hexdigest() == fx.source_sha256
+    arrays = build()
+    for k in FIELDS:
+        assert np.array_equal(arrays[k], fx.arrays[k]), k
