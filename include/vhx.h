@@ -12,6 +12,7 @@
  *                           src/raytracing/bevy/view.rs:36-137): owns the device copy of the tree
  *   vhx_upload_tree      <- prepare_bind_groups full-buffer writes (src/raytracing/bevy/pipeline/mod.rs:242-402)
  *   vhx_update_range     <- write_range_to_buffer (src/raytracing/bevy/streaming/mod.rs:344-370)
+ *   vhx_update_ranges    <- the write_range_to_buffer calls of one streaming::upload frame (streaming/mod.rs:420-635)
  *   vhx_trace_primary    <- VhxRenderNode::run main dispatch (src/raytracing/bevy/pipeline/mod.rs:96-155) running the
  *                           per-pixel kernel, with the semantics of the reference CPU raytracer
  *                           BoxTree::get_by_ray (src/raytracing/cpu.rs:296-458) and the CPU frame of
@@ -170,8 +171,25 @@ int vhx_upload_tree(vhx_ctx *ctx, const vhx_tree_desc *tree);
 #define VHX_BUF_COLOR_PALETTE 5
 #define VHX_BUF_DATA_PALETTE 6
 /* Overwrites elements [elem_offset, elem_offset+elem_count) of one uploaded buffer (element = one entry of the
- * corresponding vhx_tree_desc array) and refreshes the derived device state. VHX_E_CAPACITY past the end. */
+ * corresponding vhx_tree_desc array) and refreshes the derived device state. VHX_E_CAPACITY past the end.
+ * Stream-ordered: the source is copied into pinned staging before the call returns (the caller may reuse it at once),
+ * and the device writes, like the derived-state refresh, run on the context's stream ahead of its next trace; no host
+ * synchronisation. Same as vhx_update_ranges with one range. */
 int vhx_update_range(vhx_ctx *ctx, int buffer_id, uint64_t elem_offset, uint64_t elem_count, const void *src);
+/* One ranged write of vhx_update_ranges. */
+typedef struct vhx_range {
+    int32_t buffer_id;   /* VHX_BUF_* */
+    uint32_t reserved0;
+    uint64_t elem_offset;
+    uint64_t elem_count;
+    const void *src;     /* host memory, elem_count elements */
+} vhx_range;
+/* A frame's ranged writes in one call (the reference issues one write_range_to_buffer per range,
+ * streaming/mod.rs:420-635): the sources are packed into pinned staging, moved to HBM by ONE host-to-device copy and
+ * scattered to their buffers by one kernel; the derived state (node headers, brick bitmaps, and the child records of
+ * the written nodes and of the nodes holding written bricks) is refreshed on the device, all stream-ordered without
+ * host synchronisation. All ranges are validated before anything is written. */
+int vhx_update_ranges(vhx_ctx *ctx, const vhx_range *ranges, uint32_t n);
 /* Diagnostics: copies elements of a derived device buffer to host memory (for tests).
  * VHX_DERIVED_NODE_HDR: 16-byte {occ_lo, occ_hi, type, 0} per node; VHX_DERIVED_BRICK_OCC: u64 words, brick_dim^3
  * bits per brick (max(1, brick_dim^3/64) words), bit = flat cell index, set = cell not empty. */

@@ -18,9 +18,13 @@
  *   vhx_stream_reload       <- BoxTreeGPUView::reload (view.rs:141-145)
  *   vhx_stream_view         host mirror of the device view (for checking; pointers valid until the next call)
  *
- * The tree must stay unmodified while a stream uses it (tree-change propagation, streaming/mod.rs:36-288, is not
- * restated). The context must outlive the stream; ctx = NULL keeps the view on the host only (vhx_stream_view), which
- * is how the producer is tested without a GPU.
+ * Tree changes: inserts and updates of the tree (vhx_boxtree_insert / _insert_at_lod / _update) made while a stream
+ * exists are queued by the tree (the update trigger of BoxTreeGPUHost::new, src/raytracing/bevy/mod.rs:164-173) and
+ * re-uploaded by the next vhx_stream_upload calls (handle_tree_updates, streaming/mod.rs:35-286: up to
+ * node_uploads_per_frame changes per frame, ahead of the upload queue). One stream per tree receives them, like the
+ * reference's single changes buffer. The tree and the context must outlive the stream; ctx = NULL keeps the view on
+ * the host only (vhx_stream_view), which is how the producer is tested without a GPU. Every frame's ranged writes go
+ * to the device as one vhx_update_ranges call (stream-ordered, no host synchronisation).
  */
 #ifndef VHX_STREAM_H
 #define VHX_STREAM_H
@@ -43,7 +47,8 @@ typedef struct vhx_stream_stats {
     uint64_t nodes_in_view;   /* node capacity */
     uint64_t bricks_in_view;  /* brick capacity */
     uint64_t nodes_to_see;    /* nodes the viewport needs */
-    uint64_t pending;         /* work left: nodes to see that are not resident + queued brick requests, + 1 until a
+    uint64_t pending;         /* work left: nodes to see that are not resident + queued brick requests + queued tree
+                                 changes, + 1 until a
                                  complete walk cycle found nothing new (the node walk restarts from the root whenever
                                  it finishes, as in the reference, so a lost brick is requested on the next cycle) */
 } vhx_stream_stats;

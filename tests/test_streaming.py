@@ -102,3 +102,52 @@ def test_reload_and_small_capacity_growth(oracle):
     o, d = _rays_in_box(rng, np.zeros(3), np.full(3, 16.0), 3000)
     assert_same(oracle.trace_rays(s.view(), o, d, fields=FIELDS), oracle.trace_rays(t.flatten(), o, d, fields=FIELDS),
                 "reloaded full view")
+
+
+def _edit(t, rng, size):
+    """Inserts into empty space (new nodes and bricks), updates of existing voxels (changed bricks) and a small block
+    insert (insert_at_lod). A block that covers a node's six faces would make it occluded, and the upload walk never
+    descends into an occluded node (upload_queue.rs:528-531; its MIP stands in for it in the reference, and MIPs are
+    off by default): the view would then miss that node's inside, in the reference as here."""
+    for _ in range(60):
+        x, y, z = (int(v) for v in rng.integers(0, size, 3))
+        t.insert((x, y, z), vhx.Albedo(int(rng.integers(1, 255)), 40, 200, 255))
+    for _ in range(40):
+        x, y, z = (int(v) for v in rng.integers(0, size, 3))
+        t.update((x, y, z), vhx.Albedo(250, int(rng.integers(1, 255)), 10, 255))
+    x, y, z = (int(v) for v in rng.integers(0, size - 8, 3))
+    t.insert_at_lod((x - x % 2, y - y % 2, z - z % 2), 2, vhx.Albedo(9, 9, 250, 255))
+
+
+@pytest.mark.parametrize("size,bd,dist", [(64, 4, 128.0), (128, 8, 256.0), (32, 2, 64.0)])
+def test_tree_changes_propagate_into_the_stream(oracle, size, bd, dist):
+    """handle_tree_updates (src/raytracing/bevy/streaming/mod.rs:35-286): after the view is complete, edits of the
+    tree are queued by its update trigger and re-uploaded by the next frames, so the view renders the edited tree."""
+    t = _tree(size, bd)
+    S = float(size)
+    s = vhx.StreamingView(t, None, (S / 2, S / 2, S / 2), dist)
+    s.upload_all()
+    rng = np.random.default_rng(size + bd)
+    o = rng.uniform(-0.5 * S, 1.5 * S, (5000, 3)).astype(np.float32)
+    tgt = rng.uniform(0, S, (5000, 3)).astype(np.float32)
+    d = tgt - o
+    d = (d / np.sqrt((d * d).sum(1, keepdims=True))).astype(np.float32)
+    for rnd in range(2):
+        before = oracle.trace_rays(t.flatten(), o, d, fields=FIELDS)
+        _edit(t, rng, size)
+        stats, frames, _ = s.upload_all()
+        assert stats["pending"] == 0 and frames >= 1
+        full = oracle.trace_rays(t.flatten(), o, d, fields=FIELDS)
+        assert not np.array_equal(before["value"], full["value"])  # the edits are visible
+        assert_same(oracle.trace_rays(s.view(), o, d, fields=FIELDS), full, f"edited tree, round {rnd}")
+
+
+def test_tree_changes_are_queued_only_while_streamed():
+    t = _tree(64, 4)
+    t.insert((3, 3, 3), vhx.Albedo(1, 2, 3, 255))  # no stream yet: nothing is queued
+    s = vhx.StreamingView(t, None, (32.0, 32.0, 32.0), 128.0)
+    s.upload_all()
+    t.insert((5, 5, 5), vhx.Albedo(1, 2, 3, 255))
+    assert s.upload()[0]["pending"] >= 0
+    s.close()
+    t.insert((7, 7, 7), vhx.Albedo(1, 2, 3, 255))  # the stream is gone: not queued (nothing would pop it)

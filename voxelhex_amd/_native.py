@@ -54,6 +54,11 @@ class TreeDesc(ctypes.Structure):
     ]
 
 
+class Range(ctypes.Structure):
+    _fields_ = [("buffer_id", ctypes.c_int32), ("reserved0", c_u32), ("elem_offset", c_u64), ("elem_count", c_u64),
+                ("src", c_void_p)]
+
+
 class Camera(ctypes.Structure):
     _fields_ = [
         ("ray_model", c_u32), ("width", c_u32), ("height", c_u32), ("reserved0", c_u32),
@@ -84,6 +89,7 @@ SIGNATURES = [
     ("vhx_set_pass_budgets", c_int, [c_void_p, P(c_u32), c_u32]),
     ("vhx_upload_tree", c_int, [c_void_p, P(TreeDesc)]),
     ("vhx_update_range", c_int, [c_void_p, c_int, c_u64, c_u64, c_void_p]),
+    ("vhx_update_ranges", c_int, [c_void_p, c_void_p, c_u32]),
     ("vhx_read_derived", c_int, [c_void_p, c_int, c_u64, c_u64, c_void_p]),
     ("vhx_tree_device_bytes", c_int, [c_void_p, P(c_u64)]),
     ("vhx_trace_primary", c_int, [c_void_p, P(Camera), c_u32, c_u32, c_u32, c_u32, P(Hits), c_int]),

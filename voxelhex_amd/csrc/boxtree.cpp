@@ -875,6 +875,7 @@ int BoxTree::insert_at_lod_internal(bool overwrite, U3 pos_u32, uint32_t insert_
 
     if (!updated) return 0;
     bool simplifyable = auto_simplify;
+    const std::vector<std::pair<size_t, uint8_t>> node_stack_clone = node_stack;  // insert.rs:329
     for (uint8_t mbs : modified_bottom) {
         size_t node_key = node_stack.back().first;
         uint8_t original = node_stack.back().second;
@@ -906,6 +907,7 @@ int BoxTree::insert_at_lod_internal(bool overwrite, U3 pos_u32, uint32_t insert_
         node_stack.pop_back();
         bounds_stack.pop_back();
     }
+    if (track_changes > 0) changes.push_back(Change{node_stack_clone, modified_bottom});  // insert.rs:401-404
     return 0;
 }
 

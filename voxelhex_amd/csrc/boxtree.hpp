@@ -12,11 +12,13 @@
 //   subdivide_leaf_to_nodes    src/boxtree/detail.rs:248-337, node_empty_at 156-224, deallocate_children_of 352-370
 //   execute_for_relevant_sectants src/boxtree/iterate.rs:40-121, get_node_internal 293-343
 //   BrickData helpers          src/boxtree/node.rs:34-145, NodeContent pix_* 259-373, is_all 424-458
-// Not restated (no effect on what the raytracer reads): occlusion bits (insert.rs:451-469), MIP maps (disabled by
-// default, mipmap.rs:42-44, 351-353), update triggers (insert.rs:401-404; streaming is out of scope).
+//   update triggers            insert.rs:328-405: (node stack, modified bottom sectants) of every insert/update, queued
+//                              for a stream like BoxTreeGPUHost's changes_buffer (src/raytracing/bevy/mod.rs:164-173)
+// Not restated (no effect on what the raytracer reads): MIP maps (disabled by default, mipmap.rs:42-44, 351-353).
 #pragma once
 
 #include <array>
+#include <deque>
 #include <functional>
 #include <cstddef>
 #include <utility>
@@ -103,6 +105,15 @@ class BoxTree {
 
     bool auto_simplify = true;
     uint32_t brick_dim = 0, boxtree_size = 0;
+    // BoxTreeUpdatedSignalParams (src/boxtree/types.rs:204) of every insert/update that changed the tree, queued while
+    // a stream tracks the tree (the trigger BoxTreeGPUHost::new installs, src/raytracing/bevy/mod.rs:164-173); the
+    // stream pops them in its upload (handle_tree_updates, src/raytracing/bevy/streaming/mod.rs:35-286)
+    struct Change {
+        std::vector<std::pair<size_t, uint8_t>> node_stack;
+        std::vector<uint8_t> updated_sectants;
+    };
+    mutable std::deque<Change> changes;
+    mutable int track_changes = 0;
     ObjectPool nodes;
     std::vector<uint32_t> color_palette;
     std::vector<uint32_t> data_palette;

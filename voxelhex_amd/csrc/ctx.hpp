@@ -49,6 +49,17 @@ struct vhx_ctx {
     std::vector<uint8_t> qargs_host[2];  // the QueueArgs last written to each slot (skips the upload when unchanged)
     void *qargs_host_ptr[2] = {nullptr, nullptr};  // qargs.ptr they were written to
     DevBuf state;     // saved traversal state per output index (64 B) of rays abandoned at a budget
+    // ranged writes (vhx_update_ranges): two pinned host staging slots, alternating, each reusable once the
+    // host-to-device copy that read it has completed (event), and the device staging buffer the scatter kernel reads
+    struct Pinned {
+        void *ptr = nullptr;
+        uint64_t bytes = 0;
+        hipEvent_t done = nullptr;
+        bool used = false;
+    } pinned[2];
+    uint32_t pinned_next = 0;
+    DevBuf upd;
+    hipStream_t upd_stream = nullptr;  // the stream of the last scatter (reads upd)
     // step budgets of the passes before the final (unbounded) one; VHX_BUDGETS="64" / "32,256" style override.
     // {24, 96, 768}: with four frames in flight (bench frame) 0.697 ms per frame against 0.847 for {64}, 0.715 for
     // {32, 128, 1024} and 0.740 for four budgets {16, 64, 256, 1024}: each pass re-packs the surviving rays into full

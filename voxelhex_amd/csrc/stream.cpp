@@ -12,18 +12,22 @@
 //   upload                             streaming/mod.rs:420-635 cache updates -> ranged writes
 //   view sizing                        view.rs:50-69; set_viewport: bevy/mod.rs:110-155 (brick slot hysteresis)
 //
-// Behavioural deviation: rebuild puts the whole root -> center access path into the view set (see rebuild).
+// Behavioural deviations: rebuild puts the whole root -> center access path into the view set (see rebuild); after
+// queued tree changes the view set is recomputed (see handle_tree_updates).
 // Differences in the layout the device kernel reads: node type is one u32 per node (not 2 bits
 // packed 16 per word), occupancy one u64, a Solid brick descriptor is 0x80000000 | index into a deduplicated solid
 // value table (the reference inlines the value, losing data-palette bits), MIP data is tracked for slot accounting
 // but never uploaded (the raytracer does not read MIPs). The reference computes the view set on a worker thread; here
 // `rebuild` runs synchronously when the viewport leaves its brick slot, so the upload order is deterministic.
-// Tree-change propagation (handle_tree_updates, streaming/mod.rs:36-288) is not restated: the tree must not be
-// modified while a stream uses it.
+// Tree-change propagation: inserts and updates made to the tree while a stream tracks it are queued by the tree
+// (BoxTree::changes, the update trigger of BoxTreeGPUHost::new) and re-uploaded by handle_tree_updates
+// (streaming/mod.rs:35-286) at the start of the next upload frames, before the regular upload queue.
 #include <algorithm>
 #include <array>
 #include <cmath>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <tuple>
@@ -129,6 +133,9 @@ struct vhx_stream {
     uint64_t cycle_work = 0, last_cycle_work = UINT64_MAX;
     bool walk_started = false;
 
+    ~vhx_stream() {
+        if (tree && --tree->track_changes == 0) tree->changes.clear();
+    }
     uint32_t bd() const { return tree->brick_dim; }
     uint32_t max_mip_level() const {  // boxtree/mod.rs:320-324
         const float l = std::ceil(std::log((float)tree->boxtree_size / (float)tree->brick_dim) / std::log(4.f));
@@ -610,6 +617,97 @@ struct vhx_stream {
         }
         return true;
     }
+    // handle_tree_updates, streaming/mod.rs:35-286: up to n queued tree changes, each re-uploading the root, the nodes
+    // along the change's access stack (with their MIP slots) and the changed bricks of its bottom node. Returns false
+    // when the view ran out of capacity (re_evaluate_view_size was applied; the updates so far are still written).
+    bool handle_tree_updates(std::vector<CacheUpdate> &updates, size_t n) {
+        for (size_t k = 0; k < n; ++k) {
+            if (tree->changes.empty()) break;
+            const BoxTree::Change ch = tree->changes.front();
+            tree->changes.pop_front();
+            if (ch.node_stack.empty()) continue;  // the reference asserts a root-first stack
+            auto add_mip = [&](size_t key) -> bool {  // MIP slot of a node: re-upload when owned, else a new slot
+                Owned mip;
+                mip.kind = 2;
+                mip.node = (uint32_t)key;
+                if (owner_has(mip)) return true;  // MIP data is Empty in this restatement: nothing to re-upload
+                CacheUpdate u;
+                if (!add_brick(mip, u)) return false;
+                updates.push_back(std::move(u));
+                return true;
+            };
+            {
+                CacheUpdate u;
+                if (!add_node(0, (uint8_t)kChildren, u)) return re_evaluate_view_size();
+                updates.push_back(std::move(u));
+            }
+            if (!add_mip(0)) return re_evaluate_view_size();
+            const size_t parent_key = ch.node_stack.back().first;
+            Cube node_bounds{f3(0.f, 0.f, 0.f), (float)tree->boxtree_size};
+            for (const auto &e : ch.node_stack) nodes_to_see.insert(e.first);
+            for (const auto &e : ch.node_stack) {
+                size_t ck;
+                if (valid_child(e.first, e.second, ck)) {  // BoxTree::valid_child_for
+                    CacheUpdate u;
+                    if (!add_node(e.first, e.second, u)) return re_evaluate_view_size();
+                    updates.push_back(std::move(u));
+                    if (!add_mip(ck)) return re_evaluate_view_size();
+                }
+                node_bounds = child_bounds_for(node_bounds, e.second);
+            }
+            // the bottom node's bricks: re-upload the resident ones, request slots for the others. Deviation: a
+            // sectant whose brick is not Parted (the reference only debug-asserts that it is) is skipped; add_node
+            // above already wrote its Solid / Empty descriptor
+            const Node &pn = node(parent_key);
+            auto brick_owner = [&](uint8_t sec, const Cube &b) {
+                Owned o;
+                o.kind = 1;
+                o.node = (uint32_t)parent_key;
+                o.sectant = sec;
+                o.bl = f3(std::round(b.min.x), std::round(b.min.y), std::round(b.min.z));
+                return o;
+            };
+            std::vector<Owned> fresh;
+            if (pn.content == Content::UniformLeaf && pn.bricks[0].kind == BrickKind::Parted) {
+                const Owned o = brick_owner(0, node_bounds);
+                auto it = brick_by_owner.find(o.key());
+                if (it != brick_by_owner.end()) {
+                    CacheUpdate u;
+                    u.brick_updates.push_back({it->second, o});
+                    updates.push_back(std::move(u));
+                } else {
+                    fresh.push_back(o);
+                }
+            } else if (pn.content == Content::Leaf) {
+                for (uint8_t sec : ch.updated_sectants) {
+                    if (sec >= kChildren || pn.bricks[sec].kind != BrickKind::Parted) continue;
+                    const Owned o = brick_owner(sec, child_bounds_for(node_bounds, sec));
+                    auto it = brick_by_owner.find(o.key());
+                    if (it != brick_by_owner.end()) {
+                        CacheUpdate u;
+                        u.brick_updates.push_back({it->second, o});
+                        updates.push_back(std::move(u));
+                    } else {
+                        fresh.push_back(o);
+                    }
+                }
+            }
+            for (const Owned &o : fresh) {
+                CacheUpdate u;
+                if (!add_brick(o, u)) return re_evaluate_view_size();
+                updates.push_back(std::move(u));
+            }
+            if (tree->changes.empty()) {
+                // Deviation: the reference only restarts the tree scan here; the view set is recomputed too, so
+                // nodes an edit created off its access path (the 64 nodes of a leaf subdivided by an insert, a new
+                // subtree's children) join the view and are uploaded by the scan, instead of staying missing until
+                // the viewport moves
+                rebuild(origin, view_distance);
+                target_node_stack = node_stack_init();  // restart the tree scan
+            }
+        }
+        return true;
+    }
     bool re_evaluate_view_size() {  // streaming/mod.rs:292-340
         const size_t need_nodes = nodes_to_see.size();
         if (need_nodes > nodes_in_view) nodes_in_view = (size_t)((float)need_nodes * 1.2f);
@@ -656,17 +754,48 @@ struct vhx_stream {
         resize = false;
         return VHX_OK;
     }
+    // the frame's ranged writes, issued together by flush() as one vhx_update_ranges call (one staged host-to-device
+    // copy and one scatter kernel per frame instead of one transfer per range); the sources are the host mirror's
+    // arrays, unchanged until the flush
+    std::vector<vhx_range> frame_writes;
     int write(int buf, size_t off, size_t n, const void *src) {
         if (n == 0) return VHX_OK;
         const size_t esz = buf == VHX_BUF_NODE_OCBITS ? 8 : 4;
         last_bytes += n * esz;
-        return ctx ? vhx_update_range(ctx, buf, off, n, src) : VHX_OK;
+        vhx_range r{};
+        r.buffer_id = buf;
+        r.elem_offset = off;
+        r.elem_count = n;
+        r.src = src;
+        frame_writes.push_back(r);
+        return VHX_OK;
     }
-    int upload_frame() {  // streaming/mod.rs:420-635
+    int flush() {
+        const int rc = ctx && !frame_writes.empty()
+                           ? vhx_update_ranges(ctx, frame_writes.data(), (uint32_t)frame_writes.size())
+                           : VHX_OK;
+        frame_writes.clear();
+        return rc;
+    }
+    int upload_frame() {
+        frame_writes.clear();
+        const int rc = collect_frame();
+        const int frc = flush();  // also after a capacity stop: what was decided before it is written, as before
+        return rc ? rc : frc;
+    }
+    int collect_frame() {  // streaming/mod.rs:420-635
         last_nodes = last_bricks = last_bytes = 0;
         if (resize) return VHX_E_CAPACITY;
         std::vector<CacheUpdate> updates;
-        const bool fits = process(updates);
+        // streaming::upload (streaming/mod.rs:446-457): a reloading view runs the upload queue; otherwise queued tree
+        // changes go first, and the upload queue runs in a frame without any
+        bool fits;
+        if (reload) {
+            fits = process(updates);
+        } else {
+            fits = handle_tree_updates(updates, node_uploads_per_frame);
+            if (fits && updates.empty()) fits = process(updates);
+        }
         int rc = VHX_OK;
         // palettes: deltas of the host tree's palettes (capacity kPaletteCapacity entries on the device)
         if (tree->color_palette.size() > kPaletteCapacity || tree->data_palette.size() > kPaletteCapacity)
@@ -746,6 +875,7 @@ int vhx_stream_create(const vhx_boxtree *tree, vhx_ctx *ctx, const float origin[
     *out = nullptr;
     auto s = std::make_unique<vhx_stream>();
     s->tree = tree->tree;
+    s->tree->track_changes += 1;  // the tree queues its changes for the stream (BoxTreeGPUHost::new's trigger)
     s->ctx = ctx;
     s->origin = f3(origin[0], origin[1], origin[2]);
     s->view_distance = view_distance;
@@ -802,7 +932,8 @@ int vhx_stream_upload(vhx_stream *s, vhx_stream_stats *stats) {
         stats->nodes_to_see = s->nodes_to_see.size();
         uint64_t missing = 0;
         for (size_t k : s->nodes_to_see) missing += s->meta_by_key.count(k) ? 0u : 1u;
-        stats->pending = missing + s->bricks_to_upload.size() + (s->last_cycle_work == 0 ? 0u : 1u);
+        stats->pending = missing + s->bricks_to_upload.size() + s->tree->changes.size() +
+                         (s->last_cycle_work == 0 ? 0u : 1u);
     }
     return rc;
 }

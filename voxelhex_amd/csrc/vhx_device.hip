@@ -10,6 +10,7 @@
 //   k_untile_rgba    scatters rank-gathered tile buffers into the framebuffer (multi-GPU screen-tile split)
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -91,19 +92,44 @@ __global__ void __launch_bounds__(256) k_brick_occ_small(const uint32_t *__restr
     words[b] = m;
 }
 
-// DevTree::child_rec for brick_dim <= 4: one record per child entry
+// DevTree::child_rec for brick_dim <= 4: one record per child entry. Entries [e0, e1) are visited; with sel, only the
+// entries of nodes [node_lo, node_hi) and those holding a Parted brick in [brick_lo, brick_hi) are rewritten (a ranged
+// update: the records of written nodes and of the nodes whose bricks were written)
+struct RecSel {
+    uint32_t sel, node_lo, node_hi, brick_lo, brick_hi;
+};
 __global__ void __launch_bounds__(256) k_child_rec(const uint32_t *__restrict__ type,
                                                    const uint32_t *__restrict__ children,
                                                    const uint64_t *__restrict__ words, uint32_t brick_count,
-                                                   uint64_t n, uint4 *__restrict__ rec) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t ty = type[i >> 6];
+                                                   uint64_t e0, uint64_t e1, RecSel s, uint4 *__restrict__ rec) {
+    const uint64_t i = e0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= e1) return;
+    const uint32_t node = (uint32_t)(i >> 6);
+    const uint32_t ty = type[node];
     const bool uniform = ty == VHX_NODE_UNIFORM_LEAF;
     const uint32_t v = children[uniform ? (i & ~63ull) : i];
-    uint64_t o = 0;
-    if ((uniform || ty == VHX_NODE_LEAF) && v != VHX_EMPTY && (v & VHX_SOLID_BIT) == 0 && v < brick_count) o = words[v];
+    const bool parted = (uniform || ty == VHX_NODE_LEAF) && v != VHX_EMPTY && (v & VHX_SOLID_BIT) == 0 && v < brick_count;
+    if (s.sel && !(node >= s.node_lo && node < s.node_hi) && !(parted && v >= s.brick_lo && v < s.brick_hi)) return;
+    const uint64_t o = parted ? words[v] : 0ull;
     rec[i] = make_uint4(v, (uint32_t)o, (uint32_t)(o >> 32), 0u);
+}
+
+// Ranged writes: job j copies `words` 32-bit words from the staging buffer at src_off to the device address dst (a
+// range cut into pieces of at most 16 KiB, one workgroup per piece)
+struct UpdJob {
+    uint64_t dst, src_off;
+    uint32_t words, pad0;
+    uint64_t pad1;
+};
+#define UPD_PIECE_BYTES 16384u
+__global__ void __launch_bounds__(256) k_scatter_ranges(const uint8_t *__restrict__ stage, uint32_t j0, uint32_t j1) {
+    const UpdJob *jobs = (const UpdJob *)stage;
+    for (uint32_t j = j0 + blockIdx.x; j < j1; j += gridDim.x) {
+        const UpdJob jb = jobs[j];
+        const uint32_t *src = (const uint32_t *)(stage + jb.src_off);
+        uint32_t *dst = (uint32_t *)jb.dst;
+        for (uint32_t w = threadIdx.x; w < jb.words; w += blockDim.x) dst[w] = src[w];
+    }
 }
 
 __global__ void __launch_bounds__(256) k_pack_hdr(const uint32_t *__restrict__ type, const uint64_t *__restrict__ occ,
@@ -728,9 +754,27 @@ static int refresh_child_rec(vhx_ctx *c) {
     const uint64_t n = (uint64_t)c->tree->desc.node_count * 64;
     k_child_rec<<<(unsigned)((n + 255) / 256), 256, 0, c->stream>>>(
         (const uint32_t *)c->tree->raw[VHX_BUF_NODE_TYPE].ptr, (const uint32_t *)c->tree->raw[VHX_BUF_NODE_CHILDREN].ptr,
-        (const uint64_t *)c->tree->brick_occ.ptr, c->tree->desc.brick_count, n, (uint4 *)c->tree->child_rec.ptr);
+        (const uint64_t *)c->tree->brick_occ.ptr, c->tree->desc.brick_count, 0, n, RecSel{0, 0, 0, 0, 0},
+        (uint4 *)c->tree->child_rec.ptr);
     VHX_HIP(c, hipGetLastError());
     c->tree->child_rec_stale = false;
+    return VHX_OK;
+}
+
+// The child records of nodes [node_lo, node_hi) and of the nodes holding Parted bricks [brick_lo, brick_hi) (either
+// range may be empty): a pass over the written nodes' entries, or over every child entry when bricks were written (the
+// brick -> holder relation lives only in the children array; reading it is 256 B per node, the records are 1 KB).
+static int refresh_child_rec_sel(vhx_ctx *c, uint32_t node_lo, uint32_t node_hi, uint32_t brick_lo, uint32_t brick_hi) {
+    if (!has_child_rec(c) || c->tree->child_rec_stale) return VHX_OK;  // a stale buffer is rebuilt whole anyway
+    const bool bricks = brick_lo < brick_hi, nodes = node_lo < node_hi;
+    if (!bricks && !nodes) return VHX_OK;
+    const uint64_t e0 = bricks ? 0 : (uint64_t)node_lo * 64, e1 = bricks ? (uint64_t)c->tree->desc.node_count * 64
+                                                                           : (uint64_t)node_hi * 64;
+    k_child_rec<<<(unsigned)((e1 - e0 + 255) / 256), 256, 0, c->stream>>>(
+        (const uint32_t *)c->tree->raw[VHX_BUF_NODE_TYPE].ptr, (const uint32_t *)c->tree->raw[VHX_BUF_NODE_CHILDREN].ptr,
+        (const uint64_t *)c->tree->brick_occ.ptr, c->tree->desc.brick_count, e0, e1,
+        RecSel{1, node_lo, node_hi, brick_lo, brick_hi}, (uint4 *)c->tree->child_rec.ptr);
+    VHX_HIP(c, hipGetLastError());
     return VHX_OK;
 }
 
@@ -1066,8 +1110,12 @@ void vhx_destroy(vhx_ctx *c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     c->tree.reset();  // frees the device tree with its last context
     for (DevBuf *b : {&c->scratch, &c->rays, &c->queue[0], &c->queue[1], &c->qctl, &c->tmp, &c->counts, &c->offsets,
-                      &c->flags, &c->qargs, &c->state})
+                      &c->flags, &c->qargs, &c->state, &c->upd})
         if (b->ptr) (void)hipFree(b->ptr);
+    for (auto &P : c->pinned) {
+        if (P.ptr) (void)hipHostFree(P.ptr);
+        if (P.done) (void)hipEventDestroy(P.done);
+    }
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -1187,29 +1235,132 @@ int vhx_upload_tree(vhx_ctx *c, const vhx_tree_desc *t) {
     return finish_upload(c);
 }
 
-int vhx_update_range(vhx_ctx *c, int id, uint64_t off, uint64_t count, const void *src) {
-    if (!c || id < 0 || id > 6 || (!src && count)) return VHX_E_INVALID_ARG;
-    if (c->shared) return fail(c, VHX_E_STATE, "vhx_update_range on a shared context: update through the owner");
-    if (!c->tree->uploaded) return fail(c, VHX_E_STATE, "vhx_update_range before vhx_upload_tree");
-    const uint64_t cap = elem_count(c->tree->desc, id);
-    if (off + count > cap) return fail(c, VHX_E_CAPACITY, "vhx_update_range: range beyond the uploaded buffer");
-    if (count == 0) return VHX_OK;
+int vhx_update_ranges(vhx_ctx *c, const vhx_range *r, uint32_t n) {
+    if (!c || (n && !r)) return VHX_E_INVALID_ARG;
+    if (c->shared) return fail(c, VHX_E_STATE, "vhx_update_range(s) on a shared context: update through the owner");
+    if (!c->tree->uploaded) return fail(c, VHX_E_STATE, "vhx_update_range(s) before vhx_upload_tree");
+    // validate every range first: a failing call writes nothing
+    uint64_t data_bytes = 0, njobs = 0;
+    for (uint32_t k = 0; k < n; ++k) {
+        if (r[k].buffer_id < 0 || r[k].buffer_id > 6 || (!r[k].src && r[k].elem_count)) return VHX_E_INVALID_ARG;
+        const uint64_t cap = elem_count(c->tree->desc, r[k].buffer_id);
+        if (r[k].elem_offset > cap || r[k].elem_count > cap - r[k].elem_offset)
+            return fail(c, VHX_E_CAPACITY, "vhx_update_range(s): range beyond the uploaded buffer");
+        const uint64_t bytes = r[k].elem_count * elem_size(r[k].buffer_id);
+        data_bytes += (bytes + 15) & ~15ull;
+        njobs += (bytes + UPD_PIECE_BYTES - 1) / UPD_PIECE_BYTES;
+    }
+    if (data_bytes == 0) return VHX_OK;
+    if (njobs > 0xFFFFFFFFull) return fail(c, VHX_E_INVALID_ARG, "vhx_update_ranges: too much data in one call");
     VHX_HIP(c, hipSetDevice(c->device));
     VHX_STREAM(c);
-    const uint64_t es = elem_size(id);
-    VHX_HIP(c, hipMemcpyAsync((char *)c->tree->raw[id].ptr + off * es, src, count * es, hipMemcpyHostToDevice, c->stream));
-    int rc = VHX_OK;
-    const uint64_t n3 = (uint64_t)c->tree->desc.brick_dim * c->tree->desc.brick_dim * c->tree->desc.brick_dim;
-    if (id == VHX_BUF_NODE_TYPE || id == VHX_BUF_NODE_OCBITS) rc = rebuild_hdr(c, (uint32_t)off, (uint32_t)count);
-    else if (id == VHX_BUF_VOXELS) {
-        const uint64_t b0 = off / n3, b1 = (off + count + n3 - 1) / n3;
-        rc = rebuild_occ(c, (uint32_t)b0, (uint32_t)(b1 - b0));
-    } else if (id == VHX_BUF_COLOR_PALETTE || id == VHX_BUF_DATA_PALETTE)
-        rc = rebuild_occ(c, 0, c->tree->desc.brick_count);
+    // pinned staging slot (the one used two calls ago: its copy has normally long completed)
+    vhx_ctx::Pinned &P = c->pinned[c->pinned_next];
+    c->pinned_next ^= 1u;
+    if (P.used) VHX_HIP(c, hipEventSynchronize(P.done));
+    const uint64_t jobs_bytes = (njobs * sizeof(UpdJob) + 255) & ~255ull, total = jobs_bytes + data_bytes;
+    if (P.bytes < total) {
+        if (P.ptr) VHX_HIP(c, hipHostFree(P.ptr));
+        P.ptr = nullptr;
+        P.bytes = 0;
+        const uint64_t want = std::max<uint64_t>(total + total / 4, 1ull << 20);
+        VHX_HIP(c, hipHostMalloc(&P.ptr, want, hipHostMallocDefault));
+        P.bytes = want;
+    }
+    if (!P.done) VHX_HIP(c, hipEventCreateWithFlags(&P.done, hipEventDisableTiming));
+    // the device staging buffer: the previous batch's scatter may still read it (on this stream, or on the stream the
+    // context used then), so a growth or a stream change waits for it
+    if (c->upd_stream && (c->upd_stream != c->stream || c->upd.bytes < P.bytes))
+        VHX_HIP(c, hipStreamSynchronize(c->upd_stream));
+    int rc = ensure(c, c->upd, P.bytes);
     if (rc) return rc;
-    if (id != VHX_BUF_NODE_OCBITS && id != VHX_BUF_SOLID_VALUES) c->tree->child_rec_stale = true;
-    VHX_HIP(c, hipStreamSynchronize(c->stream));
-    return VHX_OK;
+    c->upd_stream = c->stream;
+    // pack: the job table, then each range's data (16-byte aligned)
+    UpdJob *jobs = (UpdJob *)P.ptr;
+    uint64_t off = jobs_bytes, j = 0;
+    // ranges of one scatter launch are written in no particular order, so a range that overlaps an earlier range of
+    // the call starts a new launch (launches on a stream run in order: the later write wins, as in a sequence of
+    // write_range_to_buffer calls)
+    std::vector<uint32_t> group_start{0};
+    std::vector<std::pair<uint64_t, uint64_t>> group_spans[7];  // byte spans of the current group, per buffer
+    uint32_t node_lo = UINT32_MAX, node_hi = 0, hdr_lo = UINT32_MAX, hdr_hi = 0, brick_lo = UINT32_MAX, brick_hi = 0;
+    bool palette = false;
+    const uint64_t n3 = (uint64_t)c->tree->desc.brick_dim * c->tree->desc.brick_dim * c->tree->desc.brick_dim;
+    for (uint32_t k = 0; k < n; ++k) {
+        const int id = r[k].buffer_id;
+        const uint64_t es = elem_size(id), bytes = r[k].elem_count * es;
+        if (!bytes) continue;
+        std::memcpy((uint8_t *)P.ptr + off, r[k].src, bytes);
+        const uint64_t dst = (uint64_t)(uintptr_t)c->tree->raw[id].ptr + r[k].elem_offset * es;
+        {
+            const uint64_t b0 = r[k].elem_offset * es, b1 = b0 + bytes;
+            bool overlaps = false;
+            for (const auto &sp : group_spans[id]) overlaps |= b0 < sp.second && sp.first < b1;
+            if (overlaps) {
+                group_start.push_back((uint32_t)j);
+                for (auto &g : group_spans) g.clear();
+            }
+            group_spans[id].push_back({b0, b1});
+        }
+        for (uint64_t p = 0; p < bytes; p += UPD_PIECE_BYTES) {
+            UpdJob &jb = jobs[j++];
+            jb.dst = dst + p;
+            jb.src_off = off + p;
+            jb.words = (uint32_t)(std::min<uint64_t>(UPD_PIECE_BYTES, bytes - p) / 4);
+            jb.pad0 = 0;
+            jb.pad1 = 0;
+        }
+        off += (bytes + 15) & ~15ull;
+        const uint64_t e0 = r[k].elem_offset, e1 = e0 + r[k].elem_count;
+        if (id == VHX_BUF_NODE_TYPE || id == VHX_BUF_NODE_OCBITS) {
+            hdr_lo = std::min<uint32_t>(hdr_lo, (uint32_t)e0);
+            hdr_hi = std::max<uint32_t>(hdr_hi, (uint32_t)e1);
+        }
+        if (id == VHX_BUF_NODE_TYPE) {
+            node_lo = std::min<uint32_t>(node_lo, (uint32_t)e0);
+            node_hi = std::max<uint32_t>(node_hi, (uint32_t)e1);
+        } else if (id == VHX_BUF_NODE_CHILDREN) {
+            node_lo = std::min<uint32_t>(node_lo, (uint32_t)(e0 / 64));
+            node_hi = std::max<uint32_t>(node_hi, (uint32_t)((e1 + 63) / 64));
+        } else if (id == VHX_BUF_VOXELS) {
+            brick_lo = std::min<uint32_t>(brick_lo, (uint32_t)(e0 / n3));
+            brick_hi = std::max<uint32_t>(brick_hi, (uint32_t)((e1 + n3 - 1) / n3));
+        } else if (id == VHX_BUF_COLOR_PALETTE || id == VHX_BUF_DATA_PALETTE) {
+            palette = true;
+        }
+    }
+    // one host-to-device copy of the packed batch, one scatter kernel
+    VHX_HIP(c, hipMemcpyAsync(c->upd.ptr, P.ptr, total, hipMemcpyHostToDevice, c->stream));
+    VHX_HIP(c, hipEventRecord(P.done, c->stream));
+    P.used = true;
+    group_start.push_back((uint32_t)j);
+    for (size_t g = 0; g + 1 < group_start.size(); ++g) {
+        const uint32_t j0 = group_start[g], j1 = group_start[g + 1];
+        if (j1 > j0)
+            k_scatter_ranges<<<std::min<uint32_t>(j1 - j0, 8192u), 256, 0, c->stream>>>((const uint8_t *)c->upd.ptr,
+                                                                                         j0, j1);
+    }
+    VHX_HIP(c, hipGetLastError());
+    // derived state, stream-ordered
+    if (hdr_lo < hdr_hi && (rc = rebuild_hdr(c, hdr_lo, hdr_hi - hdr_lo))) return rc;
+    if (palette) {
+        // emptiness of any cell may change: every bitmap and record
+        if ((rc = rebuild_occ(c, 0, c->tree->desc.brick_count))) return rc;
+        c->tree->child_rec_stale = true;
+        return refresh_child_rec(c);
+    }
+    if (brick_lo < brick_hi && (rc = rebuild_occ(c, brick_lo, brick_hi - brick_lo))) return rc;
+    return refresh_child_rec_sel(c, node_lo, node_hi, brick_lo, brick_hi);
+}
+
+int vhx_update_range(vhx_ctx *c, int id, uint64_t off, uint64_t count, const void *src) {
+    if (!c || id < 0 || id > 6 || (!src && count)) return VHX_E_INVALID_ARG;
+    vhx_range r{};
+    r.buffer_id = id;
+    r.elem_offset = off;
+    r.elem_count = count;
+    r.src = src;
+    return vhx_update_ranges(c, &r, 1);
 }
 
 int vhx_read_derived(vhx_ctx *c, int which, uint64_t off, uint64_t count, void *dst) {

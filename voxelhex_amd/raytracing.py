@@ -229,6 +229,14 @@ class Raytracer:
         values = np.ascontiguousarray(values)
         self._check(N.lib().vhx_update_range(self._h, buffer_id, elem_offset, values.size, values.ctypes.data))
 
+    def update_ranges(self, writes):
+        """vhx_update_ranges: writes = [(buffer_id, elem_offset, values), ...] in one staged copy + scatter."""
+        keep = [np.ascontiguousarray(v) for _, _, v in writes]
+        rs = (N.Range * max(1, len(writes)))()
+        for r, (bid, off, _), v in zip(rs, writes, keep):
+            r.buffer_id, r.elem_offset, r.elem_count, r.src = bid, off, v.size, v.ctypes.data
+        self._check(N.lib().vhx_update_ranges(self._h, ctypes.cast(rs, ctypes.c_void_p), len(writes)))
+
     def read_derived(self, which, offset, count):
         dt = np.uint32 if which == N.VHX_DERIVED_NODE_HDR else np.uint64
         k = 4 if which == N.VHX_DERIVED_NODE_HDR else 1
