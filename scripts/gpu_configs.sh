@@ -15,6 +15,8 @@ run c2_512_bd8 --size 512 --brick-dim 8 --width 1920 --height 1080 && \
 run c3_1024_bd16 --size 1024 --brick-dim 16 --no-cpu-baseline && \
 run c3_heightfield --scene 6 --no-cpu-baseline && \
 run c5_shadows --shadows && \
+run c5_shadows_f1 --shadows --inflight 1 && \
+run c3_headline_f1 --inflight 1 --no-cpu-baseline && \
 if [ -f scratch/gingerbread_house_by_kirra_luan.vox ]; then
   run c3_vox_gingerbread_bd8 --vox scratch/gingerbread_house_by_kirra_luan.vox --brick-dim 8 && \
   run c3_vox_gingerbread_bd4 --vox scratch/gingerbread_house_by_kirra_luan.vox --brick-dim 4
