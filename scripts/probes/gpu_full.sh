@@ -16,4 +16,4 @@ cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$R/gpurun_out/prof" -o bench -- python3 "$R/bench.py" --steps 10 --warmup 2 --no-cpu-baseline > "$R/gpurun_out/prof_bench.log" 2>&1; rc=$?
 echo "rocprof rc=$rc"; tail -1 "$R/gpurun_out/prof_bench.log"
 [ $rc -ne 0 ] && exit $rc
-bash "$R/scripts/gpu_pmc_traffic.sh"
+bash "$R/scripts/probes/gpu_pmc_traffic.sh"

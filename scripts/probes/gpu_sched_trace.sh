@@ -1,6 +1,6 @@
 #!/bin/bash
 # Kernel traces of the bench frame under several multi-pass schedules ('+'-joined env items in $SCHEDULES), to see
-# each pass's duration; summarised by scripts/pass_times.py.
+# each pass's duration; summarised by scripts/probes/pass_times.py.
 cd "$GRAFT_REPO_ROOT" || exit 1
 R="$GRAFT_REPO_ROOT"; D="$R/gpurun_out/sched_trace"; mkdir -p "$D"
 cd /tmp && export TMPDIR=/tmp
@@ -13,6 +13,6 @@ for item in $SCHEDULES; do
   for e in $envs; do unset "${e%%=*}"; done
   echo "[$item] rc=$rc"
   [ $rc -ne 0 ] && exit $rc
-  python3 "$R/scripts/pass_times.py" "$D/s${i}_kernel_trace.csv"
+  python3 "$R/scripts/probes/pass_times.py" "$D/s${i}_kernel_trace.csv"
 done
 exit 0

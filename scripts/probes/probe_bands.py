@@ -6,7 +6,7 @@ copy and HIP stream), band b on context b % C, so band b's tail can run while ba
 usage: probe_bands.py K C [frames]"""
 import os, sys, time
 import numpy as np
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import torch
 import voxelhex_amd as vhx
 from voxelhex_amd import _native as N

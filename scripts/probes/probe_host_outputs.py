@@ -2,7 +2,7 @@
 C ABI copies the results back over PCIe before returning), against device-resident outputs. Wall time per frame,
 median of 10 after 2 warm-up frames.  usage: probe_host_outputs.py"""
 import os, sys, time
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import numpy as np
 import torch
 import voxelhex_amd as vhx

@@ -5,7 +5,7 @@ as in bench.py; this times that launch for each rank of N = 1, 2, 4, 8 (N = 1: t
 per-rank time behind the multi-GPU bench line can be seen on a single GPU.
 usage: probe_rank_share.py [frames]"""
 import os, sys, time
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import numpy as np
 import torch
 import voxelhex_amd as vhx

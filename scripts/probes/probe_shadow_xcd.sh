@@ -1,6 +1,6 @@
 #!/bin/bash
 # Shadow frames one at a time: kernel traces with the budgeted shadow passes dealt over the XCDs (VHX_QXCD_ALL=1) or
-# not, for budgets 64 and 24,96,768 (per-pass durations: scripts/pass_times.py style summary below)
+# not, for budgets 64 and 24,96,768 (per-pass durations: scripts/probes/pass_times.py style summary below)
 cd "$GRAFT_REPO_ROOT" || exit 1
 D="$GRAFT_REPO_ROOT/gpurun_out/shadow_xcd"; mkdir -p "$D"
 cd /tmp && export TMPDIR=/tmp

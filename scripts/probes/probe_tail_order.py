@@ -7,7 +7,7 @@ a bucket), and sorted by the true step count (an upper bound). Prints the launch
 usage: probe_tail_order.py PIXELS.npz"""
 import os, sys
 import numpy as np
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import voxelhex_amd as vhx
 from voxelhex_amd import _native as N
 
