@@ -69,6 +69,9 @@ def parse():
                    help="moving camera: frame k (warm-up included) views from angle 40 + k*ORBIT rad on the glass "
                         "camera's circle (0 = the reference bench's static camera); the roofline bytes are then the "
                         "mean of the first, middle and last timed views")
+    p.add_argument("--depth-prepass", type=float, default=None, metavar="MARGIN",
+                   help="opt-in approximate mode (vhx_set_depth_prepass, not the reference semantics): a half-resolution "
+                        "depth prepass, full-resolution rays start at the min of 4 texels minus MARGIN")
     p.add_argument("--no-overlap", action="store_true",
                    help="N>1: gather each frame before tracing the next (default: frame k's gather overlaps k+1)")
     return p.parse_args()
@@ -274,6 +277,8 @@ def main():
         fb_depth = torch.zeros(W * H, dtype=torch.float32, device=dev)
     # frames in flight (single-GPU and torch paths; vhx_mgpu keeps its own): F contexts sharing the tree, F streams,
     # F output sets
+    if args.depth_prepass is not None:
+        rt.set_depth_prepass(True, args.depth_prepass)  # shared contexts inherit it
     rts, streams, outs = [rt], [stream], []
     if mg is None:
         for _ in range(F - 1):
@@ -385,7 +390,8 @@ def main():
 
     scene_tag = f"vox:{os.path.basename(args.vox)}" if args.vox else f"S{args.scene}"
     workload = f"primary {W}x{H} {scene_tag} {args.size}^3 bd{args.brick_dim} ranks{world}" + (
-        f" orbit{args.orbit}" if args.orbit else "")
+        f" orbit{args.orbit}" if args.orbit else "") + (
+        f" prepass{args.depth_prepass}" if args.depth_prepass is not None else "")
     total_rays = W * H
     n_shadow = 0
     if args.shadows:
@@ -496,6 +502,8 @@ def main():
                                       else "procedural scene S (lattice+cube)")
                                    + f", brick_dim {args.brick_dim}, glass camera"
                                    + (f" orbiting {args.orbit} rad per frame" if args.orbit else "")
+                                   + (f", APPROXIMATE depth-prepass mode (margin {args.depth_prepass}; not the "
+                                      "reference semantics)" if args.depth_prepass is not None else "")
                                    + (f", {T}x{T} tiles round-robin over {world} ranks" if world > 1 else ""),
                        "workload_key": workload,
                        "shadow_rays_per_frame": n_shadow if args.shadows else None,

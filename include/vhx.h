@@ -206,6 +206,15 @@ int vhx_tree_device_bytes(const vhx_ctx *ctx, uint64_t *bytes);
  * (host outputs). */
 int vhx_trace_primary(vhx_ctx *ctx, const vhx_camera *cam, uint32_t tile_size, uint32_t tile_start,
                       uint32_t tile_stride, uint32_t layout, const vhx_hits *out, int on_device);
+/* Depth-prepass fast mode (opt-in; NOT the reference's CPU semantics, so outside the parity bar; the WGSL path's
+ * prepass, src/raytracing/bevy/viewport_render.wgsl:702-726). When enabled, a vhx_trace_primary of a whole frame in
+ * the FRAMEBUFFER layout without byte counting first traces a half-resolution depth frame (texel (X, Y) through the
+ * centre of full pixels 2X..2X+1, 2Y..2Y+1), then starts every full-resolution ray at the minimum of depth texels
+ * (x/2, y/2), (x/2+1, y/2), (x/2, y/2+1), (x/2+1, y/2+1) minus `margin` (distance units; 0 = the WGSL's choice), and
+ * reports a miss where all four texels missed. Thin or grazing geometry that none of the four texel rays hits first can
+ * be skipped: the pixels that differ from the exact path are measured in tests/test_gpu_fast.py and DESIGN.md §10.
+ * Other traces (tiles, ray batches, shadows, byte counting) stay exact. Default off. */
+int vhx_set_depth_prepass(vhx_ctx *ctx, int enable, float margin);
 /* Traces n explicit rays; rays = 6 f32 per ray (origin xyz, direction xyz), host or device per on_device. */
 int vhx_trace_rays(vhx_ctx *ctx, const float *rays, uint64_t n, const vhx_hits *out, int on_device);
 /* Hard shadows (BASELINE config 5; the reference has no shadow rays — semantics defined in DESIGN.md §9): for

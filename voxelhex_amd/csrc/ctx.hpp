@@ -60,6 +60,10 @@ struct vhx_ctx {
     uint32_t pinned_next = 0;
     DevBuf upd;
     hipStream_t upd_stream = nullptr;  // the stream of the last scatter (reads upd)
+    // depth-prepass mode (vhx_set_depth_prepass; opt-in, not the reference path)
+    bool prepass = false, in_prepass = false;
+    float prepass_margin = 0.0f;
+    DevBuf prepass_depth;  // the half-resolution depth frame
     // step budgets of the passes before the final (unbounded) one; VHX_BUDGETS="64" / "32,256" style override.
     // {24, 96, 768}: with four frames in flight (bench frame) 0.697 ms per frame against 0.847 for {64}, 0.715 for
     // {32, 128, 1024} and 0.740 for four budgets {16, 64, 256, 1024}: each pass re-packs the surviving rays into full

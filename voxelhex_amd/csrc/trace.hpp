@@ -418,8 +418,12 @@ struct Trav {
     int32_t hflat;
 
     // false: the ray misses the root cube (a miss, nothing more to do)
+    // START (the opt-in depth-prepass mode, not the reference path): the ray enters the tree no earlier than `start`
+    // along its direction (the prepass's min-of-4 distance, viewport_render.wgsl:714-726); the exact path is START =
+    // false and compiles to the same code as before.
+    template <bool START = false>
     __device__ __forceinline__ bool begin(const DevTree &t, F3d o, F3d d, HitOut &h, const uint4 *sbase, uint32_t sidx,
-                                          bool resume) {
+                                          bool resume, float start = 0.0f) {
         h.hit = false;
         ray_setup(r, o, d);
         {
@@ -460,7 +464,15 @@ struct Trav {
                 ex = 2u;
                 return false;
             }
-            p = vadd(o, vmul(d, tmin < 0.0f ? 0.0f : tmin));
+            float t0 = tmin < 0.0f ? 0.0f : tmin;
+            if (START) {
+                if (!(start <= tmax)) {  // the neighbourhood's prepass rays left the tree (or start is +inf): a miss
+                    ex = 2u;
+                    return false;
+                }
+                t0 = __builtin_fmaxf(t0, start);
+            }
+            p = vadd(o, vmul(d, t0));
             target = offset_sectant(p, cur.size);
             tb = child_bounds(cur, target);
             node = 0, s1 = 0, s2 = 0, s3 = 0, count = 1;  // push(ROOT)
@@ -617,12 +629,12 @@ struct Trav {
     }
 };
 
-template <bool COUNT, int BD>
+template <bool COUNT, int BD, bool START = false>
 __device__ __forceinline__ bool get_by_ray(const DevTree &t, const uint64_t *occ_tab, F3d o, F3d d, HitOut &h,
                                            uint32_t budget, uint4 *sbase = nullptr, uint32_t sidx = 0,
-                                           bool resume = false) {
+                                           bool resume = false, float start = 0.0f) {
     Trav<COUNT, BD> tr;
-    if (!tr.begin(t, o, d, h, sbase, sidx, resume)) return true;
+    if (!tr.template begin<START>(t, o, d, h, sbase, sidx, resume, start)) return true;
     for (;;) {
         tr.step(t, occ_tab, h, budget);
         if (tr.ex != 0u) break;

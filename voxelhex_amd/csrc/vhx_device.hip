@@ -477,11 +477,27 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t bid, uint32_t n, uint32_t
 
 // One workgroup = 256 lanes = a 16x16 pixel block made of four 8x8 wave tiles (wave64-coherent ray bundles, the
 // 8x8 footprint of the reference's @workgroup_size(8, 8, 1)). Blocks are dealt tile by tile.
-template <bool COUNT, int BD>
+// Depth-prepass mode (opt-in, not the reference path; SURVEY.md 8f #4, viewport_render.wgsl:702-726): a half-resolution
+// depth frame traced first; a full-resolution ray starts at the minimum of the 4 depth texels (x/2, y/2) .. (x/2 + 1,
+// y/2 + 1) (clamped at the edge) minus `margin`, and misses outright where that minimum is +inf (all four missed)
+struct FastD {
+    const float *depth;
+    uint32_t w, h;
+    float margin;
+};
+__device__ __forceinline__ float prepass_start(const FastD &f, uint32_t px, uint32_t py) {
+    const uint32_t x0 = px >> 1, y0 = py >> 1;
+    const uint32_t x1 = x0 + 1 < f.w ? x0 + 1 : f.w - 1, y1 = y0 + 1 < f.h ? y0 + 1 : f.h - 1;
+    const float m = __builtin_fminf(__builtin_fminf(f.depth[(uint64_t)y0 * f.w + x0], f.depth[(uint64_t)y1 * f.w + x0]),
+                                    __builtin_fminf(f.depth[(uint64_t)y0 * f.w + x1], f.depth[(uint64_t)y1 * f.w + x1]));
+    return m - f.margin;
+}
+
+template <bool COUNT, int BD, bool FAST = false>
 __global__ void __launch_bounds__(256) VHX_PRIMARY_ATTR k_trace_primary(DevTree t, CamD cam, OutD out, uint32_t T, uint32_t tiles_x,
                                                        uint32_t tile_start, uint32_t tile_stride, uint32_t layout,
                                                        uint32_t blocks_per_tile_x, uint32_t blocks_per_tile,
-                                                       PassQ q) {
+                                                       PassQ q, FastD fast = FastD{}) {
     __shared__ uint64_t occ_tab[512];
     fill_occ_tab(occ_tab);
     __syncthreads();
@@ -502,7 +518,8 @@ __global__ void __launch_bounds__(256) VHX_PRIMARY_ATTR k_trace_primary(DevTree 
         primary_ray(cam, px, py, o, d);
         HitOut h;
         h.bytes = 0;
-        done = get_by_ray<COUNT, BD>(t, occ_tab, o, d, h, q.budget, q.state, (uint32_t)idx);
+        const float start = FAST ? prepass_start(fast, px, py) : 0.0f;
+        done = get_by_ray<COUNT, BD, FAST>(t, occ_tab, o, d, h, q.budget, q.state, (uint32_t)idx, false, start);
         if (done)
             store(t, out, idx, o, h);
         else if (COUNT && q.state)
@@ -1100,6 +1117,8 @@ int vhx_create_shared(const vhx_ctx *owner, vhx_ctx **out) {
     c->queue_waves_mid = owner->queue_waves_mid;
     c->qxcd = owner->qxcd;
     c->qxcd_all = owner->qxcd_all;
+    c->prepass = owner->prepass;
+    c->prepass_margin = owner->prepass_margin;
     *out = c;
     return VHX_OK;
 }
@@ -1110,7 +1129,7 @@ void vhx_destroy(vhx_ctx *c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     c->tree.reset();  // frees the device tree with its last context
     for (DevBuf *b : {&c->scratch, &c->rays, &c->queue[0], &c->queue[1], &c->qctl, &c->tmp, &c->counts, &c->offsets,
-                      &c->flags, &c->qargs, &c->state, &c->upd})
+                      &c->flags, &c->qargs, &c->state, &c->upd, &c->prepass_depth})
         if (b->ptr) (void)hipFree(b->ptr);
     for (auto &P : c->pinned) {
         if (P.ptr) (void)hipHostFree(P.ptr);
@@ -1448,7 +1467,34 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
     src.tiles_x = tiles_x;
     src.tile_start = tile_start;
     src.tile_stride = tile_stride;
-    VHX_HIP(c, hipEventRecord(c->ev0, c->stream));
+    if (!c->in_prepass) VHX_HIP(c, hipEventRecord(c->ev0, c->stream));
+    // depth-prepass mode (vhx_set_depth_prepass): a whole framebuffer frame without byte counting first traces the
+    // half-resolution depth frame (a nested call, same stream), then the full frame starts from it
+    const bool fast = c->prepass && !c->in_prepass && layout == VHX_LAYOUT_FRAMEBUFFER && tile_start == 0 &&
+                      tile_stride == 1 && !out->bytes;
+    FastD fd{};
+    if (fast) {
+        vhx_camera hc = *cam;
+        hc.width = (cam->width + 1) / 2;
+        hc.height = (cam->height + 1) / 2;
+        if (cam->ray_model == VHX_RAY_GLASS) {
+            // texel (X, Y) looks through the centre of full pixels 2X..2X+1, 2Y..2Y+1 (y counted upward in the glass)
+            const float ox = 0.5f * cam->pixel_width, oy = ((float)cam->height + 0.5f - 2.0f * (float)hc.height) * cam->pixel_height;
+            for (int k = 0; k < 3; ++k)
+                hc.glass_bottom_left[k] = cam->glass_bottom_left[k] + cam->glass_right[k] * ox + cam->glass_up[k] * oy;
+            hc.pixel_width = 2.0f * cam->pixel_width;
+            hc.pixel_height = 2.0f * cam->pixel_height;
+        }
+        int rc2 = ensure(c, c->prepass_depth, (uint64_t)hc.width * hc.height * 4);
+        if (rc2) return rc2;
+        vhx_hits dh{};
+        dh.depth = (float *)c->prepass_depth.ptr;
+        c->in_prepass = true;
+        rc2 = vhx_trace_primary(c, &hc, 0, 0, 1, VHX_LAYOUT_FRAMEBUFFER, &dh, 1);
+        c->in_prepass = false;
+        if (rc2) return rc2;
+        fd = FastD{(const float *)c->prepass_depth.ptr, hc.width, hc.height, c->prepass_margin};
+    }
     // no reset_passes: the flag compaction after pass 0 zeroes the queue passes' counters.
     // A rank-sharded framebuffer (tile_start > 0 or tile_stride > 1) leaves the flags of other ranks' pixels unwritten,
     // while the compaction scans every pixel: they are cleared first (stale flags would queue foreign pixels)
@@ -1466,17 +1512,29 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
                 t, cd, ho.dev, T, tiles_x, tile_start, tile_stride, layout, bpx, bpt, q0);
             qrc = launch_queue_passes<true, BD>(c, t, cd, src, ho.dev, 1, npass, nout, nblocks, true);
         } else {
-            k_trace_primary<false, BD><<<(unsigned)nblocks, 256, 0, c->stream>>>(
-                t, cd, ho.dev, T, tiles_x, tile_start, tile_stride, layout, bpx, bpt, q0);
+            if (fast)
+                k_trace_primary<false, BD, true><<<(unsigned)nblocks, 256, 0, c->stream>>>(
+                    t, cd, ho.dev, T, tiles_x, tile_start, tile_stride, layout, bpx, bpt, q0, fd);
+            else
+                k_trace_primary<false, BD><<<(unsigned)nblocks, 256, 0, c->stream>>>(
+                    t, cd, ho.dev, T, tiles_x, tile_start, tile_stride, layout, bpx, bpt, q0);
             qrc = launch_queue_passes<false, BD>(c, t, cd, src, ho.dev, 1, npass, nout, nblocks, true);
         }
     };
     if (!dispatch_bd(c->tree->desc.brick_dim, launch)) return fail(c, VHX_E_INVALID_ARG, "unsupported brick_dim");
     if (qrc) return qrc;
     VHX_HIP(c, hipGetLastError());
+    if (c->in_prepass) return VHX_OK;  // the outer call records the end and copies its outputs
     VHX_HIP(c, hipEventRecord(c->ev1, c->stream));
     c->timed = true;
     return finish_out(c, ho);
+}
+
+int vhx_set_depth_prepass(vhx_ctx *c, int enable, float margin) {
+    if (!c || !(margin >= 0.0f)) return VHX_E_INVALID_ARG;
+    c->prepass = enable != 0;
+    c->prepass_margin = margin;
+    return VHX_OK;
 }
 
 int vhx_trace_rays(vhx_ctx *c, const float *rays, uint64_t n, const vhx_hits *out, int on_device) {

@@ -259,6 +259,10 @@ class Raytracer:
         self._check(N.lib().vhx_get_stream(self._h, ctypes.byref(s)))
         return s.value
 
+    def set_depth_prepass(self, enable=True, margin=0.0):
+        """vhx_set_depth_prepass: the opt-in half-resolution depth-prepass fast mode (not the reference's semantics)."""
+        self._check(N.lib().vhx_set_depth_prepass(self._h, 1 if enable else 0, float(margin)))
+
     def set_pass_budgets(self, budgets):
         """Step budgets of the multi-pass ray scheduler (vhx_set_pass_budgets); () = one unbounded pass."""
         b = (ctypes.c_uint32 * max(1, len(budgets)))(*budgets)
