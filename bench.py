@@ -221,11 +221,39 @@ def main():
         F = 1  # the torch gather pipeline keeps one frame per rank in flight
 
     mg = None
+    mgpu_fallback = None
     if use_vhx_mgpu:
-        obj = [M.mgpu_unique_id() if rank == 0 else None]
+        # RCCL behind the ABI; if it cannot start on every rank (no loadable RCCL, communicator init failed), all ranks
+        # fall back together to the torch.distributed gather (RCCL via torch), and the line says so
+        uid = None
+        if rank == 0:
+            try:
+                uid = M.mgpu_unique_id()
+            except Exception as e:  # noqa: BLE001 (reported in the line)
+                mgpu_fallback = f"vhx_mgpu_unique_id: {e}"
+        obj = [uid]
         dist.broadcast_object_list(obj, src=0)
-        mg = M.MgpuRenderer(rt, obj[0], world, rank, tile_size=args.tile, overlap=not args.no_overlap)
-        mg.set_frames_in_flight(F)
+        ok = obj[0] is not None
+        if ok:
+            try:
+                mg = M.MgpuRenderer(rt, obj[0], world, rank, tile_size=args.tile, overlap=not args.no_overlap)
+                mg.set_frames_in_flight(min(F, N.VHX_MGPU_MAX_INFLIGHT))
+            except Exception as e:  # noqa: BLE001
+                mgpu_fallback = f"vhx_mgpu on rank {rank}: {e}"
+                mg = None
+        flag = torch.tensor([1 if mg is not None else 0], dtype=torch.int32)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        if int(flag.item()) == 0:
+            if mg is not None:
+                mg.close()
+                mg = None
+            fb = [mgpu_fallback]
+            dist.broadcast_object_list(fb, src=0)
+            mgpu_fallback = mgpu_fallback or fb[0] or "vhx_mgpu failed on another rank"
+            use_vhx_mgpu = False
+            dist.destroy_process_group()
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            F = 1
 
     # the tree: built on the host (rank 0 only when it is broadcast over RCCL), uploaded to HBM
     t0 = time.time()
@@ -514,6 +542,8 @@ def main():
         }
         if mgpu is not None:
             line["multi_gpu_check"] = mgpu
+        if mgpu_fallback:
+            line["mgpu_fallback"] = mgpu_fallback
         if cpu:
             line["gpu_over_cpu"] = round(mrays / cpu["value"], 2)
         print(json.dumps(line), flush=True)

@@ -25,6 +25,7 @@ VHX_E_NO_DEVICE = -4
 VHX_E_STATE = -5
 VHX_E_RCCL = -6
 VHX_MGPU_ID_BYTES = 128
+VHX_MGPU_MAX_INFLIGHT = 16
 VHX_E_TREE_INVALID_SIZE = -10
 VHX_E_TREE_INVALID_BRICK_DIMENSION = -11
 VHX_E_TREE_INVALID_STRUCTURE = -12
