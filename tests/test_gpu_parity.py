@@ -278,7 +278,10 @@ SCHEDULER_ENVS = [{"VHX_RESUME": "0"},                                   # aband
                   {"VHX_QXCD": "0", "VHX_XCDG": "0"},                    # one counter, pass-0 blocks in dispatch order
                   {"VHX_XCDG": "3"},                                     # odd pass-0 XCD block runs
                   {"VHX_QXCD": "4"},                                     # shorter runs dealt over the XCDs
-                  {"VHX_QXCD": "1", "VHX_RPW": "0,0", "VHX_TW": "7"}]    # ... single chunks, few adaptive waves
+                  {"VHX_QXCD": "1", "VHX_RPW": "0,0", "VHX_TW": "7"},    # ... single chunks, few adaptive waves
+                  {"VHX_SPARSE": "64,64,64"},                            # waves abandon as soon as one lane ends
+                  {"VHX_SPARSE": "0"},                                   # no sparse-wave abandonment
+                  {"VHX_QXCD_ALL": "1", "VHX_QWAVESM": "300"}]           # every queue pass dealt over the XCDs
 
 
 @pytest.mark.parametrize("env", SCHEDULER_ENVS, ids=lambda e: "+".join(f"{k}={v}" for k, v in e.items()))

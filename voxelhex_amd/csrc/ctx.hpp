@@ -85,6 +85,10 @@ struct vhx_ctx {
     uint32_t queue_waves_mid = 0;  // waves of a budgeted queue pass after the first (VHX_QWAVESM; 0 = queue_waves)
     uint32_t qxcd = 16;            // queue passes: XCD-dealt chunk runs (VHX_QXCD = run length, 0 = one counter)
     bool qxcd_all = false;         // deal every queue pass, not only the last (VHX_QXCD_ALL=1, diagnostics)
+    // budgeted passes: a wave abandons its rays once fewer than sparse[p] lanes still trace (VHX_SPARSE="8,4,4").
+    // Pass 0 at 12: eight frames in flight 0.645-0.651 ms per bench frame against 0.665-0.670 (8: 0.651-0.661, 16:
+    // 0.646-0.657, 24 and 32 slower); the later budgeted passes gained nothing (profiles/r02/sparse*.log)
+    uint32_t sparse[VHX_MAX_BUDGETS] = {12u, 0u, 0u, 0u};
 };
 
 #define VHX_HIP(ctx, call)                                                                                         \

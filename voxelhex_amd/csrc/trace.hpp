@@ -629,15 +629,22 @@ struct Trav {
     }
 };
 
+// sparse (a budgeted pass with saved state): once fewer than `sparse` lanes of the wave still trace, they are abandoned
+// like rays over the budget (their state saved, the next pass resumes them packed into full waves) instead of keeping
+// the wave's issue slots for a few lanes. 0 = off. The result is the same either way (the traversal is deterministic).
 template <bool COUNT, int BD, bool START = false>
 __device__ __forceinline__ bool get_by_ray(const DevTree &t, const uint64_t *occ_tab, F3d o, F3d d, HitOut &h,
                                            uint32_t budget, uint4 *sbase = nullptr, uint32_t sidx = 0,
-                                           bool resume = false, float start = 0.0f) {
+                                           bool resume = false, float start = 0.0f, uint32_t sparse = 0) {
     Trav<COUNT, BD> tr;
     if (!tr.template begin<START>(t, o, d, h, sbase, sidx, resume, start)) return true;
     for (;;) {
         tr.step(t, occ_tab, h, budget);
         if (tr.ex != 0u) break;
+        if (sparse && (uint32_t)__popcll(__ballot(1)) < sparse) {
+            tr.ex = 3u;
+            break;
+        }
     }
     return tr.end(t, h, sbase, sidx);
 }

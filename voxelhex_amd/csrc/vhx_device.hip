@@ -235,6 +235,7 @@ struct PassQ {
     uint4 *state;      // per output index, 4 x uint4: saved traversal state of an abandoned ray (null: re-trace)
     uint32_t xcd_group;  // pass 0: XCD-aware block runs (xcd_block), 0 = dispatch order
     uint32_t qxcd;       // queue passes: runs of this many chunks dealt over the 8 XCDs, one counter each (0 = off)
+    uint32_t sparse;     // budgeted passes with saved state: abandon a wave's rays once fewer lanes trace (0 = off)
 };
 
 // Rays per wave of a queue pass over n rays: fixed, or (rpw == 0) as many as spread the pass over about `tw` waves.
@@ -519,7 +520,8 @@ __global__ void __launch_bounds__(256) VHX_PRIMARY_ATTR k_trace_primary(DevTree 
         HitOut h;
         h.bytes = 0;
         const float start = FAST ? prepass_start(fast, px, py) : 0.0f;
-        done = get_by_ray<COUNT, BD, FAST>(t, occ_tab, o, d, h, q.budget, q.state, (uint32_t)idx, false, start);
+        done = get_by_ray<COUNT, BD, FAST>(t, occ_tab, o, d, h, q.budget, q.state, (uint32_t)idx, false, start,
+                                           q.sparse);
         if (done)
             store(t, out, idx, o, h);
         else if (COUNT && q.state)
@@ -630,7 +632,8 @@ __global__ void __launch_bounds__(256) VHX_QUEUE_ATTR k_trace_queue(DevTree t, c
             ray_of(a->cam, a->src, idx, o, d);
             HitOut h;
             h.bytes = COUNT && q.resume ? a->out.bytes[idx] : 0u;
-            const bool fin = get_by_ray<COUNT, BD>(t, occ_tab, o, d, h, q.budget, q.state, idx, q.resume != 0);
+            const bool fin = get_by_ray<COUNT, BD>(t, occ_tab, o, d, h, q.budget, q.state, idx, q.resume != 0, 0.0f,
+                                                   q.sparse);
             const QueueArgs *b = qa;
             asm volatile("" : "+s"(b));
             if (!fin) {
@@ -916,6 +919,7 @@ static PassQ pass_q(const vhx_ctx *c, uint32_t p, uint32_t npass) {
     // the state buffer is written by every pass that can abandon rays and read by every pass after the first
     q.state = c->resume && npass > 1 ? (uint4 *)c->state.ptr : nullptr;
     q.resume = c->resume && p > 0 ? 1u : 0u;
+    q.sparse = last || !q.state ? 0u : c->sparse[p];
     return q;
 }
 
@@ -1081,6 +1085,17 @@ int vhx_create(int hip_device, vhx_ctx **out) {
         if (pw0 && atoi(pw0) > 0) c->queue_waves0 = (uint32_t)atoi(pw0);
         const char *pqx = getenv("VHX_QXCD");
         if (pqx && atoi(pqx) >= 0) c->qxcd = (uint32_t)atoi(pqx);
+        const char *psp = getenv("VHX_SPARSE");  // per budgeted pass, e.g. "8,4,4"
+        if (psp) {
+            uint32_t k = 0;
+            for (const char *q = psp; *q && k < VHX_MAX_BUDGETS;) {
+                char *end = nullptr;
+                const unsigned long v = strtoul(q, &end, 10);
+                if (end == q) break;
+                c->sparse[k++] = v <= 64 ? (uint32_t)v : 0u;
+                q = *end == ',' ? end + 1 : end;
+            }
+        }
         const char *pqa = getenv("VHX_QXCD_ALL");
         if (pqa && pqa[0] == '1') c->qxcd_all = true;
     }
@@ -1117,6 +1132,7 @@ int vhx_create_shared(const vhx_ctx *owner, vhx_ctx **out) {
     c->queue_waves_mid = owner->queue_waves_mid;
     c->qxcd = owner->qxcd;
     c->qxcd_all = owner->qxcd_all;
+    std::memcpy(c->sparse, owner->sparse, sizeof(c->sparse));
     c->prepass = owner->prepass;
     c->prepass_margin = owner->prepass_margin;
     *out = c;
