@@ -519,7 +519,9 @@ struct Trav {
             const bool pop = uniform || target >= 64u || occ == 0 || (occ & omask) == 0;
             const bool push = !pop && ntype == VHX_NODE_INTERNAL && ((occ >> target) & 1ull) != 0;
             if (pop) {
-                // POP (cpu.rs:368-393)
+                // POP (cpu.rs:368-393). Its step to the next sibling (dda_step_to_next_sibling on the popped cube,
+                // step_sectant, target_bounds += step * size) is one trip of the walk below, which the lanes that
+                // advance run anyway: one copy of the DDA code per iteration instead of two.
                 count -= 1;
                 node = s1;
                 s1 = s2;
@@ -539,24 +541,6 @@ struct Trav {
                                    kz = (uint32_t)((tb.min.z - cur.min.z) * rs);
                     target = kx + ky * 4u + kz * 16u;
                 }
-                const uint32_t sel = dda_step(r, p, tb);
-                target = step_sectant(r, target, sel);
-                tb.min = vadd(tb.min, vmul(step_vec(r, sel), tb.size));
-                tbok = 1u;
-                if (count == 0) {
-                    // the stack ran empty: restart from the root (cpu.rs:441-455); target_bounds stays stale
-                    p = vadd(p, vmul(r.d, 0.1f));
-                    if (p.x < tsize && p.y < tsize && p.z < tsize && p.x > 0.0f && p.y > 0.0f && p.z > 0.0f) {
-                        target = offset_sectant(p, tsize);
-                        tbok = 0u;  // target_bounds stays stale
-                        node = 0;
-                        count = 1;
-                        cur.min = mk(0.0f, 0.0f, 0.0f);
-                        cur.size = tsize;
-                    } else {
-                        ex = 2u;  // left the tree: a miss
-                    }
-                }
             }
             if (push) {
                 // PUSH (cpu.rs:401-411)
@@ -572,12 +556,16 @@ struct Trav {
                 tbok = 1u;
                 ex = slot >= t.node_count ? 2u : 0u;  // the reference would panic on an invalid key: a miss here
             }
-            if (!pop && !push) {
-                // ADVANCE (cpu.rs:416-437); at most 9 steps across the node, the pass budget is checked after it.
-                // Same form as the brick walk (exit planes, direction-normalised sectant coordinates). Every step
-                // is committed: tb.min after a step out of the node is dead (the next iteration pops and overwrites
-                // it).
-                // The reference's target (step_sectant) is formed once at the end (>= 64: the walk left the node).
+            if (!push) {
+                // ADVANCE (cpu.rs:416-437), or POP's single step: at most 9 steps across the node, the pass budget
+                // is checked after it. Same form as the brick walk (exit planes, direction-normalised sectant
+                // coordinates); the exit-plane difference equals the reference's dda_step_to_next_sibling for a point
+                // on or inside the stepped cube (§4), which the popped cube is. Every step is committed: tb.min after
+                // a step out of the node is dead (the next iteration pops and overwrites it). The reference's target
+                // (step_sectant) is formed once at the end (>= 64: the walk left the node; POP's step_sectant gives
+                // 64 + the wrapped sectant there, which the next iteration's POP never reads).
+                // A POP lane walks with every sectant occupied: it stops after its one step.
+                const uint64_t wocc = pop ? ~0ull : occ;
                 const F3d usg = mk(tb.size * r.sgmax.x, tb.size * r.sgmax.y, tb.size * r.sgmax.z);
                 const F3d sgs = mk(r.sg.x * tb.size, r.sg.y * tb.size, r.sg.z * tb.size);
                 const uint32_t fx = r.isx > 0 ? 0u : 3u, fy = r.isy > 0 ? 0u : 3u, fz = r.isz > 0 ? 0u : 3u;
@@ -605,13 +593,31 @@ struct Trav {
                     jz += (uint32_t)mz;
                     const uint32_t oob = (jx | jy | jz) & ~3u;  // non-zero iff the walk left the node
                     const uint32_t tg = (jx + jy * 4u + jz * 16u) ^ F;
-                    const uint32_t bit = (uint32_t)(occ >> (tg & 63u)) & 1u;
+                    const uint32_t bit = (uint32_t)(wocc >> (tg & 63u)) & 1u;
                     if ((oob | bit | ((iters - 1u) >> 22)) != 0u) break;  // left | occupied | iters > 2^22
                 }
                 p = mk(pxy.x, pxy.y, pz);
                 asm volatile("" : "+v"(jx), "+v"(jy), "+v"(jz));
                 target = (jx | jy | jz) < 4u ? (jx + jy * 4u + jz * 16u) ^ F : 64u;
                 tb.min = mk(exy.x - usg.x, exy.y - usg.y, ez - usg.z);  // exact: undoes the exact e = tb.min + usg
+                if (pop) {
+                    iters -= 1u;  // POP's step is not one of the walk's steps
+                    tbok = 1u;
+                    if (count == 0) {
+                        // the stack ran empty: restart from the root (cpu.rs:441-455); target_bounds stays stale
+                        p = vadd(p, vmul(r.d, 0.1f));
+                        if (p.x < tsize && p.y < tsize && p.z < tsize && p.x > 0.0f && p.y > 0.0f && p.z > 0.0f) {
+                            target = offset_sectant(p, tsize);
+                            tbok = 0u;  // target_bounds stays stale
+                            node = 0;
+                            count = 1;
+                            cur.min = mk(0.0f, 0.0f, 0.0f);
+                            cur.size = tsize;
+                        } else {
+                            ex = 2u;  // left the tree: a miss
+                        }
+                    }
+                }
             }
             if (ex == 0u && ++iters > budget) ex = budget >= VHX_MAX_ITERS ? 2u : 3u;  // the next node iteration
         }
