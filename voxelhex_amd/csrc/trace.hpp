@@ -363,8 +363,18 @@ constexpr OccTab make_occ_tab() {
     return t;
 }
 __constant__ OccTab g_occ_tab = make_occ_tab();
-__device__ __forceinline__ void fill_occ_tab(uint64_t *occ_tab) {
+// VHX_LDS_ROOT (experiment): the root's header and its 64 child records are copied into LDS after the
+// occupancy table (OCC_TAB_WORDS words in all), and node iterations at the root read them there
+#ifndef VHX_LDS_ROOT
+#define VHX_LDS_ROOT 0
+#endif
+#define OCC_TAB_WORDS (512u + (VHX_LDS_ROOT ? 2u + 64u * 2u : 0u))
+__device__ __forceinline__ void fill_occ_tab(uint64_t *occ_tab, const DevTree &t) {
     for (uint32_t i = threadIdx.x; i < 512u; i += blockDim.x) occ_tab[i] = g_occ_tab.v[i];
+    if (VHX_LDS_ROOT && t.child_rec) {
+        uint4 *root = (uint4 *)(occ_tab + 512);
+        for (uint32_t i = threadIdx.x; i < 65u; i += blockDim.x) root[i] = i == 0 ? t.hdr[0] : t.child_rec[i - 1];
+    }
 }
 
 // Saved traversal state of a ray abandoned at a pass budget (multi-pass scheduling): everything the loop below
@@ -484,17 +494,25 @@ struct Trav {
     }
 
     __device__ __forceinline__ void step(const DevTree &t, const uint64_t *occ_tab, HitOut &h, uint32_t budget) {
-        const uint4 lh = t.hdr[node];
         // the child slot is read by both the leaf probe and the push: issue it with the header load so the
         // iteration waits for one memory latency instead of two (with brick_dim <= 4 the child record also carries
         // the brick's occupancy word, so a probe waits for no further load)
+        uint4 lh;
         uint32_t slot;
         uint64_t cocc = 0;
-        if (Brick<BD>::WORDS == 1) {
+        if (VHX_LDS_ROOT && Brick<BD>::WORDS == 1 && node == 0u) {
+            const uint4 *root = (const uint4 *)(occ_tab + 512);
+            lh = root[0];
+            const uint4 cr = root[1u + (target & 63u)];
+            slot = cr.x;
+            cocc = ((uint64_t)cr.z << 32) | (uint64_t)cr.y;
+        } else if (Brick<BD>::WORDS == 1) {
+            lh = t.hdr[node];
             const uint4 cr = t.child_rec[(uint64_t)node * 64u + (target & 63u)];
             slot = cr.x;
             cocc = ((uint64_t)cr.z << 32) | (uint64_t)cr.y;
         } else {
+            lh = t.hdr[node];
             slot = t.children[(uint64_t)node * 64u + (target & 63u)];
         }
         // the pop test's LUT word, read from LDS while the node loads are in flight (the empty asm keeps the read

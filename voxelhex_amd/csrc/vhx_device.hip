@@ -499,8 +499,8 @@ __global__ void __launch_bounds__(256) VHX_PRIMARY_ATTR k_trace_primary(DevTree 
                                                        uint32_t tile_start, uint32_t tile_stride, uint32_t layout,
                                                        uint32_t blocks_per_tile_x, uint32_t blocks_per_tile,
                                                        PassQ q, FastD fast = FastD{}) {
-    __shared__ uint64_t occ_tab[512];
-    fill_occ_tab(occ_tab);
+    __shared__ uint64_t occ_tab[OCC_TAB_WORDS];
+    fill_occ_tab(occ_tab, t);
     __syncthreads();
     const uint32_t bid = xcd_block(blockIdx.x, gridDim.x, q.xcd_group);
     const uint32_t j = bid / blocks_per_tile;  // j-th tile of this rank
@@ -536,8 +536,8 @@ __global__ void __launch_bounds__(256) VHX_PRIMARY_ATTR k_trace_primary(DevTree 
 template <bool COUNT, int BD>
 __global__ void __launch_bounds__(256) k_trace_rays(DevTree t, const float *__restrict__ rays, uint64_t n, OutD out,
                                                     PassQ q) {
-    __shared__ uint64_t occ_tab[512];
-    fill_occ_tab(occ_tab);
+    __shared__ uint64_t occ_tab[OCC_TAB_WORDS];
+    fill_occ_tab(occ_tab, t);
     __syncthreads();
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool done = true;
@@ -579,8 +579,8 @@ __global__ void k_put_queue_args(QueueArgs a, QueueArgs *dst) {
 template <bool COUNT, int BD>
 __global__ void __launch_bounds__(256) VHX_QUEUE_ATTR k_trace_queue(DevTree t, const QueueArgs *qa, const uint32_t *__restrict__ in,
                                                      const uint32_t *in_n, uint32_t *grab, PassQ q) {
-    __shared__ uint64_t occ_tab[512];
-    fill_occ_tab(occ_tab);
+    __shared__ uint64_t occ_tab[OCC_TAB_WORDS];
+    fill_occ_tab(occ_tab, t);
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t n = *in_n;
