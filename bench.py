@@ -194,10 +194,17 @@ def main():
     # rehearsal of the torch multi-GPU path on a single GPU: VHX_BENCH_REHEARSAL=1 puts every rank on cuda:0 and
     # gathers over gloo through host memory (RCCL needs one GPU per rank); timings from such a run are not scaling
     rehearsal = world > 1 and os.environ.get("VHX_BENCH_REHEARSAL") == "1"
-    use_vhx_mgpu = world > 1 and args.mgpu == "vhx" and not rehearsal
+    # VHX_BENCH_MGPU1=1 (diagnostics): the vhx_mgpu data path on a one-rank communicator, so that a one-GPU box runs
+    # every step of the multi-GPU bench path (gloo setup, RCCL id exchange, tree broadcast, frames in flight, gather,
+    # untile, frame check) that the N > 1 runs take
+    force1 = world == 1 and os.environ.get("VHX_BENCH_MGPU1") == "1"
+    use_vhx_mgpu = (world > 1 or force1) and args.mgpu == "vhx" and not rehearsal
     if rehearsal:
         local = 0
-    if world > 1:
+    if force1:
+        for k, v in (("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", "29533"), ("RANK", "0"), ("WORLD_SIZE", "1")):
+            os.environ.setdefault(k, v)
+    if world > 1 or force1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(local)
         if rehearsal or use_vhx_mgpu:
@@ -437,7 +444,7 @@ def main():
 
     # ---- multi-GPU check (untimed): the gathered, untiled frame equals rank 0 tracing the whole frame alone -------
     mgpu = None
-    if world > 1 and rank == 0:
+    if (world > 1 or mg is not None) and rank == 0:
         fields = ("rgba", "depth") if mg is not None else ("rgba",)
         whole = rt.trace_primary(cam, fields=fields)
         got = (fb_rgba if mg is not None else framebuffer).cpu().numpy().view(np.uint32)
@@ -510,7 +517,7 @@ def main():
         metric = BASELINE["metric"]
         if args.shadows:
             metric = "primary + hard-shadow Mrays/s (BASELINE config 5)"
-        if world > 1:
+        if world > 1 or mg is not None:
             par = f"screen-tile split x{world} + " + (
                 "gloo gather (single-GPU rehearsal)" if rehearsal else
                 ("RCCL ncclGather of RGBA8 + depth behind the C ABI (vhx_mgpu), tree ncclBroadcast from rank 0"
@@ -549,7 +556,7 @@ def main():
         print(json.dumps(line), flush=True)
     if mg is not None:
         mg.close()
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
     for r in rts[1:]:
         r.close()
