@@ -17,6 +17,10 @@ LIB = os.path.join(LIBDIR, "libvhx.so")
 ARCH = os.environ.get("VHX_OFFLOAD_ARCH", "gfx950")
 
 HOST_SRCS = ["boxtree.cpp", "flatten.cpp", "vox.cpp", "stream.cpp"]
+# device code generation: LLVM's iterative ILP scheduler for AMDGPU (instruction order and register pressure only; the
+# arithmetic and its rounding are unchanged). Bench frame at eight frames in flight 0.592-0.602 ms against 0.613-0.616
+# with the default scheduler; trace kernels 70 / 97 VGPRs against 75 / 102 (profiles/r02/sched_variants_f8.log)
+DEV_FLAGS = ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]
 DEV_SRCS = ["vhx_device.hip", "vhx_mgpu.hip"]
 HEADERS = ["boxtree.hpp", "trace.hpp", "ctx.hpp"]
 
@@ -41,8 +45,10 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(verbose=False, force=False, lib=None, build_dir=None, defines=()):
-    """lib / build_dir / defines: a variant build (probes), e.g. defines=("VHX_QUEUE_WPE=5",)."""
+def build(verbose=False, force=False, lib=None, build_dir=None, defines=(), flags=(), dev_flags=None):
+    """lib / build_dir / defines / flags / dev_flags: a variant build (probes), e.g. defines=("VHX_QUEUE_WPE=5",),
+    flags=("-O2",) added to the device sources, dev_flags=() for LLVM's default scheduler."""
+    dev = DEV_FLAGS if dev_flags is None else list(dev_flags)
     lib = lib or LIB
     bdir = build_dir or BUILD
     os.makedirs(os.path.dirname(lib), exist_ok=True)
@@ -63,7 +69,7 @@ def build(verbose=False, force=False, lib=None, build_dir=None, defines=()):
         o = os.path.join(bdir, src + ".o")
         if force or _stale(o, [s] + common_deps):
             _run([_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
-                  "-fno-fast-math", "-Wall", "-I", inc] + dflags + ["-c", s, "-o", o], verbose)
+                  "-fno-fast-math", "-Wall", "-I", inc] + dev + dflags + list(flags) + ["-c", s, "-o", o], verbose)
         objs.append(o)
     if force or _stale(lib, objs):
         # -ldl: RCCL is dlopen()ed by vhx_mgpu.hip (no link-time RCCL dependency)

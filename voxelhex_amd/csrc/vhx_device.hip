@@ -458,7 +458,10 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t bid, uint32_t n, uint32_t
     return ((k / G) * 8u + x) * G + k % G;
 }
 
-// occupancy of the traversal kernels (waves per SIMD the register allocation must allow; 0 = the compiler's choice)
+// occupancy of the traversal kernels (waves per SIMD the register allocation must allow; 0 = the compiler's choice).
+// Default: the queue kernel of brick_dim 1 and 4 fits 96 VGPRs (5 waves per SIMD instead of 4, no spills under the
+// iterative-ilp scheduler of _build.py); brick_dim 2 would spill 4 VGPRs and 8..32 16, so they keep 4 waves (the
+// minimum of 4 compiles to the same code as no attribute)
 #ifndef VHX_QUEUE_WPE
 #define VHX_QUEUE_WPE 0
 #endif
@@ -468,7 +471,7 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t bid, uint32_t n, uint32_t
 #if VHX_QUEUE_WPE > 0
 #define VHX_QUEUE_ATTR __attribute__((amdgpu_waves_per_eu(VHX_QUEUE_WPE)))
 #else
-#define VHX_QUEUE_ATTR
+#define VHX_QUEUE_ATTR __attribute__((amdgpu_waves_per_eu(!COUNT && (BD == 1 || BD == 4) ? 5 : 4)))
 #endif
 #if VHX_PRIMARY_WPE > 0
 #define VHX_PRIMARY_ATTR __attribute__((amdgpu_waves_per_eu(VHX_PRIMARY_WPE)))
