@@ -74,6 +74,9 @@ def parse():
                         "depth prepass, full-resolution rays start at the min of 4 texels minus MARGIN")
     p.add_argument("--no-overlap", action="store_true",
                    help="N>1: gather each frame before tracing the next (default: frame k's gather overlaps k+1)")
+    p.add_argument("--root-slots", type=int, default=0,
+                   help="N>1 (vhx_mgpu): rank 0's share of the tile slots (R of R+N-1); 0 (default) = measured before "
+                        "the warm-up by vhx_mgpu_balance (untimed)")
     return p.parse_args()
 
 
@@ -381,6 +384,18 @@ def main():
     for _ in range(len(rts) if mg is None else 1):
         step(False)
     drain()
+    split = None
+    if mg is not None:
+        # rank 0's share of the tiles (untimed): a link-bound split moves tiles to rank 0, whose parts cross no link
+        if args.root_slots > 0:
+            mg.set_root_slots(args.root_slots)
+            split = {"root_slots": args.root_slots, "source": "--root-slots"}
+        else:
+            R, a, g = mg.balance(cam, frames=4)
+            split = {"root_slots": R, "rank0_trace_ms_one_slot": round(a, 4), "transfer_ms_one_slot": round(g, 4),
+                     "source": "vhx_mgpu_balance"}
+        step(False)  # the buffers of the chosen split are allocated outside the timed region
+        drain()
     frame[0] = 0
     for _ in range(args.warmup):
         step(False)
@@ -551,6 +566,8 @@ def main():
             line["multi_gpu_check"] = mgpu
         if mgpu_fallback:
             line["mgpu_fallback"] = mgpu_fallback
+        if split is not None:
+            line["mgpu_split"] = split
         if cpu:
             line["gpu_over_cpu"] = round(mrays / cpu["value"], 2)
         print(json.dumps(line), flush=True)

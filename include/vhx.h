@@ -243,9 +243,10 @@ int vhx_untile_frame(vhx_ctx *ctx, const void *gathered, uint32_t planes, uint32
 /* ---- multi-GPU: screen-tile split over RCCL ------------------------------------------------------
  * One context per GPU and process (the reference renders one view per Bevy render world, VhxRenderNode::run,
  * src/raytracing/bevy/pipeline/mod.rs:96-155; these calls spread that view over the GPUs of a node). The frame is cut
- * into tile_size^2 screen tiles dealt round-robin over the ranks (rank r traces tiles r, r+N, ...); each frame every
- * rank traces its tiles into a contiguous RGBA8 + f32-depth buffer, one ncclGather (RCCL over xGMI) brings the
- * buffers to rank 0, and rank 0 untiles them into its framebuffers. The tree is replicated: vhx_mgpu_broadcast_tree
+ * into tile_size^2 screen tiles dealt round-robin over V = R + N - 1 slots, rank 0 owning slots 0..R-1 and rank
+ * r >= 1 slot R + r - 1 (R = 1, the default: rank r traces tiles r, r+N, ...); each frame every rank traces its slots
+ * into contiguous RGBA8 + f32-depth parts, point-to-point RCCL transfers over xGMI bring the other ranks' parts to
+ * rank 0, and rank 0 untiles them into its framebuffers. The tree is replicated: vhx_mgpu_broadcast_tree
  * uploads it on rank 0 and ncclBroadcasts the device buffers to the other ranks (no host copy of the tree there).
  * RCCL is loaded at run time (dlopen of librccl.so.1, or the path in VHX_RCCL_LIB), so libvhx itself has no link-time
  * RCCL dependency; without it these calls return VHX_E_RCCL. Errors are reported through vhx_last_error(ctx).      */
@@ -276,6 +277,16 @@ int vhx_mgpu_sync(vhx_mgpu *m, float *last_trace_ms);
  * gathers stay in frame order on the communication stream. Waits for the frames in flight before it changes them. */
 #define VHX_MGPU_MAX_INFLIGHT 16
 int vhx_mgpu_set_frames_in_flight(vhx_mgpu *m, uint32_t frames);
+/* Collective, between frames: rank 0's share of the tiles, R of the R + N - 1 slots (1..VHX_MGPU_MAX_ROOT_SLOTS; every
+ * rank must pass the same R). R > 1 suits a link-bound split: rank 0's own parts cross no link. */
+#define VHX_MGPU_MAX_ROOT_SLOTS 4
+int vhx_mgpu_set_root_slots(vhx_mgpu *m, uint32_t root_slots);
+/* Collective: renders `frames` + 1 frames of `cam` one at a time with R = 1, takes on rank 0 the median device time of
+ * its trace and of the transfers into it, and sets on every rank the R that minimises the modelled frame period
+ * (N / (R + N - 1)) * max(R * trace, transfer) (a larger R must win by 3 %). Returns R and rank 0's two figures (ms);
+ * any output pointer may be NULL. */
+int vhx_mgpu_balance(vhx_mgpu *m, const vhx_camera *cam, uint32_t frames, uint32_t *root_slots, float *trace_ms,
+                     float *transfer_ms);
 /* nranks, rank, and the rays this rank traces for a width x height frame (any pointer may be NULL). */
 int vhx_mgpu_info(const vhx_mgpu *m, uint32_t width, uint32_t height, int *nranks, int *rank, uint64_t *rays);
 void vhx_mgpu_destroy(vhx_mgpu *m);

@@ -3,9 +3,11 @@
 * The 7680x4320 frame of the bench tree is traced as the 8 rank tile sets of config 4 (64x64 tiles dealt round-robin,
   VHX_LAYOUT_TILES), concatenated rank-major as the gather delivers them ([RGBA plane | depth plane] per rank),
   scattered with vhx_untile_frame and compared with the oracle's whole 7680x4320 frame (RGBA and depth bit-exact).
-* vhx_mgpu_* (RCCL behind the C ABI) with a one-rank communicator: the tree broadcast, the per-frame ncclGather and
-  the untile on rank 0 reproduce the same frame, with and without overlapped frames. (RCCL refuses two ranks on one
-  GPU, so N > 1 runs first on the driver's 8-GPU node; the code path is the same apart from RCCL's own transport.)
+  With rank 0 holding R = 2 slots (a weighted split) the 8 ranks deal over 9 slots; the same check covers that layout.
+* vhx_mgpu_* (RCCL behind the C ABI) with a one-rank communicator: the tree broadcast, the per-frame transfers and
+  the untile on rank 0 reproduce the same frame, with and without overlapped frames, with rank 0 tracing 1-3 slots,
+  and after vhx_mgpu_balance. (RCCL refuses two ranks on one GPU, so N > 1 runs first on the driver's 8-GPU node; the
+  code path is the same apart from the point-to-point sends to rank 0 and RCCL's own transport.)
 """
 import numpy as np
 import pytest
@@ -36,27 +38,32 @@ def _check_frame(rgba, depth, ref, what):
     assert bad == 0, f"{what}: depth differs at {bad} pixels"
 
 
-def test_config4_eight_rank_tile_sets_vs_oracle(gpu, config4):
+@pytest.mark.parametrize("root_slots", [1, 2])
+def test_config4_eight_rank_tile_sets_vs_oracle(gpu, config4, root_slots):
     import torch
     flat, cam, ref = config4
     gpu.upload(flat)
-    per = M.tiles_per_rank(W4, H4, T4, R4)
+    V = R4 + root_slots - 1  # slots: rank 0 owns 0..root_slots-1, rank r >= 1 slot root_slots + r - 1
+    per = M.tiles_per_rank(W4, H4, T4, V)
     n_out = per * T4 * T4
-    gathered = torch.zeros(R4 * 2 * n_out, dtype=torch.int32, device="cuda")
-    for r in range(R4):
+    gathered = torch.zeros(V * 2 * n_out, dtype=torch.int32, device="cuda")
+    for r in range(V):
         part = gathered[r * 2 * n_out:(r + 1) * 2 * n_out]
-        gpu.trace_primary(cam, tile_size=T4, tile_start=r, tile_stride=R4, layout=N.VHX_LAYOUT_TILES,
+        gpu.trace_primary(cam, tile_size=T4, tile_start=r, tile_stride=V, layout=N.VHX_LAYOUT_TILES,
                           out={"rgba": part[:n_out], "depth": part[n_out:].view(torch.float32)})
     rgba = torch.zeros(W4 * H4, dtype=torch.int32, device="cuda")
     depth = torch.zeros(W4 * H4, dtype=torch.float32, device="cuda")
-    gpu.untile_frame(gathered.data_ptr(), 2, R4, per, T4, W4, H4, rgba.data_ptr(), depth.data_ptr())
+    gpu.untile_frame(gathered.data_ptr(), 2, V, per, T4, W4, H4, rgba.data_ptr(), depth.data_ptr())
     gpu.sync()
-    _check_frame(rgba, depth, ref, "config 4, 8 rank tile sets")
+    _check_frame(rgba, depth, ref, f"config 4, 8 rank tile sets over {V} slots")
     assert (ref["rgba"] != 0xFF808080).mean() > 0.1  # a frame with geometry, not the background
 
 
-@pytest.mark.parametrize("overlap,inflight", [(True, 1), (False, 1), (True, 3)])
-def test_mgpu_one_rank_rccl_frame_vs_oracle(config4, overlap, inflight):
+@pytest.mark.parametrize("overlap,inflight,root_slots", [(True, 1, 1), (False, 1, 1), (True, 3, 1), (True, 3, 3),
+                                                         (False, 2, 2)])
+def test_mgpu_one_rank_rccl_frame_vs_oracle(config4, overlap, inflight, root_slots):
+    """root_slots > 1: rank 0 traces several tile slots (tiles s, s + V, ... for s < R) straight into its slot-major
+    buffer and untiles V = R slots -- the rank-0 side of a weighted split, with no peer at N = 1."""
     import torch
     flat, cam, ref = config4
     rt = vhx.Raytracer(0)
@@ -64,6 +71,7 @@ def test_mgpu_one_rank_rccl_frame_vs_oracle(config4, overlap, inflight):
         m = M.MgpuRenderer(rt, M.mgpu_unique_id(), 1, 0, tile_size=T4, overlap=overlap)
         m.set_frames_in_flight(inflight)
         m.broadcast_tree(flat)
+        m.set_root_slots(root_slots)
         assert m.rays(W4, H4) == W4 * H4
         fbs = [(torch.zeros(W4 * H4, dtype=torch.int32, device="cuda"),
                 torch.zeros(W4 * H4, dtype=torch.float32, device="cuda")) for _ in range(4)]
@@ -72,6 +80,30 @@ def test_mgpu_one_rank_rccl_frame_vs_oracle(config4, overlap, inflight):
         m.sync()
         for k, (rgba, depth) in enumerate(fbs):
             _check_frame(rgba, depth, ref, f"vhx_mgpu frame {k} (overlap={overlap})")
+        m.close()
+    finally:
+        rt.close()
+
+
+def test_mgpu_balance_one_rank(config4):
+    """vhx_mgpu_balance at N = 1: there is no transfer, every share models the same period, so R stays 1; the frames
+    rendered after it match the oracle."""
+    import torch
+    flat, cam, ref = config4
+    rt = vhx.Raytracer(0)
+    try:
+        m = M.MgpuRenderer(rt, M.mgpu_unique_id(), 1, 0, tile_size=T4)
+        m.broadcast_tree(flat)
+        m.set_root_slots(2)
+        R, trace_ms, transfer_ms = m.balance(cam, frames=2)
+        assert R == 1 and trace_ms > 0.0 and transfer_ms >= 0.0
+        rgba = torch.zeros(W4 * H4, dtype=torch.int32, device="cuda")
+        depth = torch.zeros(W4 * H4, dtype=torch.float32, device="cuda")
+        m.render(cam, rgba, depth)
+        m.sync()
+        _check_frame(rgba, depth, ref, "after vhx_mgpu_balance")
+        with pytest.raises(N.VhxError):
+            m.set_root_slots(N.VHX_MGPU_MAX_ROOT_SLOTS + 1)
         m.close()
     finally:
         rt.close()

@@ -26,6 +26,7 @@ VHX_E_STATE = -5
 VHX_E_RCCL = -6
 VHX_MGPU_ID_BYTES = 128
 VHX_MGPU_MAX_INFLIGHT = 16
+VHX_MGPU_MAX_ROOT_SLOTS = 4
 VHX_E_TREE_INVALID_SIZE = -10
 VHX_E_TREE_INVALID_BRICK_DIMENSION = -11
 VHX_E_TREE_INVALID_STRUCTURE = -12
@@ -109,6 +110,8 @@ SIGNATURES = [
     ("vhx_mgpu_render", c_int, [c_void_p, P(Camera), c_void_p, c_void_p]),
     ("vhx_mgpu_sync", c_int, [c_void_p, P(c_f32)]),
     ("vhx_mgpu_info", c_int, [c_void_p, c_u32, c_u32, P(c_int), P(c_int), P(c_u64)]),
+    ("vhx_mgpu_set_root_slots", c_int, [c_void_p, c_u32]),
+    ("vhx_mgpu_balance", c_int, [c_void_p, P(Camera), c_u32, P(c_u32), P(c_f32), P(c_f32)]),
     ("vhx_mgpu_destroy", None, [c_void_p]),
     ("vhx_boxtree_new", c_int, [c_u32, c_u32, P(c_void_p)]),
     ("vhx_boxtree_free", None, [c_void_p]),

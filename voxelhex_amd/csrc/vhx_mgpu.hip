@@ -1,11 +1,15 @@
 // libvhx multi-GPU: the screen-tile split of a frame over the GPUs of one node, with RCCL over xGMI (SURVEY.md 8e,
 // include/vhx.h vhx_mgpu_*).
 //
-// Per frame and rank: trace this rank's tiles (r, r+N, ...) into a contiguous send buffer [RGBA8 plane | f32 depth
-// plane] on the context's stream; one ncclGather of the send buffers to rank 0 (xGMI point-to-point: each rank's
-// buffer crosses one link); rank 0 scatters the gathered buffer into its framebuffers (k_untile_planes). The gather and
-// the untile run on a communication stream, so with two alternating send buffers frame k's transfer overlaps frame
-// k+1's trace; events order the reuse of a buffer after its gather. The tree is replicated on every GPU (3 GB against
+// Tiles are dealt round-robin over V = R + N - 1 slots: rank 0 owns slots 0..R-1, rank r >= 1 slot R + r - 1 (R = 1:
+// rank r traces tiles r, r+N, ...). Per frame and rank: trace the rank's slots, each into a contiguous [RGBA8 plane |
+// f32 depth plane] part on the context's stream -- rank 0 straight into its gather buffer, the others into a send
+// buffer; one group of point-to-point sends / receives brings the other ranks' parts to rank 0 (xGMI: each part crosses
+// one link); rank 0 scatters the slot-major gathered buffer into its framebuffers (k_untile_planes). The transfers and
+// the untile run on a communication stream, so frame k's transfer overlaps the next frames' traces; events order the
+// reuse of a buffer after its transfer. R > 1 moves work to rank 0, whose own parts cross no link: when the transfers
+// into rank 0 take longer than a slot's trace, the frame is link-bound and a larger share on rank 0 shortens it
+// (vhx_mgpu_balance measures both and picks R). The tree is replicated on every GPU (3 GB against
 // 288 GB of HBM): rank 0 uploads it from the host, ncclBroadcast copies the device buffers to the other ranks.
 //
 // RCCL is resolved at run time (dlopen + dlsym) so that the library loads on a host without it and binds to the RCCL
@@ -16,9 +20,11 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <vector>
 
 #include "ctx.hpp"
 
@@ -35,7 +41,8 @@ struct Rccl {
     decltype(&ncclCommCount) CommCount = nullptr;
     decltype(&ncclCommUserRank) CommUserRank = nullptr;
     decltype(&ncclBroadcast) Broadcast = nullptr;
-    decltype(&ncclGather) Gather = nullptr;
+    decltype(&ncclSend) Send = nullptr;
+    decltype(&ncclRecv) Recv = nullptr;
     decltype(&ncclGroupStart) GroupStart = nullptr;
     decltype(&ncclGroupEnd) GroupEnd = nullptr;
     decltype(&ncclGetErrorString) GetErrorString = nullptr;
@@ -65,12 +72,13 @@ const Rccl &rccl() {
         sym(r.CommCount, "ncclCommCount");
         sym(r.CommUserRank, "ncclCommUserRank");
         sym(r.Broadcast, "ncclBroadcast");
-        sym(r.Gather, "ncclGather");
+        sym(r.Send, "ncclSend");
+        sym(r.Recv, "ncclRecv");
         sym(r.GroupStart, "ncclGroupStart");
         sym(r.GroupEnd, "ncclGroupEnd");
         sym(r.GetErrorString, "ncclGetErrorString");
         if (!all) {
-            r.err = "the loaded RCCL lacks a symbol libvhx needs (ncclGather needs RCCL >= 2.18)";
+            r.err = "the loaded RCCL lacks a symbol libvhx needs";
             return;
         }
         r.ok = true;
@@ -86,7 +94,10 @@ struct vhx_mgpu {
     bool own_comm = false;
     int nranks = 1, rank = 0;
     uint32_t T = 64;
+    uint32_t R = 1;  // slots of rank 0 (the others own one each)
     bool overlap = true;
+    bool timing = false;  // vhx_mgpu_balance: time rank 0's trace and the transfers of each frame
+    hipEvent_t tev[4] = {};  // trace start / end (tracing stream), transfer start / end (communication stream)
     hipStream_t cstream = nullptr;     // gather + untile
     // frames in flight: frame k is traced by context k % F (ctx, then the shared contexts extra[0..F-2], each on its
     // own stream) into the tile buffers of slot k % S, S = max(2, F)
@@ -117,13 +128,21 @@ static int mgpu_init(vhx_mgpu *m) {
         VHX_HIP(c, hipEventCreateWithFlags(&m->ready[s], hipEventDisableTiming));
         VHX_HIP(c, hipEventCreateWithFlags(&m->free_[s], hipEventDisableTiming));
     }
+    for (hipEvent_t &e : m->tev) VHX_HIP(c, hipEventCreate(&e));
     return VHX_OK;
 }
 
-static void tiles_of(const vhx_mgpu *m, uint32_t W, uint32_t H, uint32_t &ntiles, uint32_t &per_rank) {
+// V slots, per = tiles per slot (the last slots may hold fewer; their parts are padded)
+static uint32_t slots_of(const vhx_mgpu *m) { return m->R + (uint32_t)m->nranks - 1u; }
+static void tiles_of(const vhx_mgpu *m, uint32_t W, uint32_t H, uint32_t &ntiles, uint32_t &per_slot) {
     const uint32_t tx = (W + m->T - 1) / m->T, ty = (H + m->T - 1) / m->T;
     ntiles = tx * ty;
-    per_rank = (ntiles + (uint32_t)m->nranks - 1) / (uint32_t)m->nranks;
+    per_slot = (ntiles + slots_of(m) - 1) / slots_of(m);
+}
+// the slots of a rank: first and count
+static void rank_slots(const vhx_mgpu *m, int rank, uint32_t &first, uint32_t &count) {
+    first = rank == 0 ? 0u : m->R + (uint32_t)rank - 1u;
+    count = rank == 0 ? m->R : 1u;
 }
 
 extern "C" {
@@ -207,6 +226,8 @@ void vhx_mgpu_destroy(vhx_mgpu *m) {
         if (m->ready[s]) (void)hipEventDestroy(m->ready[s]);
         if (m->free_[s]) (void)hipEventDestroy(m->free_[s]);
     }
+    for (hipEvent_t e : m->tev)
+        if (e) (void)hipEventDestroy(e);
     if (m->cstream) (void)hipStreamDestroy(m->cstream);
     delete m;
 }
@@ -244,14 +265,16 @@ int vhx_mgpu_info(const vhx_mgpu *m, uint32_t W, uint32_t H, int *nranks, int *r
     if (nranks) *nranks = m->nranks;
     if (rank) *rank = m->rank;
     if (rays) {
-        uint32_t ntiles, per;
+        uint32_t ntiles, per, first, count;
         tiles_of(m, W, H, ntiles, per);
+        rank_slots(m, m->rank, first, count);
         const uint32_t tx = (W + m->T - 1) / m->T;
         uint64_t n = 0;
-        for (uint32_t t = (uint32_t)m->rank; t < ntiles; t += (uint32_t)m->nranks) {
-            const uint32_t x0 = (t % tx) * m->T, y0 = (t / tx) * m->T;
-            n += (uint64_t)std::min(m->T, W - x0) * std::min(m->T, H - y0);
-        }
+        for (uint32_t s = first; s < first + count; ++s)
+            for (uint32_t t = s; t < ntiles; t += slots_of(m)) {
+                const uint32_t x0 = (t % tx) * m->T, y0 = (t / tx) * m->T;
+                n += (uint64_t)std::min(m->T, W - x0) * std::min(m->T, H - y0);
+            }
         *rays = n;
     }
     return VHX_OK;
@@ -323,43 +346,138 @@ int vhx_mgpu_render(vhx_mgpu *m, const vhx_camera *cam, uint32_t *fb_rgba, float
     if (cam->width == 0 || cam->height == 0) return fail(c, VHX_E_INVALID_ARG, "vhx_mgpu_render: empty frame");
     const Rccl &r = rccl();
     VHX_HIP(c, hipSetDevice(c->device));
-    uint32_t ntiles, per;
+    uint32_t ntiles, per, first, count;
     tiles_of(m, cam->width, cam->height, ntiles, per);
-    const uint64_t n_out = (uint64_t)per * m->T * m->T;  // words per plane of one rank
+    rank_slots(m, m->rank, first, count);
+    const uint32_t V = slots_of(m);
+    const uint64_t n_out = (uint64_t)per * m->T * m->T;  // words per plane of one slot's part
     const uint32_t slot = (uint32_t)(m->k % m->S);
     vhx_ctx *tc = m->k % m->F == 0 ? c : m->extra[m->k % m->F - 1];  // the context tracing this frame
     VHX_STREAM(tc);
-    // a slot's buffers are rewritten only after the gather that read them (stream order on the tracing stream)
+    // a slot's buffers are rewritten only after the transfer that read them (stream order on the tracing stream)
     if (m->used[slot]) VHX_HIP(c, hipStreamWaitEvent(tc->stream, m->free_[slot], 0));
-    if (m->send[slot].bytes < n_out * 8 || (m->rank == 0 && m->gathered[slot].bytes < n_out * 8 * m->nranks)) {
-        // (re)allocation: no frame may still use the old buffers
-        int rc = vhx_mgpu_sync(m, nullptr);
+    DevBuf &buf = m->rank == 0 ? m->gathered[slot] : m->send[slot];
+    const uint64_t need = n_out * 8 * (m->rank == 0 ? (uint64_t)V : 1u);
+    if (buf.bytes < need) {
+        int rc = vhx_mgpu_sync(m, nullptr);  // (re)allocation: no frame may still use the old buffers
         if (rc) return rc;
+        if ((rc = ensure(c, buf, need))) return rc;
     }
-    int rc = ensure(c, m->send[slot], n_out * 8);
-    if (!rc && m->rank == 0) rc = ensure(c, m->gathered[slot], n_out * 8 * (uint64_t)m->nranks);
-    if (rc) return rc;
-    uint32_t *send = (uint32_t *)m->send[slot].ptr;
-    vhx_hits h{};
-    h.rgba = send;
-    h.depth = (float *)(send + n_out);
-    if ((uint32_t)m->rank < ntiles) {
-        rc = vhx_trace_primary(tc, cam, m->T, (uint32_t)m->rank, (uint32_t)m->nranks, VHX_LAYOUT_TILES, &h, 1);
+    uint32_t *parts = (uint32_t *)buf.ptr;  // this rank's parts first (rank 0: the whole slot-major buffer)
+    if (m->timing) VHX_HIP(c, hipEventRecord(m->tev[0], tc->stream));
+    for (uint32_t s = first; s < first + count && s < ntiles; ++s) {
+        vhx_hits h{};
+        h.rgba = parts + 2 * n_out * (s - first);
+        h.depth = (float *)(h.rgba + n_out);
+        const int rc = vhx_trace_primary(tc, cam, m->T, s, V, VHX_LAYOUT_TILES, &h, 1);
         if (rc) return tc == c ? rc : fail(c, rc, tc->err.c_str());
     }
+    if (m->timing) VHX_HIP(c, hipEventRecord(m->tev[1], tc->stream));
     m->last = tc;
     VHX_HIP(c, hipEventRecord(m->ready[slot], tc->stream));
     VHX_HIP(c, hipStreamWaitEvent(m->cstream, m->ready[slot], 0));
-    void *recv = m->rank == 0 ? m->gathered[slot].ptr : nullptr;
-    VHX_NCCL(m, r.Gather(send, recv, n_out * 2, ncclUint32, 0, m->comm, m->cstream));  // a local copy at N = 1
-    if (m->rank == 0)
-        if ((rc = launch_untile(c, m->cstream, recv, 2, (uint32_t)m->nranks, per, m->T, cam->width, cam->height,
-                                fb_rgba, fb_depth)))
-            return rc;
+    if (m->timing) VHX_HIP(c, hipEventRecord(m->tev[2], m->cstream));
+    if (m->nranks > 1) {
+        // every other rank's part to its place in rank 0's slot-major buffer (same counts on every rank: V and per
+        // follow from the frame, the tile size and R, which vhx_mgpu_set_root_slots / _balance keep equal on all ranks)
+        VHX_NCCL(m, r.GroupStart());
+        if (m->rank == 0) {
+            for (int q = 1; q < m->nranks; ++q) {
+                uint32_t qf, qc;
+                rank_slots(m, q, qf, qc);
+                VHX_NCCL(m, r.Recv(parts + 2 * n_out * qf, 2 * n_out, ncclUint32, q, m->comm, m->cstream));
+            }
+        } else {
+            VHX_NCCL(m, r.Send(parts, 2 * n_out, ncclUint32, 0, m->comm, m->cstream));
+        }
+        VHX_NCCL(m, r.GroupEnd());
+    }
+    if (m->timing) VHX_HIP(c, hipEventRecord(m->tev[3], m->cstream));
+    if (m->rank == 0) {
+        const int rc = launch_untile(c, m->cstream, parts, 2, V, per, m->T, cam->width, cam->height, fb_rgba, fb_depth);
+        if (rc) return rc;
+    }
     VHX_HIP(c, hipEventRecord(m->free_[slot], m->cstream));
     m->used[slot] = true;
     ++m->k;
     if (!m->overlap) VHX_HIP(c, hipStreamWaitEvent(tc->stream, m->free_[slot], 0));
+    return VHX_OK;
+}
+
+int vhx_mgpu_set_root_slots(vhx_mgpu *m, uint32_t slots) {
+    if (!m) return VHX_E_INVALID_ARG;
+    if (slots < 1 || slots > VHX_MGPU_MAX_ROOT_SLOTS)
+        return fail(m->ctx, VHX_E_INVALID_ARG, "vhx_mgpu_set_root_slots: 1..VHX_MGPU_MAX_ROOT_SLOTS");
+    const int rc = vhx_mgpu_sync(m, nullptr);  // no frame may be in flight while the split changes
+    if (rc) return rc;
+    m->R = slots;
+    return VHX_OK;
+}
+
+int vhx_mgpu_balance(vhx_mgpu *m, const vhx_camera *cam, uint32_t frames, uint32_t *root_slots, float *trace_ms,
+                     float *transfer_ms) {
+    if (!m || !cam || frames == 0) return VHX_E_INVALID_ARG;
+    vhx_ctx *c = m->ctx;
+    // measure with one slot per rank, frames one after the other (no overlap), the last frames' medians
+    int rc = vhx_mgpu_set_root_slots(m, 1);
+    if (rc) return rc;
+    const bool overlap = m->overlap;
+    m->overlap = false;
+    m->timing = true;
+    DevBuf fb, fbd;
+    if (m->rank == 0 && (rc = ensure(c, fb, (uint64_t)cam->width * cam->height * 4))) return rc;
+    if (m->rank == 0 && (rc = ensure(c, fbd, (uint64_t)cam->width * cam->height * 4))) return rc;
+    std::vector<float> tr, tx;
+    for (uint32_t i = 0; i < frames + 1 && !rc; ++i) {
+        rc = vhx_mgpu_render(m, cam, (uint32_t *)fb.ptr, (float *)fbd.ptr);
+        if (!rc) rc = vhx_mgpu_sync(m, nullptr);
+        float a = 0, b = 0;
+        if (!rc && i > 0 && hipEventElapsedTime(&a, m->tev[0], m->tev[1]) == hipSuccess &&
+            hipEventElapsedTime(&b, m->tev[2], m->tev[3]) == hipSuccess) {
+            tr.push_back(a);
+            tx.push_back(b);
+        }
+    }
+    m->timing = false;
+    m->overlap = overlap;
+    if (fb.ptr) (void)hipFree(fb.ptr);
+    if (fbd.ptr) (void)hipFree(fbd.ptr);
+    if (rc) return rc;
+    // rank 0 picks R: with V = R + N - 1 slots a slot's trace and transfer scale by N / V, the frame period is bounded by
+    // rank 0's R slots and by the transfers into rank 0 (one slot part per link, concurrent), so it is about
+    // N / V * max(R * trace, transfer) with the one-slot figures; the other ranks' single slot never exceeds rank 0's R
+    uint32_t best = 1;
+    float a32 = 0.0f, g32 = 0.0f;
+    if (m->rank == 0 && !tr.empty()) {
+        std::sort(tr.begin(), tr.end());
+        std::sort(tx.begin(), tx.end());
+        const double a = tr[tr.size() / 2], g = tx[tx.size() / 2], N = (double)m->nranks;
+        double best_t = 0;
+        for (uint32_t R = 1; R <= VHX_MGPU_MAX_ROOT_SLOTS; ++R) {
+            const double t = N / (R + N - 1.0) * std::max(R * a, g);
+            if (R == 1 || t < best_t * 0.97) {  // a larger share must win by 3 %
+                best = R;
+                best_t = t;
+            }
+        }
+        a32 = (float)a;
+        g32 = (float)g;
+    }
+    // every rank takes rank 0's choice (and its two figures)
+    if ((rc = ensure(c, m->hdr, 64))) return rc;
+    VHX_STREAM(c);
+    uint32_t msg[3] = {best, 0, 0};
+    std::memcpy(&msg[1], &a32, 4);
+    std::memcpy(&msg[2], &g32, 4);
+    VHX_HIP(c, hipMemcpyAsync(m->hdr.ptr, msg, sizeof(msg), hipMemcpyHostToDevice, c->stream));
+    VHX_NCCL(m, rccl().Broadcast(m->hdr.ptr, m->hdr.ptr, 3, ncclUint32, 0, m->comm, c->stream));
+    VHX_HIP(c, hipMemcpyAsync(msg, m->hdr.ptr, sizeof(msg), hipMemcpyDeviceToHost, c->stream));
+    VHX_HIP(c, hipStreamSynchronize(c->stream));
+    if (msg[0] < 1 || msg[0] > VHX_MGPU_MAX_ROOT_SLOTS) return fail(c, VHX_E_RCCL, "vhx_mgpu_balance: bad broadcast");
+    if ((rc = vhx_mgpu_set_root_slots(m, msg[0]))) return rc;
+    if (root_slots) *root_slots = msg[0];
+    if (trace_ms) std::memcpy(trace_ms, &msg[1], 4);
+    if (transfer_ms) std::memcpy(transfer_ms, &msg[2], 4);
     return VHX_OK;
 }
 

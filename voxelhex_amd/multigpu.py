@@ -139,7 +139,7 @@ def mgpu_unique_id():
 class MgpuRenderer:
     """The multi-GPU split behind the C ABI (vhx_mgpu_*): one libvhx context per process and GPU, an RCCL
     communicator owned by libvhx, the tree broadcast from rank 0 over RCCL, and per frame the rank's tiles traced,
-    ncclGather'ed to rank 0 (RGBA8 + f32 depth) and untiled there. `uid` = the bytes of mgpu_unique_id() created on
+    sent to rank 0 over RCCL (RGBA8 + f32 depth) and untiled there. `uid` = the bytes of mgpu_unique_id() created on
     rank 0 (exchange them with e.g. torch.distributed.broadcast_object_list over gloo)."""
 
     def __init__(self, raytracer, uid, world, rank, tile_size=64, overlap=True):
@@ -184,6 +184,21 @@ class MgpuRenderer:
         ms = ctypes.c_float()
         self._check(N.lib().vhx_mgpu_sync(self._h, ctypes.byref(ms)))
         return ms.value
+
+    def set_root_slots(self, slots):
+        """Collective: rank 0 traces `slots` of the slots + N - 1 tile slots (vhx_mgpu_set_root_slots)."""
+        from . import _native as N
+        self._check(N.lib().vhx_mgpu_set_root_slots(self._h, slots))
+
+    def balance(self, cam, frames=4):
+        """Collective: measures rank 0's trace and the transfers into it and picks rank 0's share
+        (vhx_mgpu_balance); returns (root_slots, trace_ms, transfer_ms)."""
+        import ctypes
+        from . import _native as N
+        r, a, g = ctypes.c_uint32(), ctypes.c_float(), ctypes.c_float()
+        self._check(N.lib().vhx_mgpu_balance(self._h, ctypes.byref(cam), frames, ctypes.byref(r), ctypes.byref(a),
+                                             ctypes.byref(g)))
+        return r.value, a.value, g.value
 
     def rays(self, width, height):
         import ctypes
