@@ -13,6 +13,13 @@
  *   vhx_boxtree_flatten        <- BoxTreeGPUDataHandler::add_node/add_brick with every node resident
  *                                 (src/raytracing/bevy/streaming/cache.rs:226-455, 608-716)
  *   vhx_boxtree_load_vox       <- BoxTree::load_vox_file  (src/convert/magicavoxel.rs:234-374)
+ *   vhx_boxtree_switch_mips    <- StrategyUpdater::switch_albedo_mip_maps (src/boxtree/mipmap.rs:588-609)
+ *   vhx_boxtree_set_mip_method <- StrategyUpdater::set_method_at (mipmap.rs:414-431, 505-513)
+ *   vhx_boxtree_set_mip_color_threshold <- StrategyUpdater::set_color_similarity_thr_at (mipmap.rs:365-379, 482-488)
+ *   vhx_boxtree_recalculate_mips <- StrategyUpdater::recalculate_mips (mipmap.rs:536-586)
+ *   vhx_boxtree_sample_root_mip <- StrategyUpdater::sample_root_mip (mipmap.rs:635-668, a test helper there)
+ *   vhx_boxtree_flatten_lod    <- the streamed view with every node above a depth resident and the rest not: node_mips
+ *                                 (src/raytracing/bevy/types.rs:245-247) stand in for the missing children
  *   vhx_scene_build            <- bulk builder producing exactly the flattened tree that inserting a procedural
  *                                 scene voxel by voxel (x, then y, then z loops) would produce
  *
@@ -80,6 +87,28 @@ int vhx_scene_insert(vhx_boxtree *tree, uint32_t scene, uint64_t seed);
 /* Nodes are renumbered breadth-first from the root; bricks and solid values are numbered in that node order. */
 int vhx_boxtree_flatten(const vhx_boxtree *tree, vhx_flat **out);
 int vhx_scene_build(uint32_t scene, uint32_t size, uint32_t brick_dim, uint64_t seed, int threads, vhx_flat **out);
+/* MIP maps (src/boxtree/mipmap.rs): off by default (MIPMapStrategy::default, mipmap.rs:341-354: level 1 Posterize(0.05),
+ * levels 2-4 BoxFilter, colour-matching thresholds {2: 0.1, 3: 0.05, 4: 0.02}). Once switched on, every insert updates
+ * the MIPs of the nodes on its path (insert.rs:494); switching on recalculates all of them. A node's MIP level is
+ * log2(node edge / brick_dim). Methods (MIPResamplingMethods, src/boxtree/types.rs:113-149): */
+#define VHX_MIP_BOX_FILTER 0u      /* gamma-2 average of the cell's colours                                     */
+#define VHX_MIP_POINT_FILTER 1u    /* most frequent colour                                                      */
+#define VHX_MIP_POINT_FILTER_BD 2u /* most frequent colour, sampled from the voxels instead of the child MIPs    */
+#define VHX_MIP_POSTERIZE 3u       /* average of the largest group of colours within threshold*255              */
+#define VHX_MIP_POSTERIZE_BD 4u    /* as POSTERIZE (the reference samples it like POSTERIZE too, mipmap.rs:51-55) */
+int vhx_boxtree_switch_mips(vhx_boxtree *tree, int enabled);
+int vhx_boxtree_set_mip_method(vhx_boxtree *tree, uint32_t level, uint32_t method, float threshold);
+int vhx_boxtree_set_mip_color_threshold(vhx_boxtree *tree, uint32_t level, float threshold);
+int vhx_boxtree_recalculate_mips(vhx_boxtree *tree);
+/* The root's MIP (sectant 64) or its child's (sectant < 64) at cell (x, y, z) of the brick, as an entry. */
+int vhx_boxtree_sample_root_mip(const vhx_boxtree *tree, uint32_t sectant, uint32_t x, uint32_t y, uint32_t z,
+                                uint32_t *kind, uint32_t *albedo, uint32_t *data);
+/* Flattened tree with node MIPs: nodes deeper than max_depth (root = 0) are left out (their parents' child entries
+ * are VHX_EMPTY, occupancy kept); every node's MIP brick is appended to the bricks / solid values and its descriptor
+ * stored in node_mips (VHX_EMPTY where the node has no MIP). vhx_boxtree_flatten does the same with every node
+ * included when the tree's MIPs are enabled, and leaves node_mips empty otherwise. */
+int vhx_boxtree_flatten_lod(const vhx_boxtree *tree, uint32_t max_depth, vhx_flat **out);
+int vhx_flat_node_mips(const vhx_flat *flat, const uint32_t **node_mips, uint32_t *count);
 /* Fills *desc with pointers into the flat object (valid until vhx_flat_free). */
 int vhx_flat_desc(const vhx_flat *flat, vhx_tree_desc *desc);
 void vhx_flat_free(vhx_flat *flat);

@@ -1,0 +1,148 @@
+"""MIP maps of the host BoxTree (src/boxtree/mipmap.rs, iterate.rs:349-560) against the reference's own KATs
+(`mod mipmap_tests`, src/boxtree/tests.rs:877-1330), transcribed with the same trees, inserts and expected colours.
+CPU only: MIP generation is host code in the reference as well."""
+import math
+
+import numpy as np
+import pytest
+
+from voxelhex_amd.boxtree import Albedo, BoxTree, MIPResamplingMethods
+
+BOX_NODE_CHILDREN_COUNT = 64
+
+red = Albedo.from_u32(0xFF0000FF)
+green = Albedo.from_u32(0x00FF00FF)
+blue = Albedo.from_u32(0x0000FFFF)
+
+
+def _rust_as_u32(f):
+    return int(f)  # positive finite values: `as u32` truncates
+
+
+def mix2():  # tests.rs:883-889: ((255^2 / 2).sqrt() as u32) in r and g
+    v = _rust_as_u32(math.sqrt(np_f32(255.0) ** 2 / np_f32(2.0)))
+    return Albedo.from_u32((v << 16) | (v << 24) | 0xFF)
+
+
+def mix3():  # tests.rs:1170-1177: ((255^2 / 3).sqrt() as u32) in r, g and b
+    v = _rust_as_u32(np_f32(math.sqrt(np_f32(np_f32(255.0) ** 2 / np_f32(3.0)))))
+    return Albedo.from_u32((v << 8) | (v << 16) | (v << 24) | 0xFF)
+
+
+def np_f32(x):
+    return float(np.float32(x))
+
+
+SIX = [((0, 0, 0), red), ((0, 0, 1), green), ((0, 1, 0), red), ((0, 1, 1), green), ((1, 0, 0), red),
+       ((1, 0, 1), green)]
+
+
+def _root_mip(tree, sectant, pos):
+    return tree.albedo_mip_map_resampling_strategy().sample_root_mip(sectant, pos)
+
+
+def test_mixed_mip_lvl1():  # tests.rs:880-923
+    tree = BoxTree(4, 1)
+    tree.auto_simplify = False
+    tree.albedo_mip_map_resampling_strategy().switch_albedo_mip_maps(True).set_method_at(
+        1, MIPResamplingMethods.BoxFilter)
+    for p, c in SIX:
+        tree.insert(p, c)
+    e = _root_mip(tree, BOX_NODE_CHILDREN_COUNT, (0, 0, 0))
+    assert e.albedo() is not None
+    assert e.albedo() == mix2()
+
+
+def test_mixed_mip_lvl1_where_dim_is_32():  # tests.rs:925-968
+    tree = BoxTree(128, 32)
+    tree.auto_simplify = False
+    tree.albedo_mip_map_resampling_strategy().switch_albedo_mip_maps(True).set_method_at(
+        1, MIPResamplingMethods.BoxFilter)
+    for p, c in [((126, 126, 126), red), ((126, 126, 127), green), ((126, 127, 126), red), ((126, 127, 127), green),
+                 ((127, 126, 126), red), ((127, 126, 127), green)]:
+        tree.insert(p, c)
+    e = _root_mip(tree, BOX_NODE_CHILDREN_COUNT, (31, 31, 31))
+    assert e.albedo() == mix2()
+
+
+@pytest.mark.parametrize("mixed", [False, True])
+def test_mip_lvl2_where_dim_is_2(mixed):  # tests.rs:970-1040 (solid) and 1042-1120 (mixed)
+    tree = BoxTree(8, 2)
+    tree.auto_simplify = False
+    tree.albedo_mip_map_resampling_strategy().switch_albedo_mip_maps(True).set_method_at(
+        1, MIPResamplingMethods.BoxFilter)
+    for p, c in SIX:
+        tree.insert(p, c if mixed else red)
+    e = _root_mip(tree, BOX_NODE_CHILDREN_COUNT, (0, 0, 0))
+    assert e.albedo() == (mix2() if mixed else red)
+    for pos in [(0, 0, 1), (0, 1, 0), (0, 1, 1), (1, 0, 0), (1, 0, 1), (1, 1, 0), (1, 1, 1)]:
+        assert _root_mip(tree, BOX_NODE_CHILDREN_COUNT, pos).albedo() is None
+
+
+def _lvl2_dim4_inserts(tree):
+    for p, c in SIX + [((16, 0, 0), red), ((16, 0, 1), green), ((16, 1, 0), blue), ((16, 1, 1), green),
+                       ((17, 1, 0), red), ((17, 0, 1), blue)]:
+        tree.insert(p, c)
+
+
+def _check_lvl2_dim4(tree):
+    assert _root_mip(tree, 0, (0, 0, 0)).albedo() == mix2()
+    assert _root_mip(tree, 1, (0, 0, 0)).albedo() == mix3()
+    assert _root_mip(tree, BOX_NODE_CHILDREN_COUNT, (0, 0, 0)).albedo() == mix2()
+    assert _root_mip(tree, BOX_NODE_CHILDREN_COUNT, (1, 0, 0)).albedo() == mix3()
+
+
+def test_mixed_mip_lvl2_where_dim_is_4():  # tests.rs:1122-1234
+    tree = BoxTree(64, 4)
+    tree.auto_simplify = False
+    tree.albedo_mip_map_resampling_strategy().switch_albedo_mip_maps(True).set_method_at(
+        1, MIPResamplingMethods.BoxFilter).set_method_at(2, MIPResamplingMethods.BoxFilter)
+    _lvl2_dim4_inserts(tree)
+    _check_lvl2_dim4(tree)
+
+
+def test_mixed_mip_regeneration_lvl2_where_dim_is_4():  # tests.rs:1236-1330
+    tree = BoxTree(64, 4)
+    tree.auto_simplify = False
+    _lvl2_dim4_inserts(tree)
+    for pos in [(0, 0, 0), (1, 0, 0)]:
+        assert _root_mip(tree, BOX_NODE_CHILDREN_COUNT, pos).albedo() is None  # MIPs are off by default
+    tree.albedo_mip_map_resampling_strategy().switch_albedo_mip_maps(True).set_method_at(
+        1, MIPResamplingMethods.BoxFilter).set_method_at(2, MIPResamplingMethods.BoxFilter).recalculate_mips()
+    _check_lvl2_dim4(tree)
+
+
+def test_incremental_mips_equal_recalculated():
+    """MIPs kept up to date by inserts equal the MIPs recalculated from scratch (default strategy, BoxFilter
+    levels): the incremental update_mip of every insert and recalculate_mips build the same bricks."""
+    a = BoxTree(64, 4)
+    b = BoxTree(64, 4)
+    a.auto_simplify = b.auto_simplify = False
+    a.albedo_mip_map_resampling_strategy().switch_albedo_mip_maps(True).set_method_at(
+        1, MIPResamplingMethods.BoxFilter)
+    rng = np.random.default_rng(7)
+    cols = [red, green, blue, Albedo(10, 200, 30, 255)]
+    pts = rng.integers(0, 64, size=(300, 3))
+    for i, p in enumerate(pts):
+        a.insert(tuple(p), cols[i % 4])
+        b.insert(tuple(p), cols[i % 4])
+    b.albedo_mip_map_resampling_strategy().switch_albedo_mip_maps(True).set_method_at(
+        1, MIPResamplingMethods.BoxFilter).recalculate_mips()
+    fa, fb = a.flatten(), b.flatten()
+    assert np.array_equal(fa.node_mips, fb.node_mips)
+    for s in list(range(64)) + [64]:
+        for pos in [(0, 0, 0), (3, 1, 2), (2, 3, 3)]:
+            assert _root_mip(a, s, pos) == _root_mip(b, s, pos)
+
+
+def test_flatten_lod_cuts_children_and_keeps_mips():
+    tree = BoxTree(64, 4)
+    tree.auto_simplify = False
+    _lvl2_dim4_inserts(tree)
+    tree.albedo_mip_map_resampling_strategy().switch_albedo_mip_maps(True)
+    full, cut = tree.flatten(), tree.flatten_lod(0)
+    assert len(full.node_mips) == len(full.node_type) > 1
+    assert len(cut.node_type) == len(cut.node_mips) == 1  # only the root
+    assert np.all(cut.node_children == 0xFFFFFFFF)
+    assert cut.node_ocbits[0] == full.node_ocbits[0]
+    assert cut.node_mips[0] != 0xFFFFFFFF

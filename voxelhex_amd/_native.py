@@ -139,6 +139,13 @@ SIGNATURES = [
     ("vhx_vox_rotation", c_int, [ctypes.c_uint8, P(ctypes.c_int32 * 9)]),
     ("vhx_scene_build", c_int, [c_u32, c_u32, c_u32, c_u64, c_int, P(c_void_p)]),
     ("vhx_flat_desc", c_int, [c_void_p, P(TreeDesc)]),
+    ("vhx_boxtree_switch_mips", c_int, [c_void_p, c_int]),
+    ("vhx_boxtree_set_mip_method", c_int, [c_void_p, c_u32, c_u32, c_f32]),
+    ("vhx_boxtree_set_mip_color_threshold", c_int, [c_void_p, c_u32, c_f32]),
+    ("vhx_boxtree_recalculate_mips", c_int, [c_void_p]),
+    ("vhx_boxtree_sample_root_mip", c_int, [c_void_p, c_u32, c_u32, c_u32, c_u32, P(c_u32), P(c_u32), P(c_u32)]),
+    ("vhx_boxtree_flatten_lod", c_int, [c_void_p, c_u32, P(c_void_p)]),
+    ("vhx_flat_node_mips", c_int, [c_void_p, P(c_void_p), P(c_u32)]),
     ("vhx_flat_free", None, [c_void_p]),
 ]
 

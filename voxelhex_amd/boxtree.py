@@ -133,6 +133,64 @@ class BoxTreeEntry:
         return not self.is_none()
 
 
+class MIPResamplingMethods:
+    """MIPResamplingMethods (src/boxtree/types.rs:113-149) as (code, threshold) pairs for set_method_at."""
+    BoxFilter = (0, 0.0)
+    PointFilter = (1, 0.0)
+    PointFilterBD = (2, 0.0)
+
+    @staticmethod
+    def Posterize(thr):
+        return (3, float(thr))
+
+    @staticmethod
+    def PosterizeBD(thr):
+        return (4, float(thr))
+
+
+class StrategyUpdater:
+    """StrategyUpdater (src/boxtree/mipmap.rs:458-668): chainable MIP-map settings of a BoxTree."""
+
+    def __init__(self, tree):
+        self._t = tree
+
+    def switch_albedo_mip_maps(self, enabled):
+        N.check(N.lib().vhx_boxtree_switch_mips(self._t._h, int(bool(enabled))))
+        self._t._version += 1
+        return self
+
+    def set_method_at(self, mip_level, method):
+        code, thr = method
+        N.check(N.lib().vhx_boxtree_set_mip_method(self._t._h, int(mip_level), code, thr))
+        return self
+
+    def set_color_similarity_thr_at(self, mip_level, similarity_thr):
+        N.check(N.lib().vhx_boxtree_set_mip_color_threshold(self._t._h, int(mip_level), float(similarity_thr)))
+        return self
+
+    def recalculate_mips(self):
+        N.check(N.lib().vhx_boxtree_recalculate_mips(self._t._h))
+        self._t._version += 1
+        return self
+
+    def sample_root_mip(self, sectant, position):
+        x, y, z = _pos(position)
+        k, a, d = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+        N.check(N.lib().vhx_boxtree_sample_root_mip(self._t._h, int(sectant), x, y, z, ctypes.byref(k),
+                                                    ctypes.byref(a), ctypes.byref(d)))
+        return _entry_of(k.value, a.value, d.value)
+
+
+def _entry_of(kind, albedo, data):
+    if kind == N.VHX_ENTRY_EMPTY:
+        return BoxTreeEntry.Empty()
+    if kind == N.VHX_ENTRY_VISUAL:
+        return BoxTreeEntry.Visual(Albedo.from_packed(albedo))
+    if kind == N.VHX_ENTRY_INFORMATIVE:
+        return BoxTreeEntry.Informative(data)
+    return BoxTreeEntry.Complex(Albedo.from_packed(albedo), data)
+
+
 def voxel_data(data=None):
     """The reference's voxel_data! macro (src/boxtree/mod.rs:65-72)."""
     return BoxTreeEntry.Empty() if data is None else BoxTreeEntry.Informative(data)
@@ -219,6 +277,10 @@ class FlatTree:
         self.solid_values = arr(d.solid_values, d.solid_count, np.uint32)
         self.color_palette = arr(d.color_palette, d.color_count, np.uint32)
         self.data_palette = arr(d.data_palette, d.data_count, np.uint32)
+        mp, mc = ctypes.c_void_p(), ctypes.c_uint32()
+        N.check(N.lib().vhx_flat_node_mips(self._h, ctypes.byref(mp), ctypes.byref(mc)))
+        # per node: its MIP brick descriptor (empty unless the tree was flattened with MIPs)
+        self.node_mips = arr(mp.value, mc.value, np.uint32)
 
     @property
     def boxtree_size(self):
@@ -351,14 +413,11 @@ class BoxTree:
         x, y, z = _pos(position)
         k, a, d = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
         N.check(N.lib().vhx_boxtree_get(self._h, x, y, z, ctypes.byref(k), ctypes.byref(a), ctypes.byref(d)))
-        kind = k.value
-        if kind == N.VHX_ENTRY_EMPTY:
-            return BoxTreeEntry.Empty()
-        if kind == N.VHX_ENTRY_VISUAL:
-            return BoxTreeEntry.Visual(Albedo.from_packed(a.value))
-        if kind == N.VHX_ENTRY_INFORMATIVE:
-            return BoxTreeEntry.Informative(d.value)
-        return BoxTreeEntry.Complex(Albedo.from_packed(a.value), d.value)
+        return _entry_of(k.value, a.value, d.value)
+
+    def albedo_mip_map_resampling_strategy(self):
+        """BoxTree::albedo_mip_map_resampling_strategy (src/boxtree/mod.rs:241-243)."""
+        return StrategyUpdater(self)
 
     def simplify(self, recursive=True):
         N.check(N.lib().vhx_boxtree_simplify(self._h, int(recursive)))
@@ -395,6 +454,13 @@ class BoxTree:
             self._flat = FlatTree(h.value)
             self._flat_version = self._version
         return self._flat
+
+    def flatten_lod(self, max_depth):
+        """Flattened image with node MIPs and only the nodes down to `max_depth` (root = 0): the deeper nodes are left
+        out, their parents' MIPs stand in for them in a MIP-enabled trace (vhx_boxtree_flatten_lod)."""
+        h = ctypes.c_void_p()
+        N.check(N.lib().vhx_boxtree_flatten_lod(self._h, int(max_depth), ctypes.byref(h)))
+        return FlatTree(h.value)
 
     # -- raytracing (src/raytracing/cpu.rs:296) ----------------------------------------------------------------
     def get_by_ray(self, ray, device=None):

@@ -173,6 +173,8 @@ static Node uniform_solid_node(uint32_t v) {
     n.bricks.resize(1);
     n.bricks[0].kind = BrickKind::Solid;
     n.bricks[0].solid = v;
+    n.mip.kind = BrickKind::Solid;  // node.rs:191-199: a uniform solid node is its own MIP
+    n.mip.solid = v;
     n.occupied_bits = ~0ull;
     return n;
 }
@@ -540,11 +542,10 @@ size_t BoxTree::get_node_internal(size_t key, Cube &bounds, F3 position) const {
     }
 }
 
-uint32_t BoxTree::get_raw(U3 pos) const {  // src/boxtree/mod.rs:247-317
-    Cube bounds{f3(0.f, 0.f, 0.f), (float)boxtree_size};
+uint32_t BoxTree::get_internal(size_t key, Cube bounds, U3 pos) const {  // src/boxtree/mod.rs:247-317
     F3 p = from_u3(pos);
     if (!cube_contains(bounds, p)) return kEmpty32;
-    size_t key = get_node_internal(0, bounds, p);
+    key = get_node_internal(key, bounds, p);
     const Node &n = nodes.get(key);
     switch (n.content) {
         case Content::Leaf: {
@@ -567,8 +568,11 @@ uint32_t BoxTree::get_raw(U3 pos) const {  // src/boxtree/mod.rs:247-317
         default: return kEmpty32;
     }
 }
-Entry BoxTree::get(U3 pos) const {  // pix_get_ref, src/boxtree/node.rs:335-373
-    uint32_t v = get_raw(pos);
+uint32_t BoxTree::get_raw(U3 pos) const {  // src/boxtree/mod.rs:223-233
+    return get_internal(0, Cube{f3(0.f, 0.f, 0.f), (float)boxtree_size}, pos);
+}
+Entry BoxTree::get(U3 pos) const { return entry_of(get_raw(pos)); }
+Entry BoxTree::entry_of(uint32_t v) const {  // pix_get_ref, src/boxtree/node.rs:335-373
     bool cn = !pix_color_is_some(v), dn = !pix_data_is_some(v);
     Entry e{VHX_ENTRY_EMPTY, 0, 0};
     if (cn && dn) return e;
@@ -776,6 +780,7 @@ void BoxTree::post_process_node_insert(const std::vector<std::pair<size_t, uint8
         }
     }
     nodes.get(key).occupied_bits = occ;
+    update_mip(key, nb, pos);  // insert.rs:494
 }
 
 int BoxTree::insert_at_lod_internal(bool overwrite, U3 pos_u32, uint32_t insert_size, Entry data) {
@@ -1012,5 +1017,286 @@ bool BoxTree::simplify(size_t key, bool recursive) {  // src/boxtree/update/mod.
     }
     return false;
 }
+
+// ---------------------------------------------------------------------------------------------- MIP maps
+// src/boxtree/mipmap.rs and the resampling functions of src/boxtree/iterate.rs:349-560. Albedo is packed
+// r | g<<8 | b<<16 | a<<24 here; the reference's u32 arithmetic on Albedou32 wraps like release builds (in a debug
+// build the reference panics on the subtraction in Posterize whenever a channel of the candidate is brighter).
+struct Alb {
+    uint32_t r, g, b, a;
+};
+static inline Alb alb_of(uint32_t c) { return Alb{c & 0xFFu, (c >> 8) & 0xFFu, (c >> 16) & 0xFFu, c >> 24}; }
+static inline uint32_t alb_pack_u8(uint32_t r, uint32_t g, uint32_t b, uint32_t a) {
+    return (r & 0xFFu) | ((g & 0xFFu) << 8) | ((b & 0xFFu) << 16) | ((a & 0xFFu) << 24);
+}
+// From<Albedou32> for Albedo: min(255) as u8
+static inline uint32_t alb_pack(Alb v) {
+    return alb_pack_u8(std::min(v.r, 255u), std::min(v.g, 255u), std::min(v.b, 255u), std::min(v.a, 255u));
+}
+static inline Alb alb_pow2(Alb v) { return Alb{v.r * v.r, v.g * v.g, v.b * v.b, v.a * v.a}; }
+static inline Alb alb_add(Alb x, Alb y) { return Alb{x.r + y.r, x.g + y.g, x.b + y.b, x.a + y.a}; }
+static inline Alb alb_sub(Alb x, Alb y) { return Alb{x.r - y.r, x.g - y.g, x.b - y.b, x.a - y.a}; }
+static inline uint32_t round_u32(float f) { return as_u32(std::round(f)); }
+static inline Alb alb_div(Alb v, uint32_t d) {  // Div<u32>: (x as f32 / d as f32).round() as u32
+    const float fd = (float)d;
+    return Alb{round_u32((float)v.r / fd), round_u32((float)v.g / fd), round_u32((float)v.b / fd),
+               round_u32((float)v.a / fd)};
+}
+static inline Alb alb_sqrt(Alb v) {  // (x as f32).sqrt().round() as u32
+    return Alb{round_u32(std::sqrt((float)v.r)), round_u32(std::sqrt((float)v.g)), round_u32(std::sqrt((float)v.b)),
+               round_u32(std::sqrt((float)v.a))};
+}
+static inline float alb_length(Alb v) {
+    return std::sqrt((float)(v.r * v.r + v.g * v.g + v.b * v.b + v.a * v.a));
+}
+// Albedo::distance_from, src/boxtree/detail.rs:62-69
+static inline float alb_distance(uint32_t x, uint32_t y) {
+    const Alb a = alb_of(x), b = alb_of(y);
+    const float dr = (float)a.r - (float)b.r, dg = (float)a.g - (float)b.g, db = (float)a.b - (float)b.b,
+                da = (float)a.a - (float)b.a;
+    return std::sqrt(dr * dr + dg * dg + db * db + da * da);
+}
+
+// MIPResamplingFunction::execute (iterate.rs:434-560). `sample` returns false for None. PointFilter and Posterize keep
+// their groups in first-seen order where the reference iterates a std HashMap (random order per process): results
+// that depend on that order (ties of the most frequent colour, a colour within the threshold of two groups) are not
+// reproducible by the reference itself; this restatement resolves them in first-seen order, the last group of the
+// highest count winning like Iterator::max_by_key.
+static bool mip_execute(const MipMethodCfg &m, U3 start, uint32_t size, const std::function<bool(U3, uint32_t &)> &sample,
+                        uint32_t &out) {
+    uint32_t c = 0;
+    switch (m.kind) {
+        case kBoxFilter: {
+            bool any = false;
+            int32_t count = 0;
+            float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+            for (uint32_t x = start.x; x < start.x + size; ++x)
+                for (uint32_t y = start.y; y < start.y + size; ++y)
+                    for (uint32_t z = start.z; z < start.z + size; ++z) {
+                        if (!sample(U3{x, y, z}, c)) continue;
+                        const Alb a = alb_of(c);
+                        const float r = (float)a.r, g = (float)a.g, b = (float)a.b, al = (float)a.a;
+                        if (!any) {
+                            any = true;
+                            count = 1;
+                            s0 = r * r, s1 = g * g, s2 = b * b, s3 = al * al;
+                        } else {
+                            count += 1;
+                            s0 += r * r, s1 += g * g, s2 += b * b, s3 += al * al;
+                        }
+                    }
+            if (!any) return false;
+            const float n = (float)count;
+            out = alb_pack_u8(as_u8(std::fmin(std::sqrt(s0 / n), 255.f)), as_u8(std::fmin(std::sqrt(s1 / n), 255.f)),
+                              as_u8(std::fmin(std::sqrt(s2 / n), 255.f)), as_u8(std::fmin(std::sqrt(s3 / n), 255.f)));
+            return true;
+        }
+        case kPointFilter:
+        case kPointFilterBD: {
+            std::vector<std::pair<uint32_t, uint32_t>> counts;  // (albedo, occurrences), first-seen order
+            for (uint32_t x = start.x; x < start.x + size; ++x)
+                for (uint32_t y = start.y; y < start.y + size; ++y)
+                    for (uint32_t z = start.z; z < start.z + size; ++z) {
+                        if (!sample(U3{x, y, z}, c)) continue;
+                        auto it = std::find_if(counts.begin(), counts.end(), [&](const auto &e) { return e.first == c; });
+                        if (it == counts.end())
+                            counts.push_back({c, 1});
+                        else
+                            it->second += 1;
+                    }
+            if (counts.empty()) return false;
+            size_t best = 0;
+            for (size_t i = 1; i < counts.size(); ++i)
+                if (counts[i].second >= counts[best].second) best = i;
+            out = counts[best].first;
+            return true;
+        }
+        default: {  // Posterize / PosterizeBD
+            std::vector<std::pair<Alb, uint32_t>> groups;  // (sum of squared albedo, count)
+            const float thr = m.thr * 255.f;
+            for (uint32_t x = start.x; x < start.x + size; ++x)
+                for (uint32_t y = start.y; y < start.y + size; ++y)
+                    for (uint32_t z = start.z; z < start.z + size; ++z) {
+                        if (!sample(U3{x, y, z}, c)) continue;
+                        const Alb col = alb_of(c);
+                        bool merged = false;
+                        for (auto &g : groups) {
+                            const Alb poster = alb_sqrt(alb_div(g.first, g.second));
+                            if (alb_length(alb_sub(poster, col)) < thr) {
+                                g.first = alb_add(g.first, alb_pow2(col));
+                                g.second += 1;
+                                merged = true;
+                                break;
+                            }
+                        }
+                        if (!merged) groups.push_back({alb_pow2(col), 1});
+                    }
+            if (groups.empty()) return false;
+            size_t best = 0;
+            for (size_t i = 1; i < groups.size(); ++i)
+                if (groups[i].second >= groups[best].second) best = i;
+            out = alb_pack(alb_sqrt(alb_div(groups[best].first, groups[best].second)));
+            return true;
+        }
+    }
+}
+
+// NodeContent::pix_get_ref(..).albedo() (node.rs:335-373, mod.rs:81-88): the colour of a colour-carrying value
+bool BoxTree::albedo_of(uint32_t v, uint32_t &albedo) const {
+    if (!pix_color_is_some(v) || pix_color_index(v) >= color_palette.size()) return false;
+    albedo = color_palette[pix_color_index(v)];
+    return true;
+}
+
+void BoxTree::update_mip(size_t key, const Cube &nb, U3 position) {  // src/boxtree/mipmap.rs:42-338
+    if (!mip_strategy.enabled) return;
+    const uint32_t bd = brick_dim;
+    const size_t level = as_usize(std::log2(nb.size / (float)bd));
+    const auto mit = mip_strategy.methods.find(level);
+    const MipMethodCfg sampler = mit != mip_strategy.methods.end() ? mit->second : MipMethodCfg{kBoxFilter, 0.f};
+    const bool dominant_bottom = mit != mip_strategy.methods.end() && mit->second.kind == kPointFilterBD;
+
+    const Content content = nodes.get(key).content;
+    U3 start{0, 0, 0};
+    uint32_t ssize = 0;
+    if (content == Content::Nothing) return;
+    if (content == Content::UniformLeaf) {
+        nodes.get(key).mip = Brick{};  // a uniform leaf is equivalent to its MIP
+        return;
+    }
+    if (content == Content::Leaf) {
+        ssize = std::min(as_u32(nb.size) / bd, bd * 4u);
+        auto st = [&](uint32_t p) {
+            const uint32_t q = (p - p % ssize) * 4u * bd;
+            return as_u32(std::round(std::floor((float)q / nb.size)));
+        };
+        start = U3{st(position.x), st(position.y), st(position.z)};
+    } else if (dominant_bottom) {
+        ssize = as_u32(nb.size) / bd;
+        start = U3{position.x - position.x % ssize, position.y - position.y % ssize, position.z - position.z % ssize};
+    } else {
+        ssize = 4;
+        const F3 pib = sub(from_u3(position), nb.min);
+        const F3 v1 = divs(mul(mul(pib, 4.f), (float)bd), nb.size);
+        const U3 v2 = round_u3(floor3(v1));
+        start = U3{v2.x - v2.x % 4u, v2.y - v2.y % 4u, v2.z - v2.z % 4u};
+    }
+
+    uint32_t color = 0;
+    bool sampled;
+    if (content == Content::Leaf || dominant_bottom) {
+        sampled = mip_execute(sampler, start, ssize, [&](U3 pos, uint32_t &c) {
+            return albedo_of(get_internal(key, nb, pos), c);
+        }, color);
+    } else {
+        const float mip_edge = (float)(bd * 4u);
+        sampled = mip_execute(sampler, start, ssize, [&](U3 pos, uint32_t &c) {
+            const uint8_t cs = offset_sectant(from_u3(pos), mip_edge);
+            const size_t ck = child(key, cs);
+            if (ck == (size_t)kEmpty32 || !nodes.key_is_valid(ck)) return false;
+            const F3 pic = sub(from_u3(pos), mul(lut(cs), mip_edge));
+            const Brick &m = nodes.get(ck).mip;
+            switch (m.kind) {
+                case BrickKind::Empty: return false;
+                case BrickKind::Solid: return albedo_of(m.solid, c);
+                default:
+                    return albedo_of(m.parted[flat_projection(as_usize(pic.x), as_usize(pic.y), as_usize(pic.z), bd)], c);
+            }
+        }, color);
+    }
+    if (!sampled) return;
+
+    uint32_t entry;
+    const auto tit = mip_strategy.color_thresholds.find(level);
+    bool similar = false;
+    if (tit != mip_strategy.color_thresholds.end()) {
+        const float thr = tit->second * 255.f;
+        for (size_t i = 0; i < color_palette.size(); ++i)
+            if (alb_distance(color, color_palette[i]) < thr) {
+                entry = pix_visual((uint32_t)i);
+                similar = true;
+                break;
+            }
+    }
+    if (!similar) entry = add_to_palette(Entry{VHX_ENTRY_VISUAL, color, 0});
+
+    const auto mi = matrix_index_for(nb, position, bd);
+    const size_t f = flat_projection(mi[0], mi[1], mi[2], bd);
+    Brick &mip = nodes.get(key).mip;
+    const size_t n3 = (size_t)bd * bd * bd;
+    if (mip.kind == BrickKind::Empty) {
+        mip.parted.assign(n3, kEmpty32);
+    } else if (mip.kind == BrickKind::Solid) {
+        mip.parted.assign(n3, mip.solid);
+    }
+    mip.kind = BrickKind::Parted;
+    mip.parted[f] = entry;
+}
+
+void BoxTree::recalculate_mip(size_t key, const Cube &nb) {  // mipmap.rs:613-633
+    if (!mip_strategy.enabled) return;
+    nodes.get(key).mip = Brick{};
+    const float bd = (float)brick_dim;
+    for (uint32_t x = 0; x < brick_dim; ++x)
+        for (uint32_t y = 0; y < brick_dim; ++y)
+            for (uint32_t z = 0; z < brick_dim; ++z) {
+                const F3 off = divs(mul(f3((float)x, (float)y, (float)z), nb.size), bd);
+                const F3 pos = add(nb.min, f3(std::round(off.x), std::round(off.y), std::round(off.z)));
+                update_mip(key, nb, round_u3(pos));
+            }
+}
+
+void BoxTree::recalculate_mips() {  // mipmap.rs:536-586: depth first, children before their parent
+    struct Item {
+        size_t key;
+        Cube bounds;
+        uint32_t target;
+    };
+    std::vector<Item> stack{{0, Cube{f3(0.f, 0.f, 0.f), (float)boxtree_size}, 0}};
+    while (!stack.empty()) {
+        Item &it = stack.back();
+        if (it.target >= kChildren) {
+            recalculate_mip(it.key, it.bounds);
+            stack.pop_back();
+            if (!stack.empty()) stack.back().target += 1;
+            continue;
+        }
+        switch (nodes.get(it.key).content) {
+            case Content::Internal: {
+                const size_t ck = child(it.key, (uint8_t)it.target);
+                if (nodes.key_is_valid(ck) && nodes.get(ck).content != Content::Nothing) {
+                    const Cube cb = child_bounds_for(it.bounds, (uint8_t)it.target);
+                    stack.push_back(Item{ck, cb, 0});
+                } else {
+                    it.target += 1;
+                }
+                break;
+            }
+            case Content::Nothing:  // the reference panics (unreachable); only an empty root gets here
+                stack.pop_back();
+                if (!stack.empty()) stack.back().target += 1;
+                break;
+            default: it.target = kChildren; break;
+        }
+    }
+}
+
+void BoxTree::switch_albedo_mip_maps(bool enabled) {  // mipmap.rs:588-609
+    const bool before = mip_strategy.enabled;
+    mip_strategy.enabled = enabled;
+    if (enabled && before != enabled && nodes.get(0).content != Content::Nothing) recalculate_mips();
+}
+
+uint32_t BoxTree::sample_root_mip(uint8_t sectant, U3 position) const {  // mipmap.rs:635-668
+    const size_t key = sectant >= kChildren ? 0 : child(0, sectant);
+    if (!nodes.key_is_valid(key)) return kEmpty32;
+    const Brick &m = nodes.get(key).mip;
+    switch (m.kind) {
+        case BrickKind::Empty: return kEmpty32;
+        case BrickKind::Solid: return m.solid;
+        default: return m.parted[flat_projection(position.x, position.y, position.z, brick_dim)];
+    }
+}
+
 
 }  // namespace vhx

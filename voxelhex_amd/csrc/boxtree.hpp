@@ -14,7 +14,10 @@
 //   BrickData helpers          src/boxtree/node.rs:34-145, NodeContent pix_* 259-373, is_all 424-458
 //   update triggers            insert.rs:328-405: (node stack, modified bottom sectants) of every insert/update, queued
 //                              for a stream like BoxTreeGPUHost's changes_buffer (src/raytracing/bevy/mod.rs:164-173)
-// Not restated (no effect on what the raytracer reads): MIP maps (disabled by default, mipmap.rs:42-44, 351-353).
+//   MIP maps                   update_mip src/boxtree/mipmap.rs:42-338, MIPMapStrategy defaults 341-354,
+//                              recalculate_mips / switch_albedo_mip_maps / recalculate_mip 536-633, resampling
+//                              MIPResamplingFunction::execute src/boxtree/iterate.rs:434-560 (Albedou32 349-432)
+#include <map>
 #pragma once
 
 #include <array>
@@ -62,6 +65,7 @@ struct Node {
     bool has_children = false;  // NodeChildren::Children vs NoChildren
     std::array<uint32_t, kChildren> children{};
     uint64_t occupied_bits = 0;
+    Brick mip;                   // NodeData::mip (src/boxtree/types.rs:183-186): the node's albedo MIP brick
     uint8_t occlusion_bits = 0;  // bit CubeSides: no ray enters from that side (src/boxtree/types.rs:189-200)
     bool is_occluded() const { return (occlusion_bits & 0x3F) == 0x3F; }  // node.rs:176-178
 };
@@ -91,6 +95,21 @@ class ObjectPool {
     size_t first_available_ = 0;
 };
 
+// MIPResamplingMethods (src/boxtree/types.rs:113-149); the values are the C ABI's VHX_MIP_* codes
+enum MipMethod : uint32_t { kBoxFilter = 0, kPointFilter = 1, kPointFilterBD = 2, kPosterize = 3, kPosterizeBD = 4 };
+struct MipMethodCfg {
+    uint32_t kind;
+    float thr;  // Posterize / PosterizeBD similarity threshold
+};
+// MIPMapStrategy with its defaults (src/boxtree/mipmap.rs:341-354); a level without a method uses BoxFilter
+// (MIPResamplingMethods::default, types.rs:121-122), a level without a colour threshold adds every new colour
+struct MipStrategy {
+    bool enabled = false;
+    std::map<size_t, MipMethodCfg> methods{
+        {1, {kPosterize, 0.05f}}, {2, {kBoxFilter, 0.f}}, {3, {kBoxFilter, 0.f}}, {4, {kBoxFilter, 0.f}}};
+    std::map<size_t, float> color_thresholds{{2, 0.1f}, {3, 0.05f}, {4, 0.02f}};
+};
+
 class BoxTree {
    public:
     // returns 0 or a VHX_E_TREE_* code (OctreeError)
@@ -101,7 +120,19 @@ class BoxTree {
     int update(U3 pos, Entry e) { return insert_at_lod_internal(false, pos, 1, e); }
     uint32_t get_raw(U3 pos) const;
     Entry get(U3 pos) const;
+    Entry entry_of(uint32_t value) const;
     bool simplify(size_t node_key, bool recursive);
+    // MIP maps (src/boxtree/mipmap.rs)
+    MipStrategy mip_strategy;
+    void switch_albedo_mip_maps(bool enabled);
+    void recalculate_mips();
+    void recalculate_mip(size_t node_key, const Cube &node_bounds);
+    void update_mip(size_t node_key, const Cube &node_bounds, U3 position);
+    // sample_root_mip (mipmap.rs:635-668): sectant >= 64 samples the root's MIP, else the root's child's; raw value
+    uint32_t sample_root_mip(uint8_t sectant, U3 position) const;
+    // BoxTree::get_internal (src/boxtree/mod.rs:247-317) from any node and its bounds
+    uint32_t get_internal(size_t node_key, Cube bounds, U3 position) const;
+    bool albedo_of(uint32_t value, uint32_t &albedo) const;
 
     bool auto_simplify = true;
     uint32_t brick_dim = 0, boxtree_size = 0;
@@ -122,10 +153,11 @@ class BoxTree {
     size_t get_node_internal(size_t key, Cube &bounds, F3 position) const;
     size_t child(size_t node_key, uint8_t sectant) const;
 
+    uint32_t add_to_palette(Entry e);
+
    private:
     std::unordered_map<uint32_t, size_t> color_index_, data_index_;
 
-    uint32_t add_to_palette(Entry e);
     int insert_at_lod_internal(bool overwrite_if_empty, U3 pos, uint32_t insert_size, Entry e);
     void post_process_node_insert(const std::vector<std::pair<size_t, uint8_t>> &node_stack, const Cube &node_bounds,
                                   const std::array<size_t, 3> &aus, U3 pos, uint32_t insert_size);

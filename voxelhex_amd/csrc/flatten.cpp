@@ -39,6 +39,9 @@ struct vhx_flat {
     std::vector<uint32_t> solid_values;
     std::vector<uint32_t> color_palette;
     std::vector<uint32_t> data_palette;
+    // per node: its MIP brick descriptor (same encoding as a leaf's child entry; node_mips of
+    // src/raytracing/bevy/types.rs:245-247); empty unless the tree's MIP maps are enabled
+    std::vector<uint32_t> node_mips;
 };
 
 // ---------------------------------------------------------------------------------------------- parallel helper
@@ -188,7 +191,10 @@ static uint32_t brick_desc(const Brick &b, vhx_flat &f, std::vector<const std::v
     }
 }
 
-static vhx_flat *flatten_tree(const BoxTree &t) {
+// max_depth: nodes deeper than this (root = depth 0) are left out; their parent's child entries are VHX_EMPTY while its
+// occupancy bits stay, so a MIP-enabled trace shows the parent's MIP there (the WGSL's stand-in for a child that is
+// not resident, viewport_render.wgsl:438-454). MIP bricks are numbered with the bricks, after the node's own.
+static vhx_flat *flatten_tree(const BoxTree &t, uint32_t max_depth = 0xFFFFFFFFu, bool with_mips = false) {
     auto *f = new vhx_flat();
     f->size = t.boxtree_size;
     f->brick_dim = t.brick_dim;
@@ -196,6 +202,7 @@ static vhx_flat *flatten_tree(const BoxTree &t) {
     std::deque<size_t> queue;
     std::vector<const std::vector<uint32_t> *> parted;
     std::unordered_map<uint32_t, uint32_t> solid_index;
+    std::vector<uint32_t> depth{0};  // by BFS index
     index.emplace(0, 0);
     queue.push_back(0);
     while (!queue.empty()) {
@@ -211,7 +218,7 @@ static vhx_flat *flatten_tree(const BoxTree &t) {
         f->node_ocbits.push_back(n.occupied_bits);
         f->node_children.resize((size_t)(idx + 1) * 64, VHX_EMPTY);
         uint32_t *ch = &f->node_children[(size_t)idx * 64];
-        if (n.content == Content::Internal && n.has_children) {
+        if (n.content == Content::Internal && n.has_children && depth[idx] < max_depth) {
             for (int s = 0; s < 64; ++s) {
                 size_t c = n.children[s];
                 if (!t.nodes.key_is_valid(c)) continue;  // freed / missing child: traced as empty
@@ -220,6 +227,7 @@ static vhx_flat *flatten_tree(const BoxTree &t) {
                     uint32_t ni = (uint32_t)index.size();
                     index.emplace(c, ni);
                     queue.push_back(c);
+                    depth.push_back(depth[idx] + 1);
                     ch[s] = ni;
                 } else {
                     ch[s] = it->second;
@@ -230,6 +238,7 @@ static vhx_flat *flatten_tree(const BoxTree &t) {
         } else if (n.content == Content::UniformLeaf) {
             ch[0] = brick_desc(n.bricks[0], *f, parted, solid_index);
         }
+        if (with_mips) f->node_mips.push_back(brick_desc(n.mip, *f, parted, solid_index));
     }
     size_t n3 = (size_t)t.brick_dim * t.brick_dim * t.brick_dim;
     f->brick_count = (uint32_t)parted.size();
@@ -479,7 +488,51 @@ int vhx_scene_insert(vhx_boxtree *tree, uint32_t scene, uint64_t seed) {
 }
 int vhx_boxtree_flatten(const vhx_boxtree *tree, vhx_flat **out) {
     if (!tree || !out) return VHX_E_INVALID_ARG;
-    *out = flatten_tree(*tree->tree);
+    *out = flatten_tree(*tree->tree, 0xFFFFFFFFu, tree->tree->mip_strategy.enabled);
+    return VHX_OK;
+}
+int vhx_boxtree_flatten_lod(const vhx_boxtree *tree, uint32_t max_depth, vhx_flat **out) {
+    if (!tree || !out) return VHX_E_INVALID_ARG;
+    *out = flatten_tree(*tree->tree, max_depth, true);
+    return VHX_OK;
+}
+int vhx_flat_node_mips(const vhx_flat *f, const uint32_t **node_mips, uint32_t *count) {
+    if (!f || !node_mips || !count) return VHX_E_INVALID_ARG;
+    *node_mips = f->node_mips.empty() ? nullptr : f->node_mips.data();
+    *count = (uint32_t)f->node_mips.size();
+    return VHX_OK;
+}
+int vhx_boxtree_switch_mips(vhx_boxtree *tree, int enabled) {
+    if (!tree) return VHX_E_INVALID_ARG;
+    tree->tree->switch_albedo_mip_maps(enabled != 0);
+    return VHX_OK;
+}
+int vhx_boxtree_set_mip_method(vhx_boxtree *tree, uint32_t level, uint32_t method, float threshold) {
+    if (!tree || method > VHX_MIP_POSTERIZE_BD || !(threshold == threshold)) return VHX_E_INVALID_ARG;
+    // set_method_at_internal (mipmap.rs:414-431): Posterize thresholds are clamped to [0, 1]
+    if (method == VHX_MIP_POSTERIZE || method == VHX_MIP_POSTERIZE_BD) threshold = std::clamp(threshold, 0.f, 1.f);
+    tree->tree->mip_strategy.methods[level] = MipMethodCfg{method, threshold};
+    return VHX_OK;
+}
+int vhx_boxtree_set_mip_color_threshold(vhx_boxtree *tree, uint32_t level, float threshold) {
+    if (!tree || !(threshold == threshold)) return VHX_E_INVALID_ARG;
+    // set_color_similarity_thr_internal (mipmap.rs:365-379): clamped to [0, 1]
+    tree->tree->mip_strategy.color_thresholds[level] = std::clamp(threshold, 0.f, 1.f);
+    return VHX_OK;
+}
+int vhx_boxtree_recalculate_mips(vhx_boxtree *tree) {
+    if (!tree) return VHX_E_INVALID_ARG;
+    if (tree->tree->nodes.get(0).content != Content::Nothing) tree->tree->recalculate_mips();
+    return VHX_OK;
+}
+int vhx_boxtree_sample_root_mip(const vhx_boxtree *tree, uint32_t sectant, uint32_t x, uint32_t y, uint32_t z,
+                                uint32_t *kind, uint32_t *albedo, uint32_t *data) {
+    const uint32_t bd = tree ? tree->tree->brick_dim : 0;
+    if (!tree || !kind || !albedo || !data || sectant > 64 || x >= bd || y >= bd || z >= bd) return VHX_E_INVALID_ARG;
+    const Entry e = tree->tree->entry_of(tree->tree->sample_root_mip((uint8_t)sectant, U3{x, y, z}));
+    *kind = e.kind;
+    *albedo = e.albedo;
+    *data = e.data;
     return VHX_OK;
 }
 int vhx_scene_build(uint32_t scene, uint32_t size, uint32_t brick_dim, uint64_t seed, int threads, vhx_flat **out) {
