@@ -215,6 +215,16 @@ int vhx_trace_primary(vhx_ctx *ctx, const vhx_camera *cam, uint32_t tile_size, u
  * be skipped: the pixels that differ from the exact path are measured in tests/test_gpu_fast.py and DESIGN.md §10.
  * Other traces (tiles, ray batches, shadows, byte counting) stay exact. Default off. */
 int vhx_set_depth_prepass(vhx_ctx *ctx, int enable, float margin);
+/* MIP stand-ins for absent children (the WGSL path's probe_MIP, src/raytracing/bevy/viewport_render.wgsl:328-364,
+ * 438-454, enabled by tree_properties bit 16, streaming/mod.rs:288-290): node_mips[i] is node i's MIP brick descriptor
+ * (same encoding as a leaf's child entry, VHX_EMPTY = none; the bricks live in voxels / solid_values like any other,
+ * e.g. vhx_boxtree_flatten_lod). While set, a node iteration of an Internal or Leaf node whose target sectant is
+ * occupied (occupancy bit set) but whose child entry is VHX_EMPTY (not resident) first traces the node's MIP brick
+ * over the node's cube; a MIP hit ends the ray there, a miss leaves the ray where it was and ADVANCEs past the
+ * sectant (where the reference CPU path would push into the child, which does not exist). Without MIPs (the default)
+ * such a push ends the ray as a miss, as before. A tree whose children are all present traces identically either way.
+ * NULL disables; count must equal the uploaded tree's node_count; a new vhx_upload_tree disables them. */
+int vhx_set_node_mips(vhx_ctx *ctx, const uint32_t *node_mips, uint32_t count);
 /* Traces n explicit rays; rays = 6 f32 per ray (origin xyz, direction xyz), host or device per on_device. */
 int vhx_trace_rays(vhx_ctx *ctx, const float *rays, uint64_t n, const vhx_hits *out, int on_device);
 /* Hard shadows (BASELINE config 5; the reference has no shadow rays — semantics defined in DESIGN.md §9): for

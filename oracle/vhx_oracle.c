@@ -29,6 +29,11 @@
  * f32::min/max ignore NaN (fminf/fmaxf), signum(+-0) = +-1, `as` casts saturate (NaN -> 0), % on f32 is fmodf,
  * powf(x, 2.) is x*x (LLVM folds it so), V3c<f32> -> V3c<i32> rounds half away from zero.
  *
+ * MIP stand-ins (vhx_oracle_set_node_mips; not the reference CPU path, which never reads MIPs): with node MIPs set,
+ * a node iteration whose target sectant is occupied but whose child entry is absent traces the node's MIP brick over
+ * the node's cube first -- the WGSL path's probe_MIP (src/raytracing/bevy/viewport_render.wgsl:328-364, 438-454) --
+ * and ADVANCEs past the sectant on a miss instead of pushing into the missing child.
+ *
  * Deviation (documented in DESIGN.md): the reference loops have no iteration bound; this restatement stops a ray
  * after VHX_ORACLE_MAX_ITERS inner iterations and reports a miss (the GPU kernel uses the same bound).
  */
@@ -326,6 +331,10 @@ static inline void ns_pop(node_stack *s) {
     s->head = s->head == 0 ? 3 : s->head - 1;
 }
 
+/* node MIP descriptors (vhx_oracle_set_node_mips), NULL = the reference path */
+static const uint32_t *g_node_mips;
+static uint32_t g_node_mips_count;
+
 /* BoxTree::get_by_ray, cpu.rs:296-458 */
 static void get_by_ray(const vhx_tree_desc *t, v3 o, v3 d, hit_t *h) {
     memset(h, 0, sizeof(*h));
@@ -391,6 +400,18 @@ static void get_by_ray(const vhx_tree_desc *t, v3 o, v3 d, hit_t *h) {
                     }
                 }
             }
+            int mip_adv = 0; /* MIP stand-in for an occupied but absent child (see the header) */
+            if (g_node_mips && target < 64 && (ntype == VHX_NODE_INTERNAL || ntype == VHX_NODE_LEAF) &&
+                t->node_children[(uint64_t)node * 64 + target] == VHX_EMPTY && (occ & ((uint64_t)1 << target)) != 0) {
+                mip_adv = 1;
+                h->bytes += 4;
+                const uint32_t mdesc = node < g_node_mips_count ? g_node_mips[node] : VHX_EMPTY;
+                v3 pm = p;
+                if (probe_brick(t, &r, &pm, mdesc, cur, h, &iters)) {
+                    h->hit = 1;
+                    return;
+                }
+            }
             if (backtrack || target >= 64 || occ == 0 || (occ & OCC_LUT[target][dir_idx]) == 0) {
                 /* POP */
                 h->n_pop++;
@@ -408,7 +429,7 @@ static void get_by_ray(const vhx_tree_desc *t, v3 o, v3 d, hit_t *h) {
                 if (stack.count != 0) node = stack.data[stack.head];
                 continue;
             }
-            if (ntype == VHX_NODE_INTERNAL && (occ & ((uint64_t)1 << target)) != 0) {
+            if (ntype == VHX_NODE_INTERNAL && (occ & ((uint64_t)1 << target)) != 0 && !mip_adv) {
                 /* PUSH */
                 h->n_push++;
                 EV('U');
@@ -505,6 +526,12 @@ static void primary_ray(const vhx_camera *c, uint32_t px, uint32_t py, v3 *o, v3
 }
 
 /* ---------------------------------------------------------------- exported API ------------------------------ */
+/* Sets (or with NULL clears) the node MIP descriptors every following trace uses (process-wide). */
+void vhx_oracle_set_node_mips(const uint32_t *node_mips, uint32_t count) {
+    g_node_mips = node_mips;
+    g_node_mips_count = node_mips ? count : 0;
+}
+
 int vhx_oracle_trace_rays(const vhx_tree_desc *t, const float *rays, uint64_t n, const vhx_hits *out, int threads) {
     if (!t || !rays || !out) return VHX_E_INVALID_ARG;
     ensure_luts();

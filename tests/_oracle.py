@@ -1,4 +1,5 @@
 """ctypes loader of oracle/_build/liboracle.so — the CPU restatement used as the checker (test infrastructure)."""
+import contextlib
 import ctypes
 import os
 
@@ -35,6 +36,18 @@ class Oracle:
         self.lib = l
 
     # -- traversal ----------------------------------------------------------------------------------------------
+    @contextlib.contextmanager
+    def node_mips(self, mips):
+        """Traces inside the block use the node MIP stand-ins of `mips` (vhx_oracle_set_node_mips)."""
+        arr = np.ascontiguousarray(mips, np.uint32)
+        self.lib.vhx_oracle_set_node_mips.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
+        self.lib.vhx_oracle_set_node_mips.restype = None
+        self.lib.vhx_oracle_set_node_mips(arr.ctypes.data, len(arr))
+        try:
+            yield
+        finally:
+            self.lib.vhx_oracle_set_node_mips(None, 0)
+
     def trace_rays(self, flat, origins, directions, threads=0, count_bytes=False,
                    fields=("value", "cell", "voxel", "impact", "normal", "depth", "rgba")):
         o = np.ascontiguousarray(origins, np.float32).reshape(-1, 3)

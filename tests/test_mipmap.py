@@ -146,3 +146,47 @@ def test_flatten_lod_cuts_children_and_keeps_mips():
     assert np.all(cut.node_children == 0xFFFFFFFF)
     assert cut.node_ocbits[0] == full.node_ocbits[0]
     assert cut.node_mips[0] != 0xFFFFFFFF
+
+
+def _scene_tree(size, bd, lod_enable=True):
+    from voxelhex_amd import _native as N
+    tree = BoxTree(size, bd)
+    tree.insert_scene(N.VHX_SCENE_LATTICE_CUBE)
+    if lod_enable:
+        tree.albedo_mip_map_resampling_strategy().switch_albedo_mip_maps(True)
+    return tree
+
+
+def test_oracle_mips_on_a_full_tree_change_nothing(oracle):
+    """With every child present no MIP stand-in fires: MIP-enabled traces equal the reference path."""
+    import voxelhex_amd as vhx
+    tree = _scene_tree(64, 4)
+    flat = tree.flatten()
+    assert len(flat.node_mips) == len(flat.node_type)
+    cam = vhx.glass_camera(64, 96, 64, target=(32.0,) * 3)
+    ref = oracle.trace_primary(flat, cam, 0, 0, 96, 64, count_bytes=True)
+    with oracle.node_mips(flat.node_mips):
+        got = oracle.trace_primary(flat, cam, 0, 0, 96, 64, count_bytes=True)
+    for k in ref:
+        assert np.array_equal(ref[k].view(np.uint32) if ref[k].dtype == np.float32 else ref[k],
+                              got[k].view(np.uint32) if got[k].dtype == np.float32 else got[k]), k
+
+
+def test_oracle_lod_cut_renders_from_mips(oracle):
+    """A view cut below the root: without MIPs the rays that would enter a missing child miss (the reference CPU path
+    cannot go there); with MIPs they hit the root's MIP brick, whose cells carry MIP colours."""
+    import voxelhex_amd as vhx
+    tree = _scene_tree(64, 4)
+    full, cut = tree.flatten(), tree.flatten_lod(0)
+    cam = vhx.glass_camera(64, 96, 64, target=(32.0,) * 3)
+    exact = oracle.trace_primary(full, cam, 0, 0, 96, 64, fields=("value",))
+    bare = oracle.trace_primary(cut, cam, 0, 0, 96, 64, fields=("value",))
+    with oracle.node_mips(cut.node_mips):
+        lod = oracle.trace_primary(cut, cam, 0, 0, 96, 64, fields=("value", "cell", "voxel", "depth"))
+    hit_exact = exact["value"] != 0xFFFFFFFF
+    assert not (bare["value"] != 0xFFFFFFFF).any()
+    hit_lod = lod["value"] != 0xFFFFFFFF
+    assert hit_lod.sum() > 0.5 * hit_exact.sum()
+    # every MIP hit names a cell of the root's MIP brick: voxel = a multiple of the MIP cell edge (64 / 4)
+    assert (lod["voxel"][hit_lod] % 16 == 0).all()
+    assert set(np.unique(lod["value"][hit_lod])) <= set(cut.voxels.tolist()) | set(cut.solid_values.tolist())

@@ -90,6 +90,7 @@ SIGNATURES = [
     ("vhx_sync", c_int, [c_void_p, P(c_f32)]),
     ("vhx_set_pass_budgets", c_int, [c_void_p, P(c_u32), c_u32]),
     ("vhx_upload_tree", c_int, [c_void_p, P(TreeDesc)]),
+    ("vhx_set_node_mips", c_int, [c_void_p, c_void_p, c_u32]),
     ("vhx_update_range", c_int, [c_void_p, c_int, c_u64, c_u64, c_void_p]),
     ("vhx_update_ranges", c_int, [c_void_p, c_void_p, c_u32]),
     ("vhx_set_depth_prepass", c_int, [c_void_p, c_int, ctypes.c_float]),

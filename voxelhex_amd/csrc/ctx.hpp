@@ -26,6 +26,10 @@ struct TreeStore {
     DevBuf child_rec;      // brick_dim <= 4: DevTree::child_rec, rebuilt before a trace when stale
     bool child_rec_stale = false;
     uint32_t occ_words = 1;
+    // node_mips (src/raytracing/bevy/types.rs:245-247): one MIP brick descriptor per node; while set, a node
+    // iteration whose target child is occupied but absent probes the node's MIP (vhx_set_node_mips)
+    DevBuf mips;
+    bool mips_on = false;
     ~TreeStore();
 };
 

@@ -40,6 +40,8 @@ struct DevTree {
     const uint4 *child_rec;
     const uint32_t *solid;
     const uint32_t *color;
+    // node_mips (vhx_set_node_mips): per node its MIP brick descriptor; nullptr = MIPs off (the reference path)
+    const uint32_t *mips;
     uint32_t color_count;
     uint32_t node_count;
     uint32_t size;
@@ -406,7 +408,7 @@ __device__ __forceinline__ void save_state(uint4 *st, F3d p, uint32_t iters, Cub
 // every way out of it sets the exit code `ex` and leaves through a single exit at the bottom of the iteration. The
 // NodeStack<u32, 4> ring (cpu.rs:18-76) is a shift register: `node` is its top, s1..s3 the entries below; a push onto
 // a full stack drops the oldest entry, a pop that empties it ends the walk and restarts from the root.
-template <bool COUNT, int BD>
+template <bool COUNT, int BD, bool MIP = false>
 struct Trav {
     RayD r;
     uint32_t dir_idx;
@@ -418,7 +420,8 @@ struct Trav {
     uint32_t node, s1, s2, s3, count, iters;
     // how the loop ended, one integer instead of several booleans (kept in a VGPR; boolean flags set in divergent
     // branches become 64-bit lane masks merged by scalar instructions at every join): 0 = still running, 1 = hit,
-    // 2 = miss (left the tree, invalid key, or the iteration bound), 3 = abandoned at the pass budget
+    // 2 = miss (left the tree, invalid key, or the iteration bound), 3 = abandoned at the pass budget, 4 = hit in a
+    // node's MIP brick (MIPs on, vhx_set_node_mips)
     uint32_t ex;
     // tbok: target_bounds equals child_bounds(current, target) (kept by PUSH, POP and ADVANCE; not after a restart,
     // which leaves it stale, cpu.rs:317-320), so a leaf probe takes its brick cube from tb instead of recomputing it.
@@ -530,12 +533,38 @@ struct Trav {
             if (!uniform && tbok == 0u) bb = child_bounds(cur, target);
             ex = probe_brick<COUNT, BD>(t, r, p, hdesc, cocc, bb, h, iters, hflat) ? 1u : 0u;
         }
+        // MIP stand-in (viewport_render.wgsl:438-454, probe_MIP 328-364): the target sectant is occupied but its child
+        // entry is absent (a view that does not hold it). The node's MIP brick is traced over the node's cube from a
+        // copy of the ray point; a hit ends the ray, a miss ADVANCEs past the sectant instead of pushing into the
+        // missing child. Compiled only into the MIP kernels (their own instantiations), so the reference path's code
+        // and register allocation are untouched.
+        bool mip_adv = false;
+        if (MIP) {
+            if (target < 64u && slot == VHX_EMPTY && ((occ >> target) & 1ull) != 0ull &&
+                (ntype == VHX_NODE_INTERNAL || ntype == VHX_NODE_LEAF)) {
+                mip_adv = true;
+                const uint32_t mdesc = t.mips[node];
+                if (COUNT) h.bytes += 4;
+                if (mdesc != VHX_EMPTY) {
+                    const uint64_t mocc =
+                        Brick<BD>::WORDS == 1 && (mdesc & VHX_SOLID_BIT) == 0u ? t.brick_occ[mdesc] : 0ull;
+                    F3d pm = p;
+                    int32_t mflat;
+                    if (probe_brick<COUNT, BD>(t, r, pm, mdesc, mocc, cur, h, iters, mflat)) {
+                        p = pm;
+                        hdesc = mdesc;
+                        hflat = mflat;
+                        ex = 4u;
+                    }
+                }
+            }
+        }
         if (ex == 0u) {
             // the three moves are sequential ifs over precomputed conditions rather than an if / else-if chain: each
             // updates the loop state in place, where the chain's join made the compiler copy every unchanged state
             // register twice per iteration
             const bool pop = uniform || target >= 64u || occ == 0 || (occ & omask) == 0;
-            const bool push = !pop && ntype == VHX_NODE_INTERNAL && ((occ >> target) & 1ull) != 0;
+            const bool push = !pop && !mip_adv && ntype == VHX_NODE_INTERNAL && ((occ >> target) & 1ull) != 0;
             if (pop) {
                 // POP (cpu.rs:368-393). Its step to the next sibling (dda_step_to_next_sibling on the popped cube,
                 // step_sectant, target_bounds += step * size) is one trip of the walk below, which the lanes that
@@ -648,6 +677,9 @@ struct Trav {
             h.hit = true;
             const bool huni = t.hdr[node].z == VHX_NODE_UNIFORM_LEAF;
             finish_hit<BD>(t, h, hdesc, hflat, p, huni ? cur : child_bounds(cur, target));
+        } else if (ex == 4u) {  // a MIP hit: the MIP brick spans the node's cube
+            h.hit = true;
+            finish_hit<BD>(t, h, hdesc, hflat, p, cur);
         }
         return ex != 3u;
     }
@@ -656,11 +688,11 @@ struct Trav {
 // sparse (a budgeted pass with saved state): once fewer than `sparse` lanes of the wave still trace, they are abandoned
 // like rays over the budget (their state saved, the next pass resumes them packed into full waves) instead of keeping
 // the wave's issue slots for a few lanes. 0 = off. The result is the same either way (the traversal is deterministic).
-template <bool COUNT, int BD, bool START = false>
+template <bool COUNT, int BD, bool START = false, bool MIP = false>
 __device__ __forceinline__ bool get_by_ray(const DevTree &t, const uint64_t *occ_tab, F3d o, F3d d, HitOut &h,
                                            uint32_t budget, uint4 *sbase = nullptr, uint32_t sidx = 0,
                                            bool resume = false, float start = 0.0f, uint32_t sparse = 0) {
-    Trav<COUNT, BD> tr;
+    Trav<COUNT, BD, MIP> tr;
     if (!tr.template begin<START>(t, o, d, h, sbase, sidx, resume, start)) return true;
     for (;;) {
         tr.step(t, occ_tab, h, budget);

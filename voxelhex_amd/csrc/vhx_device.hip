@@ -497,7 +497,7 @@ __device__ __forceinline__ float prepass_start(const FastD &f, uint32_t px, uint
     return m - f.margin;
 }
 
-template <bool COUNT, int BD, bool FAST = false>
+template <bool COUNT, int BD, bool FAST = false, bool MIP = false>
 __global__ void __launch_bounds__(256) VHX_PRIMARY_ATTR k_trace_primary(DevTree t, CamD cam, OutD out, uint32_t T, uint32_t tiles_x,
                                                        uint32_t tile_start, uint32_t tile_stride, uint32_t layout,
                                                        uint32_t blocks_per_tile_x, uint32_t blocks_per_tile,
@@ -523,8 +523,8 @@ __global__ void __launch_bounds__(256) VHX_PRIMARY_ATTR k_trace_primary(DevTree 
         HitOut h;
         h.bytes = 0;
         const float start = FAST ? prepass_start(fast, px, py) : 0.0f;
-        done = get_by_ray<COUNT, BD, FAST>(t, occ_tab, o, d, h, q.budget, q.state, (uint32_t)idx, false, start,
-                                           q.sparse);
+        done = get_by_ray<COUNT, BD, FAST, MIP>(t, occ_tab, o, d, h, q.budget, q.state, (uint32_t)idx, false, start,
+                                                q.sparse);
         if (done)
             store(t, out, idx, o, h);
         else if (COUNT && q.state)
@@ -536,7 +536,7 @@ __global__ void __launch_bounds__(256) VHX_PRIMARY_ATTR k_trace_primary(DevTree 
     if (q.flags && (layout == VHX_LAYOUT_FRAMEBUFFER ? valid : (lx < T && ly < T))) q.flags[idx] = done ? 0 : 1;
 }
 
-template <bool COUNT, int BD>
+template <bool COUNT, int BD, bool MIP = false>
 __global__ void __launch_bounds__(256) k_trace_rays(DevTree t, const float *__restrict__ rays, uint64_t n, OutD out,
                                                     PassQ q) {
     __shared__ uint64_t occ_tab[OCC_TAB_WORDS];
@@ -549,7 +549,7 @@ __global__ void __launch_bounds__(256) k_trace_rays(DevTree t, const float *__re
         const F3d d = mk(rays[6 * i + 3], rays[6 * i + 4], rays[6 * i + 5]);
         HitOut h;
         h.bytes = 0;
-        done = get_by_ray<COUNT, BD>(t, occ_tab, o, d, h, q.budget, q.state, (uint32_t)i);
+        done = get_by_ray<COUNT, BD, false, MIP>(t, occ_tab, o, d, h, q.budget, q.state, (uint32_t)i);
         if (done)
             store(t, out, i, o, h);
         else if (COUNT && q.state)
@@ -579,7 +579,7 @@ __global__ void k_put_queue_args(QueueArgs a, QueueArgs *dst) {
     if (threadIdx.x == 0) *dst = a;
 }
 
-template <bool COUNT, int BD>
+template <bool COUNT, int BD, bool MIP = false>
 __global__ void __launch_bounds__(256) VHX_QUEUE_ATTR k_trace_queue(DevTree t, const QueueArgs *qa, const uint32_t *__restrict__ in,
                                                      const uint32_t *in_n, uint32_t *grab, PassQ q) {
     __shared__ uint64_t occ_tab[OCC_TAB_WORDS];
@@ -635,8 +635,8 @@ __global__ void __launch_bounds__(256) VHX_QUEUE_ATTR k_trace_queue(DevTree t, c
             ray_of(a->cam, a->src, idx, o, d);
             HitOut h;
             h.bytes = COUNT && q.resume ? a->out.bytes[idx] : 0u;
-            const bool fin = get_by_ray<COUNT, BD>(t, occ_tab, o, d, h, q.budget, q.state, idx, q.resume != 0, 0.0f,
-                                                   q.sparse);
+            const bool fin = get_by_ray<COUNT, BD, false, MIP>(t, occ_tab, o, d, h, q.budget, q.state, idx,
+                                                               q.resume != 0, 0.0f, q.sparse);
             const QueueArgs *b = qa;
             asm volatile("" : "+s"(b));
             if (!fin) {
@@ -714,6 +714,7 @@ static DevTree dev_tree(const vhx_ctx *c) {
     t.size = c->tree->desc.boxtree_size;
     t.bd = c->tree->desc.brick_dim;
     t.occ_words = c->tree->occ_words;
+    t.mips = c->tree->mips_on ? (const uint32_t *)c->tree->mips.ptr : nullptr;
     return t;
 }
 
@@ -721,7 +722,7 @@ TreeStore::~TreeStore() {
     (void)hipSetDevice(device);
     for (auto &b : raw)
         if (b.ptr) (void)hipFree(b.ptr);
-    for (DevBuf *b : {&hdr, &brick_occ, &child_rec})
+    for (DevBuf *b : {&hdr, &brick_occ, &child_rec, &mips})
         if (b->ptr) (void)hipFree(b->ptr);
 }
 
@@ -956,7 +957,7 @@ static int compact_chunks(vhx_ctx *c, uint32_t nchunks_host, const uint32_t *n_i
 // Queue passes first..npass-1: pass p re-traces the queue of pass p-1 (pass 0's queue, for first == 0, is the list
 // in queue[1] with its length in qctl[7]); what exceeds its budget is listed per chunk and compacted into the next
 // pass's queue. For first == 1, pass 0 (a grid kernel of nblocks0 workgroups) has just run and is compacted first.
-template <bool COUNT, int BD>
+template <bool COUNT, int BD, bool MIP = false>
 static int launch_queue_passes(vhx_ctx *c, const DevTree &t, const CamD &cam, const RaySrc &src, const OutD &o,
                                uint32_t first, uint32_t npass, uint64_t nout, uint64_t nblocks0,
                                bool flags_pass0 = false) {
@@ -1002,8 +1003,8 @@ static int launch_queue_passes(vhx_ctx *c, const DevTree &t, const CamD &cam, co
         const uint32_t qwaves = p == 0 ? c->queue_waves0
                                 : (p + 1 < npass && c->queue_waves_mid ? c->queue_waves_mid : c->queue_waves);
         const unsigned qgrid = (qwaves * 64u + c->qblock - 1) / c->qblock;
-        k_trace_queue<COUNT, BD><<<qgrid, c->qblock, 0, c->stream>>>(t, qa, in, in_n, ctl + 16u + QCTL_PASS_WORDS * p,
-                                                                    q);
+        k_trace_queue<COUNT, BD, MIP><<<qgrid, c->qblock, 0, c->stream>>>(t, qa, in, in_n,
+                                                                         ctl + 16u + QCTL_PASS_WORDS * p, q);
         debug_passes(c, "queue pass");
         if (p + 1 < npass)
             rc = compact_chunks(c, 0, in_n, q.rpw, q.rpw, (uint32_t *)c->queue[p & 1u].ptr, ctl + p,
@@ -1220,6 +1221,7 @@ int vhx::alloc_tree(vhx_ctx *c, const vhx_tree_desc *t) {
         return fail(c, VHX_E_INVALID_ARG, "vhx_upload_tree: invalid sizes");
     VHX_HIP(c, hipSetDevice(c->device));
     c->tree->uploaded = false;
+    c->tree->mips_on = false;  // a new tree has no MIPs until vhx_set_node_mips
     for (int id = 0; id < 7; ++id) {
         int rc = ensure(c, c->tree->raw[id], elem_count(*t, id) * elem_size(id));
         if (rc) return rc;
@@ -1476,6 +1478,9 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
     if (rc) return rc;
     if ((rc = refresh_child_rec(c))) return rc;
     const DevTree t = dev_tree(c);
+    if (t.mips && (out->bytes || (c->prepass && !c->in_prepass)))
+        return fail(c, VHX_E_INVALID_ARG, "vhx_trace_primary: byte counting and the depth prepass are not available "
+                                          "with node MIPs (vhx_set_node_mips)");
     const CamD cd = cam_of(cam);
     uint32_t npass = 1;
     rc = prepare_passes(c, nout, nblocks, npass);
@@ -1526,7 +1531,11 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
         constexpr int BD = decltype(bd_tag)::value;
         PassQ q0 = pass_q(c, 0, npass);
         if (npass > 1) q0.flags = (uint8_t *)c->flags.ptr;
-        if (count) {
+        if (t.mips) {  // MIP stand-ins (no byte counting, no depth prepass: refused above)
+            k_trace_primary<false, BD, false, true><<<(unsigned)nblocks, 256, 0, c->stream>>>(
+                t, cd, ho.dev, T, tiles_x, tile_start, tile_stride, layout, bpx, bpt, q0);
+            qrc = launch_queue_passes<false, BD, true>(c, t, cd, src, ho.dev, 1, npass, nout, nblocks, true);
+        } else if (count) {
             k_trace_primary<true, BD><<<(unsigned)nblocks, 256, 0, c->stream>>>(
                 t, cd, ho.dev, T, tiles_x, tile_start, tile_stride, layout, bpx, bpt, q0);
             qrc = launch_queue_passes<true, BD>(c, t, cd, src, ho.dev, 1, npass, nout, nblocks, true);
@@ -1556,6 +1565,31 @@ int vhx_set_depth_prepass(vhx_ctx *c, int enable, float margin) {
     return VHX_OK;
 }
 
+int vhx_set_node_mips(vhx_ctx *c, const uint32_t *node_mips, uint32_t count) {
+    if (!c) return VHX_E_INVALID_ARG;
+    if (c->shared) return fail(c, VHX_E_STATE, "vhx_set_node_mips on a shared context: set them through the owner");
+    if (!node_mips) {
+        c->tree->mips_on = false;
+        return VHX_OK;
+    }
+    if (!c->tree->uploaded) return fail(c, VHX_E_STATE, "vhx_set_node_mips: no tree uploaded");
+    const vhx_tree_desc &d = c->tree->desc;
+    if (count != d.node_count) return fail(c, VHX_E_INVALID_ARG, "vhx_set_node_mips: count != node_count");
+    for (uint32_t i = 0; i < count; ++i) {  // every descriptor must name an uploaded brick or solid value
+        const uint32_t m = node_mips[i];
+        if (m == VHX_EMPTY) continue;
+        if ((m & VHX_SOLID_BIT) ? (m & 0x7FFFFFFFu) >= d.solid_count : m >= d.brick_count)
+            return fail(c, VHX_E_INVALID_ARG, "vhx_set_node_mips: descriptor out of range");
+    }
+    int rc = ensure(c, c->tree->mips, (uint64_t)count * 4);
+    if (rc) return rc;
+    VHX_STREAM(c);
+    VHX_HIP(c, hipMemcpyAsync(c->tree->mips.ptr, node_mips, (uint64_t)count * 4, hipMemcpyHostToDevice, c->stream));
+    VHX_HIP(c, hipStreamSynchronize(c->stream));
+    c->tree->mips_on = true;
+    return VHX_OK;
+}
+
 int vhx_trace_rays(vhx_ctx *c, const float *rays, uint64_t n, const vhx_hits *out, int on_device) {
     if (!c || !out || (!rays && n)) return VHX_E_INVALID_ARG;
     if (!c->tree->uploaded) return fail(c, VHX_E_STATE, "vhx_trace_rays before vhx_upload_tree");
@@ -1577,6 +1611,8 @@ int vhx_trace_rays(vhx_ctx *c, const float *rays, uint64_t n, const vhx_hits *ou
     }
     if ((rc = refresh_child_rec(c))) return rc;
     const DevTree t = dev_tree(c);
+    if (t.mips && out->bytes)
+        return fail(c, VHX_E_INVALID_ARG, "vhx_trace_rays: byte counting is not available with node MIPs");
     uint32_t npass = 1;
     const uint64_t nb64 = (n + 255) / 256;
     rc = prepare_passes(c, n, nb64, npass);
@@ -1594,7 +1630,10 @@ int vhx_trace_rays(vhx_ctx *c, const float *rays, uint64_t n, const vhx_hits *ou
     auto launch = [&](auto bd_tag) {
         constexpr int BD = decltype(bd_tag)::value;
         const PassQ q0 = pass_q(c, 0, npass);
-        if (count) {
+        if (t.mips) {
+            k_trace_rays<false, BD, true><<<nb, 256, 0, c->stream>>>(t, drays, n, ho.dev, q0);
+            qrc = launch_queue_passes<false, BD, true>(c, t, cd, src, ho.dev, 1, npass, n, nb64);
+        } else if (count) {
             k_trace_rays<true, BD><<<nb, 256, 0, c->stream>>>(t, drays, n, ho.dev, q0);
             qrc = launch_queue_passes<true, BD>(c, t, cd, src, ho.dev, 1, npass, n, nb64);
         } else {
@@ -1645,6 +1684,8 @@ int vhx_trace_shadows(vhx_ctx *c, const float light[3], uint64_t n, const uint32
     if (rc) return rc;
     if ((rc = refresh_child_rec(c))) return rc;
     const DevTree t = dev_tree(c);
+    if (t.mips && bytes)
+        return fail(c, VHX_E_INVALID_ARG, "vhx_trace_shadows: byte counting is not available with node MIPs");
     RaySrc src{};
     src.kind = 3u;
     src.impact = impact;
@@ -1672,7 +1713,9 @@ int vhx_trace_shadows(vhx_ctx *c, const float light[3], uint64_t n, const uint32
     int qrc = VHX_OK;
     auto launch = [&](auto bd_tag) {
         constexpr int BD = decltype(bd_tag)::value;
-        if (bytes)
+        if (t.mips)
+            qrc = launch_queue_passes<false, BD, true>(c, t, cd, src, so, 0, npass, n, nb64);
+        else if (bytes)
             qrc = launch_queue_passes<true, BD>(c, t, cd, src, so, 0, npass, n, nb64);
         else
             qrc = launch_queue_passes<false, BD>(c, t, cd, src, so, 0, npass, n, nb64);

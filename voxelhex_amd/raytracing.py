@@ -259,6 +259,16 @@ class Raytracer:
         self._check(N.lib().vhx_get_stream(self._h, ctypes.byref(s)))
         return s.value
 
+    def set_node_mips(self, node_mips):
+        """vhx_set_node_mips: node MIPs stand in for occupied but absent children (the WGSL path's probe_MIP);
+        None disables them. `node_mips` is FlatTree.node_mips of the uploaded tree."""
+        if node_mips is None:
+            self._check(N.lib().vhx_set_node_mips(self._h, None, 0))
+            self._mips = None
+            return
+        self._mips = np.ascontiguousarray(node_mips, np.uint32)
+        self._check(N.lib().vhx_set_node_mips(self._h, self._mips.ctypes.data, len(self._mips)))
+
     def set_depth_prepass(self, enable=True, margin=0.0):
         """vhx_set_depth_prepass: the opt-in half-resolution depth-prepass fast mode (not the reference's semantics)."""
         self._check(N.lib().vhx_set_depth_prepass(self._h, 1 if enable else 0, float(margin)))
