@@ -65,6 +65,9 @@ int vhx_stream_upload(vhx_stream *stream, vhx_stream_stats *stats);
 int vhx_stream_resize(vhx_stream *stream);
 int vhx_stream_reload(vhx_stream *stream);
 int vhx_stream_view(const vhx_stream *stream, vhx_tree_desc *out);
+/* the view's node MIP descriptors (host mirror, nodes_in_view entries; all VHX_EMPTY unless the tree's MIP maps are
+ * enabled, in which case the stream also writes the MIP bricks and hands the descriptors to vhx_set_node_mips) */
+int vhx_stream_node_mips(const vhx_stream *stream, const uint32_t **node_mips, uint32_t *count);
 
 #ifdef __cplusplus
 }

@@ -39,3 +39,25 @@ def test_tree_edits_mid_stream_on_device(oracle, size, bd):
         s.close()
     finally:
         rt.close()
+
+
+def test_streamed_mips_on_device_match_the_mirror(oracle):
+    """A MIP-enabled stream on a device context: the device view (ranged writes + vhx_set_node_mips from the stream)
+    traces exactly like the oracle on the host mirror with the mirror's node MIPs, before and after a viewport move."""
+    from tests.test_streaming import FIELDS, _mip_stream, _rays_in_box
+    rt = vhx.Raytracer(0)
+    try:
+        t, s = _mip_stream(rt)
+        rng = np.random.default_rng(9)
+        for step in range(2):
+            o, d = _rays_in_box(rng, np.array([0.0, 0.0, 0.0]), np.array([256.0, 256.0, 256.0]), 20000)
+            got = rt.trace_rays(o, d, fields=FIELDS)
+            with oracle.node_mips(s.node_mips()):
+                ref = oracle.trace_rays(s.view(), o, d, fields=FIELDS)
+            assert_same(got, ref, f"streamed MIP view, step {step}")
+            assert (ref["value"] != N.VHX_EMPTY).mean() > 0.2
+            s.set_viewport((180.0, 170.0, 160.0), 40.0)
+            s.upload_all()
+        s.close()
+    finally:
+        rt.close()

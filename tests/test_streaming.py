@@ -151,3 +151,42 @@ def test_tree_changes_are_queued_only_while_streamed():
     assert s.upload()[0]["pending"] >= 0
     s.close()
     t.insert((7, 7, 7), vhx.Albedo(1, 2, 3, 255))  # the stream is gone: not queued (nothing would pop it)
+
+
+def _mip_stream(ctx):
+    t = _tree(256, 4)
+    t.albedo_mip_map_resampling_strategy().switch_albedo_mip_maps(True)
+    s = vhx.StreamingView(t, ctx, (60.0, 50.0, 70.0), 40.0)
+    s.set_rates(16, 64, 10)
+    stats, frames, resizes = s.upload_all()
+    assert stats["pending"] == 0
+    return t, s
+
+
+def test_streamed_mips_stand_in_outside_the_region(oracle):
+    """With the tree's MIP maps on, the stream writes node MIPs (cache.rs:435-453) into its MIP slots: traced with
+    them, rays leaving the resident region hit MIP stand-ins instead of missing, and the region itself is unchanged."""
+    t, s = _mip_stream(None)
+    mips = s.node_mips()
+    view = s.view()
+    assert len(mips) == view.desc.node_count and (mips != N.VHX_EMPTY).sum() > 3
+    rng = np.random.default_rng(5)
+    o, d = _rays_in_box(rng, np.array([0.0, 0.0, 0.0]), np.array([256.0, 256.0, 256.0]), 6000)
+    base = oracle.trace_rays(view, o, d, fields=FIELDS)
+    with oracle.node_mips(mips):
+        lod = oracle.trace_rays(view, o, d, fields=FIELDS)
+    gained = (lod["value"] != N.VHX_EMPTY) & (base["value"] == N.VHX_EMPTY)
+    lo, hi = np.array([41.0, 31.0, 51.0]), np.array([79.0, 69.0, 89.0])
+    oi, di = _rays_in_box(rng, lo, hi, 6000)
+    with oracle.node_mips(mips):
+        lod_in = oracle.trace_rays(view, oi, di, fields=FIELDS)
+    full = oracle.trace_rays(t.flatten(), oi, di, fields=FIELDS)
+    inside = (full["value"] != N.VHX_EMPTY) & np.all((full["impact"] >= lo) & (full["impact"] <= hi), axis=1)
+    assert inside.sum() > 200
+    assert_same({k: v[inside] for k, v in lod_in.items()}, {k: v[inside] for k, v in full.items()}, "region, MIPs")
+    assert gained.sum() > 100, "MIP stand-ins should catch rays the partial view misses"
+    # without MIP maps the stream leaves node_mips pointing at bare slots, which no trace reads
+    t2 = _tree(64, 4)
+    s2 = vhx.StreamingView(t2, None, (20.0, 20.0, 20.0), 16.0)
+    s2.upload_all()
+    assert len(s2.node_mips()) == s2.view().desc.node_count

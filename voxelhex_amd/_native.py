@@ -133,6 +133,7 @@ SIGNATURES = [
     ("vhx_stream_resize", c_int, [c_void_p]),
     ("vhx_stream_reload", c_int, [c_void_p]),
     ("vhx_stream_view", c_int, [c_void_p, P(TreeDesc)]),
+    ("vhx_stream_node_mips", c_int, [c_void_p, P(c_void_p), P(c_u32)]),
     ("vhx_boxtree_node_info", c_int, [c_void_p, c_f32, c_f32, c_f32, P(c_u64), P(c_u32), P(c_u64), P(c_u32)]),
     ("vhx_boxtree_load_vox", c_int, [ctypes.c_char_p, c_u32, P(c_void_p)]),
     ("vhx_boxtree_load_vox_memory", c_int, [c_void_p, c_u64, c_u32, P(c_void_p)]),

@@ -177,6 +177,48 @@ struct vhx_stream {
         key_by_meta[meta] = key;
     }
 
+    // ------------------------------------------------------------------------------------------ node MIPs
+    // Streamed when the tree's MIP maps are enabled (tree_properties bit 16, streaming/mod.rs:288-290): a node's entry
+    // follows cache.rs:435-453 (Empty -> empty marker, Solid -> a solid descriptor of this view's solid table instead
+    // of the reference's inline 0x80000000 | value, Parted -> its MIP slot once uploaded) and the MIP slot's voxels
+    // are written with the brick updates. Deviation: a MIP slot is taken for every node, as in the reference
+    // (upload_queue.rs:332-341), but node_mips points at it only for a Parted MIP (the reference points at the slot for
+    // Empty and Solid MIPs too, which leaves the shader reading a slot nothing was written to).
+    bool stream_mips() const { return tree->mip_strategy.enabled; }
+    bool mips_dirty = false, device_mips_on = false;
+    void set_mip(size_t idx, uint32_t v) {
+        if (idx < node_mips.size() && node_mips[idx] != v) {
+            node_mips[idx] = v;
+            mips_dirty = true;
+        }
+    }
+    uint32_t mip_descriptor(size_t key) {
+        if (!stream_mips()) return kEmpty;
+        const Brick &m = node(key).mip;
+        if (m.kind == BrickKind::Empty) return kEmpty;
+        if (m.kind == BrickKind::Solid) return solid_descriptor(m.solid);
+        Owned o;
+        o.kind = 2;
+        o.node = (uint32_t)key;
+        auto it = brick_by_owner.find(o.key());
+        return it == brick_by_owner.end() ? kEmpty : (0x7FFFFFFFu & (uint32_t)it->second);
+    }
+    // hands the view's node MIPs to the device (vhx_set_node_mips) when they changed, or switches them off
+    int sync_device_mips(bool force) {
+        if (!ctx) return VHX_OK;
+        if (!stream_mips()) {
+            if (!device_mips_on) return VHX_OK;
+            device_mips_on = false;
+            return vhx_set_node_mips(ctx, nullptr, 0);
+        }
+        if (!force && !mips_dirty && device_mips_on) return VHX_OK;
+        const int rc = vhx_set_node_mips(ctx, node_mips.data(), (uint32_t)node_mips.size());
+        if (rc) return rc;
+        mips_dirty = false;
+        device_mips_on = true;
+        return VHX_OK;
+    }
+
     uint32_t solid_descriptor(uint32_t value) {
         auto it = solid_index.find(value);
         if (it != solid_index.end()) return 0x80000000u | it->second;
@@ -295,7 +337,7 @@ struct vhx_stream {
         const Content pc = node(parent_key).content;
         if (pc == Content::Internal) {
             // MIP connection of the erased child (MIP data is Empty in a tree without MIPs: nothing owned)
-            if (desc < node_mips.size() && node_mips[desc] != kEmpty) node_mips[desc] = kEmpty;
+            if (desc < node_mips.size() && node_mips[desc] != kEmpty) set_mip(desc, kEmpty);
             modified.push_back({desc, 0});
         } else if (pc == Content::Leaf || pc == Content::UniformLeaf) {
             if (desc != kEmpty && !(desc & 0x80000000u)) owner_remove_index(desc & 0x7FFFFFFFu);
@@ -444,7 +486,7 @@ struct vhx_stream {
         } else if (n.content == Content::Leaf) {
             for (uint8_t s = 0; s < kChildren; ++s) node_children[first + s] = brick_desc(n.bricks[s], s);
         }
-        node_mips[idx] = kEmpty;  // MIPs are not built by this restatement (BrickData::Empty)
+        set_mip(idx, mip_descriptor(key));  // cache.rs:435-453
         return true;
     }
 
@@ -463,7 +505,7 @@ struct vhx_stream {
         } else if (old.kind == 2) {
             auto m = meta_by_key.find(old.node);
             if (m != meta_by_key.end()) {
-                node_mips[m->second] = kEmpty;
+                set_mip(m->second, kEmpty);
                 upd.modified_nodes.push_back({m->second, 0});
             }
         }
@@ -475,7 +517,10 @@ struct vhx_stream {
             node_children[pm * kChildren + req.sectant] = 0x7FFFFFFFu & (uint32_t)bi;
         } else {
             upd.modified_nodes.push_back({pm, 0});
-            node_mips[pm] = 0x7FFFFFFFu & (uint32_t)bi;
+            owner_insert(bi, req);
+            set_mip(pm, stream_mips() ? mip_descriptor(req.node) : (0x7FFFFFFFu & (uint32_t)bi));
+            upd.brick_updates.push_back({bi, req});
+            return true;
         }
         owner_insert(bi, req);
         upd.brick_updates.push_back({bi, req});
@@ -630,7 +675,15 @@ struct vhx_stream {
                 Owned mip;
                 mip.kind = 2;
                 mip.node = (uint32_t)key;
-                if (owner_has(mip)) return true;  // MIP data is Empty in this restatement: nothing to re-upload
+                auto own = brick_by_owner.find(mip.key());
+                if (own != brick_by_owner.end()) {  // re-upload the (changed) MIP into its slot
+                    auto m = meta_by_key.find(key);
+                    if (m != meta_by_key.end()) set_mip(m->second, mip_descriptor(key));
+                    CacheUpdate u;
+                    u.brick_updates.push_back({own->second, mip});
+                    updates.push_back(std::move(u));
+                    return true;
+                }
                 CacheUpdate u;
                 if (!add_brick(mip, u)) return false;
                 updates.push_back(std::move(u));
@@ -747,8 +800,10 @@ struct vhx_stream {
         d.solid_values = solid.data();
         d.color_palette = color.data();
         d.data_palette = data.data();
-        const int rc = ctx ? vhx_upload_tree(ctx, &d) : VHX_OK;  // ctx == NULL: host-only view (tests)
+        int rc = ctx ? vhx_upload_tree(ctx, &d) : VHX_OK;  // ctx == NULL: host-only view (tests)
         if (rc) return rc;
+        device_mips_on = false;  // a new upload switches them off on the device
+        if ((rc = sync_device_mips(true))) return rc;
         uploaded_solid_size = solid_values.size();
         device_valid = true;
         resize = false;
@@ -780,7 +835,8 @@ struct vhx_stream {
     int upload_frame() {
         frame_writes.clear();
         const int rc = collect_frame();
-        const int frc = flush();  // also after a capacity stop: what was decided before it is written, as before
+        int frc = flush();  // also after a capacity stop: what was decided before it is written, as before
+        if (!frc && device_valid) frc = sync_device_mips(false);
         return rc ? rc : frc;
     }
     int collect_frame() {  // streaming/mod.rs:420-635
@@ -814,14 +870,14 @@ struct vhx_stream {
             if (rc) return rc;
             uploaded_data_palette_size = data_palette.size();
         }
-        // voxel data of the uploaded bricks (Parted only: MIP slots upload nothing), before the nodes point at them
+        // voxel data of the uploaded bricks (Parted only; MIP slots only with MIPs on), before the nodes point at them
         const size_t n3 = (size_t)bd() * bd() * bd();
         for (const auto &u : updates)
             for (const auto &bu : u.brick_updates) {
                 const Owned &o = bu.second;
-                if (o.kind != 1) continue;
+                if (o.kind != 1 && !(o.kind == 2 && stream_mips())) continue;
                 const Node &n = node(o.node);
-                const Brick &b = n.content == Content::UniformLeaf ? n.bricks[0] : n.bricks[o.sectant];
+                const Brick &b = o.kind == 2 ? n.mip : n.content == Content::UniformLeaf ? n.bricks[0] : n.bricks[o.sectant];
                 if (b.kind != BrickKind::Parted) continue;
                 std::copy(b.parted.begin(), b.parted.end(), voxels.begin() + (ptrdiff_t)(bu.first * n3));
                 rc = write(VHX_BUF_VOXELS, bu.first * n3, n3, voxels.data() + bu.first * n3);
@@ -946,6 +1002,13 @@ int vhx_stream_resize(vhx_stream *s) {
 int vhx_stream_reload(vhx_stream *s) {
     if (!s) return VHX_E_INVALID_ARG;
     s->reset_targets();
+    return VHX_OK;
+}
+
+int vhx_stream_node_mips(const vhx_stream *s, const uint32_t **node_mips, uint32_t *count) {
+    if (!s || !node_mips || !count) return VHX_E_INVALID_ARG;
+    *node_mips = s->node_mips.data();
+    *count = (uint32_t)s->node_mips.size();
     return VHX_OK;
 }
 

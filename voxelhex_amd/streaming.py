@@ -91,6 +91,14 @@ class StreamingView:
                 break
         return stats, frames, resizes
 
+    def node_mips(self):
+        """Copy of the view's node MIP descriptors (vhx_stream_node_mips)."""
+        ptr, cnt = ctypes.c_void_p(), ctypes.c_uint32()
+        N.check(N.lib().vhx_stream_node_mips(self._h, ctypes.byref(ptr), ctypes.byref(cnt)))
+        if not cnt.value:
+            return np.zeros(0, np.uint32)
+        return np.ctypeslib.as_array((ctypes.c_uint32 * cnt.value).from_address(ptr.value)).copy()
+
     def view(self):
         d = N.TreeDesc()
         N.check(N.lib().vhx_stream_view(self._h, ctypes.byref(d)))
