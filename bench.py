@@ -19,14 +19,21 @@ with brick_dim 4 (1024 is not a valid size for brick_dim 8, src/boxtree/mod.rs:1
 in the reference checkout), glass camera of benches/performance.rs on radius 2S at 40 rad aimed at the centre.
 
 Also printed: roofline (algorithmic bytes per launch, counted by the instrumented kernel, / measured kernel time vs
-8 TB/s; `traffic` = the PMC-measured memory-side read bytes of the same launch from profiles/, see
-scripts/pmc_traffic.py), and cpu_baseline: the CPU restatement of the reference raytracer (oracle/) on the host
+8 TB/s; `traffic` = the memory-side read bytes of the same launch, measured in this run by a `rocprofv3 --pmc
+FETCH_SIZE` child run of the same workload (N = 1; --no-pmc, or a failed child run, falls back to the committed
+profiles/traffic.json figure), and cpu_baseline: the CPU restatement of the reference raytracer (oracle/) on the host
 cores over the same frame (all cores available to the process and 1 core, 1 warm-up + median of 5).
 """
 import argparse
+import csv
+import glob
 import json
 import os
+import shutil
+import signal
+import subprocess
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -60,6 +67,8 @@ def parse():
                    help="config 5: each step = primary frame + one hard-shadow ray per hit toward (S,S,S)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-roofline", action="store_true")
+    p.add_argument("--no-pmc", action="store_true",
+                   help="skip the rocprofv3 FETCH_SIZE child run (roofline.traffic from profiles/traffic.json)")
     p.add_argument("--inflight", type=int, default=8,
                    help="frames in flight per GPU: F contexts sharing the tree (vhx_create_shared), each on its own "
                         "stream, frame i traced by context i %% F, so a frame's latency-bound long-ray tail overlaps the "
@@ -138,6 +147,53 @@ def pmc_traffic(workload):
         return None
     e = d.get(workload)
     return None if e is None else e
+
+
+FRAME_KERNELS = ("k_trace_primary<false", "k_trace_queue<false", "k_count_flags", "k_scan_counts", "k_emit_flags",
+                 "k_gather_chunks", "k_put_queue_args")
+
+
+def measure_traffic():
+    """Memory-side read bytes per frame, measured now: this bench (same arguments, 5 timed + 1 warm-up frames, no
+    roofline / CPU leg) under `rocprofv3 --pmc FETCH_SIZE --kernel-trace` as a child process, FETCH_SIZE summed over
+    the frame kernels and divided by the pass-0 dispatches, x1024 B and x2 (gfx950: FETCH_SIZE derives from
+    TCC_EA0_RDREQ and reads half the bytes; /opt/skills/guides/MI355X_MICROARCH.md, HBM section; Infinity-Cache hits
+    included, an upper bound of HBM bytes). Returns (bytes, frames) or None (no profiler, a failure or 180 s)."""
+    rp = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(rp):
+        return None
+    d = tempfile.mkdtemp(prefix="vhx_pmc_", dir="/tmp")
+    cmd = [rp, "--pmc", "FETCH_SIZE", "--kernel-trace", "-f", "csv", "-d", d, "-o", "pmc", "--", sys.executable,
+           os.path.abspath(__file__)] + sys.argv[1:] + ["--steps", "5", "--warmup", "1", "--no-cpu-baseline",
+                                                       "--no-roofline", "--no-pmc"]
+    env = dict(os.environ, TMPDIR="/tmp")
+    try:
+        proc = subprocess.Popen(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
+                                start_new_session=True)
+        try:
+            rc = proc.wait(timeout=180)
+        except subprocess.TimeoutExpired:
+            os.killpg(proc.pid, signal.SIGKILL)
+            proc.wait()
+            return None
+        if rc != 0:
+            return None
+        total, frames = 0.0, set()
+        for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+            for row in csv.DictReader(open(f)):
+                n = row["Kernel_Name"].replace("void ", "")
+                if not n.startswith(FRAME_KERNELS) or row["Counter_Name"] != "FETCH_SIZE":
+                    continue
+                total += float(row["Counter_Value"])
+                if n.startswith("k_trace_primary<false"):
+                    frames.add(row["Dispatch_Id"])
+        if not frames:
+            return None
+        return total * 1024.0 * 2.0 / len(frames), len(frames)
+    except (OSError, ValueError, KeyError):
+        return None
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
 
 
 def cpu_baseline(flat, cam, W, H, threads_all):
@@ -482,6 +538,9 @@ def main():
         period_ms = ms_per_step if world == 1 else (kernel_ms_isolated or kernel_ms)
         achieved = launch_bytes / (period_ms * 1e-3) / 1e9
         tr = pmc_traffic(workload)
+        measured = None
+        if world == 1 and rank == 0 and not args.no_pmc and mg is None:
+            measured = measure_traffic()
         roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5),
                 "basis": ("algorithmic bytes of one frame's launch / the frame period (wall time per frame with "
@@ -490,8 +549,11 @@ def main():
                 "achieved_per_launch": round(launch_bytes / (kernel_ms * 1e-3) / 1e9, 2),
                 "achieved_isolated_launch": None if not kernel_ms_isolated else
                 round(launch_bytes / (kernel_ms_isolated * 1e-3) / 1e9, 2),
-                "traffic": None if tr is None else tr["read_bytes_per_launch"],
-                "traffic_source": None if tr is None else tr["source"],
+                "traffic": measured[0] if measured else (None if tr is None else tr["read_bytes_per_launch"]),
+                "traffic_source": (f"measured in this run: rocprofv3 --pmc FETCH_SIZE child run of this workload "
+                                   f"(x1024 B, x2 gfx950), frame kernels / frames ({measured[1]})") if measured else
+                                  (None if tr is None else tr["source"] + " (committed profile)"),
+                "traffic_committed": None if tr is None else tr["read_bytes_per_launch"],
                 "kernel": "vhx_trace_primary launch = k_trace_primary (pass 0, step budget) + k_trace_queue "
                           "(the rays over budget, resumed from their saved state), timed together with HIP events "
                           "on the trace stream" + (" (N>1: rank 0's tile set; the gather runs on the communication "
