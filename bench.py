@@ -158,12 +158,14 @@ def measure_traffic():
     roofline / CPU leg) under `rocprofv3 --pmc FETCH_SIZE --kernel-trace` as a child process, FETCH_SIZE summed over
     the frame kernels and divided by the pass-0 dispatches, x1024 B and x2 (gfx950: FETCH_SIZE derives from
     TCC_EA0_RDREQ and reads half the bytes; /opt/skills/guides/MI355X_MICROARCH.md, HBM section; Infinity-Cache hits
-    included, an upper bound of HBM bytes). Returns (bytes, frames) or None (no profiler, a failure or 180 s)."""
+    included, an upper bound of HBM bytes). The same pass (one --pmc run: 3 TCC + 3 SQ counters) collects
+    SQ_INSTS_VALU, SQ_THREAD_CYCLES_VALU and SQ_ACTIVE_INST_VALU for the issue side. Returns a dict (bytes,
+    valu, active lanes per VALU instruction per trace kernel, frames) or None (no profiler, a failure or 180 s)."""
     rp = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
     if not os.path.exists(rp):
         return None
     d = tempfile.mkdtemp(prefix="vhx_pmc_", dir="/tmp")
-    cmd = [rp, "--pmc", "FETCH_SIZE", "--kernel-trace", "-f", "csv", "-d", d, "-o", "pmc", "--", sys.executable,
+    cmd = [rp, "--pmc", "FETCH_SIZE", "SQ_INSTS_VALU", "SQ_THREAD_CYCLES_VALU", "SQ_ACTIVE_INST_VALU", "--kernel-trace", "-f", "csv", "-d", d, "-o", "pmc", "--", sys.executable,
            os.path.abspath(__file__)] + sys.argv[1:] + ["--steps", "5", "--warmup", "1", "--no-cpu-baseline",
                                                        "--no-roofline", "--no-pmc"]
     env = dict(os.environ, TMPDIR="/tmp")
@@ -178,18 +180,27 @@ def measure_traffic():
             return None
         if rc != 0:
             return None
-        total, frames = 0.0, set()
+        tot, per_kernel, frames = {}, {}, set()
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             for row in csv.DictReader(open(f)):
                 n = row["Kernel_Name"].replace("void ", "")
-                if not n.startswith(FRAME_KERNELS) or row["Counter_Name"] != "FETCH_SIZE":
+                if not n.startswith(FRAME_KERNELS):
                     continue
-                total += float(row["Counter_Value"])
+                c, v = row["Counter_Name"], float(row["Counter_Value"])
+                tot[c] = tot.get(c, 0.0) + v
+                k = per_kernel.setdefault(n.split("<")[0], {})
+                k[c] = k.get(c, 0.0) + v
                 if n.startswith("k_trace_primary<false"):
                     frames.add(row["Dispatch_Id"])
-        if not frames:
+        if not frames or "FETCH_SIZE" not in tot:
             return None
-        return total * 1024.0 * 2.0 / len(frames), len(frames)
+        nf = len(frames)
+        lanes = {k: round(v["SQ_THREAD_CYCLES_VALU"] / max(1.0, v["SQ_ACTIVE_INST_VALU"]), 2)
+                 for k, v in per_kernel.items() if "trace" in k and "SQ_ACTIVE_INST_VALU" in v}
+        return {"bytes": tot["FETCH_SIZE"] * 1024.0 * 2.0 / nf, "frames": nf,
+                "valu": tot.get("SQ_INSTS_VALU", 0.0) / nf,
+                "useful": tot.get("SQ_THREAD_CYCLES_VALU", 0.0) / (64.0 * max(1.0, tot.get("SQ_ACTIVE_INST_VALU", 0.0))),
+                "lanes": lanes}
     except (OSError, ValueError, KeyError):
         return None
     finally:
@@ -549,9 +560,9 @@ def main():
                 "achieved_per_launch": round(launch_bytes / (kernel_ms * 1e-3) / 1e9, 2),
                 "achieved_isolated_launch": None if not kernel_ms_isolated else
                 round(launch_bytes / (kernel_ms_isolated * 1e-3) / 1e9, 2),
-                "traffic": measured[0] if measured else (None if tr is None else tr["read_bytes_per_launch"]),
+                "traffic": measured["bytes"] if measured else (None if tr is None else tr["read_bytes_per_launch"]),
                 "traffic_source": (f"measured in this run: rocprofv3 --pmc FETCH_SIZE child run of this workload "
-                                   f"(x1024 B, x2 gfx950), frame kernels / frames ({measured[1]})") if measured else
+                                   f"(x1024 B, x2 gfx950), frame kernels / frames ({measured['frames']})") if measured else
                                   (None if tr is None else tr["source"] + " (committed profile)"),
                 "traffic_committed": None if tr is None else tr["read_bytes_per_launch"],
                 "kernel": "vhx_trace_primary launch = k_trace_primary (pass 0, step budget) + k_trace_queue "
@@ -562,11 +573,18 @@ def main():
                 "kernel_ms_isolated": None if kernel_ms_isolated is None else round(kernel_ms_isolated, 4),
                 "frames_in_flight": F,
                 "algorithmic_bytes_per_launch": launch_bytes, "tree_bytes_per_ray": round(tree_bytes / max(1, my_rays), 2)}
-        if tr is not None and "issue" in tr:
+        iss = None
+        if measured and measured["valu"] > 0:
+            iss = {"valu_wave_instructions_per_frame": measured["valu"], "useful_lane_frac": round(measured["useful"], 4),
+                   "active_lanes_per_valu": measured["lanes"], "peak_valu_wave_instructions_per_s": 1024 * 2.4e9 / 2,
+                   "source": "measured in this run: rocprofv3 --pmc SQ_INSTS_VALU, SQ_THREAD_CYCLES_VALU / "
+                             f"SQ_ACTIVE_INST_VALU (same child run), frame kernels / frames ({measured['frames']})"}
+        elif tr is not None and "issue" in tr:
+            iss = dict(tr["issue"], source=tr["issue"]["source"] + " (committed profile)")
+        if iss is not None:
             # issue side (the traversal is bound by SIMD issue and divergence, not bytes): VALU wave-instructions of
-            # a frame (PMC, profiles/traffic.json) per frame period against 1024 SIMDs x 2.4 GHz / 2 cycles, and the
-            # share of those slots' lanes doing useful work
-            iss = tr["issue"]
+            # a frame per frame period against 1024 SIMDs x 2.4 GHz / 2 cycles, and the share of those slots' lanes
+            # doing useful work
             valu_rate = iss["valu_wave_instructions_per_frame"] / (period_ms * 1e-3) / 1e9
             peak_rate = iss["peak_valu_wave_instructions_per_s"] / 1e9
             roof["issue"] = {"bound": "valu issue", "achieved": round(valu_rate, 1), "peak": round(peak_rate, 1),
