@@ -153,6 +153,31 @@ FRAME_KERNELS = ("k_trace_primary<false", "k_trace_queue<false", "k_count_flags"
                  "k_gather_chunks", "k_put_queue_args")
 
 
+def parse_pmc_dir(d):
+    """Per-frame figures from rocprofv3 counter_collection CSVs under `d` (see measure_traffic), or None."""
+    tot, per_kernel, frames = {}, {}, set()
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for row in csv.DictReader(open(f)):
+            n = row["Kernel_Name"].replace("void ", "")
+            if not n.startswith(FRAME_KERNELS):
+                continue
+            c, v = row["Counter_Name"], float(row["Counter_Value"])
+            tot[c] = tot.get(c, 0.0) + v
+            k = per_kernel.setdefault(n.split("<")[0], {})
+            k[c] = k.get(c, 0.0) + v
+            if n.startswith("k_trace_primary<false"):
+                frames.add(row["Dispatch_Id"])
+    if not frames or "FETCH_SIZE" not in tot:
+        return None
+    nf = len(frames)
+    lanes = {k: round(v["SQ_THREAD_CYCLES_VALU"] / max(1.0, v["SQ_ACTIVE_INST_VALU"]), 2)
+             for k, v in per_kernel.items() if "trace" in k and "SQ_ACTIVE_INST_VALU" in v}
+    return {"bytes": tot["FETCH_SIZE"] * 1024.0 * 2.0 / nf, "frames": nf,
+            "valu": tot.get("SQ_INSTS_VALU", 0.0) / nf,
+            "useful": tot.get("SQ_THREAD_CYCLES_VALU", 0.0) / (64.0 * max(1.0, tot.get("SQ_ACTIVE_INST_VALU", 0.0))),
+            "lanes": lanes}
+
+
 def measure_traffic():
     """Memory-side read bytes per frame, measured now: this bench (same arguments, 5 timed + 1 warm-up frames, no
     roofline / CPU leg) under `rocprofv3 --pmc FETCH_SIZE --kernel-trace` as a child process, FETCH_SIZE summed over
@@ -165,9 +190,10 @@ def measure_traffic():
     if not os.path.exists(rp):
         return None
     d = tempfile.mkdtemp(prefix="vhx_pmc_", dir="/tmp")
-    cmd = [rp, "--pmc", "FETCH_SIZE", "SQ_INSTS_VALU", "SQ_THREAD_CYCLES_VALU", "SQ_ACTIVE_INST_VALU", "--kernel-trace", "-f", "csv", "-d", d, "-o", "pmc", "--", sys.executable,
-           os.path.abspath(__file__)] + sys.argv[1:] + ["--steps", "5", "--warmup", "1", "--no-cpu-baseline",
-                                                       "--no-roofline", "--no-pmc"]
+    counters = ["FETCH_SIZE", "SQ_INSTS_VALU", "SQ_THREAD_CYCLES_VALU", "SQ_ACTIVE_INST_VALU"]
+    cmd = ([rp, "--pmc"] + counters + ["--kernel-trace", "-f", "csv", "-d", d, "-o", "pmc", "--", sys.executable,
+                                       os.path.abspath(__file__)] + sys.argv[1:] +
+           ["--steps", "5", "--warmup", "1", "--no-cpu-baseline", "--no-roofline", "--no-pmc"])
     env = dict(os.environ, TMPDIR="/tmp")
     try:
         proc = subprocess.Popen(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
@@ -180,27 +206,7 @@ def measure_traffic():
             return None
         if rc != 0:
             return None
-        tot, per_kernel, frames = {}, {}, set()
-        for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
-            for row in csv.DictReader(open(f)):
-                n = row["Kernel_Name"].replace("void ", "")
-                if not n.startswith(FRAME_KERNELS):
-                    continue
-                c, v = row["Counter_Name"], float(row["Counter_Value"])
-                tot[c] = tot.get(c, 0.0) + v
-                k = per_kernel.setdefault(n.split("<")[0], {})
-                k[c] = k.get(c, 0.0) + v
-                if n.startswith("k_trace_primary<false"):
-                    frames.add(row["Dispatch_Id"])
-        if not frames or "FETCH_SIZE" not in tot:
-            return None
-        nf = len(frames)
-        lanes = {k: round(v["SQ_THREAD_CYCLES_VALU"] / max(1.0, v["SQ_ACTIVE_INST_VALU"]), 2)
-                 for k, v in per_kernel.items() if "trace" in k and "SQ_ACTIVE_INST_VALU" in v}
-        return {"bytes": tot["FETCH_SIZE"] * 1024.0 * 2.0 / nf, "frames": nf,
-                "valu": tot.get("SQ_INSTS_VALU", 0.0) / nf,
-                "useful": tot.get("SQ_THREAD_CYCLES_VALU", 0.0) / (64.0 * max(1.0, tot.get("SQ_ACTIVE_INST_VALU", 0.0))),
-                "lanes": lanes}
+        return parse_pmc_dir(d)
     except (OSError, ValueError, KeyError):
         return None
     finally:
