@@ -6,8 +6,9 @@ through the HIP kernel, shaded to RGBA8 + f32 depth in HBM.
 Multi-GPU (torchrun, one process per GPU): the split lives behind the C ABI (vhx_mgpu_*, include/vhx.h): libvhx owns
 an RCCL communicator (its id travels over a gloo process group, which also carries the barriers and the max-over-ranks
 timing), rank 0 builds the tree and ncclBroadcasts it to the other GPUs, and every frame each rank traces its 64x64
-screen tiles (dealt round-robin), one ncclGather brings RGBA8 + f32 depth to rank 0, rank 0 untiles them into its
-framebuffers; frame k's gather overlaps frame k+1's trace. Scaling modes (--scaling):
+screen tiles (dealt round-robin, rank 0's share balanced by vhx_mgpu_balance before the warm-up), point-to-point RCCL
+transfers bring RGBA8 + f32 depth to rank 0, rank 0 untiles them into its framebuffers; frame k's transfers overlap
+the next frames' traces. Scaling modes (--scaling):
   auto   (default) N = 1: the headline 3840x2160 frame; N > 1: BASELINE config 4, a fixed 7680x4320 frame (strong)
   strong the 7680x4320 config-4 frame at every N (N = 1 included)
   weak   the field of view fixed, W*H grown with N so that every rank keeps 3840x2160 rays
@@ -432,7 +433,7 @@ def main():
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(s_)
         if mg is not None:
-            mg.render(cam_k, fb_rgba, fb_depth)  # this rank's tiles -> ncclGather -> untile on rank 0
+            mg.render(cam_k, fb_rgba, fb_depth)  # this rank's tiles -> sends to rank 0 -> untile on rank 0
         else:
             if pipe is not None:
                 o["rgba"] = pipe.out_buffer()
@@ -621,7 +622,8 @@ def main():
         if world > 1 or mg is not None:
             par = f"screen-tile split x{world} + " + (
                 "gloo gather (single-GPU rehearsal)" if rehearsal else
-                ("RCCL ncclGather of RGBA8 + depth behind the C ABI (vhx_mgpu), tree ncclBroadcast from rank 0"
+                ("RCCL point-to-point transfers of RGBA8 + depth to rank 0 behind the C ABI (vhx_mgpu), tree "
+                 "ncclBroadcast from rank 0"
                  if mg is not None else "RCCL gather via torch.distributed")
                 + ("" if args.no_overlap else ", overlapped with the next frame's trace"))
         else:
