@@ -140,3 +140,28 @@ def test_mip_lod_trade_off(rt, mip_tree):
         rt.set_node_mips(None)
         print(f"MIP LOD depth {depth}: {flat.node_type.size} nodes, {100 * np.mean(got['value'] != exact['value']):.2f} "
               f"% pixels differ, {t:.3f} ms/frame (host-synchronised) vs full tree {t_full:.3f}")
+
+
+def test_mips_are_shared_by_frames_in_flight(oracle, mip_tree):
+    """Contexts sharing the device tree (vhx_create_shared, frames in flight) trace with the owner's node MIPs; a new
+    upload switches them off."""
+    tree, _ = mip_tree
+    flat = tree.flatten_lod(1)
+    W, H = 160, 100
+    cam = vhx.glass_camera(SIZE, W, H, target=(SIZE / 2,) * 3)
+    owner = vhx.Raytracer(0)
+    try:
+        owner.upload(flat)
+        owner.set_node_mips(flat.node_mips)
+        sh = owner.shared()
+        with oracle.node_mips(flat.node_mips):
+            ref = oracle.trace_primary(flat, cam, 0, 0, W, H, fields=("value", "depth"))
+        assert_same(sh.trace_primary(cam, fields=("value", "depth")), ref, "shared context with MIPs")
+        with pytest.raises(N.VhxError):
+            sh.set_node_mips(flat.node_mips)  # set through the owner
+        owner.upload(flat)  # a new upload: MIPs off again
+        assert_same(sh.trace_primary(cam, fields=("value", "depth")),
+                    oracle.trace_primary(flat, cam, 0, 0, W, H, fields=("value", "depth")), "after re-upload")
+        sh.close()
+    finally:
+        owner.close()
