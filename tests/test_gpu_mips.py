@@ -159,9 +159,10 @@ def test_mips_are_shared_by_frames_in_flight(oracle, mip_tree):
         assert_same(sh.trace_primary(cam, fields=("value", "depth")), ref, "shared context with MIPs")
         with pytest.raises(N.VhxError):
             sh.set_node_mips(flat.node_mips)  # set through the owner
-        owner.upload(flat)  # a new upload: MIPs off again
+        again = tree.flatten_lod(1)  # a new tree object, so Raytracer.upload really uploads
+        owner.upload(again)  # a new upload: MIPs off again
         assert_same(sh.trace_primary(cam, fields=("value", "depth")),
-                    oracle.trace_primary(flat, cam, 0, 0, W, H, fields=("value", "depth")), "after re-upload")
+                    oracle.trace_primary(again, cam, 0, 0, W, H, fields=("value", "depth")), "after re-upload")
         sh.close()
     finally:
         owner.close()
