@@ -223,7 +223,8 @@ int vhx_set_depth_prepass(vhx_ctx *ctx, int enable, float margin);
  * over the node's cube; a MIP hit ends the ray there, a miss leaves the ray where it was and ADVANCEs past the
  * sectant (where the reference CPU path would push into the child, which does not exist). Without MIPs (the default)
  * such a push ends the ray as a miss, as before. A tree whose children are all present traces identically either way.
- * NULL disables; count must equal the uploaded tree's node_count; a new vhx_upload_tree disables them. */
+ * NULL disables; count must equal the uploaded tree's node_count; a new vhx_upload_tree disables them. Like an update,
+ * it goes through the owner of a shared tree with every context of the tree idle; shared contexts trace with them. */
 int vhx_set_node_mips(vhx_ctx *ctx, const uint32_t *node_mips, uint32_t count);
 /* Traces n explicit rays; rays = 6 f32 per ray (origin xyz, direction xyz), host or device per on_device. */
 int vhx_trace_rays(vhx_ctx *ctx, const float *rays, uint64_t n, const vhx_hits *out, int on_device);
