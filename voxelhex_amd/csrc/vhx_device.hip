@@ -465,6 +465,9 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t bid, uint32_t n, uint32_t
 #ifndef VHX_QUEUE_WPE
 #define VHX_QUEUE_WPE 0
 #endif
+#ifndef VHX_WAVE_TILE
+#define VHX_WAVE_TILE 0  // pass-0 pixel footprint of a wave (experiment knob, see k_trace_primary)
+#endif
 #ifndef VHX_PRIMARY_WPE
 #define VHX_PRIMARY_WPE 0
 #endif
@@ -510,8 +513,16 @@ __global__ void __launch_bounds__(256) VHX_PRIMARY_ATTR k_trace_primary(DevTree 
     const uint32_t sb = bid - j * blocks_per_tile;
     const uint32_t tile = tile_start + j * tile_stride;
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+#if VHX_WAVE_TILE == 1  // experiment: 16x4 pixels per wave (waves stacked vertically in the 16x16 block)
+    const uint32_t lx = (sb % blocks_per_tile_x) * 16u + (lane & 15u);
+    const uint32_t ly = (sb / blocks_per_tile_x) * 16u + wave * 4u + (lane >> 4);
+#elif VHX_WAVE_TILE == 2  // experiment: 4x16 pixels per wave
+    const uint32_t lx = (sb % blocks_per_tile_x) * 16u + wave * 4u + (lane & 3u);
+    const uint32_t ly = (sb / blocks_per_tile_x) * 16u + (lane >> 2);
+#else  // 8x8 pixels per wave, four waves per 16x16 block
     const uint32_t lx = (sb % blocks_per_tile_x) * 16u + (wave & 1u) * 8u + (lane & 7u);
     const uint32_t ly = (sb / blocks_per_tile_x) * 16u + (wave >> 1) * 8u + (lane >> 3);
+#endif
     const uint32_t px = (tile % tiles_x) * T + lx, py = (tile / tiles_x) * T + ly;
     const bool valid = lx < T && ly < T && px < cam.width && py < cam.height;
     const uint64_t idx = layout == VHX_LAYOUT_FRAMEBUFFER ? (uint64_t)py * cam.width + px
