@@ -190,3 +190,26 @@ def test_oracle_lod_cut_renders_from_mips(oracle):
     # every MIP hit names a cell of the root's MIP brick: voxel = a multiple of the MIP cell edge (64 / 4)
     assert (lod["voxel"][hit_lod] % 16 == 0).all()
     assert set(np.unique(lod["value"][hit_lod])) <= set(cut.voxels.tolist()) | set(cut.solid_values.tolist())
+
+
+def test_mips_follow_lod_inserts():
+    """insert_at_lod with MIPs on (every node on the insert's path updates its MIP, insert.rs:494): large and
+    unaligned blocks keep the MIP bricks in bounds, the root's MIP shows the inserted colours, and a leaf filled
+    whole (a UniformLeaf) has no MIP of its own (mipmap.rs:71-77: its content is its MIP)."""
+    tree = BoxTree(64, 4)
+    tree.auto_simplify = True
+    tree.albedo_mip_map_resampling_strategy().switch_albedo_mip_maps(True)
+    tree.insert_at_lod((0, 0, 0), 16, red)
+    tree.insert_at_lod((10, 20, 30), 24, green)
+    tree.insert_at_lod((60, 60, 60), 8, blue)
+
+    def root_colours():
+        cells = [_root_mip(tree, BOX_NODE_CHILDREN_COUNT, (x, y, z)).albedo()
+                 for x in range(4) for y in range(4) for z in range(4)]
+        return {c for c in cells if c is not None}
+
+    assert root_colours()
+    assert tree.node_info((1, 1, 1))["content"] == "UniformLeaf"
+    assert _root_mip(tree, 0, (0, 0, 0)).albedo() is None
+    tree.albedo_mip_map_resampling_strategy().recalculate_mips()
+    assert root_colours()

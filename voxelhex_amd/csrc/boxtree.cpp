@@ -1195,12 +1195,14 @@ void BoxTree::update_mip(size_t key, const Cube &nb, U3 position) {  // src/boxt
             const size_t ck = child(key, cs);
             if (ck == (size_t)kEmpty32 || !nodes.key_is_valid(ck)) return false;
             const F3 pic = sub(from_u3(pos), mul(lut(cs), mip_edge));
+            const size_t px = as_usize(pic.x), py = as_usize(pic.y), pz = as_usize(pic.z);
             const Brick &m = nodes.get(ck).mip;
             switch (m.kind) {
                 case BrickKind::Empty: return false;
                 case BrickKind::Solid: return albedo_of(m.solid, c);
-                default:
-                    return albedo_of(m.parted[flat_projection(as_usize(pic.x), as_usize(pic.y), as_usize(pic.z), bd)], c);
+                default:  // a sample outside the child's MIP (the reference would index out of bounds) reads nothing
+                    if (px >= bd || py >= bd || pz >= bd) return false;
+                    return albedo_of(m.parted[flat_projection(px, py, pz, bd)], c);
             }
         }, color);
     }
@@ -1221,6 +1223,7 @@ void BoxTree::update_mip(size_t key, const Cube &nb, U3 position) {  // src/boxt
     if (!similar) entry = add_to_palette(Entry{VHX_ENTRY_VISUAL, color, 0});
 
     const auto mi = matrix_index_for(nb, position, bd);
+    if (mi[0] >= bd || mi[1] >= bd || mi[2] >= bd) return;  // a position outside the node (the reference panics)
     const size_t f = flat_projection(mi[0], mi[1], mi[2], bd);
     Brick &mip = nodes.get(key).mip;
     const size_t n3 = (size_t)bd * bd * bd;
