@@ -82,6 +82,10 @@ def parse():
     p.add_argument("--depth-prepass", type=float, default=None, metavar="MARGIN",
                    help="opt-in approximate mode (vhx_set_depth_prepass, not the reference semantics): a half-resolution "
                         "depth prepass, full-resolution rays start at the min of 4 texels minus MARGIN")
+    p.add_argument("--mip-lod", type=int, default=None, metavar="DEPTH",
+                   help="opt-in MIP stand-in mode (not the reference path): the scene inserted into a host BoxTree with "
+                        "MIP maps on, flattened down to DEPTH (vhx_boxtree_flatten_lod) and traced with its node MIPs "
+                        "(vhx_set_node_mips); N = 1, no roofline / CPU leg (keep --size <= 256: O(size^3) inserts)")
     p.add_argument("--no-overlap", action="store_true",
                    help="N>1: gather each frame before tracing the next (default: frame k's gather overlaps k+1)")
     p.add_argument("--root-slots", type=int, default=0,
@@ -342,7 +346,15 @@ def main():
     # the tree: built on the host (rank 0 only when it is broadcast over RCCL), uploaded to HBM
     t0 = time.time()
     flat = None
-    if args.vox:
+    if args.mip_lod is not None:
+        if world > 1 or args.shadows:
+            raise SystemExit("--mip-lod is a one-GPU primary-ray mode")
+        args.no_roofline = args.no_cpu_baseline = args.no_pmc = True
+        bt = vhx.BoxTree(args.size, args.brick_dim)
+        bt.insert_scene(args.scene)
+        bt.albedo_mip_map_resampling_strategy().switch_albedo_mip_maps(True)
+        flat = bt.flatten_lod(args.mip_lod)
+    elif args.vox:
         if mg is None or rank == 0:
             flat = vhx.BoxTree.load_vox_file(args.vox, args.brick_dim).flatten()
     elif mg is None or rank == 0:
@@ -353,6 +365,8 @@ def main():
         mg.broadcast_tree(flat if rank == 0 else None)
     else:
         rt.upload(flat)
+        if args.mip_lod is not None:
+            rt.set_node_mips(flat.node_mips)  # shared contexts trace with the owner's MIPs
     upload_s = time.time() - t0
     tree_info = None
     if rank == 0:
@@ -515,7 +529,8 @@ def main():
     scene_tag = f"vox:{os.path.basename(args.vox)}" if args.vox else f"S{args.scene}"
     workload = f"primary {W}x{H} {scene_tag} {args.size}^3 bd{args.brick_dim} ranks{world}" + (
         f" orbit{args.orbit}" if args.orbit else "") + (
-        f" prepass{args.depth_prepass}" if args.depth_prepass is not None else "")
+        f" prepass{args.depth_prepass}" if args.depth_prepass is not None else "") + (
+        f" mip-lod{args.mip_lod}" if args.mip_lod is not None else "")
     total_rays = W * H
     n_shadow = 0
     if args.shadows:
@@ -642,6 +657,8 @@ def main():
                                    + (f" orbiting {args.orbit} rad per frame" if args.orbit else "")
                                    + (f", APPROXIMATE depth-prepass mode (margin {args.depth_prepass}; not the "
                                       "reference semantics)" if args.depth_prepass is not None else "")
+                                   + (f", MIP stand-in mode: the view holds nodes down to depth {args.mip_lod}, node "
+                                      "MIPs below (not the reference CPU semantics)" if args.mip_lod is not None else "")
                                    + (f", {T}x{T} tiles round-robin over {world} ranks" if world > 1 else ""),
                        "workload_key": workload,
                        "shadow_rays_per_frame": n_shadow if args.shadows else None,
