@@ -200,6 +200,7 @@ def measure_traffic():
                                        os.path.abspath(__file__)] + sys.argv[1:] +
            ["--steps", "5", "--warmup", "1", "--no-cpu-baseline", "--no-roofline", "--no-pmc"])
     env = dict(os.environ, TMPDIR="/tmp")
+    env.pop("VHX_BENCH_MGPU1", None)  # the child times the single-GPU path only
     try:
         proc = subprocess.Popen(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
                                 start_new_session=True)
