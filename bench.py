@@ -190,7 +190,7 @@ def measure_traffic():
     TCC_EA0_RDREQ and reads half the bytes; /opt/skills/guides/MI355X_MICROARCH.md, HBM section; Infinity-Cache hits
     included, an upper bound of HBM bytes). The same pass (one --pmc run: 3 TCC + 3 SQ counters) collects
     SQ_INSTS_VALU, SQ_THREAD_CYCLES_VALU and SQ_ACTIVE_INST_VALU for the issue side. Returns a dict (bytes,
-    valu, active lanes per VALU instruction per trace kernel, frames) or None (no profiler, a failure or 180 s)."""
+    valu, active lanes per VALU instruction per trace kernel, frames) or None (no profiler, a failure or 120 s)."""
     rp = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
     if not os.path.exists(rp):
         return None
@@ -205,7 +205,7 @@ def measure_traffic():
         proc = subprocess.Popen(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
                                 start_new_session=True)
         try:
-            rc = proc.wait(timeout=180)
+            rc = proc.wait(timeout=120)
         except subprocess.TimeoutExpired:
             os.killpg(proc.pid, signal.SIGKILL)
             proc.wait()
