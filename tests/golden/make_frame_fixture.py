@@ -28,6 +28,13 @@ CASES = {
     "c2_256_bd16_1920x1080": (1, 256, 16, 1920, 1080),
     "c3_1024_bd4_3840x2160": (1, 1024, 4, 3840, 2160),
 }
+# node-MIP views: the scene inserted into a host BoxTree with MIP maps on, flattened down to a depth
+# (vhx_boxtree_flatten_lod) and traced with the MIP stand-ins -- pins the host MIP generation and the stand-in rule
+# name: (scene, tree size, brick_dim, width, height, depth)
+MIP_CASES = {
+    "mip_lod0_64_bd4_256x256": (1, 64, 4, 256, 256, 0),
+    "mip_lod1_256_bd4_480x270": (1, 256, 4, 480, 270, 1),
+}
 
 
 def digest(a):
@@ -41,6 +48,22 @@ def frame(oracle, scene, size, bd, W, H):
     return flat, cam, oracle.trace_primary(flat, cam, 0, 0, W, H, fields=FIELDS)
 
 
+def mip_view(scene, size, bd, depth):
+    from voxelhex_amd.boxtree import BoxTree
+    tree = BoxTree(size, bd)
+    tree.insert_scene(scene)
+    tree.albedo_mip_map_resampling_strategy().switch_albedo_mip_maps(True)
+    return tree.flatten_lod(depth)
+
+
+def mip_frame(oracle, scene, size, bd, W, H, depth):
+    import voxelhex_amd as vhx
+    flat = mip_view(scene, size, bd, depth)
+    cam = vhx.glass_camera(size, W, H, target=(size / 2,) * 3)
+    with oracle.node_mips(flat.node_mips):
+        return flat, cam, oracle.trace_primary(flat, cam, 0, 0, W, H, fields=FIELDS)
+
+
 def crop(a, W, H):
     x0, y0 = (W - CROP) // 2, (H - CROP) // 2
     img = a.reshape(H, W, *a.shape[1:])
@@ -51,12 +74,15 @@ def main():
     from tests._oracle import Oracle
     oracle = Oracle()
     meta, crops = {}, {}
-    for name, (scene, size, bd, W, H) in CASES.items():
-        _, _, f = frame(oracle, scene, size, bd, W, H)
+    for name, case in list(CASES.items()) + list(MIP_CASES.items()):
+        scene, size, bd, W, H = case[:5]
+        _, _, f = frame(oracle, *case[:5]) if name in CASES else mip_frame(oracle, *case)
         meta[name] = {"scene": scene, "size": size, "brick_dim": bd, "width": W, "height": H,
                       "camera": "glass_camera(size, W, H, target=(size/2,)*3)",
                       "sha256": {k: digest(f[k]) for k in FIELDS},
                       "hits": int((f["value"] != 0xFFFFFFFF).sum())}
+        if name in MIP_CASES:
+            meta[name]["mip_lod_depth"] = case[5]
         for k in ("value", "depth", "rgba"):
             crops[f"{name}__{k}"] = crop(f[k], W, H)
         print(name, meta[name]["hits"], flush=True)

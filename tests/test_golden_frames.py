@@ -7,7 +7,7 @@ import os
 import numpy as np
 import pytest
 
-from tests.golden.make_frame_fixture import CASES, FIELDS, crop, digest, frame
+from tests.golden.make_frame_fixture import CASES, FIELDS, MIP_CASES, crop, digest, frame, mip_frame
 
 HERE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 META = json.load(open(os.path.join(HERE, "frames.json")))
@@ -20,6 +20,17 @@ def test_oracle_matches_golden_frame(oracle, name):
     scene, size, bd, W, H = CASES[name]
     assert (m["scene"], m["size"], m["brick_dim"], m["width"], m["height"]) == (scene, size, bd, W, H)
     _, _, f = frame(oracle, scene, size, bd, W, H)
+    assert {k: digest(f[k]) for k in FIELDS} == m["sha256"]
+    for k in ("value", "depth", "rgba"):
+        assert np.array_equal(crop(f[k], W, H).view(np.uint32), CROPS[f"{name}__{k}"].view(np.uint32)), k
+
+
+@pytest.mark.parametrize("name", sorted(MIP_CASES))
+def test_oracle_matches_golden_mip_view(oracle, name):
+    m = META[name]
+    scene, size, bd, W, H, depth = MIP_CASES[name]
+    assert m["mip_lod_depth"] == depth
+    _, _, f = mip_frame(oracle, scene, size, bd, W, H, depth)
     assert {k: digest(f[k]) for k in FIELDS} == m["sha256"]
     for k in ("value", "depth", "rgba"):
         assert np.array_equal(crop(f[k], W, H).view(np.uint32), CROPS[f"{name}__{k}"].view(np.uint32)), k
