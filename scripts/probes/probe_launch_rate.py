@@ -5,7 +5,7 @@ import sys
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "12")
+os.environ["GPU_MAX_HW_QUEUES"] = "12"  # one hardware queue per frame in flight (the box exports 4)
 import torch  # noqa: E402
 
 import voxelhex_amd as vhx  # noqa: E402
