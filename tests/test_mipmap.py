@@ -213,3 +213,52 @@ def test_mips_follow_lod_inserts():
     assert _root_mip(tree, 0, (0, 0, 0)).albedo() is None
     tree.albedo_mip_map_resampling_strategy().recalculate_mips()
     assert root_colours()
+
+
+def _py_round(x):  # Rust f32::round (half away from zero) for non-negative values
+    return int(np.floor(np.float32(x) + np.float32(0.5))) if x >= 0 else -int(np.floor(-x + 0.5))
+
+
+def _posterize(colours, thr):
+    """Python restatement of MIPResamplingMethods::Posterize (iterate.rs:507-557) with groups in first-seen order."""
+    groups = []  # [sum of squares (r, g, b, a), count]
+    f32 = np.float32
+    for c in colours:
+        col = (c.r, c.g, c.b, c.a)
+        for g in groups:
+            poster = [_py_round(float(np.sqrt(f32(_py_round(float(f32(s) / f32(g[1]))))))) for s in g[0]]
+            d = [(p - v) % 2 ** 32 for p, v in zip(poster, col)]
+            length = float(np.sqrt(f32(sum((x * x) % 2 ** 32 for x in d) % 2 ** 32)))
+            if length < float(f32(thr) * f32(255.0)):
+                g[0] = [s + v * v for s, v in zip(g[0], col)]
+                g[1] += 1
+                break
+        else:
+            groups.append([[v * v for v in col], 1])
+    best = 0
+    for i in range(1, len(groups)):
+        if groups[i][1] >= groups[best][1]:
+            best = i
+    s, n = groups[best]
+    out = [min(255, _py_round(float(np.sqrt(f32(_py_round(float(f32(x) / f32(n)))))))) for x in s]
+    return Albedo(*out)
+
+
+def test_point_filter_and_posterize_without_ties():
+    """PointFilter takes the most frequent colour, Posterize the average of the largest group of similar colours
+    (iterate.rs:484-557); checked on a leaf root (tree 4, brick_dim 1: MIP level 2 samples its 4^3 voxels) against a
+    Python restatement, with colour counts that leave no tie (the reference's HashMap order is then irrelevant)."""
+    near_red = [Albedo(250, 0, 0, 255), Albedo(245, 5, 0, 255)]
+    voxels = [((0, 0, 0), red), ((1, 0, 0), near_red[0]), ((2, 0, 0), near_red[1]), ((3, 0, 0), near_red[0]),
+              ((0, 1, 0), green), ((1, 1, 0), green), ((0, 0, 1), blue)]
+    order = sorted(voxels, key=lambda e: (e[0][0], e[0][1], e[0][2]))  # the sampler's x, y, z loop order
+    for method, expect in ((MIPResamplingMethods.PointFilter, near_red[0]),
+                           (MIPResamplingMethods.Posterize(0.1), _posterize([c for _, c in order], 0.1))):
+        tree = BoxTree(4, 1)
+        tree.auto_simplify = False
+        tree.albedo_mip_map_resampling_strategy().set_method_at(2, method).set_color_similarity_thr_at(2, 0.0)
+        for p, c in voxels:
+            tree.insert(p, c)
+        tree.albedo_mip_map_resampling_strategy().switch_albedo_mip_maps(True)
+        got = _root_mip(tree, BOX_NODE_CHILDREN_COUNT, (0, 0, 0)).albedo()
+        assert got == expect, (method, got, expect)
