@@ -5,6 +5,10 @@
 #include <algorithm>
 #include <cmath>
 #include <functional>
+#include <atomic>
+#include <climits>
+#include <cstdint>
+#include <thread>
 
 #include "../../include/vhx_boxtree.h"
 
@@ -1150,6 +1154,18 @@ bool BoxTree::albedo_of(uint32_t v, uint32_t &albedo) const {
 
 void BoxTree::update_mip(size_t key, const Cube &nb, U3 position) {  // src/boxtree/mipmap.rs:42-338
     if (!mip_strategy.enabled) return;
+    const Content content = nodes.get(key).content;
+    if (content == Content::Nothing) return;
+    if (content == Content::UniformLeaf) {
+        nodes.get(key).mip = Brick{};  // a uniform leaf is equivalent to its MIP
+        return;
+    }
+    uint32_t color = 0;
+    if (mip_sample(key, nb, position, color)) mip_store(key, nb, position, color);
+}
+
+// mipmap.rs:42-270: the sampled colour of the MIP cell `position` falls in (Leaf / Internal nodes only)
+bool BoxTree::mip_sample(size_t key, const Cube &nb, U3 position, uint32_t &color) const {
     const uint32_t bd = brick_dim;
     const size_t level = as_usize(std::log2(nb.size / (float)bd));
     const auto mit = mip_strategy.methods.find(level);
@@ -1159,11 +1175,6 @@ void BoxTree::update_mip(size_t key, const Cube &nb, U3 position) {  // src/boxt
     const Content content = nodes.get(key).content;
     U3 start{0, 0, 0};
     uint32_t ssize = 0;
-    if (content == Content::Nothing) return;
-    if (content == Content::UniformLeaf) {
-        nodes.get(key).mip = Brick{};  // a uniform leaf is equivalent to its MIP
-        return;
-    }
     if (content == Content::Leaf) {
         ssize = std::min(as_u32(nb.size) / bd, bd * 4u);
         auto st = [&](uint32_t p) {
@@ -1182,15 +1193,13 @@ void BoxTree::update_mip(size_t key, const Cube &nb, U3 position) {  // src/boxt
         start = U3{v2.x - v2.x % 4u, v2.y - v2.y % 4u, v2.z - v2.z % 4u};
     }
 
-    uint32_t color = 0;
-    bool sampled;
     if (content == Content::Leaf || dominant_bottom) {
-        sampled = mip_execute(sampler, start, ssize, [&](U3 pos, uint32_t &c) {
+        return mip_execute(sampler, start, ssize, [&](U3 pos, uint32_t &c) {
             return albedo_of(get_internal(key, nb, pos), c);
         }, color);
     } else {
         const float mip_edge = (float)(bd * 4u);
-        sampled = mip_execute(sampler, start, ssize, [&](U3 pos, uint32_t &c) {
+        return mip_execute(sampler, start, ssize, [&](U3 pos, uint32_t &c) {
             const uint8_t cs = offset_sectant(from_u3(pos), mip_edge);
             const size_t ck = child(key, cs);
             if (ck == (size_t)kEmpty32 || !nodes.key_is_valid(ck)) return false;
@@ -1206,8 +1215,13 @@ void BoxTree::update_mip(size_t key, const Cube &nb, U3 position) {  // src/boxt
             }
         }, color);
     }
-    if (!sampled) return;
+}
 
+// mipmap.rs:272-338: the sampled colour matched against the palette (first entry within the level's threshold) or
+// added to it, stored in the node's MIP brick
+void BoxTree::mip_store(size_t key, const Cube &nb, U3 position, uint32_t color) {
+    const uint32_t bd = brick_dim;
+    const size_t level = as_usize(std::log2(nb.size / (float)bd));
     uint32_t entry;
     const auto tit = mip_strategy.color_thresholds.find(level);
     bool similar = false;
@@ -1236,17 +1250,25 @@ void BoxTree::update_mip(size_t key, const Cube &nb, U3 position) {  // src/boxt
     mip.parted[f] = entry;
 }
 
-void BoxTree::recalculate_mip(size_t key, const Cube &nb) {  // mipmap.rs:613-633
-    if (!mip_strategy.enabled) return;
-    nodes.get(key).mip = Brick{};
+// the bd^3 positions recalculate_mip visits in a node, in its order (mipmap.rs:619-631)
+static void mip_positions(const Cube &nb, uint32_t brick_dim, std::vector<U3> &out) {
+    out.clear();
     const float bd = (float)brick_dim;
     for (uint32_t x = 0; x < brick_dim; ++x)
         for (uint32_t y = 0; y < brick_dim; ++y)
             for (uint32_t z = 0; z < brick_dim; ++z) {
                 const F3 off = divs(mul(f3((float)x, (float)y, (float)z), nb.size), bd);
                 const F3 pos = add(nb.min, f3(std::round(off.x), std::round(off.y), std::round(off.z)));
-                update_mip(key, nb, round_u3(pos));
+                out.push_back(round_u3(pos));
             }
+}
+
+void BoxTree::recalculate_mip(size_t key, const Cube &nb) {  // mipmap.rs:613-633
+    if (!mip_strategy.enabled) return;
+    nodes.get(key).mip = Brick{};
+    std::vector<U3> positions;
+    mip_positions(nb, brick_dim, positions);
+    for (const U3 &p : positions) update_mip(key, nb, p);
 }
 
 void BoxTree::recalculate_mips() {  // mipmap.rs:536-586: depth first, children before their parent
@@ -1255,11 +1277,13 @@ void BoxTree::recalculate_mips() {  // mipmap.rs:536-586: depth first, children 
         Cube bounds;
         uint32_t target;
     };
+    // 1. the visiting order (post-order, children before their parent)
+    std::vector<std::pair<size_t, Cube>> order;
     std::vector<Item> stack{{0, Cube{f3(0.f, 0.f, 0.f), (float)boxtree_size}, 0}};
     while (!stack.empty()) {
         Item &it = stack.back();
         if (it.target >= kChildren) {
-            recalculate_mip(it.key, it.bounds);
+            order.push_back({it.key, it.bounds});
             stack.pop_back();
             if (!stack.empty()) stack.back().target += 1;
             continue;
@@ -1281,6 +1305,52 @@ void BoxTree::recalculate_mips() {  // mipmap.rs:536-586: depth first, children 
                 break;
             default: it.target = kChildren; break;
         }
+    }
+    if (!mip_strategy.enabled) return;
+    // 2. the leaves' resampling reads their bricks only (never a MIP, never a palette entry added below), so it runs
+    //    for every leaf up front, spread over threads
+    const uint32_t n3 = brick_dim * brick_dim * brick_dim;
+    std::vector<size_t> leaf_of(order.size(), SIZE_MAX);
+    size_t nleaves = 0;
+    for (size_t i = 0; i < order.size(); ++i)
+        if (nodes.get(order[i].first).content == Content::Leaf) leaf_of[i] = nleaves++;
+    std::vector<uint32_t> colors((size_t)nleaves * n3);
+    std::vector<uint8_t> sampled((size_t)nleaves * n3);
+    {
+        std::vector<size_t> leaves;
+        leaves.reserve(nleaves);
+        for (size_t i = 0; i < order.size(); ++i)
+            if (leaf_of[i] != SIZE_MAX) leaves.push_back(i);
+        std::atomic<size_t> next{0};
+        auto work = [&]() {
+            std::vector<U3> positions;
+            for (size_t j; (j = next.fetch_add(1)) < leaves.size();) {
+                const auto &[key, nb] = order[leaves[j]];
+                mip_positions(nb, brick_dim, positions);
+                for (uint32_t p = 0; p < n3; ++p)
+                    sampled[j * n3 + p] = mip_sample(key, nb, positions[p], colors[j * n3 + p]) ? 1 : 0;
+            }
+        };
+        const unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+        std::vector<std::thread> pool;
+        for (unsigned t = 1; t < nt && (size_t)t * 64 < leaves.size(); ++t) pool.emplace_back(work);
+        work();
+        for (auto &th : pool) th.join();
+    }
+    // 3. palette matching and stores in the reference's order (the palette grows as it goes, and a later match takes
+    //    the first entry within the threshold); other nodes resample their children's finished MIPs here
+    std::vector<U3> positions;
+    for (size_t i = 0; i < order.size(); ++i) {
+        const auto &[key, nb] = order[i];
+        if (leaf_of[i] == SIZE_MAX) {
+            recalculate_mip(key, nb);
+            continue;
+        }
+        nodes.get(key).mip = Brick{};
+        mip_positions(nb, brick_dim, positions);
+        const size_t base = leaf_of[i] * n3;
+        for (uint32_t p = 0; p < n3; ++p)
+            if (sampled[base + p]) mip_store(key, nb, positions[p], colors[base + p]);
     }
 }
 

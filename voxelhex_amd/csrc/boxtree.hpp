@@ -128,6 +128,9 @@ class BoxTree {
     void recalculate_mips();
     void recalculate_mip(size_t node_key, const Cube &node_bounds);
     void update_mip(size_t node_key, const Cube &node_bounds, U3 position);
+    // the two halves of update_mip: the resampling (reads the tree only; false for None) and the palette match + store
+    bool mip_sample(size_t node_key, const Cube &node_bounds, U3 position, uint32_t &color) const;
+    void mip_store(size_t node_key, const Cube &node_bounds, U3 position, uint32_t color);
     // sample_root_mip (mipmap.rs:635-668): sectant >= 64 samples the root's MIP, else the root's child's; raw value
     uint32_t sample_root_mip(uint8_t sectant, U3 position) const;
     // BoxTree::get_internal (src/boxtree/mod.rs:247-317) from any node and its bounds
