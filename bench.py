@@ -351,10 +351,9 @@ def main():
         if world > 1 or args.shadows:
             raise SystemExit("--mip-lod is a one-GPU primary-ray mode")
         args.no_roofline = args.no_cpu_baseline = args.no_pmc = True
-        bt = vhx.BoxTree(args.size, args.brick_dim)
-        bt.insert_scene(args.scene)
-        bt.albedo_mip_map_resampling_strategy().switch_albedo_mip_maps(True)
-        flat = bt.flatten_lod(args.mip_lod)
+        # the buffers of insert_scene + switch_albedo_mip_maps(True) + flatten_lod (tests/test_scene_builder.py)
+        flat = vhx.FlatTree.build_scene_lod(args.scene, args.size, args.brick_dim, args.mip_lod,
+                                            threads=min(16, os.cpu_count() or 1))
     elif args.vox:
         if mg is None or rank == 0:
             flat = vhx.BoxTree.load_vox_file(args.vox, args.brick_dim).flatten()

@@ -108,6 +108,11 @@ int vhx_boxtree_sample_root_mip(const vhx_boxtree *tree, uint32_t sectant, uint3
  * stored in node_mips (VHX_EMPTY where the node has no MIP). vhx_boxtree_flatten does the same with every node
  * included when the tree's MIPs are enabled, and leaves node_mips empty otherwise. */
 int vhx_boxtree_flatten_lod(const vhx_boxtree *tree, uint32_t max_depth, vhx_flat **out);
+/* vhx_scene_build, then the tree's MIP maps switched on with the default strategy and the LOD image of
+ * vhx_boxtree_flatten_lod: the same buffers as vhx_scene_insert + vhx_boxtree_switch_mips(1) + vhx_boxtree_flatten_lod
+ * without the voxel-by-voxel insert loop (minutes at 1024^3). */
+int vhx_scene_build_lod(uint32_t scene, uint32_t size, uint32_t brick_dim, uint64_t seed, int threads,
+                        uint32_t max_depth, vhx_flat **out);
 int vhx_flat_node_mips(const vhx_flat *flat, const uint32_t **node_mips, uint32_t *count);
 /* Fills *desc with pointers into the flat object (valid until vhx_flat_free). */
 int vhx_flat_desc(const vhx_flat *flat, vhx_tree_desc *desc);

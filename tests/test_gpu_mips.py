@@ -166,3 +166,23 @@ def test_mips_are_shared_by_frames_in_flight(oracle, mip_tree):
         sh.close()
     finally:
         owner.close()
+
+
+@pytest.mark.parametrize("depth", [1, 2])
+def test_headline_scale_mip_lod_frame_vs_oracle(oracle, rt, depth):
+    """The bench's --mip-lod view of the headline tree (scene S 1024^3, brick_dim 4) from vhx_scene_build_lod (equal to
+    the insert + MIP path, tests/test_scene_builder.py), a 960x540 glass frame bit-exact against the oracle."""
+    S = 1024
+    flat = vhx.FlatTree.build_scene_lod(N.VHX_SCENE_LATTICE_CUBE, S, 4, depth, threads=16)
+    W, H = 960, 540
+    cam = vhx.glass_camera(S, W, H, target=(S / 2,) * 3)
+    rt.upload(flat)
+    try:
+        rt.set_node_mips(flat.node_mips)
+        got = rt.trace_primary(cam)
+        with oracle.node_mips(flat.node_mips):
+            ref = oracle.trace_primary(flat, cam, 0, 0, W, H)
+        assert_same(got, ref, f"1024^3 MIP frame depth {depth}")
+        assert (ref["value"] != N.VHX_EMPTY).mean() > 0.2
+    finally:
+        rt.set_node_mips(None)

@@ -45,3 +45,24 @@ def test_scene_s_structure():
 def test_invalid_sizes():
     with pytest.raises(Exception):
         FlatTree.build_scene(N.VHX_SCENE_LATTICE_CUBE, 256, 8)
+
+
+LOD_CASES = [(N.VHX_SCENE_LATTICE_CUBE, 64, 4, 0), (N.VHX_SCENE_LATTICE_CUBE, 64, 4, 1),
+             (N.VHX_SCENE_LATTICE_CUBE, 64, 4, 2), (N.VHX_SCENE_HEIGHTFIELD, 64, 16, 1),
+             (N.VHX_SCENE_BOUNDARY, 32, 8, 1), (N.VHX_SCENE_LATTICE, 256, 4, 1)]
+
+
+@pytest.mark.parametrize("scene,size,bd,depth", LOD_CASES)
+def test_bulk_lod_equals_insert_mips(scene, size, bd, depth):
+    """vhx_scene_build_lod (bulk image -> host tree -> default MIPs -> LOD image) gives the buffers of the reference
+    path: insert loop, switch_albedo_mip_maps(True) (mipmap.rs:588-609), flatten_lod."""
+    t = BoxTree(size, bd)
+    t.insert_scene(scene, seed=7)
+    t.albedo_mip_map_resampling_strategy().switch_albedo_mip_maps(True)
+    a = t.flatten_lod(depth)
+    b = FlatTree.build_scene_lod(scene, size, bd, depth, seed=7, threads=4)
+    for k in list(_arrays(a)) + ["node_mips"]:
+        x, y = getattr(a, k), getattr(b, k)
+        assert x.shape == y.shape, k
+        assert np.array_equal(x, y), k
+    assert b.node_mips.size == b.node_type.size and (b.node_mips != N.VHX_EMPTY).any()

@@ -335,6 +335,15 @@ class FlatTree:
                     f"scene {scene} size {size} brick_dim {brick_dim}")
         return FlatTree(h.value)
 
+    @staticmethod
+    def build_scene_lod(scene, size, brick_dim, max_depth, seed=0x5EED, threads=0):
+        """build_scene with the default MIP maps switched on and flattened like BoxTree.flatten_lod(max_depth): the
+        image the insert loop + switch_albedo_mip_maps(True) + flatten_lod would give, without the insert loop."""
+        h = ctypes.c_void_p()
+        _tree_check(N.lib().vhx_scene_build_lod(scene, size, brick_dim, seed, threads, int(max_depth), ctypes.byref(h)),
+                    f"scene {scene} size {size} brick_dim {brick_dim}")
+        return FlatTree(h.value)
+
 
 class BoxTree:
     """BoxTree<u32> (src/boxtree/types.rs:219-255) backed by libvhx."""

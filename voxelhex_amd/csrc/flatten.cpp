@@ -250,6 +250,61 @@ static vhx_flat *flatten_tree(const BoxTree &t, uint32_t max_depth = 0xFFFFFFFFu
     return f;
 }
 
+// A BoxTree holding a flattened image's nodes, bricks and palettes (pool key = breadth-first index, so the depth-first
+// child order and therefore the MIP palette growth are those of the tree the image came from). Occlusion bits and the
+// insert bookkeeping are not restored: the tree only serves recalculate_mips + flatten_tree inside this file.
+static BoxTree *tree_of_flat(const vhx_flat &f) {
+    BoxTree *t = nullptr;
+    if (BoxTree::create(f.size, f.brick_dim, &t) != 0) return nullptr;
+    const size_t n3 = (size_t)f.brick_dim * f.brick_dim * f.brick_dim;
+    auto brick_of = [&](uint32_t desc) {
+        Brick b;
+        if (desc == VHX_EMPTY) return b;
+        if (desc & VHX_SOLID_BIT) {
+            b.kind = BrickKind::Solid;
+            b.solid = f.solid_values[desc & ~VHX_SOLID_BIT];
+        } else {
+            b.kind = BrickKind::Parted;
+            b.parted.assign(&f.voxels[(size_t)desc * n3], &f.voxels[(size_t)desc * n3] + n3);
+        }
+        return b;
+    };
+    for (size_t i = 0; i < f.node_type.size(); ++i) {
+        Node n;
+        const uint32_t *ch = &f.node_children[i * 64];
+        n.occupied_bits = f.node_ocbits[i];
+        switch (f.node_type[i]) {
+            case VHX_NODE_INTERNAL:
+                n.content = Content::Internal;
+                n.has_children = true;
+                for (int s = 0; s < 64; ++s) n.children[s] = ch[s] == VHX_EMPTY ? kEmpty32 : ch[s];
+                break;
+            case VHX_NODE_LEAF:
+                n.content = Content::Leaf;
+                for (int s = 0; s < 64; ++s) n.bricks.push_back(brick_of(ch[s]));
+                break;
+            case VHX_NODE_UNIFORM_LEAF:
+                n.content = Content::UniformLeaf;
+                n.bricks.push_back(brick_of(ch[0]));
+                break;
+            default: n.content = Content::Nothing; break;
+        }
+        if (i == 0) {
+            t->nodes.get(0) = std::move(n);
+        } else if (t->nodes.push(std::move(n)) != i) {
+            delete t;
+            return nullptr;
+        }
+    }
+    for (uint32_t c : f.color_palette) t->add_to_palette(Entry{VHX_ENTRY_VISUAL, c, 0});
+    for (uint32_t d : f.data_palette) t->add_to_palette(Entry{VHX_ENTRY_INFORMATIVE, 0, d});
+    if (t->color_palette != f.color_palette || t->data_palette != f.data_palette) {
+        delete t;
+        return nullptr;
+    }
+    return t;
+}
+
 // ---------------------------------------------------------------------------------------------- bulk builder
 static int build_scene(uint32_t scene_id, uint32_t S, uint32_t bd, uint64_t seed, int threads, vhx_flat **out) {
     BoxTree *probe = nullptr;
@@ -539,6 +594,24 @@ int vhx_scene_build(uint32_t scene, uint32_t size, uint32_t brick_dim, uint64_t 
     if (!out || !scene_valid(scene)) return VHX_E_INVALID_ARG;
     try {
         return build_scene(scene, size, brick_dim, seed, threads, out);
+    } catch (const std::bad_alloc &) {
+        return VHX_E_CAPACITY;
+    }
+}
+int vhx_scene_build_lod(uint32_t scene, uint32_t size, uint32_t brick_dim, uint64_t seed, int threads,
+                        uint32_t max_depth, vhx_flat **out) {
+    if (!out || !scene_valid(scene)) return VHX_E_INVALID_ARG;
+    try {
+        vhx_flat *full = nullptr;
+        int rc = build_scene(scene, size, brick_dim, seed, threads, &full);
+        if (rc != VHX_OK) return rc;
+        std::unique_ptr<vhx_flat> owned(full);
+        std::unique_ptr<BoxTree> t(tree_of_flat(*full));
+        if (!t) return VHX_E_STATE;
+        owned.reset();
+        t->switch_albedo_mip_maps(true);
+        *out = flatten_tree(*t, max_depth, true);
+        return VHX_OK;
     } catch (const std::bad_alloc &) {
         return VHX_E_CAPACITY;
     }
