@@ -82,6 +82,8 @@ def parse():
     p.add_argument("--depth-prepass", type=float, default=None, metavar="MARGIN",
                    help="opt-in approximate mode (vhx_set_depth_prepass, not the reference semantics): a half-resolution "
                         "depth prepass, full-resolution rays start at the min of 4 texels minus MARGIN")
+    p.add_argument("--budgets", default=None, metavar="B1,B2,...",
+                   help="step budgets of the pass schedule (vhx_set_pass_budgets; \"\" = one pass); default: the library's {24, 96, 768}, one pass with --mip-lod (its rays are short: 0.092 against 0.136 ms per depth-1 frame, profiles/r02/mips/headline/budgets)")
     p.add_argument("--mip-lod", type=int, default=None, metavar="DEPTH",
                    help="opt-in MIP stand-in mode (not the reference path): the scene inserted into a host BoxTree with "
                         "MIP maps on, flattened down to DEPTH (vhx_boxtree_flatten_lod) and traced with its node MIPs "
@@ -411,6 +413,10 @@ def main():
             r = rt.shared()
             rts.append(r)
             streams.append(torch.cuda.ExternalStream(r.stream(), device=dev))
+        budgets = args.budgets if args.budgets is not None else ("" if args.mip_lod is not None else None)
+        if budgets is not None:
+            for r in rts:
+                r.set_pass_budgets(tuple(int(b) for b in budgets.split(",") if b.strip()))
     for _ in range(len(rts)):
         o = {"rgba": torch.zeros(n_out, dtype=torch.int32, device=dev),
              "depth": torch.zeros(n_out, dtype=torch.float32, device=dev)}
@@ -649,6 +655,8 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": "f32",
             "frames_in_flight": F, "gpu_max_hw_queues": queues,
+            "pass_budgets": args.budgets if args.budgets is not None else ("one pass" if args.mip_lod is not None
+                                                                           else "library default"),
             "data": "model file" if args.vox else "synthetic",
             "config": {"workload": ("BASELINE config 4: " if cfg4 else "") + f"primary rays {W}x{H}, {args.size}^3 "
                                    + (f".vox model {os.path.basename(args.vox)}" if args.vox
