@@ -68,6 +68,8 @@ def parse():
                    help="config 5: each step = primary frame + one hard-shadow ray per hit toward (S,S,S)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-roofline", action="store_true")
+    p.add_argument("--no-frame-check", action="store_true",
+                   help="skip the untimed check of the in-flight frames (frames_equal / golden_match)")
     p.add_argument("--no-pmc", action="store_true",
                    help="skip the rocprofv3 FETCH_SIZE child run (roofline.traffic from profiles/traffic.json)")
     p.add_argument("--inflight", type=int, default=8,
@@ -200,7 +202,8 @@ def measure_traffic():
     counters = ["FETCH_SIZE", "SQ_INSTS_VALU", "SQ_THREAD_CYCLES_VALU", "SQ_ACTIVE_INST_VALU"]
     cmd = ([rp, "--pmc"] + counters + ["--kernel-trace", "-f", "csv", "-d", d, "-o", "pmc", "--", sys.executable,
                                        os.path.abspath(__file__)] + sys.argv[1:] +
-           ["--steps", "5", "--warmup", "1", "--no-cpu-baseline", "--no-roofline", "--no-pmc"])
+           ["--steps", "5", "--warmup", "1", "--no-cpu-baseline", "--no-roofline", "--no-pmc",
+            "--no-frame-check"])
     env = dict(os.environ, TMPDIR="/tmp")
     env.pop("VHX_BENCH_MGPU1", None)  # the child times the single-GPU path only
     try:
@@ -244,6 +247,82 @@ def cpu_baseline(flat, cam, W, H, threads_all):
     c1 = vhx.glass_camera(int(flat.desc.boxtree_size), w1, h1, target=(flat.desc.boxtree_size / 2.0,) * 3)
     t_one = timed(w1, h1, c1, 1)
     return t_all, t_one, (w1, h1)
+
+
+GOLDEN = os.path.join(ROOT, "tests", "golden", "frames.json")
+GOLDEN_FIELDS = ("value", "cell", "voxel", "impact", "normal", "depth", "rgba")
+
+
+def golden_case(args, W, H):
+    """The tests/golden/frames.json entry of this workload (the oracle's frame, SHA-256 per field), or None: the
+    reference-path frame of a procedural scene with the golden camera (glass_camera(size, W, H, target=centre))."""
+    if args.vox or args.orbit or args.depth_prepass is not None or args.mip_lod is not None:
+        return None
+    try:
+        meta = json.load(open(GOLDEN))
+    except (OSError, ValueError):
+        return None
+    for name, m in meta.items():
+        if (m.get("scene"), m.get("size"), m.get("brick_dim"), m.get("width"), m.get("height")) == \
+                (args.scene, args.size, args.brick_dim, W, H) and not name.startswith("mip"):
+            return name, m
+    return None
+
+
+def check_frames(args, rt, rts, outs, last_cam, light, W, H, dev):
+    """Untimed check of the timed configuration: context f's last frame (RGBA8 + f32 depth, and the shadow flags
+    with --shadows) is compared bit for bit with the owner context tracing the same camera alone, one frame at a time;
+    when the workload is a golden case every field of that lone frame and the RGBA / depth of every in-flight frame
+    are compared with the committed SHA-256 digests."""
+    import hashlib
+
+    import torch
+
+    def sha(a):
+        return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+    gc = golden_case(args, W, H)
+    torch.cuda.synchronize(dev)
+    got = {f: {k: outs[f][k].cpu().numpy().view(np.uint32).copy()
+               for k in (("rgba", "depth", "shadowed") if args.shadows else ("rgba", "depth"))}
+           for f in sorted(last_cam)}
+    refs, mism = {}, []
+    for f in sorted(last_cam):
+        cam = last_cam[f]
+        key = id(cam)
+        if key not in refs:
+            if args.shadows:
+                n = W * H
+                o = {"rgba": torch.zeros(n, dtype=torch.int32, device=dev),
+                     "depth": torch.zeros(n, dtype=torch.float32, device=dev),
+                     "value": torch.full((n,), -1, dtype=torch.int32, device=dev),
+                     "impact": torch.zeros((n, 3), dtype=torch.float32, device=dev),
+                     "normal": torch.zeros((n, 3), dtype=torch.float32, device=dev),
+                     "shadowed": torch.zeros(n, dtype=torch.int32, device=dev)}
+                rt.trace_primary(cam, out=o)
+                rt.trace_shadows(light, o, shadowed=o["shadowed"])
+                rt.sync()
+                refs[key] = {k: o[k].cpu().numpy().view(np.uint32).copy() for k in ("rgba", "depth", "shadowed")}
+            else:
+                fr = rt.trace_primary(cam, fields=GOLDEN_FIELDS if gc else ("rgba", "depth"))
+                refs[key] = {k: v.view(np.uint32) for k, v in fr.items()}
+        ref = refs[key]
+        for k, a in got[f].items():
+            if not np.array_equal(a, ref[k]):
+                mism.append({"context": f, "field": k, "pixels": int((a != ref[k]).sum())})
+    res = {"contexts": len(got), "frames_equal": not mism, "mismatches": mism[:8],
+           "basis": "last frame of each of the F contexts in flight vs the owner context tracing the same camera "
+                    "alone (bit-exact, " + ("RGBA8 + depth + shadow flags" if args.shadows else "RGBA8 + depth") + ")",
+           "golden_match": None}
+    if gc is not None and not args.shadows:
+        name, m = gc
+        lone = refs[next(iter(refs))]
+        bad = [k for k in GOLDEN_FIELDS if sha(lone[k]) != m["sha256"][k]]
+        bad += [f"context{f}.{k}" for f in got for k in ("rgba", "depth") if sha(got[f][k]) != m["sha256"][k]]
+        res.update(golden_match=not bad, golden_case=name, golden_mismatch=bad,
+                   golden_basis="tests/golden/frames.json (the oracle's frame, SHA-256 per field): every field of the "
+                                "lone frame, RGBA / depth of every in-flight frame")
+    return res
 
 
 def hw_queues(frames):
@@ -442,6 +521,7 @@ def main():
 
     ev = []
     frame = [0]
+    last_cam = {}  # context -> camera of its last frame (the frame check after the timed region)
     NOEV = os.environ.get("VHX_BENCH_NOEV") == "1"
 
     def step(timed):
@@ -449,6 +529,7 @@ def main():
         cam_k = cams[frame[0] % len(cams)]
         frame[0] += 1
         r, s_, o = rts[f], streams[f], outs[f]
+        last_cam[f] = cam_k
         if timed and mg is None and not NOEV:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(s_)
@@ -511,6 +592,12 @@ def main():
             tt = tt.to(dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
+    # ---- frame check (untimed, N = 1): the last frame of every context in flight equals one context tracing the
+    # same camera alone, and the committed golden digests where the workload is a golden case
+    frames_check = None
+    if mg is None and world == 1 and not args.no_frame_check:
+        frames_check = check_frames(args, rt, rts, outs, last_cam, light, W, H, dev)
+
     # per-launch duration: with frames in flight (HIP events on each launch's stream, over the timed region); the
     # isolated launch (one frame at a time, libvhx's own events) after it
     if ev:
@@ -675,6 +762,9 @@ def main():
                        **{k: v for k, v in tree_info.items() if k != "size"}, "build_s": round(build_s, 2), "upload_s": round(upload_s, 2)},
             "roofline": roof, "cpu_baseline": cpu,
         }
+        if frames_check is not None:
+            line.update(frames_equal=frames_check["frames_equal"], golden_match=frames_check["golden_match"],
+                        frames_check=frames_check)
         if mgpu is not None:
             line["multi_gpu_check"] = mgpu
         if mgpu_fallback:

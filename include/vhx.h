@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define VHX_ABI_VERSION 1u
+#define VHX_ABI_VERSION 2u
 
 /* ---- error codes ------------------------------------------------------------------------------------------ */
 #define VHX_OK 0
@@ -139,8 +139,11 @@ int vhx_create(int hip_device, vhx_ctx **out);
 /* A further context on the owner's device that traces the owner's uploaded tree (no second copy in HBM): one context
  * per frame in flight. Each context has its own stream, ray queues and outputs, so frame k+1's trace runs while frame
  * k's long-ray tail still occupies a few SIMDs (the frames of a renderer are independent of each other). Uploads and updates go through the owner (a shared context returns
- * VHX_E_STATE for them) and need every context of the tree idle (vhx_sync). The tree lives until its last context is
- * destroyed, in any order. */
+ * VHX_E_STATE for them) and are ordered against the frames in flight by libvhx, on the device, without host waits: a
+ * write of the tree (vhx_upload_tree, vhx_update_range(s), vhx_set_node_mips, vhx_upload_tree_device) first waits on
+ * its stream for the last trace submitted on every other context of the tree, and the next trace of every context
+ * waits on its own stream for that write. So a frame sees the tree as of its submission: every write submitted
+ * before it and none submitted after it. The tree lives until its last context is destroyed, in any order. */
 int vhx_create_shared(const vhx_ctx *owner, vhx_ctx **out);
 void vhx_destroy(vhx_ctx *ctx);
 const char *vhx_last_error(const vhx_ctx *ctx);
@@ -163,6 +166,10 @@ int vhx_set_pass_budgets(vhx_ctx *ctx, const uint32_t *budgets, uint32_t n);
 /* Tree upload ----------------------------------------------------------------------------------------------- */
 /* Copies the flattened tree to HBM (full residency) and builds the device-side layout. */
 int vhx_upload_tree(vhx_ctx *ctx, const vhx_tree_desc *tree);
+/* Same, from buffers already in device memory (the 7 array pointers of `tree` are device pointers: a tree produced on
+ * the GPU, or another device's copy where peer access is enabled): device-to-device copies on the context's stream,
+ * then the derived layout. The receive half of vhx_mgpu_broadcast_tree, which fills the same buffers by ncclBroadcast. */
+int vhx_upload_tree_device(vhx_ctx *ctx, const vhx_tree_desc *tree);
 #define VHX_BUF_NODE_TYPE 0
 #define VHX_BUF_NODE_OCBITS 1
 #define VHX_BUF_NODE_CHILDREN 2
@@ -224,7 +231,8 @@ int vhx_set_depth_prepass(vhx_ctx *ctx, int enable, float margin);
  * sectant (where the reference CPU path would push into the child, which does not exist). Without MIPs (the default)
  * such a push ends the ray as a miss, as before. A tree whose children are all present traces identically either way.
  * NULL disables; count must equal the uploaded tree's node_count; a new vhx_upload_tree disables them. Like an update,
- * it goes through the owner of a shared tree with every context of the tree idle; shared contexts trace with them. */
+ * it goes through the owner of a shared tree and is ordered against frames in flight (vhx_create_shared); shared
+ * contexts trace with them. */
 int vhx_set_node_mips(vhx_ctx *ctx, const uint32_t *node_mips, uint32_t count);
 /* Traces n explicit rays; rays = 6 f32 per ray (origin xyz, direction xyz), host or device per on_device. */
 int vhx_trace_rays(vhx_ctx *ctx, const float *rays, uint64_t n, const vhx_hits *out, int on_device);
@@ -300,6 +308,20 @@ int vhx_mgpu_balance(vhx_mgpu *m, const vhx_camera *cam, uint32_t frames, uint32
                      float *transfer_ms);
 /* nranks, rank, and the rays this rank traces for a width x height frame (any pointer may be NULL). */
 int vhx_mgpu_info(const vhx_mgpu *m, uint32_t width, uint32_t height, int *nranks, int *rank, uint64_t *rays);
+/* The tile plan of the split, as vhx_mgpu_render deals it (a pure function: no device, no communicator). For N ranks,
+ * rank 0 owning R slots, tile size T and a width x height frame: tiles = ceil(W/T) * ceil(H/T) raster-order tiles,
+ * slots = R + N - 1, slot s traces tiles s, s + slots, ... (tiles_per_slot = ceil(tiles / slots) entries each, the last
+ * ones padded), `rank` owns slots first_slot .. first_slot + slot_count - 1 and sends them to rank 0, whose
+ * slot-major gather buffer holds slot s's part at s * tiles_per_slot * T * T words per plane. */
+typedef struct vhx_tile_plan {
+    uint32_t tiles_x, tiles_y, tiles, slots, tiles_per_slot, first_slot, slot_count, reserved;
+} vhx_tile_plan;
+int vhx_mgpu_tile_plan(uint32_t nranks, uint32_t root_slots, uint32_t tile_size, uint32_t width, uint32_t height,
+                       uint32_t rank, vhx_tile_plan *plan);
+/* Collective: renders `frames` + 1 frames of `cam` one at a time at the current split and returns THIS rank's median
+ * device time of its trace and of its transfers (rank 0: its receives of the other ranks' parts; other ranks: the send), in ms
+ * (the first frame is a warm-up). Diagnostics for the scaling model of DESIGN.md §7; any output may be NULL. */
+int vhx_mgpu_measure(vhx_mgpu *m, const vhx_camera *cam, uint32_t frames, float *trace_ms, float *transfer_ms);
 void vhx_mgpu_destroy(vhx_mgpu *m);
 
 #ifdef __cplusplus

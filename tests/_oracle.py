@@ -9,7 +9,8 @@ from voxelhex_amd import _native as N
 from voxelhex_amd.raytracing import HIT_FIELDS, _hits_struct
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-ORACLE_LIB = os.path.join(ROOT, "oracle", "_build", "liboracle.so")
+# VHX_ORACLE_LIB: another build of the same source (scripts/asan_cpu.sh builds it with the sanitizers)
+ORACLE_LIB = os.environ.get("VHX_ORACLE_LIB") or os.path.join(ROOT, "oracle", "_build", "liboracle.so")
 
 
 class Oracle:

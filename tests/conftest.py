@@ -7,6 +7,15 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
+# Frames in flight (tests/test_gpu_inflight.py, the bench's configuration): every context stream needs a hardware queue
+# of its own, and HIP reads GPU_MAX_HW_QUEUES once, when it initialises -- so it is raised here, before any test
+# imports torch or loads libvhx (the same rule as bench.py's hw_queues)
+try:
+    if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 12:
+        os.environ["GPU_MAX_HW_QUEUES"] = "12"
+except ValueError:
+    os.environ["GPU_MAX_HW_QUEUES"] = "12"
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device); run with -m gpu")

@@ -145,3 +145,80 @@ def test_rank_planes_gather_and_rccl_id_exchange(tmp_path, world):
     assert same_id.all(), "ranks received different RCCL ids"
     assert np.array_equal(rgba, full_rgba)
     assert np.array_equal(depth, full_depth)
+
+
+# ---- the C tile plan of vhx_mgpu (vhx_mgpu_tile_plan) with rank 0 holding R slots ----------------------------------
+def test_c_tile_plan_deals_every_tile_once():
+    """vhx_mgpu_tile_plan for N in {1, 2, 3, 8} and R in {1..4}, incl. frames with fewer tiles than slots: the slots of
+    all ranks partition 0..V-1, slot s traces tiles s, s + V, ... (at most tiles_per_slot of them), and every tile of
+    the frame is traced exactly once."""
+    for (w, h) in ((W, H), (3840, 2160), (64, 64), (130, 70)):
+        for n in (1, 2, 3, 8):
+            for r_slots in (1, 2, 3, 4):
+                plans = [M.tile_plan(n, r_slots, T, w, h, q) for q in range(n)]
+                V = r_slots + n - 1
+                assert all(p["slots"] == V for p in plans)
+                owned = sorted(s for p in plans for s in range(p["first_slot"], p["first_slot"] + p["slot_count"]))
+                assert owned == list(range(V))
+                assert plans[0]["slot_count"] == r_slots and all(p["slot_count"] == 1 for p in plans[1:])
+                tiles = plans[0]["tiles"]
+                assert tiles == ((w + T - 1) // T) * ((h + T - 1) // T)
+                seen = np.zeros(tiles, np.int32)
+                for s_ in range(V):
+                    mine = list(range(s_, tiles, V))
+                    assert len(mine) <= plans[0]["tiles_per_slot"]
+                    seen[mine] += 1
+                assert (seen == 1).all()
+    with pytest.raises(ValueError):
+        M.tile_plan(2, 0, T, W, H, 0)  # R >= 1
+    with pytest.raises(ValueError):
+        M.tile_plan(2, 1, T, W, H, 2)  # rank < N
+
+
+def _slots_worker(rank, world, port, out_path, r_slots, w, h):
+    """vhx_mgpu_render's data path restated on the CPU with the C plan: each rank traces its slots (oracle) into
+    [RGBA | depth] parts of tiles_per_slot tiles, ranks >= 1 send their part to rank 0 point to point (gloo send/recv,
+    as the RCCL group does), rank 0 places each at its slot's offset and untiles the slot-major buffer."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import voxelhex_amd as vhx
+    from tests._oracle import Oracle
+    flat = vhx.FlatTree.build_scene(vhx.native.VHX_SCENE_LATTICE_CUBE, 64, 4)
+    cam = vhx.glass_camera(64, w, h, target=(32.0, 32.0, 32.0))
+    orc = Oracle()
+    plan = M.tile_plan(world, r_slots, T, w, h, rank)
+    V, per, n = plan["slots"], plan["tiles_per_slot"], plan["tiles_per_slot"] * T * T
+    parts = np.zeros(plan["slot_count"] * 2 * n, np.uint32)
+    for k in range(plan["slot_count"]):
+        s_ = plan["first_slot"] + k
+        for j, tile in enumerate(range(s_, plan["tiles"], V)):
+            x0, y0, tw, th = M.tile_rect(tile, w, h, T)
+            r = orc.trace_primary(flat, cam, x0, y0, tw, th, threads=1, fields=("rgba", "depth"))
+            base = k * 2 * n
+            parts[base + j * T * T:base + (j + 1) * T * T].reshape(T, T)[:th, :tw] = r["rgba"].reshape(th, tw)
+            parts[base + n + j * T * T:base + n + (j + 1) * T * T].reshape(T, T)[:th, :tw] = \
+                r["depth"].view(np.uint32).reshape(th, tw)
+    if rank == 0:
+        gathered = np.zeros(V * 2 * n, np.uint32)
+        gathered[:parts.size] = parts
+        for q in range(1, world):
+            qp = M.tile_plan(world, r_slots, T, w, h, q)
+            buf = torch.zeros(2 * n, dtype=torch.int32)
+            dist.recv(buf, src=q)
+            gathered[qp["first_slot"] * 2 * n:(qp["first_slot"] + 1) * 2 * n] = buf.numpy().view(np.uint32)
+        rgba, depth = M.untile_planes_numpy(gathered, 2, V, per, T, w, h)
+        full = orc.trace_primary(flat, cam, 0, 0, w, h, threads=1, fields=("rgba", "depth"))
+        np.save(out_path, np.stack([rgba, full["rgba"], depth, full["depth"].view(np.uint32)]))
+    else:
+        dist.send(torch.from_numpy(parts.view(np.int32)), dst=0)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,r_slots,w,h", [(2, 1, W, H), (2, 3, W, H), (3, 2, W, H), (3, 3, 130, 70)])
+def test_root_slots_split_reassembles_the_frame(tmp_path, world, r_slots, w, h):
+    """R > 1 and a frame with fewer tiles than slots ((3, 3, 130x70): 6 tiles, 5 slots, rank 2's slot holds one)."""
+    out = str(tmp_path / "slots.npy")
+    mp.spawn(_slots_worker, args=(world, _free_port(), out, r_slots, w, h), nprocs=world, join=True)
+    rgba, full_rgba, depth, full_depth = np.load(out)
+    assert np.array_equal(rgba, full_rgba)
+    assert np.array_equal(depth, full_depth)

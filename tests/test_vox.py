@@ -254,6 +254,83 @@ def test_file_roundtrip_and_errors(tmp_path):
                                                               ("S", {}, [(0, {})])]), 1)
 
 
+def _corrupt_cases():
+    """Malformed inputs a parser of untrusted bytes must refuse without reading out of bounds (VERDICT r02 next 6;
+    reference entry: magicavoxel.rs:236-253 hands the bytes to dot_vox): chunk lengths past the end, negative chunk,
+    string, dictionary, voxel, child and frame counts, negative model sizes."""
+    models, scene = _scene_cases()["single"]
+    good = write_vox(models, PALETTE, scene)
+    cases = {}
+    main_at = 8  # "MAIN" chunk header: id, content length, children length
+    b = bytearray(good)
+    struct.pack_into("<i", b, main_at + 8, 1 << 30)  # MAIN's children length far past the end
+    cases["main_children_past_end"] = bytes(b)
+    b = bytearray(good)
+    struct.pack_into("<i", b, main_at + 8, -64)
+    cases["main_children_negative"] = bytes(b)
+    b = bytearray(good)
+    struct.pack_into("<i", b, main_at + 4, -1)
+    cases["main_content_negative"] = bytes(b)
+    first = 20  # the first child chunk (SIZE)
+    b = bytearray(good)
+    struct.pack_into("<i", b, first + 4, 0x7FFFFFF0)  # SIZE content length past the end
+    cases["chunk_content_past_end"] = bytes(b)
+    b = bytearray(good)
+    struct.pack_into("<i", b, first + 4, -12)
+    cases["chunk_content_negative"] = bytes(b)
+    b = bytearray(good)
+    struct.pack_into("<i", b, first + 8, -5)
+    cases["chunk_children_negative"] = bytes(b)
+    b = bytearray(good)
+    struct.pack_into("<iii", b, first + 12, -4, 2, 2)  # negative model size
+    cases["size_negative"] = bytes(b)
+    xyzi = good.index(b"XYZI")
+    b = bytearray(good)
+    struct.pack_into("<i", b, xyzi + 12, -3)  # negative voxel count
+    cases["xyzi_count_negative"] = bytes(b)
+    b = bytearray(good)
+    struct.pack_into("<i", b, xyzi + 12, 1 << 29)  # voxel count past the chunk
+    cases["xyzi_count_past_chunk"] = bytes(b)
+    trn = write_vox(models, PALETTE, [("T", {"_name": "x"}, 1, [{"_t": "1 2 3"}]), ("S", {}, [(0, {})])])
+    at = trn.index(b"nTRN") + 12 + 4  # node id, then the attribute dictionary
+    b = bytearray(trn)
+    struct.pack_into("<i", b, at, -2)  # negative dictionary count
+    cases["dict_count_negative"] = bytes(b)
+    b = bytearray(trn)
+    struct.pack_into("<i", b, at + 4, -7)  # negative key length
+    cases["string_length_negative"] = bytes(b)
+    b = bytearray(trn)
+    struct.pack_into("<i", b, at + 4, 1 << 28)  # key length past the chunk
+    cases["string_length_past_chunk"] = bytes(b)
+    frames_at = trn.index(b"nTRN") + 12 + 4 + len(_dict({"_name": "x"})) + 12
+    b = bytearray(trn)
+    struct.pack_into("<i", b, frames_at, -1)  # negative frame count
+    cases["frame_count_negative"] = bytes(b)
+    grp = write_vox(models, PALETTE, [("T", {}, 1, [{}]), ("G", {}, [2]), ("T", {}, 3, [{}]), ("S", {}, [(0, {})])])
+    at = grp.index(b"nGRP") + 12 + 4 + len(_dict({}))
+    b = bytearray(grp)
+    struct.pack_into("<i", b, at, -9)  # negative child count
+    cases["group_children_negative"] = bytes(b)
+    b = bytearray(grp)
+    struct.pack_into("<i", b, at, 1 << 27)
+    cases["group_children_past_chunk"] = bytes(b)
+    shp = grp.index(b"nSHP") + 12 + 4 + len(_dict({}))
+    b = bytearray(grp)
+    struct.pack_into("<i", b, shp, -1)  # negative model count
+    cases["shape_models_negative"] = bytes(b)
+    cases["truncated_header"] = good[:10]
+    cases["empty"] = b""
+    return good, cases
+
+
+@pytest.mark.parametrize("name", sorted(_corrupt_cases()[1]))
+def test_corrupt_files_are_refused(name):
+    good, cases = _corrupt_cases()
+    assert vhx.BoxTree.load_vox_bytes(good, 2) is not None  # the unmodified file loads
+    with pytest.raises(N.VhxError):
+        vhx.BoxTree.load_vox_bytes(cases[name], 2)
+
+
 def _read_vox(path):
     """Independent minimal reader: models, palette and scene of a real .vox file (for the restatement)."""
     b = open(path, "rb").read()

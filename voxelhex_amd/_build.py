@@ -45,9 +45,11 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(verbose=False, force=False, lib=None, build_dir=None, defines=(), flags=(), dev_flags=None):
+def build(verbose=False, force=False, lib=None, build_dir=None, defines=(), flags=(), dev_flags=None, host_flags=()):
     """lib / build_dir / defines / flags / dev_flags: a variant build (probes), e.g. defines=("VHX_QUEUE_WPE=5",),
-    flags=("-O2",) added to the device sources, dev_flags=() for LLVM's default scheduler."""
+    flags=("-O2",) added to the device sources, dev_flags=() for LLVM's default scheduler; host_flags are added to the
+    host C++ sources (scripts/asan_cpu.sh: -fsanitize=address,undefined, resolved at run time from the preloaded
+    sanitizer runtimes)."""
     dev = DEV_FLAGS if dev_flags is None else list(dev_flags)
     lib = lib or LIB
     bdir = build_dir or BUILD
@@ -62,7 +64,7 @@ def build(verbose=False, force=False, lib=None, build_dir=None, defines=(), flag
         o = os.path.join(bdir, src + ".o")
         if force or _stale(o, [s] + common_deps):
             _run(["g++", "-O3", "-std=c++17", "-fPIC", "-pthread", "-ffp-contract=off", "-fno-fast-math",
-                  "-Wall", "-Wextra", "-I", inc, "-c", s, "-o", o], verbose)
+                  "-Wall", "-Wextra", "-I", inc] + list(host_flags) + ["-c", s, "-o", o], verbose)
         objs.append(o)
     for src in DEV_SRCS:
         s = os.path.join(CSRC, src)

@@ -70,6 +70,11 @@ class Camera(ctypes.Structure):
     ]
 
 
+class TilePlan(ctypes.Structure):
+    _fields_ = [(n, c_u32) for n in ("tiles_x", "tiles_y", "tiles", "slots", "tiles_per_slot", "first_slot",
+                                     "slot_count", "reserved")]
+
+
 class Hits(ctypes.Structure):
     _fields_ = [
         ("value", c_void_p), ("cell", c_void_p), ("voxel", c_void_p), ("impact", c_void_p),
@@ -90,6 +95,7 @@ SIGNATURES = [
     ("vhx_sync", c_int, [c_void_p, P(c_f32)]),
     ("vhx_set_pass_budgets", c_int, [c_void_p, P(c_u32), c_u32]),
     ("vhx_upload_tree", c_int, [c_void_p, P(TreeDesc)]),
+    ("vhx_upload_tree_device", c_int, [c_void_p, P(TreeDesc)]),
     ("vhx_set_node_mips", c_int, [c_void_p, c_void_p, c_u32]),
     ("vhx_update_range", c_int, [c_void_p, c_int, c_u64, c_u64, c_void_p]),
     ("vhx_update_ranges", c_int, [c_void_p, c_void_p, c_u32]),
@@ -113,6 +119,8 @@ SIGNATURES = [
     ("vhx_mgpu_info", c_int, [c_void_p, c_u32, c_u32, P(c_int), P(c_int), P(c_u64)]),
     ("vhx_mgpu_set_root_slots", c_int, [c_void_p, c_u32]),
     ("vhx_mgpu_balance", c_int, [c_void_p, P(Camera), c_u32, P(c_u32), P(c_f32), P(c_f32)]),
+    ("vhx_mgpu_tile_plan", c_int, [c_u32, c_u32, c_u32, c_u32, c_u32, c_u32, P(TilePlan)]),
+    ("vhx_mgpu_measure", c_int, [c_void_p, P(Camera), c_u32, P(c_f32), P(c_f32)]),
     ("vhx_mgpu_destroy", None, [c_void_p]),
     ("vhx_boxtree_new", c_int, [c_u32, c_u32, P(c_void_p)]),
     ("vhx_boxtree_free", None, [c_void_p]),

@@ -5,6 +5,7 @@
 
 #include <cstdint>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -30,6 +31,15 @@ struct TreeStore {
     // iteration whose target child is occupied but absent probes the node's MIP (vhx_set_node_mips)
     DevBuf mips;
     bool mips_on = false;
+    // Ordering of tree writes against frames in flight (any context of the tree, any stream; no host waits): a write
+    // (upload, ranged update, node MIPs) first makes its stream wait for the last submitted trace of every other
+    // context (their use_ev), and records write_ev after it; a context's next trace waits for write_ev once per write
+    // (write_seq against its seen_write). Contexts register in `users` at creation and leave at destruction.
+    std::mutex mu;
+    std::vector<struct vhx_ctx *> users;
+    hipEvent_t write_ev = nullptr;
+    hipStream_t write_stream = nullptr;
+    uint64_t write_seq = 0;
     ~TreeStore();
 };
 
@@ -42,6 +52,9 @@ struct vhx_ctx {
     std::string err;
     std::shared_ptr<TreeStore> tree;  // shared by the contexts of one tree
     bool shared = false;              // made by vhx_create_shared: traces only (uploads and updates go to the owner)
+    hipEvent_t use_ev = nullptr;      // recorded after every trace submitted on this context (TreeStore ordering)
+    bool use_recorded = false;
+    uint64_t seen_write = 0;          // the TreeStore write_seq this context's stream already waits for
     DevBuf scratch, rays;
     DevBuf queue[2];  // multi-pass ray queues (ping-pong), output indices of abandoned rays in increasing order
     DevBuf qctl;      // QCTL_WORDS: [0..7] queue lengths after pass p (7: shadow hit list), [16 + 16p ..] counters
@@ -135,5 +148,22 @@ int finish_upload(vhx_ctx *c);
 int launch_untile(vhx_ctx *c, hipStream_t stream, const void *gathered, uint32_t planes, uint32_t ranks,
                   uint32_t tiles_per_rank, uint32_t T, uint32_t width, uint32_t height, uint32_t *fb_rgba,
                   float *fb_depth);
+// tree-write ordering (TreeStore): before a write of the tree on c's stream, wait for every other context's last
+// submitted trace; after it, record the write
+int write_begin(vhx_ctx *c);
+int write_end(vhx_ctx *c);
+// before a trace on c's stream: wait for the tree's last write (once per write); after it: record c's use
+int trace_begin(vhx_ctx *c);
+int trace_end(vhx_ctx *c);
+// the tree counts as 8 u32 (the message of a device-side tree transfer) and back
+void pack_counts(const vhx_tree_desc &d, uint32_t counts[8]);
+vhx_tree_desc unpack_counts(const uint32_t counts[8]);
+// A tree whose raw buffers arrive device-side (ncclBroadcast from rank 0, a peer copy): allocates the raw buffers for
+// `counts`, calls fill(id, dst, bytes) for each of the 7 buffers (it enqueues the transfer on c's stream), then
+// derives the device layout (synchronises). Ordered against the traces of every context of the tree.
+int receive_tree(vhx_ctx *c, const vhx_tree_desc &counts,
+                 int (*fill)(void *arg, void *const dst[7], const uint64_t bytes[7]), void *arg);
+// the scheduling settings (pass budgets, rays per wave, queue shapes, sparse thresholds, depth prepass) of src
+void copy_sched(vhx_ctx *dst, const vhx_ctx *src);
 }  // namespace vhx
 

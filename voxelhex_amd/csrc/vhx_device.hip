@@ -731,6 +731,7 @@ static DevTree dev_tree(const vhx_ctx *c) {
 
 TreeStore::~TreeStore() {
     (void)hipSetDevice(device);
+    if (write_ev) (void)hipEventDestroy(write_ev);
     for (auto &b : raw)
         if (b.ptr) (void)hipFree(b.ptr);
     for (DevBuf *b : {&hdr, &brick_occ, &child_rec, &mips})
@@ -746,6 +747,76 @@ int vhx::ensure(vhx_ctx *c, DevBuf &b, uint64_t bytes) {
     VHX_HIP(c, hipMalloc(&b.ptr, bytes));
     b.bytes = bytes;
     return VHX_OK;
+}
+
+// ---- tree-write ordering (TreeStore): frames in flight on shared contexts and writes through the owner ----------
+int vhx::write_begin(vhx_ctx *c) {
+    TreeStore &ts = *c->tree;
+    std::lock_guard<std::mutex> lock(ts.mu);
+    for (vhx_ctx *u : ts.users)
+        if (u != c && u->use_recorded && u->stream != c->stream) VHX_HIP(c, hipStreamWaitEvent(c->stream, u->use_ev, 0));
+    // a write on another stream than the previous write also follows it (writes are ordered among themselves)
+    if (ts.write_seq && ts.write_stream != c->stream) VHX_HIP(c, hipStreamWaitEvent(c->stream, ts.write_ev, 0));
+    return VHX_OK;
+}
+
+int vhx::write_end(vhx_ctx *c) {
+    TreeStore &ts = *c->tree;
+    std::lock_guard<std::mutex> lock(ts.mu);
+    if (!ts.write_ev) VHX_HIP(c, hipEventCreateWithFlags(&ts.write_ev, hipEventDisableTiming));
+    VHX_HIP(c, hipEventRecord(ts.write_ev, c->stream));
+    ts.write_stream = c->stream;
+    ++ts.write_seq;
+    c->seen_write = ts.write_seq;
+    return VHX_OK;
+}
+
+int vhx::trace_begin(vhx_ctx *c) {
+    TreeStore &ts = *c->tree;
+    std::lock_guard<std::mutex> lock(ts.mu);
+    if (c->seen_write != ts.write_seq) {
+        if (ts.write_stream != c->stream) VHX_HIP(c, hipStreamWaitEvent(c->stream, ts.write_ev, 0));
+        c->seen_write = ts.write_seq;
+    }
+    return VHX_OK;
+}
+
+int vhx::trace_end(vhx_ctx *c) {
+    if (!c->use_ev) VHX_HIP(c, hipEventCreateWithFlags(&c->use_ev, hipEventDisableTiming));
+    std::lock_guard<std::mutex> lock(c->tree->mu);  // write_begin reads use_recorded / waits on use_ev
+    VHX_HIP(c, hipEventRecord(c->use_ev, c->stream));
+    c->use_recorded = true;
+    return VHX_OK;
+}
+
+static void register_user(vhx_ctx *c) {
+    std::lock_guard<std::mutex> lock(c->tree->mu);
+    c->tree->users.push_back(c);
+    c->seen_write = 0;  // the first trace waits for the tree's last write (if any, and on another stream)
+}
+
+static void unregister_user(vhx_ctx *c) {
+    std::lock_guard<std::mutex> lock(c->tree->mu);
+    auto &u = c->tree->users;
+    u.erase(std::remove(u.begin(), u.end(), c), u.end());
+}
+
+void vhx::pack_counts(const vhx_tree_desc &d, uint32_t counts[8]) {
+    const uint32_t v[8] = {d.boxtree_size, d.brick_dim, d.node_count, d.brick_count,
+                           d.solid_count, d.color_count, d.data_count, 0};
+    std::memcpy(counts, v, sizeof(v));
+}
+
+vhx_tree_desc vhx::unpack_counts(const uint32_t counts[8]) {
+    vhx_tree_desc d{};
+    d.boxtree_size = counts[0];
+    d.brick_dim = counts[1];
+    d.node_count = counts[2];
+    d.brick_count = counts[3];
+    d.solid_count = counts[4];
+    d.color_count = counts[5];
+    d.data_count = counts[6];
+    return d;
 }
 
 uint64_t vhx::elem_size(int id) {
@@ -1047,6 +1118,7 @@ int vhx_create(int hip_device, vhx_ctx **out) {
     c->device = hip_device;
     c->tree = std::make_shared<TreeStore>();
     c->tree->device = hip_device;
+    register_user(c);
     auto bail = [&](const char *what, hipError_t e) {
         fprintf(stderr, "vhx_create: %s: %s\n", what, hipGetErrorString(e));
         delete c;
@@ -1131,25 +1203,10 @@ int vhx_create_shared(const vhx_ctx *owner, vhx_ctx **out) {
     vhx_ctx *c = nullptr;
     int rc = vhx_create(owner->device, &c);
     if (rc) return rc;
-    c->tree = owner->tree;  // the same device tree (reference-counted)
+    c->tree = owner->tree;  // the same device tree (reference-counted); the context's fresh store goes with it
+    register_user(c);
     c->shared = true;
-    // the owner's scheduling settings
-    std::memcpy(c->budgets, owner->budgets, sizeof(c->budgets));
-    std::memcpy(c->rpw, owner->rpw, sizeof(c->rpw));
-    c->npass = owner->npass;
-    c->tw = owner->tw;
-    c->resume = owner->resume;
-    c->xcd_group = owner->xcd_group;
-    c->qblock = owner->qblock;
-    c->queue_blocks = owner->queue_blocks;
-    c->queue_waves = owner->queue_waves;
-    c->queue_waves0 = owner->queue_waves0;
-    c->queue_waves_mid = owner->queue_waves_mid;
-    c->qxcd = owner->qxcd;
-    c->qxcd_all = owner->qxcd_all;
-    std::memcpy(c->sparse, owner->sparse, sizeof(c->sparse));
-    c->prepass = owner->prepass;
-    c->prepass_margin = owner->prepass_margin;
+    copy_sched(c, owner);  // the owner's scheduling settings (as of now; vhx_mgpu re-copies them per frame)
     *out = c;
     return VHX_OK;
 }
@@ -1158,7 +1215,9 @@ void vhx_destroy(vhx_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    unregister_user(c);
     c->tree.reset();  // frees the device tree with its last context
+    if (c->use_ev) (void)hipEventDestroy(c->use_ev);
     for (DevBuf *b : {&c->scratch, &c->rays, &c->queue[0], &c->queue[1], &c->qctl, &c->tmp, &c->counts, &c->offsets,
                       &c->flags, &c->qargs, &c->state, &c->upd, &c->prepass_depth})
         if (b->ptr) (void)hipFree(b->ptr);
@@ -1231,6 +1290,11 @@ int vhx::alloc_tree(vhx_ctx *c, const vhx_tree_desc *t) {
         (t->boxtree_size & (t->boxtree_size - 1)) != 0 || t->boxtree_size > (1u << 24))
         return fail(c, VHX_E_INVALID_ARG, "vhx_upload_tree: invalid sizes");
     VHX_HIP(c, hipSetDevice(c->device));
+    // a buffer that grows is freed and reallocated: the frames in flight on the tree's contexts (which c's stream
+    // already waits for, write_begin) finish first
+    bool grows = false;
+    for (int id = 0; id < 7; ++id) grows |= c->tree->raw[id].bytes < elem_count(*t, id) * elem_size(id);
+    if (grows && c->stream) VHX_HIP(c, hipStreamSynchronize(c->stream));
     c->tree->uploaded = false;
     c->tree->mips_on = false;  // a new tree has no MIPs until vhx_set_node_mips
     for (int id = 0; id < 7; ++id) {
@@ -1276,14 +1340,80 @@ int vhx_upload_tree(vhx_ctx *c, const vhx_tree_desc *t) {
     for (int id = 0; id < 7; ++id)
         if (elem_count(*t, id) && !src[id])
             return fail(c, VHX_E_INVALID_ARG, "vhx_upload_tree: null array with non-zero count");
-    int rc = alloc_tree(c, t);
-    if (rc) return rc;
+    VHX_HIP(c, hipSetDevice(c->device));
     VHX_STREAM(c);
+    int rc = write_begin(c);  // frames in flight on the tree's other contexts finish reading it first
+    if (!rc) rc = alloc_tree(c, t);
+    if (rc) return rc;
     for (int id = 0; id < 7; ++id) {
         const uint64_t bytes = elem_count(*t, id) * elem_size(id);
         if (bytes) VHX_HIP(c, hipMemcpyAsync(c->tree->raw[id].ptr, src[id], bytes, hipMemcpyHostToDevice, c->stream));
     }
-    return finish_upload(c);
+    if ((rc = finish_upload(c))) return rc;
+    return write_end(c);
+}
+
+}  // extern "C"
+
+int vhx::receive_tree(vhx_ctx *c, const vhx_tree_desc &counts,
+                      int (*fill)(void *, void *const[7], const uint64_t[7]), void *arg) {
+    VHX_HIP(c, hipSetDevice(c->device));
+    VHX_STREAM(c);
+    int rc = write_begin(c);
+    if (!rc) rc = alloc_tree(c, &counts);
+    if (rc) return rc;
+    void *dst[7];
+    uint64_t bytes[7];
+    for (int id = 0; id < 7; ++id) {
+        dst[id] = c->tree->raw[id].ptr;
+        bytes[id] = elem_count(c->tree->desc, id) * elem_size(id);
+    }
+    if ((rc = fill(arg, dst, bytes))) return rc;  // the transfers, enqueued on c's stream
+    if ((rc = finish_upload(c))) return rc;       // derived layout from the received buffers (synchronises)
+    return write_end(c);
+}
+
+void vhx::copy_sched(vhx_ctx *c, const vhx_ctx *owner) {
+    std::memcpy(c->budgets, owner->budgets, sizeof(c->budgets));
+    std::memcpy(c->rpw, owner->rpw, sizeof(c->rpw));
+    c->npass = owner->npass;
+    c->tw = owner->tw;
+    c->resume = owner->resume;
+    c->xcd_group = owner->xcd_group;
+    c->qblock = owner->qblock;
+    c->queue_blocks = owner->queue_blocks;
+    c->queue_waves = owner->queue_waves;
+    c->queue_waves0 = owner->queue_waves0;
+    c->queue_waves_mid = owner->queue_waves_mid;
+    c->qxcd = owner->qxcd;
+    c->qxcd_all = owner->qxcd_all;
+    std::memcpy(c->sparse, owner->sparse, sizeof(c->sparse));
+    c->prepass = owner->prepass;
+    c->prepass_margin = owner->prepass_margin;
+}
+
+extern "C" {
+
+static int fill_device_copies(void *arg, void *const dst[7], const uint64_t bytes[7]) {
+    const std::pair<vhx_ctx *, const vhx_tree_desc *> &a = *(const std::pair<vhx_ctx *, const vhx_tree_desc *> *)arg;
+    vhx_ctx *c = a.first;
+    const void *src[7] = {a.second->node_type,  a.second->node_ocbits,    a.second->node_children, a.second->voxels,
+                          a.second->solid_values, a.second->color_palette, a.second->data_palette};
+    for (int id = 0; id < 7; ++id)
+        if (bytes[id]) VHX_HIP(c, hipMemcpyAsync(dst[id], src[id], bytes[id], hipMemcpyDefault, c->stream));
+    return VHX_OK;
+}
+
+int vhx_upload_tree_device(vhx_ctx *c, const vhx_tree_desc *t) {
+    if (!c || !t) return VHX_E_INVALID_ARG;
+    if (c->shared) return fail(c, VHX_E_STATE, "vhx_upload_tree_device on a shared context: upload through the owner");
+    const void *src[7] = {t->node_type, t->node_ocbits, t->node_children, t->voxels,
+                          t->solid_values, t->color_palette, t->data_palette};
+    for (int id = 0; id < 7; ++id)
+        if (elem_count(*t, id) && !src[id])
+            return fail(c, VHX_E_INVALID_ARG, "vhx_upload_tree_device: null array with non-zero count");
+    std::pair<vhx_ctx *, const vhx_tree_desc *> arg{c, t};
+    return receive_tree(c, *t, fill_device_copies, &arg);
 }
 
 int vhx_update_ranges(vhx_ctx *c, const vhx_range *r, uint32_t n) {
@@ -1305,6 +1435,9 @@ int vhx_update_ranges(vhx_ctx *c, const vhx_range *r, uint32_t n) {
     if (njobs > 0xFFFFFFFFull) return fail(c, VHX_E_INVALID_ARG, "vhx_update_ranges: too much data in one call");
     VHX_HIP(c, hipSetDevice(c->device));
     VHX_STREAM(c);
+    // the scatter and the derived-state rebuilds write the tree: frames in flight on the other contexts first
+    int rc = write_begin(c);
+    if (rc) return rc;
     // pinned staging slot (the one used two calls ago: its copy has normally long completed)
     vhx_ctx::Pinned &P = c->pinned[c->pinned_next];
     c->pinned_next ^= 1u;
@@ -1323,7 +1456,7 @@ int vhx_update_ranges(vhx_ctx *c, const vhx_range *r, uint32_t n) {
     // context used then), so a growth or a stream change waits for it
     if (c->upd_stream && (c->upd_stream != c->stream || c->upd.bytes < P.bytes))
         VHX_HIP(c, hipStreamSynchronize(c->upd_stream));
-    int rc = ensure(c, c->upd, P.bytes);
+    rc = ensure(c, c->upd, P.bytes);
     if (rc) return rc;
     c->upd_stream = c->stream;
     // pack: the job table, then each range's data (16-byte aligned)
@@ -1398,10 +1531,13 @@ int vhx_update_ranges(vhx_ctx *c, const vhx_range *r, uint32_t n) {
         // emptiness of any cell may change: every bitmap and record
         if ((rc = rebuild_occ(c, 0, c->tree->desc.brick_count))) return rc;
         c->tree->child_rec_stale = true;
-        return refresh_child_rec(c);
+        rc = refresh_child_rec(c);
+    } else {
+        if (brick_lo < brick_hi && (rc = rebuild_occ(c, brick_lo, brick_hi - brick_lo))) return rc;
+        rc = refresh_child_rec_sel(c, node_lo, node_hi, brick_lo, brick_hi);
     }
-    if (brick_lo < brick_hi && (rc = rebuild_occ(c, brick_lo, brick_hi - brick_lo))) return rc;
-    return refresh_child_rec_sel(c, node_lo, node_hi, brick_lo, brick_hi);
+    if (rc) return rc;
+    return write_end(c);  // the next trace of every context of the tree waits for this write
 }
 
 int vhx_update_range(vhx_ctx *c, int id, uint64_t off, uint64_t count, const void *src) {
@@ -1424,6 +1560,8 @@ int vhx_read_derived(vhx_ctx *c, int which, uint64_t off, uint64_t count, void *
     const DevBuf &b = which == VHX_DERIVED_NODE_HDR ? c->tree->hdr : c->tree->brick_occ;
     VHX_HIP(c, hipSetDevice(c->device));
     VHX_STREAM(c);
+    int rc = trace_begin(c);  // after the tree's last write
+    if (rc) return rc;
     VHX_HIP(c, hipMemcpyAsync(dst, (const char *)b.ptr + off * es, count * es, hipMemcpyDeviceToHost, c->stream));
     VHX_HIP(c, hipStreamSynchronize(c->stream));
     return VHX_OK;
@@ -1484,8 +1622,10 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
                                                            : (uint64_t)my_tiles * T * T;
     VHX_HIP(c, hipSetDevice(c->device));
     VHX_STREAM(c);
+    int rc = trace_begin(c);  // after the tree's last write (an update through the owner, on its stream)
+    if (rc) return rc;
     HostOut ho;
-    int rc = map_out(c, out, nout, on_device, ho, layout == VHX_LAYOUT_TILES);
+    rc = map_out(c, out, nout, on_device, ho, layout == VHX_LAYOUT_TILES);
     if (rc) return rc;
     if ((rc = refresh_child_rec(c))) return rc;
     const DevTree t = dev_tree(c);
@@ -1566,6 +1706,7 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
     if (c->in_prepass) return VHX_OK;  // the outer call records the end and copies its outputs
     VHX_HIP(c, hipEventRecord(c->ev1, c->stream));
     c->timed = true;
+    if ((rc = trace_end(c))) return rc;  // a later write of the tree waits for this frame
     return finish_out(c, ho);
 }
 
@@ -1592,13 +1733,16 @@ int vhx_set_node_mips(vhx_ctx *c, const uint32_t *node_mips, uint32_t count) {
         if ((m & VHX_SOLID_BIT) ? (m & 0x7FFFFFFFu) >= d.solid_count : m >= d.brick_count)
             return fail(c, VHX_E_INVALID_ARG, "vhx_set_node_mips: descriptor out of range");
     }
-    int rc = ensure(c, c->tree->mips, (uint64_t)count * 4);
-    if (rc) return rc;
+    VHX_HIP(c, hipSetDevice(c->device));
     VHX_STREAM(c);
+    int rc = write_begin(c);  // frames in flight may still read the previous descriptors
+    if (!rc && c->tree->mips.bytes < (uint64_t)count * 4) VHX_HIP(c, hipStreamSynchronize(c->stream));  // regrowth
+    if (!rc) rc = ensure(c, c->tree->mips, (uint64_t)count * 4);
+    if (rc) return rc;
     VHX_HIP(c, hipMemcpyAsync(c->tree->mips.ptr, node_mips, (uint64_t)count * 4, hipMemcpyHostToDevice, c->stream));
     VHX_HIP(c, hipStreamSynchronize(c->stream));
     c->tree->mips_on = true;
-    return VHX_OK;
+    return write_end(c);
 }
 
 int vhx_trace_rays(vhx_ctx *c, const float *rays, uint64_t n, const vhx_hits *out, int on_device) {
@@ -1608,8 +1752,10 @@ int vhx_trace_rays(vhx_ctx *c, const float *rays, uint64_t n, const vhx_hits *ou
     if ((n + 255) / 256 > 0x7FFFFFFFull) return fail(c, VHX_E_INVALID_ARG, "too many rays");
     VHX_HIP(c, hipSetDevice(c->device));
     VHX_STREAM(c);
+    int rc = trace_begin(c);
+    if (rc) return rc;
     HostOut ho;
-    int rc = map_out(c, out, n, on_device, ho);
+    rc = map_out(c, out, n, on_device, ho);
     if (rc) return rc;
     const float *drays = rays;
     if (!on_device) {
@@ -1657,6 +1803,7 @@ int vhx_trace_rays(vhx_ctx *c, const float *rays, uint64_t n, const vhx_hits *ou
     VHX_HIP(c, hipGetLastError());
     VHX_HIP(c, hipEventRecord(c->ev1, c->stream));
     c->timed = true;
+    if ((rc = trace_end(c))) return rc;
     return finish_out(c, ho);
 }
 
@@ -1689,9 +1836,11 @@ int vhx_trace_shadows(vhx_ctx *c, const float light[3], uint64_t n, const uint32
     }
     VHX_HIP(c, hipSetDevice(c->device));
     VHX_STREAM(c);
+    int rc = trace_begin(c);
+    if (rc) return rc;
     uint32_t npass = 1;
     const uint64_t nb64 = (n + 255) / 256;
-    int rc = prepare_passes(c, n, nb64, npass, true);
+    rc = prepare_passes(c, n, nb64, npass, true);
     if (rc) return rc;
     if ((rc = refresh_child_rec(c))) return rc;
     const DevTree t = dev_tree(c);
@@ -1736,7 +1885,7 @@ int vhx_trace_shadows(vhx_ctx *c, const float light[3], uint64_t n, const uint32
     VHX_HIP(c, hipGetLastError());
     VHX_HIP(c, hipEventRecord(c->ev1, c->stream));
     c->timed = true;
-    return VHX_OK;
+    return trace_end(c);
 }
 
 int vhx_untile_frame(vhx_ctx *c, const void *gathered, uint32_t planes, uint32_t ranks, uint32_t tiles_per_rank,

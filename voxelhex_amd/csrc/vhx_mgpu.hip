@@ -132,18 +132,43 @@ static int mgpu_init(vhx_mgpu *m) {
     return VHX_OK;
 }
 
-// V slots, per = tiles per slot (the last slots may hold fewer; their parts are padded)
+// The tile plan (vhx_mgpu_tile_plan, exported for the host tests): V = R + N - 1 slots, slot s traces tiles s, s + V, ...
+// (per = tiles per slot; the last slots may hold fewer, their parts are padded); rank 0 owns slots 0..R-1, rank r >= 1
+// slot R + r - 1
+static vhx_tile_plan plan_of(uint32_t N, uint32_t R, uint32_t T, uint32_t W, uint32_t H, uint32_t rank) {
+    vhx_tile_plan p{};
+    p.tiles_x = (W + T - 1) / T;
+    p.tiles_y = (H + T - 1) / T;
+    p.tiles = p.tiles_x * p.tiles_y;
+    p.slots = R + N - 1u;
+    p.tiles_per_slot = (p.tiles + p.slots - 1) / p.slots;
+    p.first_slot = rank == 0 ? 0u : R + rank - 1u;
+    p.slot_count = rank == 0 ? R : 1u;
+    return p;
+}
 static uint32_t slots_of(const vhx_mgpu *m) { return m->R + (uint32_t)m->nranks - 1u; }
 static void tiles_of(const vhx_mgpu *m, uint32_t W, uint32_t H, uint32_t &ntiles, uint32_t &per_slot) {
-    const uint32_t tx = (W + m->T - 1) / m->T, ty = (H + m->T - 1) / m->T;
-    ntiles = tx * ty;
-    per_slot = (ntiles + slots_of(m) - 1) / slots_of(m);
+    const vhx_tile_plan p = plan_of((uint32_t)m->nranks, m->R, m->T, W, H, 0);
+    ntiles = p.tiles;
+    per_slot = p.tiles_per_slot;
 }
 // the slots of a rank: first and count
 static void rank_slots(const vhx_mgpu *m, int rank, uint32_t &first, uint32_t &count) {
-    first = rank == 0 ? 0u : m->R + (uint32_t)rank - 1u;
-    count = rank == 0 ? m->R : 1u;
+    const vhx_tile_plan p = plan_of((uint32_t)m->nranks, m->R, m->T, 1, 1, (uint32_t)rank);
+    first = p.first_slot;
+    count = p.slot_count;
 }
+
+// a failed RCCL call inside a group still closes the group, so this rank's later collectives are not swallowed by it
+#define VHX_NCCL_GROUP(m, call)                                                                                    \
+    do {                                                                                                           \
+        ncclResult_t r_ = (call);                                                                                  \
+        if (r_ != ncclSuccess) {                                                                                   \
+            rccl().GroupEnd();                                                                                     \
+            (m)->ctx->err = std::string(#call) + ": " + rccl().GetErrorString(r_);                                 \
+            return VHX_E_RCCL;                                                                                     \
+        }                                                                                                          \
+    } while (0)
 
 extern "C" {
 
@@ -280,6 +305,23 @@ int vhx_mgpu_info(const vhx_mgpu *m, uint32_t W, uint32_t H, int *nranks, int *r
     return VHX_OK;
 }
 
+// The raw tree buffers, device to device over xGMI from rank 0 (the root sends, the others receive in place), in
+// chunks of at most 1 GiB per call, one RCCL group: the fill step of receive_tree on ranks >= 1, and the send on rank 0
+static int broadcast_raw(void *arg, void *const dst[7], const uint64_t bytes[7]) {
+    vhx_mgpu *m = (vhx_mgpu *)arg;
+    vhx_ctx *c = m->ctx;
+    const Rccl &r = rccl();
+    VHX_NCCL(m, r.GroupStart());
+    for (int id = 0; id < 7; ++id)
+        for (uint64_t off = 0; off < bytes[id]; off += 1ull << 30) {
+            const uint64_t n = std::min<uint64_t>(1ull << 30, bytes[id] - off);
+            char *p = (char *)dst[id] + off;
+            VHX_NCCL_GROUP(m, r.Broadcast(p, p, n, ncclUint8, 0, m->comm, c->stream));
+        }
+    VHX_NCCL(m, r.GroupEnd());
+    return VHX_OK;
+}
+
 int vhx_mgpu_broadcast_tree(vhx_mgpu *m, const vhx_tree_desc *t) {
     if (!m) return VHX_E_INVALID_ARG;
     vhx_ctx *c = m->ctx;
@@ -287,53 +329,32 @@ int vhx_mgpu_broadcast_tree(vhx_mgpu *m, const vhx_tree_desc *t) {
     const Rccl &r = rccl();
     VHX_HIP(c, hipSetDevice(c->device));
     if (c->shared) return fail(c, VHX_E_STATE, "vhx_mgpu_broadcast_tree on a shared context");
+    // no frame of this renderer may still be in flight on the buffers about to be replaced (its gathers included)
+    int rc = vhx_mgpu_sync(m, nullptr);
+    if (rc) return rc;
     VHX_STREAM(c);
     if (m->rank == 0) {
-        int rc = vhx_upload_tree(c, t);  // host -> HBM of rank 0, derived layout included
+        rc = vhx_upload_tree(c, t);  // host -> HBM of rank 0, derived layout included
         if (rc) return rc;
     }
     // the counts first (8 u32), so the other ranks can size their buffers
-    int rc = ensure(c, m->hdr, 64);
-    if (rc) return rc;
+    if ((rc = ensure(c, m->hdr, 64))) return rc;
     uint32_t counts[8] = {0};
     if (m->rank == 0) {
-        const vhx_tree_desc &d = c->tree->desc;
-        const uint32_t v[8] = {d.boxtree_size, d.brick_dim, d.node_count, d.brick_count,
-                               d.solid_count, d.color_count, d.data_count, 0};
-        std::memcpy(counts, v, sizeof(v));
+        pack_counts(c->tree->desc, counts);
         VHX_HIP(c, hipMemcpyAsync(m->hdr.ptr, counts, sizeof(counts), hipMemcpyHostToDevice, c->stream));
     }
     VHX_NCCL(m, r.Broadcast(m->hdr.ptr, m->hdr.ptr, 8, ncclUint32, 0, m->comm, c->stream));
     VHX_HIP(c, hipMemcpyAsync(counts, m->hdr.ptr, sizeof(counts), hipMemcpyDeviceToHost, c->stream));
     VHX_HIP(c, hipStreamSynchronize(c->stream));
-    if (m->rank != 0) {
-        vhx_tree_desc d{};
-        d.boxtree_size = counts[0];
-        d.brick_dim = counts[1];
-        d.node_count = counts[2];
-        d.brick_count = counts[3];
-        d.solid_count = counts[4];
-        d.color_count = counts[5];
-        d.data_count = counts[6];
-        if ((rc = alloc_tree(c, &d))) return rc;
-    }
-    // the raw buffers, device to device over xGMI, in chunks of at most 1 GiB per call
-    VHX_NCCL(m, r.GroupStart());
+    if (m->rank != 0) return receive_tree(c, unpack_counts(counts), broadcast_raw, m);  // alloc, receive, derive
+    void *src[7];
+    uint64_t bytes[7];
     for (int id = 0; id < 7; ++id) {
-        const uint64_t bytes = elem_count(c->tree->desc, id) * elem_size(id);
-        for (uint64_t off = 0; off < bytes; off += 1ull << 30) {
-            const uint64_t n = std::min<uint64_t>(1ull << 30, bytes - off);
-            char *p = (char *)c->tree->raw[id].ptr + off;
-            const ncclResult_t e = r.Broadcast(p, p, n, ncclUint8, 0, m->comm, c->stream);
-            if (e != ncclSuccess) {
-                r.GroupEnd();
-                c->err = std::string("ncclBroadcast (tree): ") + r.GetErrorString(e);
-                return VHX_E_RCCL;
-            }
-        }
+        src[id] = c->tree->raw[id].ptr;
+        bytes[id] = elem_count(c->tree->desc, id) * elem_size(id);
     }
-    VHX_NCCL(m, r.GroupEnd());
-    if (m->rank != 0) return finish_upload(c);  // derived layout from the received buffers (synchronises)
+    if ((rc = broadcast_raw(m, src, bytes))) return rc;
     VHX_HIP(c, hipStreamSynchronize(c->stream));
     return VHX_OK;
 }
@@ -353,6 +374,7 @@ int vhx_mgpu_render(vhx_mgpu *m, const vhx_camera *cam, uint32_t *fb_rgba, float
     const uint64_t n_out = (uint64_t)per * m->T * m->T;  // words per plane of one slot's part
     const uint32_t slot = (uint32_t)(m->k % m->S);
     vhx_ctx *tc = m->k % m->F == 0 ? c : m->extra[m->k % m->F - 1];  // the context tracing this frame
+    if (tc != c) copy_sched(tc, c);  // the caller's settings (vhx_set_pass_budgets, ...) go to the owner context
     VHX_STREAM(tc);
     // a slot's buffers are rewritten only after the transfer that read them (stream order on the tracing stream)
     if (m->used[slot]) VHX_HIP(c, hipStreamWaitEvent(tc->stream, m->free_[slot], 0));
@@ -385,10 +407,10 @@ int vhx_mgpu_render(vhx_mgpu *m, const vhx_camera *cam, uint32_t *fb_rgba, float
             for (int q = 1; q < m->nranks; ++q) {
                 uint32_t qf, qc;
                 rank_slots(m, q, qf, qc);
-                VHX_NCCL(m, r.Recv(parts + 2 * n_out * qf, 2 * n_out, ncclUint32, q, m->comm, m->cstream));
+                VHX_NCCL_GROUP(m, r.Recv(parts + 2 * n_out * qf, 2 * n_out, ncclUint32, q, m->comm, m->cstream));
             }
         } else {
-            VHX_NCCL(m, r.Send(parts, 2 * n_out, ncclUint32, 0, m->comm, m->cstream));
+            VHX_NCCL_GROUP(m, r.Send(parts, 2 * n_out, ncclUint32, 0, m->comm, m->cstream));
         }
         VHX_NCCL(m, r.GroupEnd());
     }
@@ -414,19 +436,20 @@ int vhx_mgpu_set_root_slots(vhx_mgpu *m, uint32_t slots) {
     return VHX_OK;
 }
 
-int vhx_mgpu_balance(vhx_mgpu *m, const vhx_camera *cam, uint32_t frames, uint32_t *root_slots, float *trace_ms,
-                     float *transfer_ms) {
-    if (!m || !cam || frames == 0) return VHX_E_INVALID_ARG;
+// Renders frames + 1 frames of cam one at a time (no overlap) at the current split with the trace / transfer events on,
+// and returns this rank's medians of the last `frames` (device ms). Restores the overlap mode and frees its buffers on
+// every exit. Collective (every rank renders the same frames).
+static int measure_frames(vhx_mgpu *m, const vhx_camera *cam, uint32_t frames, float &trace_ms, float &xfer_ms) {
     vhx_ctx *c = m->ctx;
-    // measure with one slot per rank, frames one after the other (no overlap), the last frames' medians
-    int rc = vhx_mgpu_set_root_slots(m, 1);
-    if (rc) return rc;
     const bool overlap = m->overlap;
     m->overlap = false;
     m->timing = true;
     DevBuf fb, fbd;
-    if (m->rank == 0 && (rc = ensure(c, fb, (uint64_t)cam->width * cam->height * 4))) return rc;
-    if (m->rank == 0 && (rc = ensure(c, fbd, (uint64_t)cam->width * cam->height * 4))) return rc;
+    int rc = VHX_OK;
+    if (m->rank == 0) {
+        rc = ensure(c, fb, (uint64_t)cam->width * cam->height * 4);
+        if (!rc) rc = ensure(c, fbd, (uint64_t)cam->width * cam->height * 4);
+    }
     std::vector<float> tr, tx;
     for (uint32_t i = 0; i < frames + 1 && !rc; ++i) {
         rc = vhx_mgpu_render(m, cam, (uint32_t *)fb.ptr, (float *)fbd.ptr);
@@ -442,38 +465,76 @@ int vhx_mgpu_balance(vhx_mgpu *m, const vhx_camera *cam, uint32_t frames, uint32
     m->overlap = overlap;
     if (fb.ptr) (void)hipFree(fb.ptr);
     if (fbd.ptr) (void)hipFree(fbd.ptr);
-    if (rc) return rc;
-    // rank 0 picks R: with V = R + N - 1 slots a slot's trace and transfer scale by N / V, the frame period is bounded by
-    // rank 0's R slots and by the transfers into rank 0 (one slot part per link, concurrent), so it is about
-    // N / V * max(R * trace, transfer) with the one-slot figures; the other ranks' single slot never exceeds rank 0's R
-    uint32_t best = 1;
-    float a32 = 0.0f, g32 = 0.0f;
-    if (m->rank == 0 && !tr.empty()) {
+    trace_ms = xfer_ms = 0.0f;
+    if (!rc && !tr.empty()) {
         std::sort(tr.begin(), tr.end());
         std::sort(tx.begin(), tx.end());
-        const double a = tr[tr.size() / 2], g = tx[tx.size() / 2], N = (double)m->nranks;
+        trace_ms = tr[tr.size() / 2];
+        xfer_ms = tx[tx.size() / 2];
+    }
+    return rc;
+}
+
+int vhx_mgpu_measure(vhx_mgpu *m, const vhx_camera *cam, uint32_t frames, float *trace_ms, float *transfer_ms) {
+    if (!m || !cam || frames == 0) return VHX_E_INVALID_ARG;
+    if (!m->ctx->tree->uploaded) return fail(m->ctx, VHX_E_STATE, "vhx_mgpu_measure before the tree is uploaded");
+    float a = 0, g = 0;
+    const int rc = measure_frames(m, cam, frames, a, g);
+    if (rc) return rc;
+    if (trace_ms) *trace_ms = a;
+    if (transfer_ms) *transfer_ms = g;
+    return VHX_OK;
+}
+
+int vhx_mgpu_tile_plan(uint32_t nranks, uint32_t root_slots, uint32_t T, uint32_t W, uint32_t H, uint32_t rank,
+                       vhx_tile_plan *plan) {
+    if (!plan || nranks < 1 || rank >= nranks || root_slots < 1 || root_slots > VHX_MGPU_MAX_ROOT_SLOTS || T == 0 ||
+        T > 4096 || W == 0 || H == 0)
+        return VHX_E_INVALID_ARG;
+    const uint64_t tiles = (uint64_t)((W + T - 1) / T) * ((H + T - 1) / T);
+    if (tiles > 0xFFFFFFFFull) return VHX_E_INVALID_ARG;
+    *plan = plan_of(nranks, root_slots, T, W, H, rank);
+    return VHX_OK;
+}
+
+int vhx_mgpu_balance(vhx_mgpu *m, const vhx_camera *cam, uint32_t frames, uint32_t *root_slots, float *trace_ms,
+                     float *transfer_ms) {
+    if (!m || !cam || frames == 0) return VHX_E_INVALID_ARG;
+    vhx_ctx *c = m->ctx;
+    // measure with one slot per rank, frames one after the other (no overlap), the last frames' medians
+    int rc = vhx_mgpu_set_root_slots(m, 1);
+    if (rc) return rc;
+    float a = 0.0f, g = 0.0f;
+    const int mrc = measure_frames(m, cam, frames, a, g);
+    // rank 0 picks R: with V = R + N - 1 slots a slot's trace and transfer scale by N / V, the frame period is bounded by
+    // rank 0's R slots and by the transfers into rank 0 (one slot part per link, concurrent), so it is about
+    // N / V * max(R * trace, transfer) with the one-slot figures; the other ranks' single slot never exceeds rank 0's R.
+    // A rank whose measurement failed still joins the closing broadcast (rank 0 then sends R = 0: every rank fails)
+    uint32_t best = mrc ? 0u : 1u;
+    if (m->rank == 0 && !mrc) {
+        const double N = (double)m->nranks;
         double best_t = 0;
         for (uint32_t R = 1; R <= VHX_MGPU_MAX_ROOT_SLOTS; ++R) {
-            const double t = N / (R + N - 1.0) * std::max(R * a, g);
+            const double t = N / (R + N - 1.0) * std::max(R * (double)a, (double)g);
             if (R == 1 || t < best_t * 0.97) {  // a larger share must win by 3 %
                 best = R;
                 best_t = t;
             }
         }
-        a32 = (float)a;
-        g32 = (float)g;
     }
     // every rank takes rank 0's choice (and its two figures)
     if ((rc = ensure(c, m->hdr, 64))) return rc;
     VHX_STREAM(c);
     uint32_t msg[3] = {best, 0, 0};
-    std::memcpy(&msg[1], &a32, 4);
-    std::memcpy(&msg[2], &g32, 4);
+    std::memcpy(&msg[1], &a, 4);
+    std::memcpy(&msg[2], &g, 4);
     VHX_HIP(c, hipMemcpyAsync(m->hdr.ptr, msg, sizeof(msg), hipMemcpyHostToDevice, c->stream));
     VHX_NCCL(m, rccl().Broadcast(m->hdr.ptr, m->hdr.ptr, 3, ncclUint32, 0, m->comm, c->stream));
     VHX_HIP(c, hipMemcpyAsync(msg, m->hdr.ptr, sizeof(msg), hipMemcpyDeviceToHost, c->stream));
     VHX_HIP(c, hipStreamSynchronize(c->stream));
-    if (msg[0] < 1 || msg[0] > VHX_MGPU_MAX_ROOT_SLOTS) return fail(c, VHX_E_RCCL, "vhx_mgpu_balance: bad broadcast");
+    if (mrc) return mrc;
+    if (msg[0] < 1 || msg[0] > VHX_MGPU_MAX_ROOT_SLOTS)
+        return fail(c, VHX_E_RCCL, "vhx_mgpu_balance: rank 0 reported a failed measurement");
     if ((rc = vhx_mgpu_set_root_slots(m, msg[0]))) return rc;
     if (root_slots) *root_slots = msg[0];
     if (trace_ms) std::memcpy(trace_ms, &msg[1], 4);

@@ -32,6 +32,18 @@ def rank_rays(width, height, T, rank, world):
     return sum(w * h for _, _, w, h in (tile_rect(t, width, height, T) for t in rank_tiles(width, height, T, rank, world)))
 
 
+def tile_plan(nranks, root_slots, T, width, height, rank):
+    """vhx_mgpu_tile_plan (the C deal vhx_mgpu_render uses; pure, no device): dict with tiles_x, tiles_y, tiles, slots,
+    tiles_per_slot, first_slot, slot_count."""
+    import ctypes
+    from . import _native as N
+    p = N.TilePlan()
+    rc = N.lib().vhx_mgpu_tile_plan(nranks, root_slots, T, width, height, rank, ctypes.byref(p))
+    if rc != N.VHX_OK:
+        raise ValueError(f"vhx_mgpu_tile_plan({nranks}, {root_slots}, {T}, {width}, {height}, {rank}) = {rc}")
+    return {name: getattr(p, name) for name, _ in N.TilePlan._fields_ if name != "reserved"}
+
+
 def untile_numpy(gathered, ranks, per_rank, T, width, height):
     """Host restatement of k_untile_rgba: gathered = concatenation over ranks of per_rank*T*T pixels."""
     fb = np.zeros(width * height, gathered.dtype)
@@ -199,6 +211,15 @@ class MgpuRenderer:
         self._check(N.lib().vhx_mgpu_balance(self._h, ctypes.byref(cam), frames, ctypes.byref(r), ctypes.byref(a),
                                              ctypes.byref(g)))
         return r.value, a.value, g.value
+
+    def measure(self, cam, frames=4):
+        """Collective: this rank's median trace and transfer device times (ms) at the current split, frames rendered
+        one at a time (vhx_mgpu_measure)."""
+        import ctypes
+        from . import _native as N
+        a, g = ctypes.c_float(), ctypes.c_float()
+        self._check(N.lib().vhx_mgpu_measure(self._h, ctypes.byref(cam), frames, ctypes.byref(a), ctypes.byref(g)))
+        return a.value, g.value
 
     def rays(self, width, height):
         import ctypes
