@@ -507,6 +507,7 @@ def main():
                      shadowed=torch.zeros(n_out, dtype=torch.int32, device=dev))
         outs.append(o)
     out = outs[0]
+    torch.cuda.synchronize(dev)  # the zero fills run on torch's stream: complete before the context streams write
     pipe = None
     framebuffer = None
     if world > 1 and mg is None:

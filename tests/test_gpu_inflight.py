@@ -51,6 +51,7 @@ def test_eight_frames_in_flight_match_golden():
         dev = torch.device("cuda", 0)
         streams = [torch.cuda.ExternalStream(r.stream(), device=dev) for r in ctxs]  # each context's own stream
         outs = [_outs(W * H, dev) for _ in ctxs]
+        torch.cuda.synchronize()  # the zero fills (torch's stream) complete before the context streams write
         ref_b = owner.trace_primary(cam_b, fields=("rgba", "depth", "value"))  # one frame alone
         for rnd in range(2):
             # round 0: even contexts trace the golden camera, odd ones camera B; round 1 swaps them. Every context's

@@ -83,6 +83,7 @@ def test_ranged_writes_between_frames_in_flight(oracle):
         dev = torch.device("cuda", 0)
         before = [[_frame_out(W * H, dev) for _ in range(F)] for _ in edits]
         after = [[_frame_out(W * H, dev) for _ in range(F)] for _ in edits]
+        torch.cuda.synchronize()  # the zero fills (torch's stream) complete before the context streams write
         for v, e in enumerate(edits):
             for r, c, o in zip(ctxs, cams, before[v]):
                 r.trace_primary(c, out=o)
@@ -143,7 +144,9 @@ def test_streaming_with_eight_frames_in_flight(oracle):
         ctxs, streams = _contexts(owner)
         dev = torch.device("cuda", 0)
         rng = np.random.default_rng(3)
-        frames, snaps, cams, outs, resizes = 40, [], [], [], 0
+        frames, snaps, cams, resizes = 40, [], [], 0
+        outs = [_frame_out(W * H, dev) for _ in range(frames)]
+        torch.cuda.synchronize()  # the zero fills (torch's stream) complete before the context streams write
         for k in range(frames):
             if k in (12, 26):
                 _edit(t, rng, size)
@@ -156,9 +159,7 @@ def test_streaming_with_eight_frames_in_flight(oracle):
             snaps.append(_Snapshot(s.view()))
             cam = vhx.glass_camera(size, W, H, angle=40.0 + 0.03 * k, target=(S / 2,) * 3)
             cams.append(cam)
-            o = _frame_out(W * H, dev)
-            ctxs[k % F].trace_primary(cam, out=o)
-            outs.append(o)
+            ctxs[k % F].trace_primary(cam, out=outs[k])
         assert resizes >= 2
         torch.cuda.synchronize()
         changed = 0
