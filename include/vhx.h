@@ -234,6 +234,10 @@ int vhx_set_depth_prepass(vhx_ctx *ctx, int enable, float margin);
  * it goes through the owner of a shared tree and is ordered against frames in flight (vhx_create_shared); shared
  * contexts trace with them. */
 int vhx_set_node_mips(vhx_ctx *ctx, const uint32_t *node_mips, uint32_t count);
+/* Diagnostics of a VHX_PROF build (scripts/probes/probe_blocks.py; a regular build returns VHX_E_STATE): per pass
+ * (4) and traversal block (16), the wave executions and the lanes active in them, as out[2 * (pass * 16 + block)] and
+ * out[2 * (pass * 16 + block) + 1], accumulated over every trace since the last reset. */
+int vhx_profile_counters(vhx_ctx *ctx, uint64_t *out, uint32_t n, int reset);
 /* Traces n explicit rays; rays = 6 f32 per ray (origin xyz, direction xyz), host or device per on_device. */
 int vhx_trace_rays(vhx_ctx *ctx, const float *rays, uint64_t n, const vhx_hits *out, int on_device);
 /* Hard shadows (BASELINE config 5; the reference has no shadow rays — semantics defined in DESIGN.md §9): for

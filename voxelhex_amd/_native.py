@@ -103,6 +103,7 @@ SIGNATURES = [
     ("vhx_read_derived", c_int, [c_void_p, c_int, c_u64, c_u64, c_void_p]),
     ("vhx_tree_device_bytes", c_int, [c_void_p, P(c_u64)]),
     ("vhx_trace_primary", c_int, [c_void_p, P(Camera), c_u32, c_u32, c_u32, c_u32, P(Hits), c_int]),
+    ("vhx_profile_counters", c_int, [c_void_p, P(c_u64), c_u32, c_int]),
     ("vhx_trace_rays", c_int, [c_void_p, c_void_p, c_u64, P(Hits), c_int]),
     ("vhx_trace_shadows", c_int, [c_void_p, P(c_f32), c_u64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                   c_void_p]),

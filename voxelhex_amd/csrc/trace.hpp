@@ -29,6 +29,31 @@ namespace vhx {
 
 #define VHX_MAX_ITERS (1u << 22)  // same bound as the oracle (iteration bound)
 
+// VHX_PROF (diagnostic builds only, scripts/probes/probe_blocks.py): per pass and per block of the traversal, the number
+// of wave executions and the lanes active in them (wave ballot), accumulated in g_prof and read by
+// vhx_profile_counters. The pass is told apart by its budget (pass_of_budget); 16 blocks per pass.
+#ifndef VHX_PROF
+#define VHX_PROF 0
+#endif
+#if VHX_PROF
+__device__ unsigned long long g_prof[4 * 16 * 2];
+#define VHX_PROF_BLOCK(pass, id)                                                                                  \
+    do {                                                                                                          \
+        const uint64_t m_ = __ballot(1);                                                                          \
+        if ((threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(m_)) {                                               \
+            atomicAdd(&vhx::g_prof[((pass) * 16u + (id)) * 2u], 1ull);                                            \
+            atomicAdd(&vhx::g_prof[((pass) * 16u + (id)) * 2u + 1u], (unsigned long long)__popcll(m_));           \
+        }                                                                                                         \
+    } while (0)
+#else
+#define VHX_PROF_BLOCK(pass, id) \
+    do {                         \
+    } while (0)
+#endif
+__device__ __forceinline__ uint32_t pass_of_budget(uint32_t b) {
+    return b >= VHX_MAX_ITERS ? 3u : (b <= 24u ? 0u : (b <= 96u ? 1u : 2u));
+}
+
 struct DevTree {
     const uint4 *hdr;          // {occ_lo, occ_hi, type, 0} per node
     const uint32_t *children;  // 64 per node
@@ -245,7 +270,7 @@ __device__ __forceinline__ void fill_hit(HitOut &h, uint32_t v, uint32_t cell, F
 // traversal loop (finish_hit), so the loop carries two registers for it instead of a dozen.
 template <bool COUNT, int BD>
 __device__ __forceinline__ bool probe_brick(const DevTree &t, const RayD &r, F3d &p, uint32_t desc, uint64_t cocc,
-                                            CubeD bb, HitOut &h, uint32_t &iters, int32_t &hflat) {
+                                            CubeD bb, HitOut &h, uint32_t &iters, int32_t &hflat, uint32_t pp = 0) {
     // one branch (a Parted brick's walk); Empty and Solid (cpu.rs:249-260) resolve by selects. VHX_EMPTY has the
     // Solid bit set, so "Parted" is simply the bit clear.
     const bool solid = (desc & VHX_SOLID_BIT) != 0u && desc != VHX_EMPTY;
@@ -253,6 +278,7 @@ __device__ __forceinline__ bool probe_brick(const DevTree &t, const RayD &r, F3d
     bool hit = solid;
     int32_t flat = -1;  // hflat of a Solid brick
     if ((desc & VHX_SOLID_BIT) == 0u) {
+        VHX_PROF_BLOCK(pp, 8);
         using B = Brick<BD>;
         // (p - min) * dim / size: both scalings are by powers of two, so one multiply by dim/size is the same value
         const F3d pib = vmul(vsub(p, bb.min), (float)BD * rcp_pow2(bb.size));
@@ -269,6 +295,7 @@ __device__ __forceinline__ bool probe_brick(const DevTree &t, const RayD &r, F3d
         hit = ((word >> (flat & 63)) & 1ull) != 0ull;
         if (COUNT) h.bytes += 4 + pal_bytes<COUNT>(vox[flat]);  // the reference reads the palettes of every cell
         if (!hit) {
+            VHX_PROF_BLOCK(pp, 9);
             // Cell walk in exit-plane form. The reference's st_k = unit * max(sg_k, 0) - sg_k * (p_k - cmin_k): the
             // difference p_k - cmin_k is exact (cmin_k is a multiple of unit and p_k lies within a unit of it, so
             // Sterbenz applies, or cmin_k = 0), hence for sg_k = +1 st_k = unit - (p_k - cmin_k) and
@@ -291,6 +318,7 @@ __device__ __forceinline__ bool probe_brick(const DevTree &t, const RayD &r, F3d
             const uint32_t F = fx + fy * BD + fz * (BD * BD);
             uint32_t jx = (uint32_t)ix ^ fx, jy = (uint32_t)iy ^ fy, jz = (uint32_t)iz ^ fz;
             for (;;) {
+                VHX_PROF_BLOCK(pp, 2);
                 ++iters;
                 // dda_step_to_next_sibling (cpu.rs:104-132) on the cell {cmin, unit}
                 const F2 sxy = (exy - pxy) * sfxy;
@@ -526,12 +554,14 @@ struct Trav {
         const uint32_t ntype = lh.z;
         if (COUNT) h.bytes += 12;
         const bool uniform = ntype == VHX_NODE_UNIFORM_LEAF;
+        const uint32_t pp = VHX_PROF ? pass_of_budget(budget) : 0u;
         if (target < 64u && (uniform || ntype == VHX_NODE_LEAF)) {
+            VHX_PROF_BLOCK(pp, 1);
             if (COUNT) h.bytes += 4;
             hdesc = Brick<BD>::WORDS == 1 || !uniform ? slot : t.children[(uint64_t)node * 64u];
             CubeD bb = uniform ? cur : tb;
             if (!uniform && tbok == 0u) bb = child_bounds(cur, target);
-            ex = probe_brick<COUNT, BD>(t, r, p, hdesc, cocc, bb, h, iters, hflat) ? 1u : 0u;
+            ex = probe_brick<COUNT, BD>(t, r, p, hdesc, cocc, bb, h, iters, hflat, pp) ? 1u : 0u;
         }
         // MIP stand-in (viewport_render.wgsl:438-454, probe_MIP 328-364): the target sectant is occupied but its child
         // entry is absent (a view that does not hold it). The node's MIP brick is traced over the node's cube from a
@@ -566,6 +596,7 @@ struct Trav {
             const bool pop = uniform || target >= 64u || occ == 0 || (occ & omask) == 0;
             const bool push = !pop && !mip_adv && ntype == VHX_NODE_INTERNAL && ((occ >> target) & 1ull) != 0;
             if (pop) {
+                VHX_PROF_BLOCK(pp, 3);
                 // POP (cpu.rs:368-393). Its step to the next sibling (dda_step_to_next_sibling on the popped cube,
                 // step_sectant, target_bounds += step * size) is one trip of the walk below, which the lanes that
                 // advance run anyway: one copy of the DDA code per iteration instead of two.
@@ -590,6 +621,7 @@ struct Trav {
                 }
             }
             if (push) {
+                VHX_PROF_BLOCK(pp, 4);
                 // PUSH (cpu.rs:401-411)
                 if (COUNT) h.bytes += 4;
                 s3 = s2;
@@ -604,6 +636,7 @@ struct Trav {
                 ex = slot >= t.node_count ? 2u : 0u;  // the reference would panic on an invalid key: a miss here
             }
             if (!push) {
+                VHX_PROF_BLOCK(pp, 5);
                 // ADVANCE (cpu.rs:416-437), or POP's single step: at most 9 steps across the node, the pass budget
                 // is checked after it. Same form as the brick walk (exit planes, direction-normalised sectant
                 // coordinates); the exit-plane difference equals the reference's dda_step_to_next_sibling for a point
@@ -624,6 +657,7 @@ struct Trav {
                 F2 pxy = mk2(p.x, p.y);
                 float pz = p.z;
                 for (;;) {
+                    VHX_PROF_BLOCK(pp, 6);
                     ++iters;
                     const F2 sxy = (exy - pxy) * sfxy;
                     const float dx = __builtin_fabsf(sxy.x), dy = __builtin_fabsf(sxy.y),
@@ -651,6 +685,7 @@ struct Trav {
                     iters -= 1u;  // POP's step is not one of the walk's steps
                     tbok = 1u;
                     if (count == 0) {
+                        VHX_PROF_BLOCK(pp, 7);
                         // the stack ran empty: restart from the root (cpu.rs:441-455); target_bounds stays stale
                         p = vadd(p, vmul(r.d, 0.1f));
                         if (p.x < tsize && p.y < tsize && p.z < tsize && p.x > 0.0f && p.y > 0.0f && p.z > 0.0f) {
@@ -693,8 +728,11 @@ __device__ __forceinline__ bool get_by_ray(const DevTree &t, const uint64_t *occ
                                            uint32_t budget, uint4 *sbase = nullptr, uint32_t sidx = 0,
                                            bool resume = false, float start = 0.0f, uint32_t sparse = 0) {
     Trav<COUNT, BD, MIP> tr;
+    VHX_PROF_BLOCK(pass_of_budget(budget), 10);
     if (!tr.template begin<START>(t, o, d, h, sbase, sidx, resume, start)) return true;
+    VHX_PROF_BLOCK(pass_of_budget(budget), 11);
     for (;;) {
+        VHX_PROF_BLOCK(pass_of_budget(budget), 0);
         tr.step(t, occ_tab, h, budget);
         if (tr.ex != 0u) break;
         if (sparse && (uint32_t)__popcll(__ballot(1)) < sparse) {
@@ -702,6 +740,7 @@ __device__ __forceinline__ bool get_by_ray(const DevTree &t, const uint64_t *occ
             break;
         }
     }
+    VHX_PROF_BLOCK(pass_of_budget(budget), 12);
     return tr.end(t, h, sbase, sidx);
 }
 

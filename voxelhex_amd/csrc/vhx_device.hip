@@ -1710,6 +1710,25 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
     return finish_out(c, ho);
 }
 
+int vhx_profile_counters(vhx_ctx *c, uint64_t *out, uint32_t n, int reset) {
+    if (!c || (n && !out)) return VHX_E_INVALID_ARG;
+#if VHX_PROF
+    uint64_t v[4 * 16 * 2];
+    VHX_HIP(c, hipSetDevice(c->device));
+    VHX_HIP(c, hipDeviceSynchronize());
+    VHX_HIP(c, hipMemcpyFromSymbol(v, HIP_SYMBOL(vhx::g_prof), sizeof(v)));
+    for (uint32_t i = 0; i < n && i < 4 * 16 * 2; ++i) out[i] = v[i];
+    if (reset) {
+        std::memset(v, 0, sizeof(v));
+        VHX_HIP(c, hipMemcpyToSymbol(HIP_SYMBOL(vhx::g_prof), v, sizeof(v)));
+    }
+    return VHX_OK;
+#else
+    (void)reset;
+    return fail(c, VHX_E_STATE, "vhx_profile_counters: libvhx was built without VHX_PROF");
+#endif
+}
+
 int vhx_set_depth_prepass(vhx_ctx *c, int enable, float margin) {
     if (!c || !(margin >= 0.0f)) return VHX_E_INVALID_ARG;
     c->prepass = enable != 0;
