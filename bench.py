@@ -492,10 +492,11 @@ def main():
             r = rt.shared()
             rts.append(r)
             streams.append(torch.cuda.ExternalStream(r.stream(), device=dev))
-        budgets = args.budgets if args.budgets is not None else ("" if args.mip_lod is not None else None)
-        if budgets is not None:
-            for r in rts:
-                r.set_pass_budgets(tuple(int(b) for b in budgets.split(",") if b.strip()))
+    # the pass schedule of every context (vhx_mgpu re-copies the owner context's settings to its frames' contexts)
+    budgets = args.budgets if args.budgets is not None else ("" if args.mip_lod is not None else None)
+    if budgets is not None:
+        for r in rts:
+            r.set_pass_budgets(tuple(int(b) for b in budgets.split(",") if b.strip()))
     for _ in range(len(rts)):
         o = {"rgba": torch.zeros(n_out, dtype=torch.int32, device=dev),
              "depth": torch.zeros(n_out, dtype=torch.float32, device=dev)}
@@ -639,6 +640,18 @@ def main():
         total_rays += n_shadow
     mrays = total_rays * args.steps / elapsed / 1e6
     ms_per_step = elapsed * 1e3 / args.steps
+
+    # ---- multi-GPU per-rank figures (untimed, after the timed region): every rank's trace and transfer device time
+    # at the split that was timed, frames one at a time (vhx_mgpu_measure), to test DESIGN.md §7's model ---------------
+    if mg is not None:
+        tr_ms, tx_ms = mg.measure(cam, frames=4)
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, {"rank": rank, "trace_ms": round(tr_ms, 4), "transfer_ms": round(tx_ms, 4),
+                                          "rays": int(mg.rays(W, H))})
+        if split is not None:
+            split["per_rank"] = per_rank
+            split["per_rank_basis"] = ("vhx_mgpu_measure at the timed split, 4 frames one at a time (median): trace = "
+                                       "the rank's tile slots, transfer = rank 0 its receives / ranks >= 1 their send")
 
     # ---- multi-GPU check (untimed): the gathered, untiled frame equals rank 0 tracing the whole frame alone -------
     mgpu = None

@@ -1,0 +1,388 @@
+/* Wave-level simulation of the traversal kernels' SIMT schedule (diagnostics for DESIGN.md §3 / §12; not product code).
+ *
+ * Per-ray event sequences come from the oracle (vhx_oracle_ray_events: N node iteration, P probe, B brick cell step,
+ * O pop, U push, A advance step, R restart) and are cut into node iterations. The simulator replays the multi-pass
+ * schedule of libvhx (pass 0 over 8x8-pixel waves with a step budget and sparse-wave abandonment, queue passes over
+ * 64 consecutive rays in frame order, budgets counted like Trav: node iterations + brick steps + advance steps) and,
+ * per wave iteration, counts the wave executions and active lanes of every block of Trav::step, the block structure of
+ * the kernel. `design` selects alternative loop structures:
+ *   0  current: per iteration top, probe, brick walk loop (max brick steps), pop / push / walk setup, advance loop
+ *   1  capped brick walks: at most `cap` brick trips per iteration; a lane whose walk is unfinished carries it into
+ *      the next iteration (it skips the node blocks there)
+ * Output: per pass and block, waves and lanes (same blocks as the VHX_PROF kernel build), so that design 0 can be
+ * checked against the GPU counts of scripts/probes/probe_blocks.py.
+ *
+ * Build: gcc -O2 -fopenmp -shared -fPIC scripts/sim/wavesim.c -o scripts/sim/_build/libwavesim.so
+ * Driver: scripts/sim/wavesim.py */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../include/vhx.h"
+
+int64_t vhx_oracle_ray_events(const vhx_tree_desc *t, const vhx_camera *cam, const uint32_t *px, const uint32_t *py,
+                              uint64_t n, uint8_t *buf, uint64_t cap, uint64_t *off);
+
+#define VHX_MAX_ITERS_SIM (1u << 22)
+
+typedef struct {
+    uint8_t probe, nb, pop, push, na, restart;
+} it_t;
+
+static it_t *g_its;
+static uint64_t *g_off; /* per pixel: first iteration; g_off[n] = total */
+static uint32_t g_W, g_H;
+
+/* events of every pixel, cut into iterations (rows in parallel) */
+int64_t wavesim_build(const vhx_tree_desc *t, const vhx_camera *cam, uint32_t W, uint32_t H) {
+    const uint64_t n = (uint64_t)W * H;
+    free(g_its);
+    free(g_off);
+    g_W = W;
+    g_H = H;
+    g_off = (uint64_t *)calloc(n + 1, sizeof(uint64_t));
+    it_t **rows = (it_t **)calloc(H, sizeof(it_t *));
+    uint64_t *row_n = (uint64_t *)calloc(H, sizeof(uint64_t));
+    int bad = 0;
+#pragma omp parallel for schedule(dynamic, 4)
+    for (uint32_t y = 0; y < H; ++y) {
+        uint32_t *px = (uint32_t *)malloc(W * 4), *py = (uint32_t *)malloc(W * 4);
+        for (uint32_t x = 0; x < W; ++x) px[x] = x, py[x] = y;
+        uint64_t cap = (uint64_t)W * 64;
+        uint8_t *buf = NULL;
+        uint64_t *off = (uint64_t *)malloc((W + 1) * 8);
+        int64_t used;
+        for (;;) {
+            buf = (uint8_t *)realloc(buf, cap);
+            used = vhx_oracle_ray_events(t, cam, px, py, W, buf, cap, off);
+            if (used >= 0) break;
+            cap *= 4;
+        }
+        /* count iterations */
+        uint64_t nit = 0;
+        for (int64_t i = 0; i < used; ++i) nit += buf[i] == 'N';
+        it_t *its = (it_t *)calloc(nit ? nit : 1, sizeof(it_t));
+        uint64_t k = 0;
+        for (uint32_t x = 0; x < W; ++x) {
+            uint64_t cnt = 0;
+            it_t *cur = NULL;
+            for (uint64_t i = off[x]; i < off[x + 1]; ++i) {
+                const uint8_t ch = buf[i];
+                if (ch == 'N') {
+                    cur = &its[k++];
+                    ++cnt;
+                } else if (cur) {
+                    switch (ch) {
+                        case 'P': cur->probe = 1; break;
+                        case 'B': cur->nb = (uint8_t)(cur->nb < 255 ? cur->nb + 1 : 255); break;
+                        case 'O': cur->pop = 1; break;
+                        case 'U': cur->push = 1; break;
+                        case 'A': cur->na = (uint8_t)(cur->na < 255 ? cur->na + 1 : 255); break;
+                        case 'R': cur->restart = 1; break;
+                    }
+                }
+            }
+            g_off[(uint64_t)y * W + x] = cnt;  /* count for now */
+        }
+        if (k != nit) bad = 1;
+        rows[y] = its;
+        row_n[y] = nit;
+        free(px), free(py), free(buf), free(off);
+    }
+    if (bad) return -1;
+    uint64_t total = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint64_t c = g_off[i];
+        g_off[i] = total;
+        total += c;
+    }
+    g_off[n] = total;
+    g_its = (it_t *)malloc(total * sizeof(it_t) + 1);
+    uint64_t at = 0;
+    for (uint32_t y = 0; y < H; ++y) {
+        memcpy(g_its + at, rows[y], row_n[y] * sizeof(it_t));
+        at += row_n[y];
+        free(rows[y]);
+    }
+    free(rows), free(row_n);
+    return (int64_t)total;
+}
+
+/* blocks (as the VHX_PROF build): 0 iteration, 1 leaf target (probe), 2 brick trip, 3 pop, 4 push, 5 walk setup,
+ * 6 advance trip, 7 restart, 13 iteration-end bookkeeping, 14 carried walk (design 1) */
+#define NB 16
+typedef struct {
+    uint64_t waves[4][NB], lanes[4][NB];
+    uint64_t rays_in[4], waves_pass[4];
+} stats_t;
+
+typedef struct {
+    uint32_t budgets[4]; /* budget of pass p (p < npass - 1); the last pass is unbounded */
+    uint32_t npass;
+    uint32_t sparse0;    /* pass-0 sparse-wave threshold */
+    uint32_t design, cap;
+} cfg_t;
+
+typedef struct {
+    uint32_t ray;  /* pixel index */
+    uint32_t cur;  /* next iteration index */
+    uint32_t iters;
+    uint32_t carry; /* design 1: brick steps still to walk of the current iteration */
+} lane_t;
+
+static void add(stats_t *s, int p, int b, uint32_t lanes) {
+    s->waves[p][b] += 1;
+    s->lanes[p][b] += lanes;
+}
+
+/* one wave of a pass; abandoned rays are appended to `out` (in lane order) */
+static void sim_wave(const cfg_t *c, int p, lane_t *L, int n, uint32_t budget, uint32_t sparse, stats_t *s,
+                     lane_t *out, uint64_t *nout) {
+    int done[64] = {0};
+    for (;;) {
+        int act[64], na = 0;
+        for (int i = 0; i < n; ++i)
+            if (!done[i]) act[na++] = i;
+        if (!na) break;
+        add(s, p, 13, na);  /* a trip of the wave's loop */
+        /* this iteration's records */
+        const it_t *r[64];
+        uint32_t mb = 0, ma = 0, npr = 0, npop = 0, npush = 0, nws = 0, nres = 0, nb_now[64];
+        int fresh[64];
+        for (int a = 0; a < na; ++a) {
+            lane_t *l = &L[act[a]];
+            r[a] = &g_its[g_off[l->ray] + l->cur];
+            fresh[a] = l->carry == 0;
+            uint32_t nbw = fresh[a] ? r[a]->nb : l->carry;
+            if (c->design == 1 && nbw > c->cap) nbw = c->cap;
+            nb_now[a] = nbw;
+            if (nbw > mb) mb = nbw;
+        }
+        /* node iteration top (loads, decode): fresh lanes; probe block: fresh lanes with a probe */
+        uint32_t nfresh = 0;
+        for (int a = 0; a < na; ++a) nfresh += fresh[a];
+        if (nfresh) add(s, p, 0, nfresh);
+        for (int a = 0; a < na; ++a) npr += fresh[a] && r[a]->probe;
+        if (npr) add(s, p, 1, npr);
+        for (uint32_t t = 0; t < mb; ++t) {
+            uint32_t k = 0;
+            for (int a = 0; a < na; ++a) k += nb_now[a] > t;
+            add(s, p, 2, k);
+        }
+        /* lanes that finish their brick walk this iteration go on with the rest of the iteration */
+        int cont[64];
+        for (int a = 0; a < na; ++a) {
+            lane_t *l = &L[act[a]];
+            const uint32_t left = (fresh[a] ? r[a]->nb : l->carry) - nb_now[a];
+            cont[a] = left == 0;
+            l->carry = left;
+        }
+        for (int a = 0; a < na; ++a) {
+            if (!cont[a]) continue;
+            npop += r[a]->pop;
+            npush += r[a]->push;
+            const uint32_t w = r[a]->pop ? 1u : r[a]->na;
+            if (r[a]->pop || r[a]->na) ++nws;
+            if (w > ma) ma = w;
+            nres += r[a]->restart;
+        }
+        if (npop) add(s, p, 3, npop);
+        if (npush) add(s, p, 4, npush);
+        if (nws) add(s, p, 5, nws);
+        for (uint32_t t = 0; t < ma; ++t) {
+            uint32_t k = 0;
+            for (int a = 0; a < na; ++a) k += cont[a] && (r[a]->pop ? 1u : r[a]->na) > t;
+            add(s, p, 6, k);
+        }
+        if (nres) add(s, p, 7, nres);
+        /* end of iteration: finished, abandoned at the budget, or on */
+        uint32_t still = 0;
+        for (int a = 0; a < na; ++a) {
+            lane_t *l = &L[act[a]];
+            if (!cont[a]) {  /* carried walk: the budget is checked when the iteration completes */
+                l->iters += nb_now[a];
+                ++still;
+                continue;
+            }
+            l->iters += nb_now[a] + r[a]->na;
+            l->cur += 1;
+            const uint32_t nit = (uint32_t)(g_off[l->ray + 1] - g_off[l->ray]);
+            if (l->cur >= nit) {
+                done[act[a]] = 1;
+                continue;
+            }
+            l->iters += 1;  /* the next node iteration */
+            if (l->iters > budget) {
+                done[act[a]] = 1;
+                out[(*nout)++] = *l;
+                continue;
+            }
+            ++still;
+        }
+        if (sparse && still && still < sparse) {
+            for (int i = 0; i < n; ++i)
+                if (!done[i]) {
+                    done[i] = 1;
+                    out[(*nout)++] = L[i];
+                }
+        }
+    }
+}
+
+/* design 2 (vote-aligned phases): a lane is at PRE (next: top + probe setup of iteration cur), WALK (brick steps
+ * pending) or POST (the rest of iteration cur: pop / push / walk setup / advance / end). A wave trip runs an N-phase
+ * (POST lanes do their post and go on with the next iteration's pre; PRE lanes do their pre) and/or a W-phase (WALK
+ * lanes walk to the end of their bricks), each only when enough lanes need it (kn, kw) or nothing else is pending. */
+enum { ST_PRE = 0, ST_WALK = 1, ST_POST = 2 };
+static void sim_wave2(const cfg_t *c, int p, lane_t *L, int n, uint32_t budget, uint32_t sparse, stats_t *s,
+                      lane_t *out, uint64_t *nout) {
+    int done[64] = {0}, st[64];
+    for (int i = 0; i < n; ++i) st[i] = ST_PRE;
+    const uint32_t kn = c->cap & 0xFF, kw = c->cap >> 8;
+    for (;;) {
+        uint32_t nN = 0, nW = 0, nact = 0;
+        for (int i = 0; i < n; ++i)
+            if (!done[i]) {
+                ++nact;
+                if (st[i] == ST_WALK) ++nW; else ++nN;
+            }
+        if (!nact) break;
+        add(s, p, 13, nact);
+        int doN = nN && (nN >= kn || nW == 0), doW = nW && (nW >= kw || nN == 0);
+        if (!doN && !doW) doN = doW = 1;
+        if (doN) {
+            /* post stage */
+            uint32_t npost = 0, npop = 0, npush = 0, nws = 0, nres = 0, ma = 0;
+            for (int i = 0; i < n; ++i) {
+                if (done[i] || st[i] != ST_POST) continue;
+                const it_t *r = &g_its[g_off[L[i].ray] + L[i].cur];
+                ++npost;
+                npop += r->pop, npush += r->push, nres += r->restart;
+                const uint32_t w = r->pop ? 1u : r->na;
+                if (r->pop || r->na) ++nws;
+                if (w > ma) ma = w;
+            }
+            if (npost) add(s, p, 8, npost);
+            if (npop) add(s, p, 3, npop);
+            if (npush) add(s, p, 4, npush);
+            if (nws) add(s, p, 5, nws);
+            for (uint32_t t = 0; t < ma; ++t) {
+                uint32_t k = 0;
+                for (int i = 0; i < n; ++i) {
+                    if (done[i] || st[i] != ST_POST) continue;
+                    const it_t *r = &g_its[g_off[L[i].ray] + L[i].cur];
+                    k += (r->pop ? 1u : r->na) > t;
+                }
+                add(s, p, 6, k);
+            }
+            if (nres) add(s, p, 7, nres);
+            /* end of iteration for the POST lanes: done, abandoned, or on to the next iteration's pre */
+            uint32_t still = 0;
+            for (int i = 0; i < n; ++i) {
+                if (done[i] || st[i] != ST_POST) continue;
+                const it_t *r = &g_its[g_off[L[i].ray] + L[i].cur];
+                L[i].iters += r->nb + r->na;
+                L[i].cur += 1;
+                const uint32_t nit = (uint32_t)(g_off[L[i].ray + 1] - g_off[L[i].ray]);
+                if (L[i].cur >= nit) { done[i] = 1; continue; }
+                L[i].iters += 1;
+                if (L[i].iters > budget) { done[i] = 1; out[(*nout)++] = L[i]; continue; }
+                st[i] = ST_PRE;
+                ++still;
+            }
+            (void)still;
+            /* pre stage */
+            uint32_t npre = 0, npr = 0;
+            for (int i = 0; i < n; ++i) {
+                if (done[i] || st[i] != ST_PRE) continue;
+                const it_t *r = &g_its[g_off[L[i].ray] + L[i].cur];
+                ++npre;
+                npr += r->probe;
+                if (r->nb) { st[i] = ST_WALK; L[i].carry = r->nb; }
+                else if (r->probe && (uint32_t)(g_off[L[i].ray + 1] - g_off[L[i].ray]) == L[i].cur + 1 && !r->pop &&
+                         !r->na && !r->push) { done[i] = 1; }  /* hit at the entry cell: the ray ends */
+                else st[i] = ST_POST;
+            }
+            if (npre) add(s, p, 0, npre);
+            if (npr) add(s, p, 1, npr);
+        }
+        if (doW) {
+            uint32_t mb = 0;
+            for (int i = 0; i < n; ++i)
+                if (!done[i] && st[i] == ST_WALK && L[i].carry > mb) mb = L[i].carry;
+            for (uint32_t t = 0; t < mb; ++t) {
+                uint32_t k = 0;
+                for (int i = 0; i < n; ++i) k += !done[i] && st[i] == ST_WALK && L[i].carry > t;
+                add(s, p, 2, k);
+            }
+            for (int i = 0; i < n; ++i) {
+                if (done[i] || st[i] != ST_WALK) continue;
+                L[i].carry = 0;
+                const it_t *r = &g_its[g_off[L[i].ray] + L[i].cur];
+                const uint32_t nit = (uint32_t)(g_off[L[i].ray + 1] - g_off[L[i].ray]);
+                /* a walk that ends the ray (hit) with nothing after it in the iteration */
+                if (L[i].cur + 1 == nit && !r->pop && !r->na && !r->push && !r->restart) { done[i] = 1; continue; }
+                st[i] = ST_POST;
+            }
+        }
+        if (sparse) {
+            uint32_t left = 0;
+            for (int i = 0; i < n; ++i) left += !done[i];
+            if (left && left < sparse)
+                for (int i = 0; i < n; ++i)
+                    if (!done[i]) { done[i] = 1; out[(*nout)++] = L[i]; }
+        }
+    }
+}
+
+static int cmp_ray(const void *a, const void *b) {
+    const uint32_t x = ((const lane_t *)a)->ray, y = ((const lane_t *)b)->ray;
+    return x < y ? -1 : x > y;
+}
+
+int wavesim_run(const cfg_t *c, stats_t *s) {
+    memset(s, 0, sizeof(*s));
+    const uint32_t W = g_W, H = g_H;
+    const uint64_t n = (uint64_t)W * H;
+    lane_t *q = (lane_t *)malloc(n * sizeof(lane_t)), *q2 = (lane_t *)malloc(n * sizeof(lane_t));
+    uint64_t nq = 0;
+    /* pass 0: 8x8-pixel waves (four per 16x16 workgroup, blocks in raster order) */
+    const uint32_t bx = (W + 15) / 16, by = (H + 15) / 16;
+    const uint32_t b0 = c->npass > 1 ? c->budgets[0] : VHX_MAX_ITERS_SIM;
+    for (uint32_t b = 0; b < bx * by; ++b)
+        for (uint32_t w = 0; w < 4; ++w) {
+            lane_t L[64];
+            int nl = 0;
+            for (uint32_t k = 0; k < 64; ++k) {
+                const uint32_t x = (b % bx) * 16 + (w & 1) * 8 + (k & 7), y = (b / bx) * 16 + (w >> 1) * 8 + (k >> 3);
+                if (x >= W || y >= H) continue;
+                const uint32_t ray = y * W + x;
+                s->rays_in[0] += 1;
+                if (g_off[ray + 1] == g_off[ray]) continue; /* misses the root: no iteration */
+                L[nl].ray = ray, L[nl].cur = 0, L[nl].iters = 1, L[nl].carry = 0;
+                ++nl;
+            }
+            s->waves_pass[0] += 1;
+            if (nl) (c->design == 2 ? sim_wave2 : sim_wave)(c, c->npass > 1 ? 0 : 3, L, nl, b0, c->npass > 1 ? c->sparse0 : 0, s, q, &nq);
+        }
+    for (uint32_t p = 1; p < c->npass; ++p) {
+        qsort(q, nq, sizeof(lane_t), cmp_ray); /* frame order (pass 1: flag compaction; later: chunk order) */
+        const int last = p + 1 >= c->npass;
+        const uint32_t budget = last ? VHX_MAX_ITERS_SIM : c->budgets[p];
+        const int slot = last ? 3 : (int)p;
+        uint64_t nq2 = 0;
+        s->rays_in[slot] += nq;
+        for (uint64_t i = 0; i < nq; i += 64) {
+            const int nl = (int)(nq - i < 64 ? nq - i : 64);
+            s->waves_pass[slot] += 1;
+            (c->design == 2 ? sim_wave2 : sim_wave)(c, slot, q + i, nl, budget, 0, s, q2, &nq2);
+        }
+        lane_t *t = q;
+        q = q2;
+        q2 = t;
+        nq = nq2;
+    }
+    free(q), free(q2);
+    return 0;
+}

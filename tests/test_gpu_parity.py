@@ -100,6 +100,29 @@ def test_random_rays_vs_oracle(gpu, oracle, scene, size, bd):
     assert (got["value"] != N.VHX_EMPTY).sum() > 100
 
 
+def test_degenerate_directions_vs_oracle(gpu, oracle):
+    """Rays whose distances are NaN or infinite (zero, NaN and infinite direction components, from inside and outside
+    the tree): the reference loops until the iteration bound and reports a miss where such a ray stops making progress;
+    the kernels without byte counting end it as a miss at once (VHX_WALK_PROGRESS), which must give the same result
+    in every field, for every pass schedule."""
+    flat = vhx.FlatTree.build_scene(N.VHX_SCENE_LATTICE_CUBE, 64, 4)
+    gpu.upload(flat)
+    nan, inf = np.float32("nan"), np.float32("inf")
+    dirs = [(0, 0, 0), (nan, 0, 0), (nan, nan, nan), (0, nan, 1), (inf, 0, 0), (inf, inf, 0), (-inf, 1, 1),
+            (1e-30, 0, 0), (0, -1e-30, 0), (1, 1, 1), (-0.0, -0.0, -1)]
+    origins = [(32.5, 32.5, 32.5), (1.0, 63.0, 17.25), (-10.0, 30.0, 30.0), (30.0, 80.0, 30.0), (0.0, 0.0, 0.0)]
+    o = np.array([oo for oo in origins for _ in dirs], np.float32)
+    d = np.array([dd for _ in origins for dd in dirs], np.float32)
+    fields = ("value", "cell", "voxel", "impact", "normal", "depth")
+    ref = oracle.trace_rays(flat, o, d, fields=fields)
+    try:
+        for budgets in (DEFAULT_BUDGETS, (), (1, 2, 3)):
+            gpu.set_pass_budgets(budgets)
+            assert_same(gpu.trace_rays(o, d, fields=fields), ref, f"degenerate directions, budgets {budgets}")
+    finally:
+        gpu.set_pass_budgets(DEFAULT_BUDGETS)
+
+
 def test_insert_built_tree_with_palettes(gpu, oracle):
     """Complex / informative / updated voxels and an explicitly simplified tree (Solid bricks, UniformLeaf)."""
     t = vhx.BoxTree(64, 4)

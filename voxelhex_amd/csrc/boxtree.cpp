@@ -3,6 +3,11 @@
 #include "boxtree.hpp"
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <ctime>
 #include <cmath>
 #include <functional>
 #include <atomic>
@@ -1061,13 +1066,23 @@ static inline float alb_distance(uint32_t x, uint32_t y) {
     return std::sqrt(dr * dr + dg * dg + db * db + da * da);
 }
 
+// VHX_MIP_GENERIC=1 (tests): the leaf resampling through get_internal and the palette matching by a full scan, the
+// direct restatements that leaf_value and mip_palette_match shortcut
+static bool mip_generic() {
+    static const bool g = getenv("VHX_MIP_GENERIC") != nullptr;
+    return g;
+}
+
 // MIPResamplingFunction::execute (iterate.rs:434-560). `sample` returns false for None. PointFilter and Posterize keep
 // their groups in first-seen order where the reference iterates a std HashMap (random order per process): results
 // that depend on that order (ties of the most frequent colour, a colour within the threshold of two groups) are not
 // reproducible by the reference itself; this restatement resolves them in first-seen order, the last group of the
 // highest count winning like Iterator::max_by_key.
-static bool mip_execute(const MipMethodCfg &m, U3 start, uint32_t size, const std::function<bool(U3, uint32_t &)> &sample,
-                        uint32_t &out) {
+// `sample` is a template parameter rather than a std::function: the samplers capture three references, beyond
+// std::function's inline buffer, and the heap allocation per call serialised the parallel leaf resampling of
+// recalculate_mips on the allocator (8 threads ran at the speed of one on a fresh process)
+template <class Sample>
+static bool mip_execute(const MipMethodCfg &m, U3 start, uint32_t size, const Sample &sample, uint32_t &out) {
     uint32_t c = 0;
     switch (m.kind) {
         case kBoxFilter: {
@@ -1193,6 +1208,11 @@ bool BoxTree::mip_sample(size_t key, const Cube &nb, U3 position, uint32_t &colo
         start = U3{v2.x - v2.x % 4u, v2.y - v2.y % 4u, v2.z - v2.z % 4u};
     }
 
+    if (content == Content::Leaf && !mip_generic()) {
+        const Node &n = nodes.get(key);
+        return mip_execute(sampler, start, ssize, [&](U3 pos, uint32_t &c) { return albedo_of(leaf_value(n, nb, pos), c); },
+                           color);
+    }
     if (content == Content::Leaf || dominant_bottom) {
         return mip_execute(sampler, start, ssize, [&](U3 pos, uint32_t &c) {
             return albedo_of(get_internal(key, nb, pos), c);
@@ -1217,6 +1237,44 @@ bool BoxTree::mip_sample(size_t key, const Cube &nb, U3 position, uint32_t &colo
     }
 }
 
+// get_internal(key, nb, pos) (src/boxtree/mod.rs:247-317) for a Leaf node `n` with bounds nb: every quantity is an
+// integer below 2^24 and every cube size a power of two, so cube_contains, sectant_for (offset_sectant, clamped to 3),
+// child_bounds_for and matrix_index_for reduce to integer compares, divisions and remainders with the same results
+uint32_t BoxTree::leaf_value(const Node &n, const Cube &nb, U3 pos) const {
+    const int64_t size = (int64_t)nb.size, sub = size / 4, bd = brick_dim;
+    const int64_t rx = (int64_t)pos.x - (int64_t)nb.min.x, ry = (int64_t)pos.y - (int64_t)nb.min.y,
+                  rz = (int64_t)pos.z - (int64_t)nb.min.z;
+    if (rx < 0 || ry < 0 || rz < 0 || rx >= size || ry >= size || rz >= size) return kEmpty32;
+    const int64_t sx = std::min<int64_t>(rx / sub, 3), sy = std::min<int64_t>(ry / sub, 3), sz = std::min<int64_t>(rz / sub, 3);
+    const Brick &b = n.bricks[(size_t)(sx + sy * 4 + sz * 16)];
+    if (b.kind == BrickKind::Empty) return kEmpty32;
+    if (b.kind == BrickKind::Solid) return b.solid;
+    const size_t mx = (size_t)((rx - sx * sub) * bd / sub), my = (size_t)((ry - sy * sub) * bd / sub),
+                 mz = (size_t)((rz - sz * sub) * bd / sub);
+    const uint32_t v = b.parted[flat_projection(mx, my, mz, brick_dim)];
+    return points_to_empty(v) ? kEmpty32 : v;
+}
+
+uint32_t BoxTree::mip_palette_match(uint32_t color, float thr) {
+    uint32_t tb;
+    std::memcpy(&tb, &thr, 4);
+    const uint64_t key = ((uint64_t)tb << 32) | color;
+    // neighbouring MIP cells mostly carry the same colour: the last found match answers them without a map lookup
+    if (key == mip_last_key_ && mip_last_index_ != UINT32_MAX) return mip_last_index_;
+    MipMatch &m = mip_match_.try_emplace(key, MipMatch{UINT32_MAX, 0}).first->second;
+    if (m.index != UINT32_MAX) return m.index;
+    if (m.checked > color_palette.size()) m.checked = 0;  // (the palette never shrinks; defensive)
+    for (size_t i = m.checked; i < color_palette.size(); ++i)
+        if (alb_distance(color, color_palette[i]) < thr) {
+            m.index = (uint32_t)i;
+            break;
+        }
+    if (m.index == UINT32_MAX) m.checked = (uint32_t)color_palette.size();
+    mip_last_key_ = key;
+    mip_last_index_ = m.index;
+    return m.index;
+}
+
 // mipmap.rs:272-338: the sampled colour matched against the palette (first entry within the level's threshold) or
 // added to it, stored in the node's MIP brick
 void BoxTree::mip_store(size_t key, const Cube &nb, U3 position, uint32_t color) {
@@ -1227,12 +1285,20 @@ void BoxTree::mip_store(size_t key, const Cube &nb, U3 position, uint32_t color)
     bool similar = false;
     if (tit != mip_strategy.color_thresholds.end()) {
         const float thr = tit->second * 255.f;
-        for (size_t i = 0; i < color_palette.size(); ++i)
-            if (alb_distance(color, color_palette[i]) < thr) {
-                entry = pix_visual((uint32_t)i);
+        if (mip_generic()) {
+            for (size_t i = 0; i < color_palette.size(); ++i)
+                if (alb_distance(color, color_palette[i]) < thr) {
+                    entry = pix_visual((uint32_t)i);
+                    similar = true;
+                    break;
+                }
+        } else {
+            const uint32_t i = mip_palette_match(color, thr);
+            if (i != UINT32_MAX) {
+                entry = pix_visual(i);
                 similar = true;
-                break;
             }
+        }
     }
     if (!similar) entry = add_to_palette(Entry{VHX_ENTRY_VISUAL, color, 0});
 
@@ -1307,6 +1373,15 @@ void BoxTree::recalculate_mips() {  // mipmap.rs:536-586: depth first, children 
         }
     }
     if (!mip_strategy.enabled) return;
+    const bool tm = getenv("VHX_MIP_TIMING") != nullptr;
+    auto t0 = std::chrono::steady_clock::now();
+    auto lap = [&](const char *what) {
+        if (!tm) return;
+        const auto t1 = std::chrono::steady_clock::now();
+        fprintf(stderr, "[mips] %-28s %.3f s\n", what, std::chrono::duration<double>(t1 - t0).count());
+        t0 = t1;
+    };
+    lap("order");
     // 2. the leaves' resampling reads their bricks only (never a MIP, never a palette entry added below), so it runs
     //    for every leaf up front, spread over threads
     const uint32_t n3 = brick_dim * brick_dim * brick_dim;
@@ -1324,19 +1399,40 @@ void BoxTree::recalculate_mips() {  // mipmap.rs:536-586: depth first, children 
         std::atomic<size_t> next{0};
         auto work = [&]() {
             std::vector<U3> positions;
-            for (size_t j; (j = next.fetch_add(1)) < leaves.size();) {
-                const auto &[key, nb] = order[leaves[j]];
-                mip_positions(nb, brick_dim, positions);
-                for (uint32_t p = 0; p < n3; ++p)
-                    sampled[j * n3 + p] = mip_sample(key, nb, positions[p], colors[j * n3 + p]) ? 1 : 0;
-            }
+            const auto w0 = std::chrono::steady_clock::now();
+            size_t mine = 0;
+            struct Report {
+                bool on;
+                std::chrono::steady_clock::time_point w0;
+                size_t *mine;
+                ~Report() {
+                    timespec ts;
+                    clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
+                    if (on) fprintf(stderr, "[mips]   worker: %zu leaves in %.3f s (thread cpu %.3f s)\n", *mine,
+                                    std::chrono::duration<double>(std::chrono::steady_clock::now() - w0).count(),
+                                    ts.tv_sec + 1e-9 * ts.tv_nsec);
+                }
+            } rep{tm, w0, &mine};
+            // runs of 64 leaves per grab: each thread writes its own contiguous stretch of `colors` / `sampled` (one
+            // leaf per grab put neighbouring leaves' results, written by different threads, on shared cache lines:
+            // 8 threads ran slower than one)
+            constexpr size_t RUN = 64;
+            for (size_t j0; (j0 = next.fetch_add(RUN)) < leaves.size();)
+                for (size_t j = j0; j < std::min(j0 + RUN, leaves.size()); ++j, ++mine) {
+                    const auto &[key, nb] = order[leaves[j]];
+                    mip_positions(nb, brick_dim, positions);
+                    for (uint32_t p = 0; p < n3; ++p)
+                        sampled[j * n3 + p] = mip_sample(key, nb, positions[p], colors[j * n3 + p]) ? 1 : 0;
+                }
         };
-        const unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+        unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+        if (const char *e = getenv("VHX_MIP_THREADS")) nt = std::max(1, atoi(e));
         std::vector<std::thread> pool;
         for (unsigned t = 1; t < nt && (size_t)t * 64 < leaves.size(); ++t) pool.emplace_back(work);
         work();
         for (auto &th : pool) th.join();
     }
+    lap("leaf resampling");
     // 3. palette matching and stores in the reference's order (the palette grows as it goes, and a later match takes
     //    the first entry within the threshold); other nodes resample their children's finished MIPs here
     std::vector<U3> positions;
@@ -1352,6 +1448,7 @@ void BoxTree::recalculate_mips() {  // mipmap.rs:536-586: depth first, children 
         for (uint32_t p = 0; p < n3; ++p)
             if (sampled[base + p]) mip_store(key, nb, positions[p], colors[base + p]);
     }
+    lap("stores + upper levels");
 }
 
 void BoxTree::switch_albedo_mip_maps(bool enabled) {  // mipmap.rs:588-609

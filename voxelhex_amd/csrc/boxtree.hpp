@@ -160,6 +160,19 @@ class BoxTree {
 
    private:
     std::unordered_map<uint32_t, size_t> color_index_, data_index_;
+    // mip_store's palette matching (the first entry within a level's colour threshold, mipmap.rs:252-274): per
+    // (threshold bits, colour) the first matching index, or none among the first `checked` entries. Entries are never
+    // changed or removed, only appended, so a found match stays the first one and a miss needs only the new entries.
+    struct MipMatch {
+        uint32_t index;    // UINT32_MAX: no match among the first `checked` entries
+        uint32_t checked;
+    };
+    std::unordered_map<uint64_t, MipMatch> mip_match_;
+    uint64_t mip_last_key_ = ~0ull;
+    uint32_t mip_last_index_ = UINT32_MAX;
+    uint32_t mip_palette_match(uint32_t color, float thr);  // index or UINT32_MAX
+    // get_internal(key, nb, pos) of a Leaf node at an integer position, in integer arithmetic (the leaf resampling)
+    uint32_t leaf_value(const struct Node &n, const Cube &nb, U3 pos) const;
 
     int insert_at_lod_internal(bool overwrite_if_empty, U3 pos, uint32_t insert_size, Entry e);
     void post_process_node_insert(const std::vector<std::pair<size_t, uint8_t>> &node_stack, const Cube &node_bounds,
