@@ -2,7 +2,10 @@
 (the pass-0 dispatches after the setup and warm-up ones), the span from the first timed pass-0 start to the last
 frame-kernel end divided by the frame count (the frame period, to compare with bench's ms_per_step), and the mean
 per-frame sum of kernel durations by kernel (with frames in flight the kernels of different frames overlap, so these
-sums exceed the period). usage: trace_frames.py KERNEL_TRACE_CSV SKIP STEPS"""
+sums exceed the period), and per kernel class the BUSY time: the union of its dispatches' [start, end) intervals
+over the timed span (the time at least one dispatch of that class ran), per frame and as a fraction of the span, so that
+overlapping frames are not double counted; "any frame kernel" is the union over all classes.
+usage: trace_frames.py KERNEL_TRACE_CSV SKIP STEPS"""
 import csv
 import sys
 from collections import defaultdict
@@ -24,3 +27,28 @@ for s, e, n in sel:
     dur[n.split("(")[0]] += (e - s) / 1e6
 for n, v in sorted(dur.items(), key=lambda x: -x[1]):
     print(f"  {n:32s} {v / steps:.4f} ms per frame (summed over its dispatches)")
+
+
+def union(iv):
+    tot, cs, ce = 0, None, None
+    for a, b in sorted(iv):
+        if cs is None or a > ce:
+            if cs is not None:
+                tot += ce - cs
+            cs, ce = a, b
+        else:
+            ce = max(ce, b)
+    return tot + (ce - cs if cs is not None else 0)
+
+
+span = end - t0
+classes = defaultdict(list)
+for s_, e_, n in sel:
+    k = n.split("(")[0]
+    classes["trace (pass 0 + queue passes)" if "trace" in k else "compaction (count/scan/emit/gather/args)"].append((s_, e_))
+    classes[k].append((s_, e_))
+classes["any frame kernel"] = [(s_, e_) for s_, e_, _ in sel]
+print("busy time (union of dispatch intervals) per frame:")
+for n, iv in sorted(classes.items(), key=lambda x: -union(x[1])):
+    u = union(iv)
+    print(f"  {n:40s} {u / 1e6 / steps:.4f} ms per frame, {u / span:6.1%} of the span")

@@ -75,11 +75,13 @@ __device__ __forceinline__ void perturb_trip() {
     }
 #endif
 }
-// VHX_WALK_PROGRESS (default 1): in builds without byte counting the walk loops end a ray that makes no progress (no
-// axis stepped: NaN distances) as a miss, where the reference loops until the iteration bound and then reports a miss
-// (the same result), instead of testing the bound in every trip; the pass budget counts the walk's axis steps.
+// VHX_WALK_PROGRESS (experiment, default 0): in builds without byte counting the walk loops end a ray that makes no
+// progress (no axis stepped: NaN distances) as a miss, where the reference loops until the iteration bound and then
+// reports a miss (the same result), instead of testing the bound in every trip; the pass budget counts the walk's axis
+// steps. Two VALU instructions fewer per trip, but 3 more VGPRs in pass 0 (73: 6 waves per SIMD instead of 7): the bench
+// frame took 0.597 against 0.583 ms (profiles/r03/variants_r03d.txt), so it stays off.
 #ifndef VHX_WALK_PROGRESS
-#define VHX_WALK_PROGRESS 1
+#define VHX_WALK_PROGRESS 0
 #endif
 __device__ __forceinline__ uint32_t pass_of_budget(uint32_t b) {
     return b >= VHX_MAX_ITERS ? 3u : (b <= 24u ? 0u : (b <= 96u ? 1u : 2u));

@@ -750,7 +750,15 @@ int vhx::ensure(vhx_ctx *c, DevBuf &b, uint64_t bytes) {
 }
 
 // ---- tree-write ordering (TreeStore): frames in flight on shared contexts and writes through the owner ----------
+// VHX_UNORDERED_WRITES=1 (diagnostics only): no waits either way, the behaviour before round 3, to show that
+// tests/test_gpu_ordering.py detects the missing ordering
+static bool unordered_writes() {
+    static const bool u = getenv("VHX_UNORDERED_WRITES") != nullptr && getenv("VHX_UNORDERED_WRITES")[0] == '1';
+    return u;
+}
+
 int vhx::write_begin(vhx_ctx *c) {
+    if (unordered_writes()) return VHX_OK;
     TreeStore &ts = *c->tree;
     std::lock_guard<std::mutex> lock(ts.mu);
     for (vhx_ctx *u : ts.users)
@@ -772,6 +780,7 @@ int vhx::write_end(vhx_ctx *c) {
 }
 
 int vhx::trace_begin(vhx_ctx *c) {
+    if (unordered_writes()) return VHX_OK;
     TreeStore &ts = *c->tree;
     std::lock_guard<std::mutex> lock(ts.mu);
     if (c->seen_write != ts.write_seq) {
