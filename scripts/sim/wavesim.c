@@ -112,16 +112,20 @@ int64_t wavesim_build(const vhx_tree_desc *t, const vhx_camera *cam, uint32_t W,
 /* blocks (as the VHX_PROF build): 0 iteration, 1 leaf target (probe), 2 brick trip, 3 pop, 4 push, 5 walk setup,
  * 6 advance trip, 7 restart, 13 iteration-end bookkeeping, 14 carried walk (design 1) */
 #define NB 16
+#define NP 8 /* passes */
 typedef struct {
-    uint64_t waves[4][NB], lanes[4][NB];
-    uint64_t rays_in[4], waves_pass[4];
+    uint64_t waves[NP][NB], lanes[NP][NB];
+    uint64_t rays_in[NP], waves_pass[NP];
+    double max_wave[NP]; /* the costliest wave of each pass (cost units: the instructions of cfg.cost per block) */
 } stats_t;
 
 typedef struct {
-    uint32_t budgets[4]; /* budget of pass p (p < npass - 1); the last pass is unbounded */
+    uint32_t budgets[NP]; /* budget of pass p (p < npass - 1); the last pass is unbounded */
     uint32_t npass;
     uint32_t sparse0;    /* pass-0 sparse-wave threshold */
     uint32_t design, cap;
+    uint32_t rpw[NP];    /* rays per wave of queue pass p (0 = 64) */
+    uint32_t cost[NB];   /* instructions per wave execution of each block */
 } cfg_t;
 
 typedef struct {
@@ -131,9 +135,12 @@ typedef struct {
     uint32_t carry; /* design 1: brick steps still to walk of the current iteration */
 } lane_t;
 
+static const cfg_t *g_cfg;
+static double g_wave_cost; /* cost of the wave being simulated */
 static void add(stats_t *s, int p, int b, uint32_t lanes) {
     s->waves[p][b] += 1;
     s->lanes[p][b] += lanes;
+    g_wave_cost += g_cfg->cost[b];
 }
 
 /* one wave of a pass; abandoned rays are appended to `out` (in lane order) */
@@ -343,6 +350,7 @@ static int cmp_ray(const void *a, const void *b) {
 
 int wavesim_run(const cfg_t *c, stats_t *s) {
     memset(s, 0, sizeof(*s));
+    g_cfg = c;
     const uint32_t W = g_W, H = g_H;
     const uint64_t n = (uint64_t)W * H;
     lane_t *q = (lane_t *)malloc(n * sizeof(lane_t)), *q2 = (lane_t *)malloc(n * sizeof(lane_t));
@@ -364,19 +372,24 @@ int wavesim_run(const cfg_t *c, stats_t *s) {
                 ++nl;
             }
             s->waves_pass[0] += 1;
-            if (nl) (c->design == 2 ? sim_wave2 : sim_wave)(c, c->npass > 1 ? 0 : 3, L, nl, b0, c->npass > 1 ? c->sparse0 : 0, s, q, &nq);
+            g_wave_cost = 0;
+            if (nl) (c->design == 2 ? sim_wave2 : sim_wave)(c, 0, L, nl, b0, c->npass > 1 ? c->sparse0 : 0, s, q, &nq);
+            if (g_wave_cost > s->max_wave[0]) s->max_wave[0] = g_wave_cost;
         }
     for (uint32_t p = 1; p < c->npass; ++p) {
         qsort(q, nq, sizeof(lane_t), cmp_ray); /* frame order (pass 1: flag compaction; later: chunk order) */
         const int last = p + 1 >= c->npass;
         const uint32_t budget = last ? VHX_MAX_ITERS_SIM : c->budgets[p];
-        const int slot = last ? 3 : (int)p;
+        const int slot = (int)p;
+        const uint32_t rpw = c->rpw[p] ? c->rpw[p] : 64u;
         uint64_t nq2 = 0;
         s->rays_in[slot] += nq;
-        for (uint64_t i = 0; i < nq; i += 64) {
-            const int nl = (int)(nq - i < 64 ? nq - i : 64);
+        for (uint64_t i = 0; i < nq; i += rpw) {
+            const int nl = (int)(nq - i < rpw ? nq - i : rpw);
             s->waves_pass[slot] += 1;
+            g_wave_cost = 0;
             (c->design == 2 ? sim_wave2 : sim_wave)(c, slot, q + i, nl, budget, 0, s, q2, &nq2);
+            if (g_wave_cost > s->max_wave[slot]) s->max_wave[slot] = g_wave_cost;
         }
         lane_t *t = q;
         q = q2;

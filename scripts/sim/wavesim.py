@@ -22,14 +22,19 @@ COSTS = {13: 15, 0: 25, 1: 55, 2: 28, 8: 15, 3: 30, 4: 40, 5: 20, 6: 28, 7: 55}
 RAY_SETUP = 250  # ray generation + begin (divisions, square roots) per pass-0 wave
 
 
+NP = 8
+
+
 class Stats(ctypes.Structure):
-    _fields_ = [("waves", (ctypes.c_uint64 * 16) * 4), ("lanes", (ctypes.c_uint64 * 16) * 4),
-                ("rays_in", ctypes.c_uint64 * 4), ("waves_pass", ctypes.c_uint64 * 4)]
+    _fields_ = [("waves", (ctypes.c_uint64 * 16) * NP), ("lanes", (ctypes.c_uint64 * 16) * NP),
+                ("rays_in", ctypes.c_uint64 * NP), ("waves_pass", ctypes.c_uint64 * NP),
+                ("max_wave", ctypes.c_double * NP)]
 
 
 class Cfg(ctypes.Structure):
-    _fields_ = [("budgets", ctypes.c_uint32 * 4), ("npass", ctypes.c_uint32), ("sparse0", ctypes.c_uint32),
-                ("design", ctypes.c_uint32), ("cap", ctypes.c_uint32)]
+    _fields_ = [("budgets", ctypes.c_uint32 * NP), ("npass", ctypes.c_uint32), ("sparse0", ctypes.c_uint32),
+                ("design", ctypes.c_uint32), ("cap", ctypes.c_uint32), ("rpw", ctypes.c_uint32 * NP),
+                ("cost", ctypes.c_uint32 * 16)]
 
 
 def build():
@@ -40,10 +45,14 @@ def build():
     return ctypes.CDLL(LIB)
 
 
-def run(lib, budgets, design, cap, sparse0=12):
+def run(lib, budgets, design, cap, sparse0=12, rpw=()):
     c = Cfg()
     for i, b in enumerate(budgets):
         c.budgets[i] = b
+    for i, r in enumerate(rpw):
+        c.rpw[i] = r
+    for b, v in COSTS.items():
+        c.cost[b] = v
     c.npass = len(budgets) + 1
     c.sparse0, c.design, c.cap = sparse0, design, cap
     s = Stats()
@@ -54,7 +63,7 @@ def run(lib, budgets, design, cap, sparse0=12):
 def report(s, label):
     tot = 0.0
     print(f"== {label}")
-    for p in range(4):
+    for p in range(NP):
         if not s.waves_pass[p]:
             continue
         valu = RAY_SETUP * s.waves_pass[p] if p == 0 or s.rays_in[p] else 0
@@ -65,7 +74,8 @@ def report(s, label):
                 valu += w * COSTS[b]
                 line.append(f"{name} {w} ({l / w:.1f})")
         tot += valu
-        print(f"  pass {p}: rays {s.rays_in[p]} waves {s.waves_pass[p]} VALU~{valu / 1e6:.1f}M | " + "; ".join(line))
+        print(f"  pass {p}: rays {s.rays_in[p]} waves {s.waves_pass[p]} VALU~{valu / 1e6:.1f}M max-wave {s.max_wave[p] / 1e3:.0f}k"
+              f" | " + "; ".join(line))
     print(f"  total VALU~{tot / 1e6:.1f}M")
     return tot
 

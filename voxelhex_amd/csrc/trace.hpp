@@ -759,7 +759,10 @@ struct Trav {
                     }
                 }
             }
-            if (ex == 0u && ++iters > budget) ex = budget >= VHX_MAX_ITERS ? 2u : 3u;  // the next node iteration
+            // the next node iteration; past the iteration bound the ray ends as a miss in every pass (the reference
+            // stops at the top of that iteration): a ray whose walks ran past the bound inside a budgeted pass must
+            // not be resumed for one more iteration (its probe could hit; tests/test_gpu_parity.py, degenerate rays)
+            if (ex == 0u && ++iters > budget) ex = budget >= VHX_MAX_ITERS || iters > VHX_MAX_ITERS ? 2u : 3u;
         }
     }
 
