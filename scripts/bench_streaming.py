@@ -1,20 +1,36 @@
-"""Streaming-frame timing: a device view of the 256^3 scene-S tree (brick_dim 4) around a viewport that
-moves every frame, at the reference's default rates (node_uploads_per_frame 25, brick_uploads_per_frame 50,
-view.rs:109-111). Per frame: the producer's host time (vhx_stream_upload: decisions + packing + one staged copy), the
-device time of the frame's ranged writes (HIP events around the upload on the context's stream) and the trace of a
-1920x1080 frame of the view. usage: bench_streaming.py [frames]"""
+"""Streaming-frame timing: a device view of the 256^3 scene-S tree (brick_dim 4) around a viewport
+that moves every frame, at the reference's default rates (node_uploads_per_frame 25, brick_uploads_per_frame 50,
+view.rs:109-111), each frame a 1920x1080 trace of the view -- the reference's render loop (upload::<T> then dispatch,
+streaming/mod.rs:420-635, pipeline/mod.rs:96-155).
+
+--inflight 1 (default): one frame at a time; per frame the producer's host time (vhx_stream_upload: decisions +
+packing + one staged copy), the device time of the frame's ranged writes (HIP events around the upload on the context's
+stream) and the trace.
+--inflight F > 1: F contexts share the device view (vhx_create_shared), frame k is traced by context k % F into its own
+outputs, the uploads go through the owner, and nothing is synchronised between frames (libvhx orders every write after
+the frames submitted before it and every frame after the writes submitted before it); the figure is the frame period
+(wall time / frames) next to the same loop at F = 1 without per-frame synchronisation.
+usage: bench_streaming.py [frames] [--inflight F]"""
+import argparse
 import os
 import sys
 import time
 
+ap = argparse.ArgumentParser()
+ap.add_argument("frames", nargs="?", type=int, default=200)
+ap.add_argument("--inflight", type=int, default=1)
+args = ap.parse_args()
+if args.inflight > 1 and int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < args.inflight + 4:
+    os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, args.inflight + 4))  # before HIP starts (bench.py's hw_queues)
+
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-import numpy as np
-import torch
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
 
-import voxelhex_amd as vhx
-from voxelhex_amd import _native as N
+import voxelhex_amd as vhx  # noqa: E402
+from voxelhex_amd import _native as N  # noqa: E402
 
-frames = int(sys.argv[1]) if len(sys.argv) > 1 else 200
+frames = args.frames
 t = vhx.BoxTree(256, 4)
 t.insert_scene(N.VHX_SCENE_LATTICE_CUBE)
 rt = vhx.Raytracer(0)
@@ -23,33 +39,78 @@ torch.cuda.set_stream(stream)
 S = 256.0
 s = vhx.StreamingView(t, rt, (S / 2, S / 2, S / 2), 64.0)
 s.set_rates(25, 50, 10)
-out = {"rgba": torch.zeros(1920 * 1080, dtype=torch.int32, device="cuda"),
-       "depth": torch.zeros(1920 * 1080, dtype=torch.float32, device="cuda")}
-host, dev, trace, written, resizes = [], [], [], [], 0
-for k in range(frames):
+
+
+def view(k):
     a = 2.0 * np.pi * k / frames
     c = (S / 2 + 60.0 * np.cos(a), S / 2, S / 2 + 60.0 * np.sin(a))
-    s.set_viewport(c, 64.0)
-    e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
-    e0.record(stream)
-    t0 = time.perf_counter()
-    st, grow = s.upload()
-    host.append((time.perf_counter() - t0) * 1e3)
-    if grow:
-        s.resize()
-        resizes += 1
-    e1.record(stream)
-    cam = vhx.glass_camera(256, 1920, 1080, angle=40.0 + a, target=c)
-    rt.trace_primary(cam, out=out)
-    e2.record(stream)
-    written.append(st["bytes_written"])
+    return a, c
+
+
+def outputs():
+    return {"rgba": torch.zeros(1920 * 1080, dtype=torch.int32, device="cuda"),
+            "depth": torch.zeros(1920 * 1080, dtype=torch.float32, device="cuda")}
+
+
+q = lambda v: f"median {np.median(v):.3f} p90 {np.percentile(v, 90):.3f} max {np.max(v):.3f}"  # noqa: E731
+
+if args.inflight <= 1:
+    out = outputs()
+    host, dev, trace, written, resizes = [], [], [], [], 0
+    for k in range(frames):
+        a, c = view(k)
+        s.set_viewport(c, 64.0)
+        e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+        e0.record(stream)
+        t0 = time.perf_counter()
+        st, grow = s.upload()
+        host.append((time.perf_counter() - t0) * 1e3)
+        if grow:
+            s.resize()
+            resizes += 1
+        e1.record(stream)
+        cam = vhx.glass_camera(256, 1920, 1080, angle=40.0 + a, target=c)
+        rt.trace_primary(cam, out=out)
+        e2.record(stream)
+        written.append(st["bytes_written"])
+        torch.cuda.synchronize()
+        dev.append(e0.elapsed_time(e1))
+        trace.append(e1.elapsed_time(e2))
+    print(f"{frames} frames, {resizes} resizes, bytes written per frame median {int(np.median(written))} max {max(written)}")
+    print(f"producer host ms (vhx_stream_upload): {q(host)}")
+    print(f"ranged writes device ms (update batch on the stream): {q(dev)}")
+    print(f"trace 1920x1080 of the view ms: {q(trace)}")
+else:
+    F = args.inflight
+    ctxs = [rt] + [rt.shared() for _ in range(F - 1)]
+    for r in ctxs:
+        r.stream()  # each context's own stream, created back to back (one hardware queue each)
+    outs = [outputs() for _ in range(F)]
     torch.cuda.synchronize()
-    dev.append(e0.elapsed_time(e1))
-    trace.append(e1.elapsed_time(e2))
-q = lambda v: f"median {np.median(v):.3f} p90 {np.percentile(v, 90):.3f} max {np.max(v):.3f}"
-print(f"{frames} frames, {resizes} resizes, bytes written per frame median {int(np.median(written))} max {max(written)}")
-print(f"producer host ms (vhx_stream_upload): {q(host)}")
-print(f"ranged writes device ms (update batch on the stream): {q(dev)}")
-print(f"trace 1920x1080 of the view ms: {q(trace)}")
+
+    def loop(nctx, k0):
+        host, resizes = [], 0
+        t0 = time.perf_counter()
+        for k in range(k0, k0 + frames):
+            a, c = view(k)
+            s.set_viewport(c, 64.0)
+            h0 = time.perf_counter()
+            _, grow = s.upload()  # through the owner, no host wait
+            host.append((time.perf_counter() - h0) * 1e3)
+            if grow:
+                s.resize()
+                resizes += 1
+            cam = vhx.glass_camera(256, 1920, 1080, angle=40.0 + a, target=c)
+            ctxs[k % nctx].trace_primary(cam, out=outs[k % nctx])
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) * 1e3 / frames, host, resizes
+
+    loop(F, 0)  # warm-up: every context allocates its queues, the view reaches its size
+    for nctx in (1, F):
+        period, host, resizes = loop(nctx, frames)
+        print(f"frames in flight {nctx}: {frames} frames, period {period:.4f} ms per frame (upload + 1920x1080 trace), "
+              f"producer host ms {q(host)}, {resizes} resizes")
+    for r in ctxs[1:]:
+        r.close()
 s.close()
 rt.close()
