@@ -225,45 +225,52 @@ __device__ __forceinline__ F3d impact_normal(CubeD c, F3d p) {
     return vnorm(n);
 }
 
+// The signs of a ray's direction live in sg only (signum(d): +-1, NaN for a NaN component); the reference's
+// max(sg, 0) and `sg as i32` are formed where used (three registers fewer than carrying them: pass 0 fits 64 VGPRs)
+// d and sf are kept as an (x, y) pair plus z: the walk loops' packed f32 instructions read them in place, where
+// separate x / y registers had to be copied into aligned pairs that stayed live beside the originals
 struct RayD {
-    F3d o, d, sf, sg, sgmax;
-    int32_t isx, isy, isz;  // `as i32` of signum(d) (= of round(signum(d))): the integer DDA steps
+    F3d o, sg;
+    F2 dxy, sfxy;
+    float dz, sfz;
 };
+__device__ __forceinline__ F3d dvec(const RayD &r) { return mk(r.dxy.x, r.dxy.y, r.dz); }
+// sg_k > 0 <=> (sg_k as i32) > 0 (NaN: false both ways); max(sg_k, 0) is 1 exactly then, else 0
+__device__ __forceinline__ bool spos(float s) { return s > 0.0f; }
 
 __device__ __forceinline__ void ray_setup(RayD &r, F3d o, F3d d) {
     r.o = o;
-    r.d = d;
+    r.dxy = mk2(d.x, d.y);
+    r.dz = d.z;
     r.sg = mk(rsignum(d.x), rsignum(d.y), rsignum(d.z));
-    r.sgmax = mk(__builtin_fmaxf(r.sg.x, 0.0f), __builtin_fmaxf(r.sg.y, 0.0f), __builtin_fmaxf(r.sg.z, 0.0f));
-    r.isx = ras_i32(r.sg.x);
-    r.isy = ras_i32(r.sg.y);
-    r.isz = ras_i32(r.sg.z);
 }
 // get_dda_scale_factors, cpu.rs:79-92 (only needed once the ray enters the root cube)
 __device__ __forceinline__ void ray_scale_factors(RayD &r) {
-    const F3d d = r.d;
+    const F3d d = dvec(r);
     const float zx = d.z / d.x, yx = d.y / d.x, xy = d.x / d.y, zy = d.z / d.y, xz = d.x / d.z, yz = d.y / d.z;
-    r.sf = mk(__builtin_sqrtf((1.0f + zx * zx) + yx * yx), __builtin_sqrtf((xy * xy + 1.0f) + zy * zy),
-              __builtin_sqrtf((xz * xz + 1.0f) + yz * yz));
+    r.sfxy = mk2(__builtin_sqrtf((1.0f + zx * zx) + yx * yx), __builtin_sqrtf((xy * xy + 1.0f) + zy * zy));
+    r.sfz = __builtin_sqrtf((xz * xz + 1.0f) + yz * yz);
 }
 
 // dda_step_to_next_sibling, src/raytracing/cpu.rs:104-132. Returns the axis mask of the step (bit k set where
 // min_step == d_k); the float step of the reference is sg_k on those axes and 0.0 elsewhere.
 __device__ __forceinline__ uint32_t dda_step(const RayD &r, F3d &p, CubeD b) {
     const F3d diff = vsub(p, b.min);
-    const F3d st = mk(b.size * r.sgmax.x - r.sg.x * diff.x, b.size * r.sgmax.y - r.sg.y * diff.y,
-                      b.size * r.sgmax.z - r.sg.z * diff.z);
-    const float dx = __builtin_fabsf(st.x * r.sf.x), dy = __builtin_fabsf(st.y * r.sf.y),
-                dz = __builtin_fabsf(st.z * r.sf.z);
+    const F3d st = mk(b.size * __builtin_fmaxf(r.sg.x, 0.0f) - r.sg.x * diff.x,
+                      b.size * __builtin_fmaxf(r.sg.y, 0.0f) - r.sg.y * diff.y,
+                      b.size * __builtin_fmaxf(r.sg.z, 0.0f) - r.sg.z * diff.z);
+    const float dx = __builtin_fabsf(st.x * r.sfxy.x), dy = __builtin_fabsf(st.y * r.sfxy.y),
+                dz = __builtin_fabsf(st.z * r.sfz);
     const float m = __builtin_fminf(__builtin_fminf(dx, dy), dz);
-    p = vadd(p, vmul(r.d, m));
+    p = vadd(p, vmul(dvec(r), m));
     return (m == dx ? 1u : 0u) | (m == dy ? 2u : 0u) | (m == dz ? 4u : 0u);
 }
 __device__ __forceinline__ F3d step_vec(const RayD &r, uint32_t sel) {
     return mk((sel & 1u) ? r.sg.x : 0.0f, (sel & 2u) ? r.sg.y : 0.0f, (sel & 4u) ? r.sg.z : 0.0f);
 }
 __device__ __forceinline__ uint32_t step_sectant(const RayD &r, uint32_t s, uint32_t sel) {
-    return step_sectant_i(s, (sel & 1u) ? r.isx : 0, (sel & 2u) ? r.isy : 0, (sel & 4u) ? r.isz : 0);
+    return step_sectant_i(s, (sel & 1u) ? ras_i32(r.sg.x) : 0, (sel & 2u) ? ras_i32(r.sg.y) : 0,
+                          (sel & 4u) ? ras_i32(r.sg.z) : 0);
 }
 
 // brick geometry helpers
@@ -341,15 +348,16 @@ __device__ __forceinline__ bool probe_brick(const DevTree &t, const RayD &r, F3d
             // step adds 1 and the flat index is j-flat ^ F.
             // e_k = min_k + (i_k + max(sg_k, 0)) * unit: every term is an exact multiple of unit below 2^24 * unit,
             // so the fused form is the value of the reference-order sum (min + i*unit) + unit*max(sg, 0) exactly
-            F2 exy = mk2(__builtin_fmaf((float)(ix + (int32_t)(r.isx > 0)), unit, bb.min.x),
-                         __builtin_fmaf((float)(iy + (int32_t)(r.isy > 0)), unit, bb.min.y));
-            float ez = __builtin_fmaf((float)(iz + (int32_t)(r.isz > 0)), unit, bb.min.z);
+            F2 exy = mk2(__builtin_fmaf((float)(ix + (int32_t)spos(r.sg.x)), unit, bb.min.x),
+                         __builtin_fmaf((float)(iy + (int32_t)spos(r.sg.y)), unit, bb.min.y));
+            float ez = __builtin_fmaf((float)(iz + (int32_t)spos(r.sg.z)), unit, bb.min.z);
             const F2 sguxy = mk2(r.sg.x * unit, r.sg.y * unit);
             const float sguz = r.sg.z * unit;
-            const F2 sfxy = mk2(r.sf.x, r.sf.y), dxy = mk2(r.d.x, r.d.y);
+            const F2 sfxy = r.sfxy, dxy = r.dxy;
             F2 pxy = mk2(p.x, p.y);
             float pz = p.z;
-            const uint32_t fx = r.isx > 0 ? 0u : BD - 1u, fy = r.isy > 0 ? 0u : BD - 1u, fz = r.isz > 0 ? 0u : BD - 1u;
+            const uint32_t fx = spos(r.sg.x) ? 0u : BD - 1u, fy = spos(r.sg.y) ? 0u : BD - 1u,
+                           fz = spos(r.sg.z) ? 0u : BD - 1u;
             const uint32_t F = fx + fy * BD + fz * (BD * BD);
             uint32_t jx = (uint32_t)ix ^ fx, jy = (uint32_t)iy ^ fy, jz = (uint32_t)iz ^ fz;
             const uint32_t js0 = jx + jy + jz;
@@ -360,10 +368,10 @@ __device__ __forceinline__ bool probe_brick(const DevTree &t, const RayD &r, F3d
                 // dda_step_to_next_sibling (cpu.rs:104-132) on the cell {cmin, unit}
                 const F2 sxy = (exy - pxy) * sfxy;
                 const float dx = __builtin_fabsf(sxy.x), dy = __builtin_fabsf(sxy.y),
-                            dz = __builtin_fabsf((ez - pz) * r.sf.z);
+                            dz = __builtin_fabsf((ez - pz) * r.sfz);
                 const float m = __builtin_fminf(__builtin_fminf(dx, dy), dz);
                 pxy = pxy + dxy * m;
-                pz = pz + r.d.z * m;
+                pz = pz + r.dz * m;
                 const bool mx = m == dx, my = m == dy, mz = m == dz;
                 const F2 en = exy + sguxy;
                 exy = mk2(mx ? en.x : exy.x, my ? en.y : exy.y);
@@ -598,6 +606,10 @@ struct Trav {
         if (COUNT) h.bytes += 12;
         const bool uniform = ntype == VHX_NODE_UNIFORM_LEAF;
         const uint32_t pp = VHX_PROF ? pass_of_budget(budget) : 0u;
+        // the hit descriptor and cell are defined afresh in every iteration (they are read only after the iteration
+        // that sets ex to 1 or 4): not loop-carried, two registers fewer across the loop
+        hdesc = slot;
+        hflat = -1;
         if (target < 64u && (uniform || ntype == VHX_NODE_LEAF)) {
             VHX_PROF_BLOCK(pp, 1);
             if (COUNT) h.bytes += 4;
@@ -693,14 +705,16 @@ struct Trav {
                 // 64 + the wrapped sectant there, which the next iteration's POP never reads).
                 // A POP lane walks with every sectant occupied: it stops after its one step.
                 const uint64_t wocc = pop ? ~0ull : occ;
-                const F3d usg = mk(tb.size * r.sgmax.x, tb.size * r.sgmax.y, tb.size * r.sgmax.z);
+                // tb.size * max(sg, 0): tb.size or 0 (the reference's product, exactly)
+                const F3d usg = mk(spos(r.sg.x) ? tb.size : 0.0f, spos(r.sg.y) ? tb.size : 0.0f,
+                                   spos(r.sg.z) ? tb.size : 0.0f);
                 const F3d sgs = mk(r.sg.x * tb.size, r.sg.y * tb.size, r.sg.z * tb.size);
-                const uint32_t fx = r.isx > 0 ? 0u : 3u, fy = r.isy > 0 ? 0u : 3u, fz = r.isz > 0 ? 0u : 3u;
+                const uint32_t fx = spos(r.sg.x) ? 0u : 3u, fy = spos(r.sg.y) ? 0u : 3u, fz = spos(r.sg.z) ? 0u : 3u;
                 const uint32_t F = fx + fy * 4u + fz * 16u;
                 uint32_t jx = (target & 3u) ^ fx, jy = ((target >> 2) & 3u) ^ fy, jz = (target >> 4) ^ fz;
                 F2 exy = mk2(tb.min.x + usg.x, tb.min.y + usg.y);
                 float ez = tb.min.z + usg.z;
-                const F2 sgsxy = mk2(sgs.x, sgs.y), sfxy = mk2(r.sf.x, r.sf.y), dxy = mk2(r.d.x, r.d.y);
+                const F2 sgsxy = mk2(sgs.x, sgs.y), sfxy = r.sfxy, dxy = r.dxy;
                 F2 pxy = mk2(p.x, p.y);
                 float pz = p.z;
                 constexpr bool PROG = !COUNT && VHX_WALK_PROGRESS;
@@ -712,10 +726,10 @@ struct Trav {
                     if (!PROG) ++iters;
                     const F2 sxy = (exy - pxy) * sfxy;
                     const float dx = __builtin_fabsf(sxy.x), dy = __builtin_fabsf(sxy.y),
-                                dz = __builtin_fabsf((ez - pz) * r.sf.z);
+                                dz = __builtin_fabsf((ez - pz) * r.sfz);
                     const float m = __builtin_fminf(__builtin_fminf(dx, dy), dz);
                     pxy = pxy + dxy * m;
-                    pz = pz + r.d.z * m;
+                    pz = pz + r.dz * m;
                     const bool mx = m == dx, my = m == dy, mz = m == dz;
                     const F2 en = exy + sgsxy;
                     exy = mk2(mx ? en.x : exy.x, my ? en.y : exy.y);
@@ -745,7 +759,7 @@ struct Trav {
                     if (count == 0) {
                         VHX_PROF_BLOCK(pp, 7);
                         // the stack ran empty: restart from the root (cpu.rs:441-455); target_bounds stays stale
-                        p = vadd(p, vmul(r.d, 0.1f));
+                        p = vadd(p, vmul(dvec(r), 0.1f));
                         if (p.x < tsize && p.y < tsize && p.z < tsize && p.x > 0.0f && p.y > 0.0f && p.z > 0.0f) {
                             target = offset_sectant(p, tsize);
                             tbok = 0u;  // target_bounds stays stale
