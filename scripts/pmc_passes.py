@@ -1,0 +1,77 @@
+"""Per-pass PMC figures of the bench frame from a gpu_profile.sh directory: every counter of every pmc*_counter_collection
+.csv summed per pass of the multi-pass schedule and divided by the frames of that run. A frame's dispatches are told
+apart by their hardware queue (each context of the frames in flight submits on its own): on one queue, a
+k_trace_primary<false..> dispatch opens a frame (pass 0) and the k_trace_queue<false..> dispatches after it are passes
+1, 2, ...
+Derived per pass: active lanes per VALU instruction (SQ_THREAD_CYCLES_VALU / SQ_ACTIVE_INST_VALU), VALU and SALU
+wave-instructions per frame, the fraction of wave cycles spent issuing / waiting on dependencies / waiting on memory
+(SQ_ACTIVE_INST_ANY, SQ_WAIT_INST_ANY, SQ_WAIT_ANY over SQ_WAVE_CYCLES; quad-cycle units cancel) and the memory-side
+reads (FETCH_SIZE x 1024 B x 2, the gfx950 correction of scripts/pmc_frame.py).
+usage: pmc_passes.py PROFILE_DIR [OUT_TXT]"""
+import csv
+import glob
+import os
+import sys
+from collections import defaultdict
+
+d = sys.argv[1]
+sums = defaultdict(lambda: defaultdict(float))  # (run, pass) -> counter -> total
+runs = {}  # run -> (counter names, frames)
+for path in sorted(glob.glob(os.path.join(d, "pmc*_counter_collection.csv"))):
+    run = os.path.basename(path).split("_")[0]
+    disp, names = {}, set()
+    for r in csv.DictReader(open(path)):  # one row per (dispatch, counter)
+        e = disp.setdefault(int(r["Dispatch_Id"]),
+                            {"name": r["Kernel_Name"].replace("void ", ""), "queue": r["Queue_Id"], "c": defaultdict(float)})
+        e["c"][r["Counter_Name"]] += float(r["Counter_Value"])
+        names.add(r["Counter_Name"])
+    cur, nf = {}, 0  # queue -> pass index of its latest trace dispatch
+    for k in sorted(disp):
+        e = disp[k]
+        if e["name"].startswith("k_trace_primary<false"):
+            cur[e["queue"]] = 0
+            nf += 1
+        elif e["name"].startswith("k_trace_queue<false") and e["queue"] in cur:
+            cur[e["queue"]] += 1
+        else:
+            continue
+        for c, v in e["c"].items():
+            sums[(run, cur[e["queue"]])][c] += v
+    runs[run] = (names, nf)
+
+passes = sorted({p for (_, p) in sums})
+
+
+def per_frame(p, c):
+    for run, (names, nf) in runs.items():
+        if c in names and nf:
+            return sums[(run, p)][c] / nf
+    return None
+
+
+lines = [f"per-pass PMC figures per frame, {os.path.basename(os.path.normpath(d))} (frames per pmc run: "
+         + ", ".join(f"{run} {nf}" for run, (_, nf) in runs.items()) + ")"]
+for p in passes:
+    valu, salu = per_frame(p, "SQ_INSTS_VALU"), per_frame(p, "SQ_INSTS_SALU")
+    tc, ai = per_frame(p, "SQ_THREAD_CYCLES_VALU"), per_frame(p, "SQ_ACTIVE_INST_VALU")
+    wc, waves = per_frame(p, "SQ_WAVE_CYCLES"), per_frame(p, "SQ_WAVES")
+    act, wi, wa = per_frame(p, "SQ_ACTIVE_INST_ANY"), per_frame(p, "SQ_WAIT_INST_ANY"), per_frame(p, "SQ_WAIT_ANY")
+    fetch = per_frame(p, "FETCH_SIZE")
+    parts = [f"pass {p}:"]
+    if waves is not None:
+        parts.append(f"waves {waves:.0f}")
+    if valu is not None:
+        parts.append(f"VALU {valu / 1e6:.1f} M")
+    if salu is not None:
+        parts.append(f"SALU {salu / 1e6:.1f} M")
+    if tc and ai:
+        parts.append(f"lanes/VALU {tc / ai:.1f}")
+    if wc:
+        parts.append(f"issuing {act / wc:.0%}, dependency waits {wi / wc:.0%}, memory waits {wa / wc:.0%} of wave cycles")
+    if fetch is not None:
+        parts.append(f"reads {fetch * 2048 / 1e6:.1f} MB")
+    lines.append("  " + "  ".join(parts))
+txt = "\n".join(lines)
+print(txt)
+if len(sys.argv) > 2:
+    open(sys.argv[2], "w").write(txt + "\n")

@@ -91,6 +91,9 @@ struct vhx_ctx {
     uint32_t rpw[VHX_MAX_BUDGETS + 1] = {64u, 64u, 64u, 64u, 64u};  // rays per wave of each pass (VHX_RPW="64,16" style override; 0 = adaptive)
     uint32_t tw = 1024;            // adaptive rays per wave: target waves per queue pass (VHX_TW)
     bool resume = true;            // abandoned rays continue from saved state (VHX_RESUME=0: re-traced from scratch)
+    // passes before save_from keep no state: the rays they abandon are traced again from scratch by pass save_from,
+    // which saves (VHX_SAVE_FROM; 0 = every budgeted pass saves)
+    uint32_t save_from = 0;
     uint32_t xcd_group = 16;       // pass-0 XCD-aware block runs (VHX_XCDG; 0 = dispatch order)
     uint32_t qblock = 256;         // threads per workgroup of a queue pass (VHX_QBLOCK=64: one wave per workgroup)
     uint32_t queue_blocks = 2048;  // workgroups of a queue pass (CUs x resident workgroups)

@@ -1012,8 +1012,8 @@ static PassQ pass_q(const vhx_ctx *c, uint32_t p, uint32_t npass) {
     q.counts = (uint32_t *)c->counts.ptr;
     q.flags = nullptr;
     // the state buffer is written by every pass that can abandon rays and read by every pass after the first
-    q.state = c->resume && npass > 1 ? (uint4 *)c->state.ptr : nullptr;
-    q.resume = c->resume && p > 0 ? 1u : 0u;
+    q.state = c->resume && npass > 1 && p >= c->save_from ? (uint4 *)c->state.ptr : nullptr;
+    q.resume = c->resume && p > c->save_from ? 1u : 0u;
     q.sparse = last || !q.state ? 0u : c->sparse[p];
     return q;
 }
@@ -1086,7 +1086,12 @@ static int launch_queue_passes(vhx_ctx *c, const DevTree &t, const CamD &cam, co
             c->qargs_host_ptr[slot] = c->qargs.ptr;
         }
     }
-    for (uint32_t p = first; p < npass && !rc; ++p) {
+#ifdef VHX_PROBE_PASSES  // diagnostic builds only: run the first VHX_PROBE_PASSES passes (the frame is incomplete)
+    const uint32_t np_run = std::min<uint32_t>(npass, VHX_PROBE_PASSES);
+#else
+    const uint32_t np_run = npass;
+#endif
+    for (uint32_t p = first; p < np_run && !rc; ++p) {
         const uint32_t *in = (const uint32_t *)c->queue[(p - 1) & 1u].ptr;  // p = 0: queue[1]
         const uint32_t *in_n = p > 0 ? ctl + (p - 1) : ctl + 7;
         const PassQ q = pass_q(c, p, npass);
@@ -1166,6 +1171,8 @@ int vhx_create(int hip_device, vhx_ctx **out) {
         if (pg) c->xcd_group = (uint32_t)atoi(pg);
         const char *pz = getenv("VHX_RESUME");
         if (pz && pz[0] == '0') c->resume = false;
+        const char *psf = getenv("VHX_SAVE_FROM");
+        if (psf && atoi(psf) >= 0) c->save_from = (uint32_t)atoi(psf);
         const char *pq = getenv("VHX_QBLOCK");
         if (pq && (atoi(pq) == 64 || atoi(pq) == 128)) c->qblock = (uint32_t)atoi(pq);
         hipDeviceProp_t prop;
@@ -1388,6 +1395,7 @@ void vhx::copy_sched(vhx_ctx *c, const vhx_ctx *owner) {
     c->npass = owner->npass;
     c->tw = owner->tw;
     c->resume = owner->resume;
+    c->save_from = owner->save_from;
     c->xcd_group = owner->xcd_group;
     c->qblock = owner->qblock;
     c->queue_blocks = owner->queue_blocks;
