@@ -85,7 +85,7 @@ def parse():
                    help="opt-in approximate mode (vhx_set_depth_prepass, not the reference semantics): a half-resolution "
                         "depth prepass, full-resolution rays start at the min of 4 texels minus MARGIN")
     p.add_argument("--budgets", default=None, metavar="B1,B2,...",
-                   help="step budgets of the pass schedule (vhx_set_pass_budgets; \"\" = one pass); default: the library's {24, 96, 768}, one pass with --mip-lod (its rays are short: 0.092 against 0.136 ms per depth-1 frame, profiles/r02/mips/headline/budgets)")
+                   help="step budgets of the pass schedule (vhx_set_pass_budgets; \"\" = one pass); default: the library's {24, 72, 216, 648}, one pass with --mip-lod (its rays are short: 0.092 against 0.136 ms per depth-1 frame, profiles/r02/mips/headline/budgets)")
     p.add_argument("--mip-lod", type=int, default=None, metavar="DEPTH",
                    help="opt-in MIP stand-in mode (not the reference path): the scene inserted into a host BoxTree with "
                         "MIP maps on, flattened down to DEPTH (vhx_boxtree_flatten_lod) and traced with its node MIPs "

@@ -158,9 +158,9 @@ int vhx_sync(vhx_ctx *ctx, float *last_trace_ms);
 /* Ray scheduling (no reference counterpart; results do not depend on it). A trace runs n+1 passes: pass i abandons
  * rays that need more than budgets[i] loop steps (saving their traversal state) and the next pass resumes them, 64
  * such rays per wave; the last pass is unbounded. n = 0 is a single pass. Budgets strictly increasing,
- * 0 < b < 2^22, n <= VHX_MAX_BUDGETS. Default {24, 96, 768}, tuned for frames in flight (vhx_create_shared);
+ * 0 < b < 2^22, n <= VHX_MAX_BUDGETS. Default {24, 72, 216, 648}, tuned for frames in flight (vhx_create_shared);
  * {64} gives the shortest latency of a lone frame (environment override VHX_BUDGETS="64"). */
-#define VHX_MAX_BUDGETS 4
+#define VHX_MAX_BUDGETS 6
 int vhx_set_pass_budgets(vhx_ctx *ctx, const uint32_t *budgets, uint32_t n);
 
 /* Tree upload ----------------------------------------------------------------------------------------------- */
@@ -235,8 +235,9 @@ int vhx_set_depth_prepass(vhx_ctx *ctx, int enable, float margin);
  * contexts trace with them. */
 int vhx_set_node_mips(vhx_ctx *ctx, const uint32_t *node_mips, uint32_t count);
 /* Diagnostics of a VHX_PROF build (scripts/probes/probe_blocks.py; a regular build returns VHX_E_STATE): per pass
- * (4) and traversal block (16), the wave executions and the lanes active in them, as out[2 * (pass * 16 + block)] and
- * out[2 * (pass * 16 + block) + 1], accumulated over every trace since the last reset. */
+ * slot (5: budgets <= 24, <= 96, <= 256, larger, the unbounded pass) and traversal block (16), the wave executions
+ * and the lanes active in them, as out[2 * (pass * 16 + block)] and out[2 * (pass * 16 + block) + 1], accumulated
+ * over every trace since the last reset. */
 int vhx_profile_counters(vhx_ctx *ctx, uint64_t *out, uint32_t n, int reset);
 /* Traces n explicit rays; rays = 6 f32 per ray (origin xyz, direction xyz), host or device per on_device. */
 int vhx_trace_rays(vhx_ctx *ctx, const float *rays, uint64_t n, const vhx_hits *out, int on_device);

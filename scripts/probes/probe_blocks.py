@@ -33,13 +33,13 @@ def main():
     rt.upload(flat)
     rt.set_pass_budgets(tuple(int(b) for b in a.budgets.split(",") if b))
     cam = vhx.glass_camera(a.size, a.width, a.height, target=(a.size / 2,) * 3)
-    buf = (ctypes.c_uint64 * 128)()
+    buf = (ctypes.c_uint64 * 160)()
     rt.trace_primary(cam, fields=("rgba",))  # warm-up
-    N.check(N.lib().vhx_profile_counters(rt._h, buf, 128, 1), rt._h)
+    N.check(N.lib().vhx_profile_counters(rt._h, buf, 160, 1), rt._h)
     rt.trace_primary(cam, fields=("rgba",))
-    N.check(N.lib().vhx_profile_counters(rt._h, buf, 128, 1), rt._h)
+    N.check(N.lib().vhx_profile_counters(rt._h, buf, 160, 1), rt._h)
     out = {}
-    for p in range(4):
+    for p in range(5):  # pass slots (vhx.h, vhx_profile_counters)
         for b, name in BLOCKS.items():
             n, lanes = buf[2 * (p * 16 + b)], buf[2 * (p * 16 + b) + 1]
             if n:

@@ -22,7 +22,7 @@ for spec in sys.argv[1:] or ["64"]:
     for r in ctxs:
         r.set_pass_budgets(b)
     for F in FS:
-        K = 40
+        K = int(os.environ.get("VHX_PROBE_K", "40"))
         for i in range(6):
             ctxs[i % F].trace_primary(cam, out=outs[i % F])
         torch.cuda.synchronize()

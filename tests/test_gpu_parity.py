@@ -260,7 +260,7 @@ def test_full_size_shadows_vs_oracle(gpu, oracle):
     assert sh.sum() > 100000
 
 
-DEFAULT_BUDGETS = (24, 96, 768)
+DEFAULT_BUDGETS = (24, 72, 216, 648)  # the library default (ctx.hpp)
 
 
 @pytest.mark.parametrize("budgets", [(), (1,), (1, 2, 3), (1, 2, 3, 4), (4, 40), (8, 64, 512), (64,),

@@ -82,13 +82,14 @@ struct vhx_ctx {
     float prepass_margin = 0.0f;
     DevBuf prepass_depth;  // the half-resolution depth frame
     // step budgets of the passes before the final (unbounded) one; VHX_BUDGETS="64" / "32,256" style override.
-    // {24, 96, 768}: with four frames in flight (bench frame) 0.697 ms per frame against 0.847 for {64}, 0.715 for
-    // {32, 128, 1024} and 0.740 for four budgets {16, 64, 256, 1024}: each pass re-packs the surviving rays into full
-    // waves, and the other frames fill the SIMDs a pass leaves idle. One frame at a time, {64} is faster (1.295 against
-    // 1.390 ms): the extra passes lengthen a lone frame's critical path (profiles/r02/sched_sweep_*.log).
-    uint32_t budgets[VHX_MAX_BUDGETS] = {24u, 96u, 768u, 0u};
-    uint32_t npass = 4;         // passes including the final one (1 = single pass)
-    uint32_t rpw[VHX_MAX_BUDGETS + 1] = {64u, 64u, 64u, 64u, 64u};  // rays per wave of each pass (VHX_RPW="64,16" style override; 0 = adaptive)
+    // {24, 72, 216, 648} (round 3): with eight frames in flight the bench frame takes 0.569-0.579 ms against 0.593-0.598
+    // for round 2's {24, 96, 768} (profiles/r03/sched_r03.log): the queue passes are most of the frame period
+    // (profiles/r03/pass_share_r03.log) and a finer ladder re-packs the surviving rays into full waves more often, while
+    // the other frames fill the SIMDs a pass leaves idle. One frame at a time the extra pass costs 2.6 % (1.38 against
+    // 1.345 ms), and {64} is faster still (1.295 ms): the passes lengthen a lone frame's critical path.
+    uint32_t budgets[VHX_MAX_BUDGETS] = {24u, 72u, 216u, 648u};
+    uint32_t npass = 5;         // passes including the final one (1 = single pass)
+    uint32_t rpw[VHX_MAX_BUDGETS + 1] = {64u, 64u, 64u, 64u, 64u, 64u, 64u};  // rays per wave of each pass (VHX_RPW="64,16" style override; 0 = adaptive)
     uint32_t tw = 1024;            // adaptive rays per wave: target waves per queue pass (VHX_TW)
     bool resume = true;            // abandoned rays continue from saved state (VHX_RESUME=0: re-traced from scratch)
     // passes before save_from keep no state: the rays they abandon are traced again from scratch by pass save_from,
@@ -108,7 +109,7 @@ struct vhx_ctx {
     // budgeted passes: a wave abandons its rays once fewer than sparse[p] lanes still trace (VHX_SPARSE="8,4,4").
     // Pass 0 at 12: eight frames in flight 0.645-0.651 ms per bench frame against 0.665-0.670 (8: 0.651-0.661, 16:
     // 0.646-0.657, 24 and 32 slower); the later budgeted passes gained nothing (profiles/r02/sparse*.log)
-    uint32_t sparse[VHX_MAX_BUDGETS] = {12u, 0u, 0u, 0u};
+    uint32_t sparse[VHX_MAX_BUDGETS] = {12u};
 };
 
 #define VHX_HIP(ctx, call)                                                                                         \

@@ -36,7 +36,7 @@ namespace vhx {
 #define VHX_PROF 0
 #endif
 #if VHX_PROF
-__device__ unsigned long long g_prof[4 * 16 * 2];
+__device__ unsigned long long g_prof[5 * 16 * 2];
 #define VHX_PROF_BLOCK(pass, id)                                                                                  \
     do {                                                                                                          \
         const uint64_t m_ = __ballot(1);                                                                          \
@@ -83,8 +83,9 @@ __device__ __forceinline__ void perturb_trip() {
 #ifndef VHX_WALK_PROGRESS
 #define VHX_WALK_PROGRESS 0
 #endif
+// pass slots of the default schedule {24, 72, 216, 648} (round 2's {24, 96, 768} uses slots 0, 1, 3, 4)
 __device__ __forceinline__ uint32_t pass_of_budget(uint32_t b) {
-    return b >= VHX_MAX_ITERS ? 3u : (b <= 24u ? 0u : (b <= 96u ? 1u : 2u));
+    return b >= VHX_MAX_ITERS ? 4u : (b <= 24u ? 0u : (b <= 96u ? 1u : (b <= 256u ? 2u : 3u)));
 }
 
 struct DevTree {

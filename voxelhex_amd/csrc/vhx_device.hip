@@ -1730,11 +1730,11 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
 int vhx_profile_counters(vhx_ctx *c, uint64_t *out, uint32_t n, int reset) {
     if (!c || (n && !out)) return VHX_E_INVALID_ARG;
 #if VHX_PROF
-    uint64_t v[4 * 16 * 2];
+    uint64_t v[5 * 16 * 2];
     VHX_HIP(c, hipSetDevice(c->device));
     VHX_HIP(c, hipDeviceSynchronize());
     VHX_HIP(c, hipMemcpyFromSymbol(v, HIP_SYMBOL(vhx::g_prof), sizeof(v)));
-    for (uint32_t i = 0; i < n && i < 4 * 16 * 2; ++i) out[i] = v[i];
+    for (uint32_t i = 0; i < n && i < 5 * 16 * 2; ++i) out[i] = v[i];
     if (reset) {
         std::memset(v, 0, sizeof(v));
         VHX_HIP(c, hipMemcpyToSymbol(HIP_SYMBOL(vhx::g_prof), v, sizeof(v)));
