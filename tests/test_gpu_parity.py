@@ -103,8 +103,8 @@ def test_random_rays_vs_oracle(gpu, oracle, scene, size, bd):
 def test_degenerate_directions_vs_oracle(gpu, oracle):
     """Rays whose distances are NaN or infinite (zero, NaN and infinite direction components, from inside and outside
     the tree): the reference loops until the iteration bound and reports a miss where such a ray stops making progress;
-    the kernels without byte counting end it as a miss at once (VHX_WALK_PROGRESS), which must give the same result
-    in every field, for every pass schedule."""
+    so do the kernels (a VHX_WALK_PROGRESS build ends it as a miss at once), and a ray that runs past the bound inside a
+    budgeted pass must not be resumed; the same result in every field, for every pass schedule."""
     flat = vhx.FlatTree.build_scene(N.VHX_SCENE_LATTICE_CUBE, 64, 4)
     gpu.upload(flat)
     nan, inf = np.float32("nan"), np.float32("inf")
@@ -264,7 +264,7 @@ DEFAULT_BUDGETS = (24, 72, 216, 648)  # the library default (ctx.hpp)
 
 
 @pytest.mark.parametrize("budgets", [(), (1,), (1, 2, 3), (1, 2, 3, 4), (4, 40), (8, 64, 512), (64,),
-                                     (16, 64, 256, 1024), DEFAULT_BUDGETS])
+                                     (16, 64, 256, 1024), (1, 2, 4, 8, 16, 32), DEFAULT_BUDGETS])
 def test_multipass_schedule_is_bit_identical(gpu, oracle, budgets):
     """The multi-pass scheduler (vhx_set_pass_budgets) abandons and re-traces rays; every schedule, down to a
     1-step first budget that requeues nearly every ray, must give the oracle's results (incl. byte counts)."""
@@ -342,7 +342,7 @@ def test_scheduler_variants_are_bit_identical(oracle, monkeypatch, env):
 
 
 def test_pass_budget_validation(gpu):
-    for bad in ((0,), (5, 5), (9, 3), (1, 2, 3, 4, 5), (1 << 22,)):
+    for bad in ((0,), (5, 5), (9, 3), (1, 2, 3, 4, 5, 6, 7), (1 << 22,)):  # VHX_MAX_BUDGETS = 6
         with pytest.raises(N.VhxError):
             gpu.set_pass_budgets(bad)
     gpu.set_pass_budgets(DEFAULT_BUDGETS)
