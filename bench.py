@@ -85,7 +85,7 @@ def parse():
                    help="opt-in approximate mode (vhx_set_depth_prepass, not the reference semantics): a half-resolution "
                         "depth prepass, full-resolution rays start at the min of 4 texels minus MARGIN")
     p.add_argument("--budgets", default=None, metavar="B1,B2,...",
-                   help="step budgets of the pass schedule (vhx_set_pass_budgets; \"\" = one pass); default: the library's {24, 72, 216, 648}, one pass with --mip-lod (its rays are short: 0.092 against 0.136 ms per depth-1 frame, profiles/r02/mips/headline/budgets)")
+                   help="step budgets of the pass schedule (vhx_set_pass_budgets; \"\" = one pass); default: the library's adaptive choice ({24, 72, 216, 648} with frames in flight, {64} for a lone frame), one pass with --mip-lod (its rays are short: 0.092 against 0.136 ms per depth-1 frame, profiles/r02/mips/headline/budgets)")
     p.add_argument("--mip-lod", type=int, default=None, metavar="DEPTH",
                    help="opt-in MIP stand-in mode (not the reference path): the scene inserted into a host BoxTree with "
                         "MIP maps on, flattened down to DEPTH (vhx_boxtree_flatten_lod) and traced with its node MIPs "
@@ -596,6 +596,9 @@ def main():
         elapsed = float(tt.item())
     # ---- frame check (untimed, N = 1): the last frame of every context in flight equals one context tracing the
     # same camera alone, and the committed golden digests where the workload is a golden case
+    # the schedule the timed frames ran (adaptive by default: the frames-in-flight one once other contexts' frames are
+    # in flight; vhx_get_pass_budgets), read before the untimed frames below
+    sched_timed = None if mg is not None else rts[-1].pass_budgets()
     frames_check = None
     if mg is None and world == 1 and not args.no_frame_check:
         frames_check = check_frames(args, rt, rts, outs, last_cam, light, W, H, dev)
@@ -618,6 +621,7 @@ def main():
                 break
             iso.append(rt.sync())
     kernel_ms_isolated = float(np.median(iso)) if iso else None
+    sched_iso = None if mg is not None else rt.pass_budgets()
     if not ev:
         kernel_ms = kernel_ms_isolated
 
@@ -757,7 +761,11 @@ def main():
             "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": "f32",
             "frames_in_flight": F, "gpu_max_hw_queues": queues,
             "pass_budgets": args.budgets if args.budgets is not None else ("one pass" if args.mip_lod is not None
-                                                                           else "library default"),
+                                                                           else "library default (adaptive)"),
+            "schedule": None if sched_timed is None else {
+                "timed_frames": {"budgets": list(sched_timed[0]), "choice": sched_timed[1]},
+                "isolated_frames": None if sched_iso is None else {"budgets": list(sched_iso[0]),
+                                                                   "choice": sched_iso[1]}},
             "data": "model file" if args.vox else "synthetic",
             "config": {"workload": ("BASELINE config 4: " if cfg4 else "") + f"primary rays {W}x{H}, {args.size}^3 "
                                    + (f".vox model {os.path.basename(args.vox)}" if args.vox

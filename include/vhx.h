@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define VHX_ABI_VERSION 2u
+#define VHX_ABI_VERSION 3u
 
 /* ---- error codes ------------------------------------------------------------------------------------------ */
 #define VHX_OK 0
@@ -158,10 +158,18 @@ int vhx_sync(vhx_ctx *ctx, float *last_trace_ms);
 /* Ray scheduling (no reference counterpart; results do not depend on it). A trace runs n+1 passes: pass i abandons
  * rays that need more than budgets[i] loop steps (saving their traversal state) and the next pass resumes them, 64
  * such rays per wave; the last pass is unbounded. n = 0 is a single pass. Budgets strictly increasing,
- * 0 < b < 2^22, n <= VHX_MAX_BUDGETS. Default {24, 72, 216, 648}, tuned for frames in flight (vhx_create_shared);
- * {64} gives the shortest latency of a lone frame (environment override VHX_BUDGETS="64"). */
+ * 0 < b < 2^22, n <= VHX_MAX_BUDGETS.
+ * By default the schedule is adaptive: a trace submitted while another context of the same tree (vhx_create_shared)
+ * has a frame in flight on another stream runs the frames-in-flight schedule {24, 72, 216, 648}; otherwise (one frame
+ * at a time, or frames serialised on one stream) the lone-frame schedule {64}. vhx_set_pass_budgets fixes the
+ * budgets (and ends the adaptive choice; vhx_set_adaptive_schedule(ctx, 1) restores it); the environment overrides
+ * VHX_BUDGETS, VHX_SPARSE and VHX_QWAVES fix it likewise. */
 #define VHX_MAX_BUDGETS 6
 int vhx_set_pass_budgets(vhx_ctx *ctx, const uint32_t *budgets, uint32_t n);
+int vhx_set_adaptive_schedule(vhx_ctx *ctx, int on);
+/* The budgets of the context's last trace (or the fixed ones before any), n of them (budgets: VHX_MAX_BUDGETS entries,
+ * may be NULL); *schedule (may be NULL) = 1 the frames-in-flight schedule, 0 the lone-frame one, -1 fixed. */
+int vhx_get_pass_budgets(const vhx_ctx *ctx, uint32_t *budgets, uint32_t *n, int *schedule);
 
 /* Tree upload ----------------------------------------------------------------------------------------------- */
 /* Copies the flattened tree to HBM (full residency) and builds the device-side layout. */

@@ -59,6 +59,12 @@ def test_eight_frames_in_flight_match_golden():
             cams = [(cam_a if (f + rnd) % 2 == 0 else cam_b) for f in range(F)]
             for r, c, o in zip(ctxs, cams, outs):
                 r.trace_primary(c, out=o)
+            # the adaptive schedule (vhx.h, vhx_get_pass_budgets): the first frame of a round is submitted with nothing
+            # in flight (the lone-frame schedule), every later one while the first is still running (a 3840x2160
+            # frame takes > 1 ms; the frames-in-flight schedule) -- and the frames are the same either way
+            sched = [r.pass_budgets() for r in ctxs]
+            assert sched[0] == ((64,), "idle"), sched[0]
+            assert all(sc == ((24, 72, 216, 648), "busy") for sc in sched[1:]), sched
             for s in streams:
                 s.synchronize()
             for f, (c, o) in enumerate(zip(cams, outs)):

@@ -348,6 +348,24 @@ def test_pass_budget_validation(gpu):
     gpu.set_pass_budgets(DEFAULT_BUDGETS)
 
 
+def test_adaptive_schedule_api(gpu):
+    """vhx_set_pass_budgets fixes the schedule, vhx_set_adaptive_schedule restores the adaptive choice (a lone
+    context: the lone-frame schedule {64}); vhx_get_pass_budgets reports the last trace's."""
+    flat = vhx.FlatTree.build_scene(N.VHX_SCENE_LATTICE_CUBE, 64, 4)
+    gpu.upload(flat)
+    o, d = rand_rays(np.random.default_rng(5), 64, 5000)
+    try:
+        gpu.set_pass_budgets((8, 64))
+        ref = gpu.trace_rays(o, d, fields=("value", "depth"))
+        assert gpu.pass_budgets() == ((8, 64), "fixed")
+        gpu.set_adaptive_schedule(True)
+        got = gpu.trace_rays(o, d, fields=("value", "depth"))
+        assert gpu.pass_budgets() == ((64,), "idle")
+        assert_same(got, ref, "adaptive vs fixed schedule")
+    finally:
+        gpu.set_pass_budgets(DEFAULT_BUDGETS)
+
+
 def _device_hits(n):
     import torch
     return {"value": torch.empty(n, dtype=torch.int32, device="cuda"),

@@ -27,6 +27,7 @@ VHX_E_RCCL = -6
 VHX_MGPU_ID_BYTES = 128
 VHX_MGPU_MAX_INFLIGHT = 16
 VHX_MGPU_MAX_ROOT_SLOTS = 4
+VHX_MAX_BUDGETS = 6
 VHX_E_TREE_INVALID_SIZE = -10
 VHX_E_TREE_INVALID_BRICK_DIMENSION = -11
 VHX_E_TREE_INVALID_STRUCTURE = -12
@@ -94,6 +95,8 @@ SIGNATURES = [
     ("vhx_get_stream", c_int, [c_void_p, P(c_void_p)]),
     ("vhx_sync", c_int, [c_void_p, P(c_f32)]),
     ("vhx_set_pass_budgets", c_int, [c_void_p, P(c_u32), c_u32]),
+    ("vhx_set_adaptive_schedule", c_int, [c_void_p, c_int]),
+    ("vhx_get_pass_budgets", c_int, [c_void_p, P(c_u32), P(c_u32), P(c_int)]),
     ("vhx_upload_tree", c_int, [c_void_p, P(TreeDesc)]),
     ("vhx_upload_tree_device", c_int, [c_void_p, P(TreeDesc)]),
     ("vhx_set_node_mips", c_int, [c_void_p, c_void_p, c_u32]),

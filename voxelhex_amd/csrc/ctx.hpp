@@ -81,14 +81,32 @@ struct vhx_ctx {
     bool prepass = false, in_prepass = false;
     float prepass_margin = 0.0f;
     DevBuf prepass_depth;  // the half-resolution depth frame
-    // step budgets of the passes before the final (unbounded) one; VHX_BUDGETS="64" / "32,256" style override.
-    // {24, 72, 216, 648} (round 3): with eight frames in flight the bench frame takes 0.569-0.579 ms against 0.593-0.598
-    // for round 2's {24, 96, 768} (profiles/r03/sched_r03.log): the queue passes are most of the frame period
-    // (profiles/r03/pass_share_r03.log) and a finer ladder re-packs the surviving rays into full waves more often, while
-    // the other frames fill the SIMDs a pass leaves idle. One frame at a time the extra pass costs 2.6 % (1.38 against
-    // 1.345 ms), and {64} is faster still (1.295 ms): the passes lengthen a lone frame's critical path.
+    // Ray schedule of a trace: step budgets of the passes before the final (unbounded) one, the sparse-wave thresholds
+    // of the budgeted passes and the waves of a queue pass. Results never depend on it (bit-identical for any
+    // schedule); the frame time does, and what is best depends on whether the frame shares the GPU with other frames.
+    struct Sched {
+        uint32_t budgets[VHX_MAX_BUDGETS];
+        uint32_t npass;                      // passes including the final one (1 = single pass)
+        uint32_t sparse[VHX_MAX_BUDGETS];    // abandon a wave's rays once fewer lanes still trace (0 = off)
+        uint32_t queue_waves_per_cu;         // waves of a queue pass per CU
+    };
+    // Adaptive scheduling (default; vhx_set_pass_budgets or an environment knob fixes the schedule instead): at each
+    // trace the context looks at the other contexts of its tree (vhx_create_shared) and picks
+    //  * `busy` when any of them still has a frame in flight on another stream: {24, 72, 216, 648} with 4 queue waves per
+    //    CU -- the bench frame at eight frames in flight 0.561-0.567 ms against 0.593-0.598 for round 2's {24, 96, 768}
+    //    at 8 waves per CU (profiles/r03/sched_r03.log, ladder_r03b.log, qwaves_r03.log): the queue passes are most of
+    //    the frame period (pass_share_r03.log); a finer ladder re-packs the surviving rays into full waves more often,
+    //    and fewer queue waves leave the SIMDs to the other frames' first passes;
+    //  * `idle` otherwise (one frame at a time, or frames serialised on one stream): {64} without sparse-wave
+    //    abandonment at 8 queue waves per CU -- 1.22 ms for the lone bench frame against 1.37 ms for the busy schedule
+    //    (profiles/r03/isolated_r03*.log): every extra pass lengthens a lone frame's critical path.
+    bool adaptive = true;
+    Sched sched_busy = {{24u, 72u, 216u, 648u}, 5u, {12u}, 4u};
+    Sched sched_idle = {{64u}, 2u, {0u}, 8u};
+    int last_sched = -1;  // the schedule of the last trace: 1 busy, 0 idle, -1 fixed (vhx_get_pass_budgets)
+    // the schedule in force (the selected one, or the fixed one)
     uint32_t budgets[VHX_MAX_BUDGETS] = {24u, 72u, 216u, 648u};
-    uint32_t npass = 5;         // passes including the final one (1 = single pass)
+    uint32_t npass = 5;
     uint32_t rpw[VHX_MAX_BUDGETS + 1] = {64u, 64u, 64u, 64u, 64u, 64u, 64u};  // rays per wave of each pass (VHX_RPW="64,16" style override; 0 = adaptive)
     uint32_t tw = 1024;            // adaptive rays per wave: target waves per queue pass (VHX_TW)
     bool resume = true;            // abandoned rays continue from saved state (VHX_RESUME=0: re-traced from scratch)
@@ -98,17 +116,19 @@ struct vhx_ctx {
     uint32_t xcd_group = 16;       // pass-0 XCD-aware block runs (VHX_XCDG; 0 = dispatch order)
     uint32_t qblock = 256;         // threads per workgroup of a queue pass (VHX_QBLOCK=64: one wave per workgroup)
     uint32_t queue_blocks = 2048;  // workgroups of a queue pass (CUs x resident workgroups)
-    // waves of a queue pass (VHX_QWAVES): 8 per CU. The bench frame's tail pass (148 k rays, 2316 chunks of 64) took
-    // 1.55 ms/frame at 2048 waves against 1.62 at 8192 and 1.82 at 1024 (fewer busy waves per CU at the start of the
-    // pass, while every chunk still starts at once)
-    uint32_t queue_waves = 2048;
+    // waves of a queue pass (VHX_QWAVES; the schedule's per-CU figure times the CUs). One frame at a time, 8 per CU:
+    // round 1's tail pass (148 k rays, 2316 chunks of 64) took 1.55 ms/frame at 2048 waves against 1.62 at 8192 and
+    // 1.82 at 1024 (fewer busy waves per CU at the start of the pass, while every chunk still starts at once); with
+    // frames in flight 4 per CU (profiles/r03/qwaves_r03.log)
+    uint32_t queue_waves = 1024;
+    uint32_t cus = 256;            // compute units of the device (the adaptive schedules' queue waves are per CU)
     uint32_t queue_waves0 = 8192;  // waves of a first queue pass over fresh rays (VHX_QWAVES0)
     uint32_t queue_waves_mid = 0;  // waves of a budgeted queue pass after the first (VHX_QWAVESM; 0 = queue_waves)
     uint32_t qxcd = 16;            // queue passes: XCD-dealt chunk runs (VHX_QXCD = run length, 0 = one counter)
     bool qxcd_all = false;         // deal every queue pass, not only the last (VHX_QXCD_ALL=1, diagnostics)
     // budgeted passes: a wave abandons its rays once fewer than sparse[p] lanes still trace (VHX_SPARSE="8,4,4").
-    // Pass 0 at 12: eight frames in flight 0.645-0.651 ms per bench frame against 0.665-0.670 (8: 0.651-0.661, 16:
-    // 0.646-0.657, 24 and 32 slower); the later budgeted passes gained nothing (profiles/r02/sparse*.log)
+    // Pass 0 at 12 under frames in flight: eight frames 0.645-0.651 ms per bench frame against 0.665-0.670 (8:
+    // 0.651-0.661, 16: 0.646-0.657, 24 and 32 slower); the later budgeted passes gained nothing (profiles/r02/sparse*.log)
     uint32_t sparse[VHX_MAX_BUDGETS] = {12u};
 };
 

@@ -965,7 +965,33 @@ static int finish_out(vhx_ctx *c, HostOut &ho) {
 
 // Multi-pass plumbing: allocates queues, chunk lists and counters for `nout` rays whose pass 0 runs in `nblocks0`
 // workgroups of 256 (may synchronise; called before the trace is timed). Returns the number of passes to run.
+// Adaptive scheduling (ctx.hpp, Sched): the busy schedule while another context of the tree has a frame in flight on
+// another stream (its last trace's use event not yet reached), else the idle one. A host-side query per other context;
+// no waits.
+static void select_schedule(vhx_ctx *c) {
+    if (!c->adaptive) {
+        c->last_sched = -1;
+        return;
+    }
+    bool busy = false;
+    {
+        std::lock_guard<std::mutex> lock(c->tree->mu);
+        for (vhx_ctx *u : c->tree->users)
+            if (u != c && u->use_recorded && u->stream != c->stream && hipEventQuery(u->use_ev) == hipErrorNotReady) {
+                busy = true;
+                break;
+            }
+    }
+    const vhx_ctx::Sched &s = busy ? c->sched_busy : c->sched_idle;
+    std::memcpy(c->budgets, s.budgets, sizeof(c->budgets));
+    std::memcpy(c->sparse, s.sparse, sizeof(c->sparse));
+    c->npass = s.npass;
+    c->queue_waves = s.queue_waves_per_cu * c->cus;
+    c->last_sched = busy ? 1 : 0;
+}
+
 static int prepare_passes(vhx_ctx *c, uint64_t nout, uint64_t nblocks0, uint32_t &npass, bool shadow = false) {
+    select_schedule(c);
     npass = nout < 0x7FFFFFFFull ? c->npass : 1u;
     if (npass < 2 && !shadow) return VHX_OK;
     uint64_t chunks = std::max(nblocks0, (nout + 1023) / 1024), list = nblocks0 * 256;
@@ -1152,8 +1178,10 @@ int vhx_create(int hip_device, vhx_ctx **out) {
                 if (v > 0 && v < VHX_MAX_ITERS) b[nb++] = (uint32_t)v;
                 q = *end == ',' ? end + 1 : end;
             }
-            vhx_set_pass_budgets(c, b, nb);
+            vhx_set_pass_budgets(c, b, nb);  // fixes the schedule (no adaptive choice)
         }
+        const char *pa = getenv("VHX_ADAPTIVE");  // "0": the busy schedule always (diagnostics)
+        if (pa && pa[0] == '0') c->adaptive = false;
         const char *pr = getenv("VHX_RPW");  // rays per wave of the queue passes 1.., e.g. "64,16"
         if (pr) {
             uint32_t k = 1;
@@ -1177,11 +1205,15 @@ int vhx_create(int hip_device, vhx_ctx **out) {
         if (pq && (atoi(pq) == 64 || atoi(pq) == 128)) c->qblock = (uint32_t)atoi(pq);
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, hip_device) == hipSuccess && prop.multiProcessorCount > 0) {
-            c->queue_blocks = (uint32_t)prop.multiProcessorCount * 8u;
-            c->queue_waves = (uint32_t)prop.multiProcessorCount * 8u;
+            c->cus = (uint32_t)prop.multiProcessorCount;
+            c->queue_blocks = c->cus * 8u;
+            c->queue_waves = c->sched_busy.queue_waves_per_cu * c->cus;
         }
-        const char *pw = getenv("VHX_QWAVES");  // after the device default
-        if (pw && atoi(pw) > 0) c->queue_waves = (uint32_t)atoi(pw);
+        const char *pw = getenv("VHX_QWAVES");  // after the device default; fixes the schedule
+        if (pw && atoi(pw) > 0) {
+            c->queue_waves = (uint32_t)atoi(pw);
+            c->adaptive = false;
+        }
         const char *pwm = getenv("VHX_QWAVESM");
         if (pwm && atoi(pwm) > 0) c->queue_waves_mid = (uint32_t)atoi(pwm);
         const char *pw0 = getenv("VHX_QWAVES0");
@@ -1198,6 +1230,7 @@ int vhx_create(int hip_device, vhx_ctx **out) {
                 c->sparse[k++] = v <= 64 ? (uint32_t)v : 0u;
                 q = *end == ',' ? end + 1 : end;
             }
+            c->adaptive = false;  // fixes the schedule
         }
         const char *pqa = getenv("VHX_QXCD_ALL");
         if (pqa && pqa[0] == '1') c->qxcd_all = true;
@@ -1254,6 +1287,27 @@ int vhx_set_pass_budgets(vhx_ctx *c, const uint32_t *budgets, uint32_t n) {
             return fail(c, VHX_E_INVALID_ARG, "pass budgets must be increasing, > 0 and < 2^22");
     for (uint32_t i = 0; i < VHX_MAX_BUDGETS; ++i) c->budgets[i] = i < n ? budgets[i] : 0u;
     c->npass = n + 1;
+    if (c->adaptive) {  // leaving the adaptive choice: the rest of the schedule is the busy one's
+        std::memcpy(c->sparse, c->sched_busy.sparse, sizeof(c->sparse));
+        c->queue_waves = c->sched_busy.queue_waves_per_cu * c->cus;
+        c->adaptive = false;
+    }
+    c->last_sched = -1;
+    return VHX_OK;
+}
+
+int vhx_set_adaptive_schedule(vhx_ctx *c, int on) {
+    if (!c) return VHX_E_INVALID_ARG;
+    c->adaptive = on != 0;
+    return VHX_OK;
+}
+
+int vhx_get_pass_budgets(const vhx_ctx *c, uint32_t *budgets, uint32_t *n, int *sched) {
+    if (!c || !n) return VHX_E_INVALID_ARG;
+    *n = c->npass > 0 ? c->npass - 1 : 0;
+    if (budgets)
+        for (uint32_t i = 0; i < VHX_MAX_BUDGETS; ++i) budgets[i] = i < *n ? c->budgets[i] : 0u;
+    if (sched) *sched = c->last_sched;
     return VHX_OK;
 }
 
@@ -1396,6 +1450,10 @@ void vhx::copy_sched(vhx_ctx *c, const vhx_ctx *owner) {
     c->tw = owner->tw;
     c->resume = owner->resume;
     c->save_from = owner->save_from;
+    c->adaptive = owner->adaptive;
+    c->sched_busy = owner->sched_busy;
+    c->sched_idle = owner->sched_idle;
+    c->cus = owner->cus;
     c->xcd_group = owner->xcd_group;
     c->qblock = owner->qblock;
     c->queue_blocks = owner->queue_blocks;

@@ -278,6 +278,17 @@ class Raytracer:
         b = (ctypes.c_uint32 * max(1, len(budgets)))(*budgets)
         self._check(N.lib().vhx_set_pass_budgets(self._h, b, len(budgets)))
 
+    def set_adaptive_schedule(self, on=True):
+        """Restores (or ends) the adaptive choice between the frames-in-flight and the lone-frame schedule."""
+        self._check(N.lib().vhx_set_adaptive_schedule(self._h, 1 if on else 0))
+
+    def pass_budgets(self):
+        """(budgets of the last trace, schedule): schedule "busy" (frames in flight), "idle" (lone frame) or "fixed"."""
+        b = (ctypes.c_uint32 * N.VHX_MAX_BUDGETS)()
+        n, sched = ctypes.c_uint32(), ctypes.c_int()
+        self._check(N.lib().vhx_get_pass_budgets(self._h, b, ctypes.byref(n), ctypes.byref(sched)))
+        return tuple(b[:n.value]), {1: "busy", 0: "idle"}.get(sched.value, "fixed")
+
     def sync(self):
         ms = ctypes.c_float()
         self._check(N.lib().vhx_sync(self._h, ctypes.byref(ms)))
