@@ -1,6 +1,6 @@
 """Isolated-frame latency (one frame at a time, synchronised; libvhx's own events, like bench.py's kernel_ms_isolated)
 of the bench frame for each pass schedule given on the command line ("" = one pass); env knobs such as VHX_QWAVES
-apply.   usage: probe_isolated_r03.py "64" "24,72,216,648" ..."""
+apply.   usage: probe_isolated_r03.py "64" "24,72,216,648" adaptive ..."""
 import os
 import sys
 
@@ -22,7 +22,8 @@ torch.cuda.synchronize()
 ref = None
 env = " ".join(f"{k}={v}" for k, v in sorted(os.environ.items()) if k.startswith("VHX_"))
 for spec in sys.argv[1:]:
-    rt.set_pass_budgets(tuple(int(x) for x in spec.split(",") if x))
+    if spec != "adaptive":  # "adaptive": the library's own choice (the lone-frame schedule here)
+        rt.set_pass_budgets(tuple(int(x) for x in spec.split(",") if x))
     ms = []
     for i in range(23):
         rt.trace_primary(cam, out=out)
