@@ -94,12 +94,15 @@ struct vhx_ctx {
     // trace the context looks at the other contexts of its tree (vhx_create_shared) and picks
     //  * `busy` when any of them still has a frame in flight on another stream: {24, 72, 216, 648} with 4 queue waves per
     //    CU -- the bench frame at eight frames in flight 0.561-0.567 ms against 0.593-0.598 for round 2's {24, 96, 768}
-    //    at 8 waves per CU (profiles/r03/sched_r03.log, ladder_r03b.log, qwaves_r03.log): the queue passes are most of
+    //    at 8 waves per CU (profiles/r03/sched_r03.log, ladder_r03b.log; 4 against 8 queue waves per CU is within noise
+    //    at eight frames in flight, 0.562-0.566 against 0.563-0.565 ms, qwaves_r03.log): the queue passes are most of
     //    the frame period (pass_share_r03.log); a finer ladder re-packs the surviving rays into full waves more often,
     //    and fewer queue waves leave the SIMDs to the other frames' first passes;
     //  * `idle` otherwise (one frame at a time, or frames serialised on one stream): {64} without sparse-wave
-    //    abandonment at 8 queue waves per CU -- 1.22 ms for the lone bench frame against 1.37 ms for the busy schedule
-    //    (profiles/r03/isolated_r03*.log): every extra pass lengthens a lone frame's critical path.
+    //    abandonment at 8 queue waves per CU -- 1.22 ms for the lone bench frame against 1.54 ms for the busy schedule
+    //    run alone (profiles/r03/isolated_r03.log, reentry_r03c/isolated.log; {64, 1024}, {64, 512}, {48, 768} and
+    //    three-budget ladders 1.31-1.51 ms, fewer rays per wave in a last pass no better): every extra pass lengthens a
+    //    lone frame's critical path.
     bool adaptive = true;
     Sched sched_busy = {{24u, 72u, 216u, 648u}, 5u, {12u}, 4u};
     Sched sched_idle = {{64u}, 2u, {0u}, 8u};
@@ -119,7 +122,7 @@ struct vhx_ctx {
     // waves of a queue pass (VHX_QWAVES; the schedule's per-CU figure times the CUs). One frame at a time, 8 per CU:
     // round 1's tail pass (148 k rays, 2316 chunks of 64) took 1.55 ms/frame at 2048 waves against 1.62 at 8192 and
     // 1.82 at 1024 (fewer busy waves per CU at the start of the pass, while every chunk still starts at once); with
-    // frames in flight 4 per CU (profiles/r03/qwaves_r03.log)
+    // frames in flight 4 per CU (equal within noise there; profiles/r03/qwaves_r03.log)
     uint32_t queue_waves = 1024;
     uint32_t cus = 256;            // compute units of the device (the adaptive schedules' queue waves are per CU)
     uint32_t queue_waves0 = 8192;  // waves of a first queue pass over fresh rays (VHX_QWAVES0)
