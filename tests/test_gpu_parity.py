@@ -304,7 +304,10 @@ SCHEDULER_ENVS = [{"VHX_RESUME": "0"},                                   # aband
                   {"VHX_QXCD": "1", "VHX_RPW": "0,0", "VHX_TW": "7"},    # ... single chunks, few adaptive waves
                   {"VHX_SPARSE": "64,64,64"},                            # waves abandon as soon as one lane ends
                   {"VHX_SPARSE": "0"},                                   # no sparse-wave abandonment
-                  {"VHX_QXCD_ALL": "1", "VHX_QWAVESM": "300"}]           # every queue pass dealt over the XCDs
+                  {"VHX_QXCD_ALL": "1", "VHX_QWAVESM": "300"},           # every queue pass dealt over the XCDs
+                  {"VHX_QORDER": "16"},                                  # pass-0 queue in 16x16 tile order
+                  {"VHX_QORDER": "m8"},                                  # ... in Morton order of 8x8 tiles
+                  {"VHX_QORDER": "m32z"}]                                # ... every pixel in Morton order
 
 
 @pytest.mark.parametrize("env", SCHEDULER_ENVS, ids=lambda e: "+".join(f"{k}={v}" for k, v in e.items()))

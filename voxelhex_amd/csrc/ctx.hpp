@@ -43,6 +43,10 @@ struct TreeStore {
     ~TreeStore();
 };
 
+// default pass-0 queue orders of the two schedules (vhx_ctx::qorder encoding)
+#define VHX_QORDER_BUSY 38u  // 64x64 tiles row-major, Morton order inside ("64z")
+#define VHX_QORDER_IDLE 0u  // output-index order
+
 struct vhx_ctx {
     int device = 0;
     hipStream_t own_stream = nullptr;
@@ -89,6 +93,7 @@ struct vhx_ctx {
         uint32_t npass;                      // passes including the final one (1 = single pass)
         uint32_t sparse[VHX_MAX_BUDGETS];    // abandon a wave's rays once fewer lanes still trace (0 = off)
         uint32_t queue_waves_per_cu;         // waves of a queue pass per CU
+        uint32_t qorder;                     // order of a primary frame's pass-0 queue (vhx_ctx::qorder below)
     };
     // Adaptive scheduling (default; vhx_set_pass_budgets or an environment knob fixes the schedule instead): at each
     // trace the context looks at the other contexts of its tree (vhx_create_shared) and picks
@@ -104,8 +109,8 @@ struct vhx_ctx {
     //    three-budget ladders 1.31-1.51 ms, fewer rays per wave in a last pass no better): every extra pass lengthens a
     //    lone frame's critical path.
     bool adaptive = true;
-    Sched sched_busy = {{24u, 72u, 216u, 648u}, 5u, {12u}, 4u};
-    Sched sched_idle = {{64u}, 2u, {0u}, 8u};
+    Sched sched_busy = {{24u, 72u, 216u, 648u}, 5u, {12u}, 4u, VHX_QORDER_BUSY};
+    Sched sched_idle = {{64u}, 2u, {0u}, 8u, VHX_QORDER_IDLE};
     int last_sched = -1;  // the schedule of the last trace: 1 busy, 0 idle, -1 fixed (vhx_get_pass_budgets)
     // the schedule in force (the selected one, or the fixed one)
     uint32_t budgets[VHX_MAX_BUDGETS] = {24u, 72u, 216u, 648u};
@@ -129,6 +134,10 @@ struct vhx_ctx {
     uint32_t queue_waves_mid = 0;  // waves of a budgeted queue pass after the first (VHX_QWAVESM; 0 = queue_waves)
     uint32_t qxcd = 16;            // queue passes: XCD-dealt chunk runs (VHX_QXCD = run length, 0 = one counter)
     bool qxcd_all = false;         // deal every queue pass, not only the last (VHX_QXCD_ALL=1, diagnostics)
+    // pass-0 queue of a framebuffer frame (the schedule's, or VHX_QORDER = "[m]N[z]"): 0 output-index order; else
+    // log2 of the tile size (bits 0-3), bit 4 Morton order of the tiles, bit 5 Morton order of the pixels inside a tile
+    // (FlagOrder in vhx_device.hip)
+    uint32_t qorder = VHX_QORDER_BUSY;
     // budgeted passes: a wave abandons its rays once fewer than sparse[p] lanes still trace (VHX_SPARSE="8,4,4").
     // Pass 0 at 12 under frames in flight: eight frames 0.645-0.651 ms per bench frame against 0.665-0.670 (8:
     // 0.651-0.661, 16: 0.646-0.657, 24 and 32 slower); the later budgeted passes gained nothing (profiles/r02/sparse*.log)

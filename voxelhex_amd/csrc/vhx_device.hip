@@ -350,17 +350,68 @@ __device__ __forceinline__ uint32_t flag_bits(const void *src, uint64_t i, uint6
 #define QCTL_WORDS (16u + QCTL_PASS_WORDS * (VHX_MAX_BUDGETS + 1u))
 // zero: the queue passes' work counters (qctl[16..79]), zeroed here instead of by a separate memset launch;
 // clear (optional, n entries): an output array zeroed alongside (the shadow flags of a shadow frame)
+// Order of the pass-0 queue of a primary frame (vhx_ctx::qorder): W = 0 keeps output-index order (row-major in the
+// framebuffer layout); W > 0 lists the rays tile by tile -- TS x TS pixel tiles (TS = 1 << tsl >= 8), the tiles
+// row-major over the frame (tx per row) or, with mdim > 0, in Morton order over a 2^mdim x 2^mdim grid (tiles outside
+// the frame hold no rays), and inside a tile either its 8x8 sub-tiles row-major with their pixels row-major (a pass-0
+// wave's footprint) or, with zin, every pixel in Morton order. 2-D neighbourhoods instead of rows: a queue wave's 64
+// rays are neighbours in both directions. Only the order of the queue changes, never a result.
+struct FlagOrder {
+    uint32_t W, H, tx, ty, tsl, mdim, zin;
+};
+__device__ __forceinline__ uint32_t compact_bits(uint32_t v) {  // even bits of v -> low half
+    v &= 0x55555555u;
+    v = (v | (v >> 1)) & 0x33333333u;
+    v = (v | (v >> 2)) & 0x0F0F0F0Fu;
+    v = (v | (v >> 4)) & 0x00FF00FFu;
+    return (v | (v >> 8)) & 0x0000FFFFu;
+}
+// pixel of position k; false if it lies outside the frame
+__device__ __forceinline__ bool order_pixel(const FlagOrder &o, uint64_t k, uint32_t &px, uint32_t &py) {
+    const uint32_t t = (uint32_t)(k >> (2u * o.tsl)), r = (uint32_t)k & ((1u << (2u * o.tsl)) - 1u);
+    uint32_t gx, gy;
+    if (o.mdim) {
+        gx = compact_bits(t);
+        gy = compact_bits(t >> 1);
+    } else {
+        gx = t % o.tx;
+        gy = t / o.tx;
+    }
+    uint32_t ix, iy;
+    if (o.zin) {
+        ix = compact_bits(r);
+        iy = compact_bits(r >> 1);
+    } else {
+        const uint32_t spr = 1u << (o.tsl - 3u), sub = r >> 6, u = r & 63u;
+        ix = (sub % spr) * 8u + (u & 7u);
+        iy = (sub / spr) * 8u + (u >> 3);
+    }
+    px = (gx << o.tsl) + ix;
+    py = (gy << o.tsl) + iy;
+    return gx < o.tx && gy < o.ty && px < o.W && py < o.H;
+}
+// flags of positions k..k+3 (bit j: position k + j)
+__device__ __forceinline__ uint32_t order_bits(const uint8_t *flags, const FlagOrder &o, uint64_t k) {
+    uint32_t bits = 0;
+    for (uint32_t j = 0; j < 4u; ++j) {
+        uint32_t px, py;
+        if (order_pixel(o, k + j, px, py) && flags[(uint64_t)py * o.W + px]) bits |= 1u << j;
+    }
+    return bits;
+}
+
 template <bool HITS>
 __global__ void __launch_bounds__(256) k_count_flags(const void *__restrict__ src, uint64_t n,
                                                      uint32_t *__restrict__ counts, uint32_t *zero,
-                                                     uint32_t *__restrict__ clear = nullptr) {
+                                                     uint32_t *__restrict__ clear = nullptr, FlagOrder ord = {}) {
     __shared__ uint32_t s_cnt[4];
     if (blockIdx.x == 0)
         for (uint32_t w = threadIdx.x; w < QCTL_WORDS - 16u; w += blockDim.x) zero[w] = 0u;
     const uint64_t i = ((uint64_t)blockIdx.x * 256u + threadIdx.x) * 4u;
     if (clear)
         for (uint64_t k = i; k < n && k < i + 4u; ++k) clear[k] = 0u;
-    uint32_t c = __popc(flag_bits<HITS>(src, i, n));
+    uint32_t c = __popc(!HITS && ord.W ? (i < n ? order_bits((const uint8_t *)src, ord, i) : 0u)
+                                       : flag_bits<HITS>(src, i, n));
     for (uint32_t d = 32; d > 0; d >>= 1) c += __shfl_down(c, d);
     if ((threadIdx.x & 63u) == 0) s_cnt[threadIdx.x >> 6] = c;
     __syncthreads();
@@ -369,11 +420,13 @@ __global__ void __launch_bounds__(256) k_count_flags(const void *__restrict__ sr
 
 template <bool HITS>
 __global__ void __launch_bounds__(256) k_emit_flags(const void *__restrict__ src, uint64_t n,
-                                                    const uint32_t *__restrict__ offsets, uint32_t *__restrict__ out) {
+                                                    const uint32_t *__restrict__ offsets, uint32_t *__restrict__ out,
+                                                    FlagOrder ord = {}) {
     __shared__ uint32_t s_wave[4];
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     const uint64_t i = ((uint64_t)blockIdx.x * 256u + threadIdx.x) * 4u;
-    const uint32_t bits = flag_bits<HITS>(src, i, n);
+    const uint32_t bits = !HITS && ord.W ? (i < n ? order_bits((const uint8_t *)src, ord, i) : 0u)
+                                         : flag_bits<HITS>(src, i, n);
     const uint32_t c = __popc(bits);
     uint32_t inc = c;
     for (uint32_t d = 1; d < 64; d <<= 1) {
@@ -385,7 +438,11 @@ __global__ void __launch_bounds__(256) k_emit_flags(const void *__restrict__ src
     uint32_t o = offsets[blockIdx.x] + inc - c;
     for (uint32_t w = 0; w < wave; ++w) o += s_wave[w];
     for (uint32_t k = 0; k < 4; ++k)
-        if (bits & (1u << k)) out[o++] = (uint32_t)(i + k);
+        if (bits & (1u << k)) {
+            uint32_t px = 0, py = 0;
+            if (!HITS && ord.W) order_pixel(ord, i + k, px, py);
+            out[o++] = !HITS && ord.W ? py * ord.W + px : (uint32_t)(i + k);
+        }
 }
 
 // One wave per chunk: copies the chunk's list to the queue at its offset.
@@ -987,6 +1044,7 @@ static void select_schedule(vhx_ctx *c) {
     std::memcpy(c->sparse, s.sparse, sizeof(c->sparse));
     c->npass = s.npass;
     c->queue_waves = s.queue_waves_per_cu * c->cus;
+    c->qorder = s.qorder;
     c->last_sched = busy ? 1 : 0;
 }
 
@@ -1077,17 +1135,30 @@ static int compact_chunks(vhx_ctx *c, uint32_t nchunks_host, const uint32_t *n_i
 template <bool COUNT, int BD, bool MIP = false>
 static int launch_queue_passes(vhx_ctx *c, const DevTree &t, const CamD &cam, const RaySrc &src, const OutD &o,
                                uint32_t first, uint32_t npass, uint64_t nout, uint64_t nblocks0,
-                               bool flags_pass0 = false) {
+                               bool flags_pass0 = false, uint32_t order_w = 0, uint32_t order_h = 0) {
     uint32_t *ctl = (uint32_t *)c->qctl.ptr;
     int rc = VHX_OK;
     if (first > 0 && npass > 1) {
         if (flags_pass0) {  // primary frames: per-ray flags compacted in output-index (frame) order
-            const unsigned nb = (unsigned)((nout + 1023) / 1024);
+            // block order (c->qorder, framebuffer layout only): positions over the frame's 16x16 blocks
+            FlagOrder ord{};
+            uint64_t npos = nout;
+            if (c->qorder && order_w) {
+                const uint32_t tsl = c->qorder & 15u, ts = 1u << tsl;
+                ord = FlagOrder{order_w, order_h, (order_w + ts - 1u) / ts, (order_h + ts - 1u) / ts, tsl, 0u,
+                                (c->qorder & 32u) ? 1u : 0u};
+                if (c->qorder & 16u)  // Morton order over the smallest 2^m x 2^m grid of tiles covering the frame
+                    while ((1u << ord.mdim) < std::max(ord.tx, ord.ty)) ++ord.mdim;
+                const uint64_t tiles = ord.mdim ? 1ull << (2u * ord.mdim) : (uint64_t)ord.tx * ord.ty;
+                npos = tiles << (2u * tsl);
+                if (ord.mdim == 0 && (c->qorder & 16u)) npos = 1ull << (2u * tsl);  // one tile: Morton = row-major
+            }
+            const unsigned nb = (unsigned)((npos + 1023) / 1024);
             uint32_t *counts = (uint32_t *)c->counts.ptr, *offsets = (uint32_t *)c->offsets.ptr;
             const uint8_t *flags = (const uint8_t *)c->flags.ptr;
-            k_count_flags<false><<<nb, 256, 0, c->stream>>>(flags, nout, counts, ctl + 16);
+            k_count_flags<false><<<nb, 256, 0, c->stream>>>(flags, npos, counts, ctl + 16, nullptr, ord);
             k_scan_counts<<<1, SCAN_THREADS, 0, c->stream>>>(counts, nb, nullptr, 1, c->tw, offsets, ctl);
-            k_emit_flags<false><<<nb, 256, 0, c->stream>>>(flags, nout, offsets, (uint32_t *)c->queue[0].ptr);
+            k_emit_flags<false><<<nb, 256, 0, c->stream>>>(flags, npos, offsets, (uint32_t *)c->queue[0].ptr, ord);
             VHX_HIP(c, hipGetLastError());
             debug_passes(c, "compacted flags");
         } else {
@@ -1232,6 +1303,19 @@ int vhx_create(int hip_device, vhx_ctx **out) {
             }
             c->adaptive = false;  // fixes the schedule
         }
+        // pass-0 queue order: "[m]N[z]": NxN tiles, row-major or (m) in Morton order, inside each tile 8x8 sub-tiles
+        // row-major or (z) every pixel in Morton order; "0" = output index
+        const char *pqo = getenv("VHX_QORDER");
+        if (pqo) {
+            const bool m = pqo[0] == 'm';
+            char *end = nullptr;
+            const long ts = strtol(pqo + (m ? 1 : 0), &end, 10);
+            const bool z = end && *end == 'z';
+            uint32_t l = 0;
+            while (l < 12u && (1l << l) < ts) ++l;
+            c->qorder = ts >= 8 && ts <= 4096 && (1l << l) == ts ? l | (m ? 16u : 0u) | (z ? 32u : 0u) : 0u;
+            c->sched_busy.qorder = c->sched_idle.qorder = c->qorder;  // both schedules (the rest stays adaptive)
+        }
         const char *pqa = getenv("VHX_QXCD_ALL");
         if (pqa && pqa[0] == '1') c->qxcd_all = true;
     }
@@ -1290,6 +1374,7 @@ int vhx_set_pass_budgets(vhx_ctx *c, const uint32_t *budgets, uint32_t n) {
     if (c->adaptive) {  // leaving the adaptive choice: the rest of the schedule is the busy one's
         std::memcpy(c->sparse, c->sched_busy.sparse, sizeof(c->sparse));
         c->queue_waves = c->sched_busy.queue_waves_per_cu * c->cus;
+        c->qorder = c->sched_busy.qorder;
         c->adaptive = false;
     }
     c->last_sched = -1;
@@ -1450,6 +1535,7 @@ void vhx::copy_sched(vhx_ctx *c, const vhx_ctx *owner) {
     c->tw = owner->tw;
     c->resume = owner->resume;
     c->save_from = owner->save_from;
+    c->qorder = owner->qorder;
     c->adaptive = owner->adaptive;
     c->sched_busy = owner->sched_busy;
     c->sched_idle = owner->sched_idle;
@@ -1753,6 +1839,7 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
 
     const bool count = ho.dev.bytes != nullptr;
     int qrc = VHX_OK;
+    const uint32_t ow = layout == VHX_LAYOUT_FRAMEBUFFER ? cam->width : 0u;  // the queue order's frame (c->qorder)
     auto launch = [&](auto bd_tag) {
         constexpr int BD = decltype(bd_tag)::value;
         PassQ q0 = pass_q(c, 0, npass);
@@ -1760,11 +1847,11 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
         if (t.mips) {  // MIP stand-ins (no byte counting, no depth prepass: refused above)
             k_trace_primary<false, BD, false, true><<<(unsigned)nblocks, 256, 0, c->stream>>>(
                 t, cd, ho.dev, T, tiles_x, tile_start, tile_stride, layout, bpx, bpt, q0);
-            qrc = launch_queue_passes<false, BD, true>(c, t, cd, src, ho.dev, 1, npass, nout, nblocks, true);
+            qrc = launch_queue_passes<false, BD, true>(c, t, cd, src, ho.dev, 1, npass, nout, nblocks, true, ow, cam->height);
         } else if (count) {
             k_trace_primary<true, BD><<<(unsigned)nblocks, 256, 0, c->stream>>>(
                 t, cd, ho.dev, T, tiles_x, tile_start, tile_stride, layout, bpx, bpt, q0);
-            qrc = launch_queue_passes<true, BD>(c, t, cd, src, ho.dev, 1, npass, nout, nblocks, true);
+            qrc = launch_queue_passes<true, BD>(c, t, cd, src, ho.dev, 1, npass, nout, nblocks, true, ow, cam->height);
         } else {
             if (fast)
                 k_trace_primary<false, BD, true><<<(unsigned)nblocks, 256, 0, c->stream>>>(
@@ -1772,7 +1859,7 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
             else
                 k_trace_primary<false, BD><<<(unsigned)nblocks, 256, 0, c->stream>>>(
                     t, cd, ho.dev, T, tiles_x, tile_start, tile_stride, layout, bpx, bpt, q0);
-            qrc = launch_queue_passes<false, BD>(c, t, cd, src, ho.dev, 1, npass, nout, nblocks, true);
+            qrc = launch_queue_passes<false, BD>(c, t, cd, src, ho.dev, 1, npass, nout, nblocks, true, ow, cam->height);
         }
     };
     if (!dispatch_bd(c->tree->desc.brick_dim, launch)) return fail(c, VHX_E_INVALID_ARG, "unsupported brick_dim");
