@@ -138,6 +138,7 @@ struct vhx_ctx {
     // log2 of the tile size (bits 0-3), bit 4 Morton order of the tiles, bit 5 Morton order of the pixels inside a tile
     // (FlagOrder in vhx_device.hip)
     uint32_t qorder = VHX_QORDER_BUSY;
+    uint32_t last_fb_w = 0, last_fb_h = 0;  // the last primary framebuffer frame traced on this context
     // budgeted passes: a wave abandons its rays once fewer than sparse[p] lanes still trace (VHX_SPARSE="8,4,4").
     // Pass 0 at 12 under frames in flight: eight frames 0.645-0.651 ms per bench frame against 0.665-0.670 (8:
     // 0.651-0.661, 16: 0.646-0.657, 24 and 32 slower); the later budgeted passes gained nothing (profiles/r02/sparse*.log)

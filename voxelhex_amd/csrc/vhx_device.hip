@@ -390,12 +390,15 @@ __device__ __forceinline__ bool order_pixel(const FlagOrder &o, uint64_t k, uint
     py = (gy << o.tsl) + iy;
     return gx < o.tx && gy < o.ty && px < o.W && py < o.H;
 }
-// flags of positions k..k+3 (bit j: position k + j)
-__device__ __forceinline__ uint32_t order_bits(const uint8_t *flags, const FlagOrder &o, uint64_t k) {
+// flags of positions k..k+3 (bit j: position k + j): a pass-0 flag byte, or with HITS a hit value != VHX_EMPTY
+template <bool HITS>
+__device__ __forceinline__ uint32_t order_bits(const void *src, const FlagOrder &o, uint64_t k) {
     uint32_t bits = 0;
     for (uint32_t j = 0; j < 4u; ++j) {
         uint32_t px, py;
-        if (order_pixel(o, k + j, px, py) && flags[(uint64_t)py * o.W + px]) bits |= 1u << j;
+        if (!order_pixel(o, k + j, px, py)) continue;
+        const uint64_t i = (uint64_t)py * o.W + px;
+        if (HITS ? ((const uint32_t *)src)[i] != VHX_EMPTY : ((const uint8_t *)src)[i] != 0) bits |= 1u << j;
     }
     return bits;
 }
@@ -403,15 +406,15 @@ __device__ __forceinline__ uint32_t order_bits(const uint8_t *flags, const FlagO
 template <bool HITS>
 __global__ void __launch_bounds__(256) k_count_flags(const void *__restrict__ src, uint64_t n,
                                                      uint32_t *__restrict__ counts, uint32_t *zero,
-                                                     uint32_t *__restrict__ clear = nullptr, FlagOrder ord = {}) {
+                                                     uint32_t *__restrict__ clear = nullptr, FlagOrder ord = {},
+                                                     uint64_t nclear = 0) {
     __shared__ uint32_t s_cnt[4];
     if (blockIdx.x == 0)
         for (uint32_t w = threadIdx.x; w < QCTL_WORDS - 16u; w += blockDim.x) zero[w] = 0u;
     const uint64_t i = ((uint64_t)blockIdx.x * 256u + threadIdx.x) * 4u;
     if (clear)
-        for (uint64_t k = i; k < n && k < i + 4u; ++k) clear[k] = 0u;
-    uint32_t c = __popc(!HITS && ord.W ? (i < n ? order_bits((const uint8_t *)src, ord, i) : 0u)
-                                       : flag_bits<HITS>(src, i, n));
+        for (uint64_t k = i; k < nclear && k < i + 4u; ++k) clear[k] = 0u;
+    uint32_t c = __popc(ord.W ? (i < n ? order_bits<HITS>(src, ord, i) : 0u) : flag_bits<HITS>(src, i, n));
     for (uint32_t d = 32; d > 0; d >>= 1) c += __shfl_down(c, d);
     if ((threadIdx.x & 63u) == 0) s_cnt[threadIdx.x >> 6] = c;
     __syncthreads();
@@ -425,8 +428,7 @@ __global__ void __launch_bounds__(256) k_emit_flags(const void *__restrict__ src
     __shared__ uint32_t s_wave[4];
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     const uint64_t i = ((uint64_t)blockIdx.x * 256u + threadIdx.x) * 4u;
-    const uint32_t bits = !HITS && ord.W ? (i < n ? order_bits((const uint8_t *)src, ord, i) : 0u)
-                                         : flag_bits<HITS>(src, i, n);
+    const uint32_t bits = ord.W ? (i < n ? order_bits<HITS>(src, ord, i) : 0u) : flag_bits<HITS>(src, i, n);
     const uint32_t c = __popc(bits);
     uint32_t inc = c;
     for (uint32_t d = 1; d < 64; d <<= 1) {
@@ -440,8 +442,8 @@ __global__ void __launch_bounds__(256) k_emit_flags(const void *__restrict__ src
     for (uint32_t k = 0; k < 4; ++k)
         if (bits & (1u << k)) {
             uint32_t px = 0, py = 0;
-            if (!HITS && ord.W) order_pixel(ord, i + k, px, py);
-            out[o++] = !HITS && ord.W ? py * ord.W + px : (uint32_t)(i + k);
+            if (ord.W) order_pixel(ord, i + k, px, py);
+            out[o++] = ord.W ? py * ord.W + px : (uint32_t)(i + k);
         }
 }
 
@@ -1129,6 +1131,23 @@ static int compact_chunks(vhx_ctx *c, uint32_t nchunks_host, const uint32_t *n_i
     return VHX_OK;
 }
 
+// The FlagOrder of code `qorder` for a W x H framebuffer frame (W = 0 or qorder = 0: output-index order) and the
+// number of positions its compaction scans (npos: in / out)
+static FlagOrder flag_order(uint32_t qorder, uint32_t W, uint32_t H, uint64_t &npos) {
+    FlagOrder ord{};
+    if (!qorder || !W || !H) return ord;
+    const uint32_t tsl = qorder & 15u, ts = 1u << tsl;
+    ord = FlagOrder{W, H, (W + ts - 1u) / ts, (H + ts - 1u) / ts, tsl, 0u, (qorder & 32u) ? 1u : 0u};
+    if (qorder & 16u)  // Morton order over the smallest 2^m x 2^m grid of tiles covering the frame
+        while ((1u << ord.mdim) < std::max(ord.tx, ord.ty)) ++ord.mdim;
+    const uint64_t np = (ord.mdim ? 1ull << (2u * ord.mdim) : (uint64_t)ord.tx * ord.ty) << (2u * tsl);
+    // the chunk counts are sized for ceil(pixels / 256) chunks, the compaction needs ceil(npos / 1024): a tile far
+    // larger than the frame keeps output-index order
+    if (np > 4ull * W * H) return FlagOrder{};
+    npos = np;
+    return ord;
+}
+
 // Queue passes first..npass-1: pass p re-traces the queue of pass p-1 (pass 0's queue, for first == 0, is the list
 // in queue[1] with its length in qctl[7]); what exceeds its budget is listed per chunk and compacted into the next
 // pass's queue. For first == 1, pass 0 (a grid kernel of nblocks0 workgroups) has just run and is compacted first.
@@ -1140,19 +1159,9 @@ static int launch_queue_passes(vhx_ctx *c, const DevTree &t, const CamD &cam, co
     int rc = VHX_OK;
     if (first > 0 && npass > 1) {
         if (flags_pass0) {  // primary frames: per-ray flags compacted in output-index (frame) order
-            // block order (c->qorder, framebuffer layout only): positions over the frame's 16x16 blocks
-            FlagOrder ord{};
+            // tile order (c->qorder, framebuffer layout only): positions over the frame's tiles
             uint64_t npos = nout;
-            if (c->qorder && order_w) {
-                const uint32_t tsl = c->qorder & 15u, ts = 1u << tsl;
-                ord = FlagOrder{order_w, order_h, (order_w + ts - 1u) / ts, (order_h + ts - 1u) / ts, tsl, 0u,
-                                (c->qorder & 32u) ? 1u : 0u};
-                if (c->qorder & 16u)  // Morton order over the smallest 2^m x 2^m grid of tiles covering the frame
-                    while ((1u << ord.mdim) < std::max(ord.tx, ord.ty)) ++ord.mdim;
-                const uint64_t tiles = ord.mdim ? 1ull << (2u * ord.mdim) : (uint64_t)ord.tx * ord.ty;
-                npos = tiles << (2u * tsl);
-                if (ord.mdim == 0 && (c->qorder & 16u)) npos = 1ull << (2u * tsl);  // one tile: Morton = row-major
-            }
+            const FlagOrder ord = flag_order(c->qorder, order_w, order_h, npos);
             const unsigned nb = (unsigned)((npos + 1023) / 1024);
             uint32_t *counts = (uint32_t *)c->counts.ptr, *offsets = (uint32_t *)c->offsets.ptr;
             const uint8_t *flags = (const uint8_t *)c->flags.ptr;
@@ -1866,6 +1875,9 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
     if (qrc) return qrc;
     VHX_HIP(c, hipGetLastError());
     if (c->in_prepass) return VHX_OK;  // the outer call records the end and copies its outputs
+    // a shadow trace of this frame's hit records lists them in the same tile order (vhx_trace_shadows)
+    c->last_fb_w = layout == VHX_LAYOUT_FRAMEBUFFER ? cam->width : 0u;
+    c->last_fb_h = layout == VHX_LAYOUT_FRAMEBUFFER ? cam->height : 0u;
     VHX_HIP(c, hipEventRecord(c->ev1, c->stream));
     c->timed = true;
     if ((rc = trace_end(c))) return rc;  // a later write of the tree waits for this frame
@@ -2043,12 +2055,18 @@ int vhx_trace_shadows(vhx_ctx *c, const float light[3], uint64_t n, const uint32
     // no reset_passes: the hit compaction (k_count_flags) zeroes the queue passes' counters
     if (bytes) VHX_HIP(c, hipMemsetAsync(bytes, 0, n * 4, c->stream));
     // wave-dense secondary rays: the hit pixels, in frame order, are pass 0's queue
+    // (when n is the pixel count of this context's last framebuffer frame, in the tile order of c->qorder: any
+    // order is a permutation of 0..n-1, so the records need not even be that frame's for the result to be exact)
     {
-        const unsigned nb = (unsigned)((n + 1023) / 1024);
+        uint64_t npos = n;
+        const bool fb = c->last_fb_w && (uint64_t)c->last_fb_w * c->last_fb_h == n;
+        const FlagOrder ord = flag_order(fb ? c->qorder : 0u, c->last_fb_w, c->last_fb_h, npos);
+        const unsigned nb = (unsigned)((npos + 1023) / 1024);
         uint32_t *counts = (uint32_t *)c->counts.ptr, *offsets = (uint32_t *)c->offsets.ptr;
-        k_count_flags<true><<<nb, 256, 0, c->stream>>>(value, n, counts, (uint32_t *)c->qctl.ptr + 16, shadowed);
+        k_count_flags<true><<<nb, 256, 0, c->stream>>>(value, npos, counts, (uint32_t *)c->qctl.ptr + 16, shadowed,
+                                                       ord, n);
         k_scan_counts<<<1, SCAN_THREADS, 0, c->stream>>>(counts, nb, nullptr, 1, c->tw, offsets, (uint32_t *)c->qctl.ptr + 7);
-        k_emit_flags<true><<<nb, 256, 0, c->stream>>>(value, n, offsets, (uint32_t *)c->queue[1].ptr);
+        k_emit_flags<true><<<nb, 256, 0, c->stream>>>(value, npos, offsets, (uint32_t *)c->queue[1].ptr, ord);
         VHX_HIP(c, hipGetLastError());
     }
     int qrc = VHX_OK;
