@@ -307,7 +307,8 @@ SCHEDULER_ENVS = [{"VHX_RESUME": "0"},                                   # aband
                   {"VHX_QXCD_ALL": "1", "VHX_QWAVESM": "300"},           # every queue pass dealt over the XCDs
                   {"VHX_QORDER": "16"},                                  # pass-0 queue in 16x16 tile order
                   {"VHX_QORDER": "m8"},                                  # ... in Morton order of 8x8 tiles
-                  {"VHX_QORDER": "m32z"}]                                # ... every pixel in Morton order
+                  {"VHX_QORDER": "m32z"},                                # ... every pixel in Morton order
+                  {"VHX_QORDER": "32r"}]                                 # ... 32x32 tiles by rows
 
 
 @pytest.mark.parametrize("env", SCHEDULER_ENVS, ids=lambda e: "+".join(f"{k}={v}" for k, v in e.items()))

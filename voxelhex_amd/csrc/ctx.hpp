@@ -44,8 +44,13 @@ struct TreeStore {
 };
 
 // default pass-0 queue orders of the two schedules (vhx_ctx::qorder encoding)
-#define VHX_QORDER_BUSY 38u  // 64x64 tiles row-major, Morton order inside ("64z")
-#define VHX_QORDER_IDLE 0u  // output-index order
+// Frames in flight: 64x64 tiles row-major, Morton order inside ("64z"): the bench frame at eight in flight 0.516-0.525
+// ms against 0.564-0.567 in output-index (row-major) order, queue passes at 20.3 instead of 17.4 lanes per VALU
+// instruction; 32r 0.515-0.523, 64 / 64r 0.524-0.530, 128r 0.536-0.539, Morton orders of tiles 0.509-0.540 from box to
+// box (profiles/r03/qorder/). A lone frame keeps output-index order: 1.21-1.24 ms against 1.33-1.42 with tile orders
+// (its critical path is its slowest chunk, and 2-D clusters gather the longest rays into fewer, longer chunks).
+#define VHX_QORDER_BUSY 38u
+#define VHX_QORDER_IDLE 0u
 
 struct vhx_ctx {
     int device = 0;

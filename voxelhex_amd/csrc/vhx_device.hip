@@ -348,14 +348,13 @@ __device__ __forceinline__ uint32_t flag_bits(const void *src, uint64_t i, uint6
 // 3.6 times as long as with one counter: DESIGN.md §3)
 #define QCTL_PASS_WORDS (9u * 64u)
 #define QCTL_WORDS (16u + QCTL_PASS_WORDS * (VHX_MAX_BUDGETS + 1u))
-// zero: the queue passes' work counters (qctl[16..79]), zeroed here instead of by a separate memset launch;
-// clear (optional, n entries): an output array zeroed alongside (the shadow flags of a shadow frame)
 // Order of the pass-0 queue of a primary frame (vhx_ctx::qorder): W = 0 keeps output-index order (row-major in the
 // framebuffer layout); W > 0 lists the rays tile by tile -- TS x TS pixel tiles (TS = 1 << tsl >= 8), the tiles
 // row-major over the frame (tx per row) or, with mdim > 0, in Morton order over a 2^mdim x 2^mdim grid (tiles outside
 // the frame hold no rays), and inside a tile either its 8x8 sub-tiles row-major with their pixels row-major (a pass-0
-// wave's footprint) or, with zin, every pixel in Morton order. 2-D neighbourhoods instead of rows: a queue wave's 64
-// rays are neighbours in both directions. Only the order of the queue changes, never a result.
+// wave's footprint), or (zin 1) every pixel in Morton order, or (zin 2) the tile's rows. 2-D neighbourhoods instead
+// of frame rows: a queue wave's 64 rays are neighbours in both directions. Only the order of the queue changes, never
+// a result.
 struct FlagOrder {
     uint32_t W, H, tx, ty, tsl, mdim, zin;
 };
@@ -378,7 +377,10 @@ __device__ __forceinline__ bool order_pixel(const FlagOrder &o, uint64_t k, uint
         gy = t / o.tx;
     }
     uint32_t ix, iy;
-    if (o.zin) {
+    if (o.zin == 2u) {  // rows of the tile
+        ix = r & ((1u << o.tsl) - 1u);
+        iy = r >> o.tsl;
+    } else if (o.zin) {
         ix = compact_bits(r);
         iy = compact_bits(r >> 1);
     } else {
@@ -403,6 +405,9 @@ __device__ __forceinline__ uint32_t order_bits(const void *src, const FlagOrder 
     return bits;
 }
 
+// k_count_flags: the number of set flags per 1024 positions. zero: the queue passes' work counters (qctl[16..79]),
+// zeroed here instead of by a separate memset launch; clear (optional, nclear entries): an output array zeroed
+// alongside (the shadow flags of a shadow frame)
 template <bool HITS>
 __global__ void __launch_bounds__(256) k_count_flags(const void *__restrict__ src, uint64_t n,
                                                      uint32_t *__restrict__ counts, uint32_t *zero,
@@ -1137,7 +1142,7 @@ static FlagOrder flag_order(uint32_t qorder, uint32_t W, uint32_t H, uint64_t &n
     FlagOrder ord{};
     if (!qorder || !W || !H) return ord;
     const uint32_t tsl = qorder & 15u, ts = 1u << tsl;
-    ord = FlagOrder{W, H, (W + ts - 1u) / ts, (H + ts - 1u) / ts, tsl, 0u, (qorder & 32u) ? 1u : 0u};
+    ord = FlagOrder{W, H, (W + ts - 1u) / ts, (H + ts - 1u) / ts, tsl, 0u, (qorder & 64u) ? 2u : (qorder & 32u) ? 1u : 0u};
     if (qorder & 16u)  // Morton order over the smallest 2^m x 2^m grid of tiles covering the frame
         while ((1u << ord.mdim) < std::max(ord.tx, ord.ty)) ++ord.mdim;
     const uint64_t np = (ord.mdim ? 1ull << (2u * ord.mdim) : (uint64_t)ord.tx * ord.ty) << (2u * tsl);
@@ -1312,17 +1317,18 @@ int vhx_create(int hip_device, vhx_ctx **out) {
             }
             c->adaptive = false;  // fixes the schedule
         }
-        // pass-0 queue order: "[m]N[z]": NxN tiles, row-major or (m) in Morton order, inside each tile 8x8 sub-tiles
-        // row-major or (z) every pixel in Morton order; "0" = output index
+        // pass-0 queue order: "[m]N[z|r]": NxN tiles, row-major or (m) in Morton order, inside each tile 8x8 sub-tiles
+        // row-major, (z) every pixel in Morton order or (r) the tile's rows; "0" = output index
         const char *pqo = getenv("VHX_QORDER");
         if (pqo) {
             const bool m = pqo[0] == 'm';
             char *end = nullptr;
             const long ts = strtol(pqo + (m ? 1 : 0), &end, 10);
-            const bool z = end && *end == 'z';
+            const bool z = end && *end == 'z', rows = end && *end == 'r';
             uint32_t l = 0;
             while (l < 12u && (1l << l) < ts) ++l;
-            c->qorder = ts >= 8 && ts <= 4096 && (1l << l) == ts ? l | (m ? 16u : 0u) | (z ? 32u : 0u) : 0u;
+            c->qorder = ts >= 8 && ts <= 4096 && (1l << l) == ts ? l | (m ? 16u : 0u) | (z ? 32u : 0u) | (rows ? 64u : 0u)
+                                                                 : 0u;
             c->sched_busy.qorder = c->sched_idle.qorder = c->qorder;  // both schedules (the rest stays adaptive)
         }
         const char *pqa = getenv("VHX_QXCD_ALL");
@@ -1848,7 +1854,11 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
 
     const bool count = ho.dev.bytes != nullptr;
     int qrc = VHX_OK;
-    const uint32_t ow = layout == VHX_LAYOUT_FRAMEBUFFER ? cam->width : 0u;  // the queue order's frame (c->qorder)
+    // the queue order's frame (c->qorder): the framebuffer layout only. The tile layout's output index is already
+    // tile-major with T-wide rows inside a tile (config 4 on one rank, 64x64 tiles: 2.019-2.025 ms per frame in that
+    // order against 2.071-2.074 with the tiles re-ordered Morton inside, profiles/r03/qorder/mgpu1_*.log)
+    const uint32_t ow = layout == VHX_LAYOUT_FRAMEBUFFER ? cam->width : 0u;
+    const uint32_t oh = cam->height;
     auto launch = [&](auto bd_tag) {
         constexpr int BD = decltype(bd_tag)::value;
         PassQ q0 = pass_q(c, 0, npass);
@@ -1856,11 +1866,11 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
         if (t.mips) {  // MIP stand-ins (no byte counting, no depth prepass: refused above)
             k_trace_primary<false, BD, false, true><<<(unsigned)nblocks, 256, 0, c->stream>>>(
                 t, cd, ho.dev, T, tiles_x, tile_start, tile_stride, layout, bpx, bpt, q0);
-            qrc = launch_queue_passes<false, BD, true>(c, t, cd, src, ho.dev, 1, npass, nout, nblocks, true, ow, cam->height);
+            qrc = launch_queue_passes<false, BD, true>(c, t, cd, src, ho.dev, 1, npass, nout, nblocks, true, ow, oh);
         } else if (count) {
             k_trace_primary<true, BD><<<(unsigned)nblocks, 256, 0, c->stream>>>(
                 t, cd, ho.dev, T, tiles_x, tile_start, tile_stride, layout, bpx, bpt, q0);
-            qrc = launch_queue_passes<true, BD>(c, t, cd, src, ho.dev, 1, npass, nout, nblocks, true, ow, cam->height);
+            qrc = launch_queue_passes<true, BD>(c, t, cd, src, ho.dev, 1, npass, nout, nblocks, true, ow, oh);
         } else {
             if (fast)
                 k_trace_primary<false, BD, true><<<(unsigned)nblocks, 256, 0, c->stream>>>(
@@ -1868,7 +1878,7 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
             else
                 k_trace_primary<false, BD><<<(unsigned)nblocks, 256, 0, c->stream>>>(
                     t, cd, ho.dev, T, tiles_x, tile_start, tile_stride, layout, bpx, bpt, q0);
-            qrc = launch_queue_passes<false, BD>(c, t, cd, src, ho.dev, 1, npass, nout, nblocks, true, ow, cam->height);
+            qrc = launch_queue_passes<false, BD>(c, t, cd, src, ho.dev, 1, npass, nout, nblocks, true, ow, oh);
         }
     };
     if (!dispatch_bd(c->tree->desc.brick_dim, launch)) return fail(c, VHX_E_INVALID_ARG, "unsupported brick_dim");
