@@ -8,9 +8,9 @@ from voxelhex_amd import _native as N
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def declared_functions():
+def declared_functions(headers=("vhx.h", "vhx_boxtree.h", "vhx_stream.h")):
     names = set()
-    for h in ("vhx.h", "vhx_boxtree.h", "vhx_stream.h"):
+    for h in headers:
         text = open(os.path.join(ROOT, "include", h)).read()
         text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
         for m in re.finditer(r"^\s*[A-Za-z_][\w \*]*?\b(vhx_\w+)\s*\(", text, flags=re.M):
@@ -26,6 +26,16 @@ def test_every_declared_symbol_is_exported_and_bound():
     assert declared == bound, (declared ^ bound)
     for name in declared:
         assert hasattr(lib, name), name
+
+
+def test_integration_binds_every_declared_function():
+    """INTEGRATION.md's Rust `extern "C"` block names every function of the device and streaming headers (the
+    reference-side binding a maintainer would add; the C++ host tree of vhx_boxtree.h stands in for the Rust BoxTree
+    and is not bound from Rust)."""
+    text = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    bound = set(re.findall(r"pub fn (vhx_\w+)\s*\(", text))
+    missing = declared_functions(("vhx.h", "vhx_stream.h")) - bound
+    assert not missing, sorted(missing)
 
 
 def test_abi_version_and_struct_sizes():
