@@ -170,6 +170,11 @@ int vhx_set_adaptive_schedule(vhx_ctx *ctx, int on);
 /* The budgets of the context's last trace (or the fixed ones before any), n of them (budgets: VHX_MAX_BUDGETS entries,
  * may be NULL); *schedule (may be NULL) = 1 the frames-in-flight schedule, 0 the lone-frame one, -1 fixed. */
 int vhx_get_pass_budgets(const vhx_ctx *ctx, uint32_t *budgets, uint32_t *n, int *schedule);
+/* Tail split of the last trace (the lone-frame schedule's unbounded last pass shares its slowest rays out between
+ * waves: DESIGN.md section 14.10; VHX_SPLIT=0/1 forces it off / on): synchronises the context's stream and reports the
+ * rays handed over from one wave to another (*handed_over) and hand-offs that never completed (*errors, always 0
+ * unless something is broken). Both 0 when the last trace ran no split pass. Diagnostics; results never depend on it. */
+int vhx_get_split_stats(vhx_ctx *ctx, uint32_t *handed_over, uint32_t *errors);
 
 /* Tree upload ----------------------------------------------------------------------------------------------- */
 /* Copies the flattened tree to HBM (full residency) and builds the device-side layout. */

@@ -32,6 +32,7 @@ for spec in sys.argv[1:]:
             ms.append(t)
     if ref is None:
         ref = out["rgba"].clone()
+    handed, err = rt.split_stats()
     print(f"{env:30s} budgets={spec or '()':>22}: isolated {np.median(ms):.4f} ms (min {min(ms):.4f})  "
-          f"equal {torch.equal(ref, out['rgba'])}", flush=True)
+          f"equal {torch.equal(ref, out['rgba'])}  split handed {handed} err {err}", flush=True)
 rt.close()

@@ -99,6 +99,7 @@ struct vhx_ctx {
         uint32_t sparse[VHX_MAX_BUDGETS];    // abandon a wave's rays once fewer lanes still trace (0 = off)
         uint32_t queue_waves_per_cu;         // waves of a queue pass per CU
         uint32_t qorder;                     // order of a primary frame's pass-0 queue (vhx_ctx::qorder below)
+        uint32_t split;                      // the unbounded last pass shares its tail rays out (k_trace_queue_split)
     };
     // Adaptive scheduling (default; vhx_set_pass_budgets or an environment knob fixes the schedule instead): at each
     // trace the context looks at the other contexts of its tree (vhx_create_shared) and picks
@@ -114,8 +115,8 @@ struct vhx_ctx {
     //    three-budget ladders 1.31-1.51 ms, fewer rays per wave in a last pass no better): every extra pass lengthens a
     //    lone frame's critical path.
     bool adaptive = true;
-    Sched sched_busy = {{24u, 72u, 216u, 648u}, 5u, {12u}, 4u, VHX_QORDER_BUSY};
-    Sched sched_idle = {{64u}, 2u, {0u}, 8u, VHX_QORDER_IDLE};
+    Sched sched_busy = {{24u, 72u, 216u, 648u}, 5u, {12u}, 4u, VHX_QORDER_BUSY, 0u};
+    Sched sched_idle = {{64u}, 2u, {0u}, 8u, VHX_QORDER_IDLE, 0u};
     int last_sched = -1;  // the schedule of the last trace: 1 busy, 0 idle, -1 fixed (vhx_get_pass_budgets)
     // the schedule in force (the selected one, or the fixed one)
     uint32_t budgets[VHX_MAX_BUDGETS] = {24u, 72u, 216u, 648u};
@@ -148,6 +149,16 @@ struct vhx_ctx {
     // Pass 0 at 12 under frames in flight: eight frames 0.645-0.651 ms per bench frame against 0.665-0.670 (8:
     // 0.651-0.661, 16: 0.646-0.657, 24 and 32 slower); the later budgeted passes gained nothing (profiles/r02/sparse*.log)
     uint32_t sparse[VHX_MAX_BUDGETS] = {12u};
+    // tail split of the unbounded last pass (k_trace_queue_split in vhx_device.hip): in force for this trace (the
+    // selected schedule's `split`; off under a fixed schedule), VHX_SPLIT=0/1 forces it either way (-1: not forced);
+    // ovf holds the overflow slots, split_epoch tags this context's frames in them
+    uint32_t split = 0;
+    int split_force = -1;
+    uint32_t split_epoch = 0;
+    uint32_t split_period = 8, split_min_lanes = 2, split_min_idle = 1, split_take = 64;  // SplitQ (VHX_SPLIT_TUNE)
+    uint32_t split_diag = 0;  // SplitQ::diag (VHX_SPLIT_DIAG)
+    uint32_t split_max_wait = 64;  // SplitQ::max_wait (VHX_SPLIT_WAIT)
+    DevBuf ovf;
 };
 
 #define VHX_HIP(ctx, call)                                                                                         \

@@ -462,14 +462,27 @@ __device__ __forceinline__ void fill_occ_tab(uint64_t *occ_tab, const DevTree &t
 // Saved traversal state of a ray abandoned at a pass budget (multi-pass scheduling): everything the loop below
 // carries from one node iteration to the next, 64 bytes. Cube sizes are powers of two (zero mantissa), so the
 // current cube's size word also holds the target sectant (7 bits) and the stack depth (3 bits).
+struct St4 {
+    uint4 a, b, c, e;
+};
+__device__ __forceinline__ St4 pack_state(F3d p, uint32_t iters, CubeD cur, CubeD tb, uint32_t target, uint32_t count,
+                                          uint32_t node, uint32_t s1, uint32_t s2, uint32_t s3) {
+    St4 s;
+    s.a = make_uint4(__float_as_uint(p.x), __float_as_uint(p.y), __float_as_uint(p.z), iters);
+    s.b = make_uint4(__float_as_uint(cur.min.x), __float_as_uint(cur.min.y), __float_as_uint(cur.min.z),
+                     __float_as_uint(cur.size) | target | (count << 8));
+    s.c = make_uint4(__float_as_uint(tb.min.x), __float_as_uint(tb.min.y), __float_as_uint(tb.min.z),
+                     __float_as_uint(tb.size));
+    s.e = make_uint4(node, s1, s2, s3);
+    return s;
+}
 __device__ __forceinline__ void save_state(uint4 *st, F3d p, uint32_t iters, CubeD cur, CubeD tb, uint32_t target,
                                            uint32_t count, uint32_t node, uint32_t s1, uint32_t s2, uint32_t s3) {
-    st[0] = make_uint4(__float_as_uint(p.x), __float_as_uint(p.y), __float_as_uint(p.z), iters);
-    st[1] = make_uint4(__float_as_uint(cur.min.x), __float_as_uint(cur.min.y), __float_as_uint(cur.min.z),
-                       __float_as_uint(cur.size) | target | (count << 8));
-    st[2] = make_uint4(__float_as_uint(tb.min.x), __float_as_uint(tb.min.y), __float_as_uint(tb.min.z),
-                       __float_as_uint(tb.size));
-    st[3] = make_uint4(node, s1, s2, s3);
+    const St4 s = pack_state(p, iters, cur, tb, target, count, node, s1, s2, s3);
+    st[0] = s.a;
+    st[1] = s.b;
+    st[2] = s.c;
+    st[3] = s.e;
 }
 
 // BoxTree::get_by_ray, src/raytracing/cpu.rs:296-458, as a traversal state with three steps: begin (ray setup and the
@@ -574,6 +587,39 @@ struct Trav {
         ray_scale_factors(r);
         tbok = resume ? 0u : 1u;
         return true;
+    }
+
+    // begin() of a resumed ray whose saved state is already in registers (the words save_state writes; the tail split
+    // of k_trace_queue_split hands rays over that way)
+    __device__ __forceinline__ void begin_resumed(const DevTree &t, F3d o, F3d d, HitOut &h, const St4 &s) {
+        h.hit = false;
+        ray_setup(r, o, d);
+        {
+            const F3d od = vadd(mk(1.0f, 1.0f, 1.0f), d);
+            dir_idx = (uint32_t)(od.x >= 1.0f) + (uint32_t)(od.z >= 1.0f) * 2u + (uint32_t)(od.y >= 1.0f) * 4u;
+        }
+        tsize = (float)t.size;
+        ex = 0;
+        hdesc = 0;
+        hflat = 0;
+        p = mk(__uint_as_float(s.a.x), __uint_as_float(s.a.y), __uint_as_float(s.a.z));
+        iters = s.a.w;
+        cur.min = mk(__uint_as_float(s.b.x), __uint_as_float(s.b.y), __uint_as_float(s.b.z));
+        cur.size = __uint_as_float(s.b.w & 0xFF800000u);
+        target = s.b.w & 0x7Fu;
+        count = (s.b.w >> 8) & 7u;
+        tb.min = mk(__uint_as_float(s.c.x), __uint_as_float(s.c.y), __uint_as_float(s.c.z));
+        tb.size = __uint_as_float(s.c.w);
+        node = s.e.x;
+        s1 = s.e.y;
+        s2 = s.e.z;
+        s3 = s.e.w;
+        ray_scale_factors(r);
+        tbok = 0u;
+    }
+    // the loop state as save_state would write it
+    __device__ __forceinline__ St4 packed() const {
+        return pack_state(p, iters, cur, tb, target, count, node, s1, s2, s3);
     }
 
     __device__ __forceinline__ void step(const DevTree &t, const uint64_t *occ_tab, HitOut &h, uint32_t budget) {

@@ -347,7 +347,10 @@ __device__ __forceinline__ uint32_t flag_bits(const void *src, uint64_t i, uint6
 // one line, the drain of a budgeted pass over many short chunks, every wave probing every exhausted counter, took 2.5 -
 // 3.6 times as long as with one counter: DESIGN.md §3)
 #define QCTL_PASS_WORDS (9u * 64u)
-#define QCTL_WORDS (16u + QCTL_PASS_WORDS * (VHX_MAX_BUDGETS + 1u))
+// the tail split's counters (k_trace_queue_split), each on a 256-byte line: reserved overflow slots, taken slots, waves
+// waiting for work, waves holding rays, error word
+#define QCTL_SPLIT (16u + QCTL_PASS_WORDS * (VHX_MAX_BUDGETS + 1u))
+#define QCTL_WORDS (QCTL_SPLIT + 7u * 64u)
 // Order of the pass-0 queue of a primary frame (vhx_ctx::qorder): W = 0 keeps output-index order (row-major in the
 // framebuffer layout); W > 0 lists the rays tile by tile -- TS x TS pixel tiles (TS = 1 << tsl >= 8), the tiles
 // row-major over the frame (tx per row) or, with mdim > 0, in Morton order over a 2^mdim x 2^mdim grid (tiles outside
@@ -540,6 +543,8 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t bid, uint32_t n, uint32_t
 #else
 #define VHX_QUEUE_ATTR __attribute__((amdgpu_waves_per_eu(!COUNT && (BD == 1 || BD == 4) ? 5 : 4)))
 #endif
+// the split pass runs 8 waves per CU (2 per SIMD): no occupancy bound for the register allocation
+#define VHX_QUEUE_ATTR_SPLIT
 #if VHX_PRIMARY_WPE > 0
 #define VHX_PRIMARY_ATTR __attribute__((amdgpu_waves_per_eu(VHX_PRIMARY_WPE)))
 #else
@@ -730,6 +735,268 @@ __global__ void __launch_bounds__(256) VHX_QUEUE_ATTR k_trace_queue(DevTree t, c
             if (lane == 0) q.counts[chunk] = (uint32_t)__popcll(m);
         }
     }
+}
+
+// ------------------------------------------------------------------------------------------------ tail split
+// A lone frame's unbounded last pass ends on its slowest chunks: 64 neighbouring long rays in one wave, which runs the
+// union of their divergent paths while the rest of the GPU has gone idle (bench frame: the last pass is 0.83-0.86 of
+// the 1.22 ms; the 256 longest rays take 1.05 ms at 64 per wave and 0.56 ms at one per wave). k_trace_queue_split runs
+// that pass with work sharing: a wave that finds the queue drained waits for work (the `idle` count), and a tracing
+// wave that sees idle waves hands the upper half of its still-tracing rays over -- their loop state, packed as
+// save_state would, goes to overflow slots -- and goes on with the lower half; waiting waves take the slots (up to 64
+// at a time) and resume the rays, splitting again while other waves wait. Results are the same (a ray's traversal is
+// deterministic and its state is handed over whole); only which wave runs which iterations changes.
+//
+// Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility, form R2: the data is the flag): every word of a slot is
+// an 8-byte granule {tag = the frame's epoch, value} written by ONE agent-scope atomic store (sc1) and read by
+// agent-scope atomic loads until every tag matches; no fences. Epochs count per context from 1 and the slots are
+// zeroed when allocated, so a slot of an earlier frame never matches. Termination needs no barrier: a wave leaves only
+// when the queue is drained, no slot is left untaken and no wave holds rays; a wave that hands rays over keeps looking
+// for slots itself before it can leave, so no slot is ever orphaned, whatever the other waves do. Every wait is
+// bounded (VHX_SPLIT_SPINS; a slot that never fills sets the error word and its ray is dropped, which the parity tests
+// would show).
+#define VHX_OVF_CAP 65536u   // overflow slots per context (a frame hands over fewer: the tail is a few thousand rays)
+#define VHX_OVF_STRIDE 32u   // granules per slot (17 used: output index + 16 state words); 256 B
+#define VHX_OVF_SKIP 0xFFFFFFFFu
+#define VHX_SPLIT_SPINS (1u << 20)
+typedef __attribute__((address_space(1))) uint32_t gu32;
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+struct SplitQ {
+    unsigned long long *ovf;  // VHX_OVF_CAP slots of VHX_OVF_STRIDE granules
+    uint32_t *ctl;            // qctl + QCTL_SPLIT
+    uint32_t epoch;
+    uint32_t period;     // a tracing wave looks at the idle count every `period` iterations (a power of two)
+    uint32_t min_lanes;  // ... and splits only with at least this many rays still tracing
+    uint32_t min_idle;   // ... and at least this many waves waiting
+    uint32_t take;       // a waiting wave takes up to this many slots at a time
+    uint32_t diag;       // bit 0: poll slots by atomic read-modify-write (fetch_or 0); bit 1: count polls (ctl[320], [384])
+    uint32_t max_wait;   // at most this many waves wait for slots; the others leave once the queue is drained
+};
+__device__ __forceinline__ uint32_t ld_agent(const uint32_t *p) {
+    return __hip_atomic_load((gu32 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void put_granule(unsigned long long *g, uint32_t epoch, uint32_t v) {
+    __hip_atomic_store((gu64 *)g, ((unsigned long long)epoch << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void publish_slot(const SplitQ &s, uint32_t slot, uint32_t idx, const St4 &st) {
+    unsigned long long *g = s.ovf + (uint64_t)slot * VHX_OVF_STRIDE;
+    const uint32_t w[16] = {st.a.x, st.a.y, st.a.z, st.a.w, st.b.x, st.b.y, st.b.z, st.b.w,
+                            st.c.x, st.c.y, st.c.z, st.c.w, st.e.x, st.e.y, st.e.z, st.e.w};
+    put_granule(g, s.epoch, idx);
+#pragma unroll
+    for (uint32_t k = 0; k < 16u; ++k) put_granule(g + 1 + k, s.epoch, w[k]);
+}
+// polls one slot until all 17 granules carry this frame's epoch; false after VHX_SPLIT_SPINS polls
+__device__ __forceinline__ bool take_slot(const SplitQ &s, uint32_t slot, uint32_t &idx, St4 &st) {
+    unsigned long long *g = s.ovf + (uint64_t)slot * VHX_OVF_STRIDE;
+    uint32_t w[17];
+    for (uint32_t spins = 0; spins < VHX_SPLIT_SPINS; ++spins) {
+        bool ok = true;
+#pragma unroll
+        for (uint32_t k = 0; k < 17u; ++k) {
+            const unsigned long long x =
+                (s.diag & 1u) ? __hip_atomic_fetch_or((gu64 *)(g + k), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                              : __hip_atomic_load((const gu64 *)(g + k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            w[k] = (uint32_t)x;
+            ok &= (uint32_t)(x >> 32) == s.epoch;
+        }
+        if ((s.diag & 2u) && !ok) atomicAdd(s.ctl + 320, 1u);
+        if (ok) {
+            idx = w[0];
+            st.a = make_uint4(w[1], w[2], w[3], w[4]);
+            st.b = make_uint4(w[5], w[6], w[7], w[8]);
+            st.c = make_uint4(w[9], w[10], w[11], w[12]);
+            st.e = make_uint4(w[13], w[14], w[15], w[16]);
+            return true;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    return false;
+}
+
+// One resumed ray of the split pass, unbounded. Every s.period-th iteration of the wave reads the idle count (issued
+// before the iteration's node loads, used after them); with at least s.min_idle waves waiting and s.min_lanes rays
+// still tracing, the upper half of them (in lane order: the wave's rays stay spatial neighbours) is handed over. Returns false when this lane's
+// ray was handed over, true when it finished here (h filled).
+template <int BD>
+__device__ __forceinline__ bool trace_split(const DevTree &t, const uint64_t *occ_tab, F3d o, F3d d, HitOut &h,
+                                            const St4 &st, uint32_t idx, const SplitQ &s) {
+    Trav<false, BD, false> tr;
+    tr.begin_resumed(t, o, d, h, st);
+    const uint32_t lane = threadIdx.x & 63u;
+    for (uint32_t k = 0;; ++k) {
+        // not before `period` iterations of this wave: a wave that just took handed-over rays first traces them
+        // (checking at once made rays bounce from wave to wave, each hop costing more than the iterations it ran)
+        const bool chk = ((k + 1u) & (s.period - 1u)) == 0u;
+        uint32_t want = 0;
+        if (chk) want = ld_agent(s.ctl + 128);
+        tr.step(t, occ_tab, h, VHX_MAX_ITERS);
+        if (tr.ex != 0u) break;
+        if (chk && want >= s.min_idle) {
+            const uint64_t act = __ballot(1);
+            const uint32_t na = (uint32_t)__popcll(act);
+            if (na >= s.min_lanes) {
+                const uint32_t rank = (uint32_t)__popcll(act & ((1ull << lane) - 1ull));
+                const uint32_t nk = na >> 1, first = na - nk;
+                const bool go = rank >= first;
+                const uint32_t leader = (uint32_t)__builtin_ctzll(__ballot(go));
+                uint32_t base = 0;
+                if (lane == leader) base = atomicAdd(s.ctl, nk);
+                base = __shfl(base, (int)leader);
+                if (go) {
+                    const uint32_t slot = base + rank - first;
+                    if (base + nk <= VHX_OVF_CAP) {
+                        publish_slot(s, slot, idx, tr.packed());
+                        tr.ex = 5u;  // handed over
+                    } else if (slot < VHX_OVF_CAP) {
+                        publish_slot(s, slot, VHX_OVF_SKIP, tr.packed());  // no room: a skip entry, the ray stays
+                    }
+                }
+                if (tr.ex != 0u) break;
+            }
+        }
+    }
+    if (tr.ex == 5u) return false;
+    tr.end(t, h, nullptr, 0);
+    return true;
+}
+
+// The unbounded last pass of a lone frame with the tail split (q.state holds every queued ray's saved state).
+template <int BD>
+__global__ void __launch_bounds__(256) VHX_QUEUE_ATTR_SPLIT k_trace_queue_split(DevTree t, const QueueArgs *qa,
+                                                                                const uint32_t *__restrict__ in,
+                                                                                const uint32_t *in_n, uint32_t *grab,
+                                                                                PassQ q, SplitQ s) {
+    __shared__ uint64_t occ_tab[OCC_TAB_WORDS];
+    fill_occ_tab(occ_tab, t);
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t n = *in_n;
+    const uint32_t rpw = pass_rpw(q.rpw, q.tw, n);
+    uint32_t xcd = blockIdx.x & 7u, tries = 0;
+    const uint32_t qxcd = (n + rpw - 1) / rpw > gridDim.x * (blockDim.x / 64u) ? q.qxcd : 0u;
+    uint32_t *const tail = s.ctl, *const head = s.ctl + 64, *const idle = s.ctl + 128, *const active = s.ctl + 192;
+    bool drained = false, waiting = false;
+    uint32_t spins = 0;
+    for (;;) {
+        uint32_t base = 0, cnt = 0;
+        bool from_ovf = false;
+        if (!drained) {  // the pass's queue, as k_trace_queue takes it
+            if (qxcd == 0u) {
+                if (lane == 0) base = atomicAdd(grab, rpw);
+                base = __shfl(base, 0);
+                if (base >= n) drained = true;
+            } else {
+                const uint32_t G = qxcd;
+                const uint32_t nch = (n + rpw - 1) / rpw, nfull = nch / G, rem = nch % G;
+                uint32_t chunk = 0xFFFFFFFFu;
+                while (tries < 8u) {
+                    const uint32_t kmax = (nfull > xcd ? (nfull - xcd + 7u) / 8u : 0u) * G +
+                                          (rem > 0u && nfull % 8u == xcd ? rem : 0u);
+                    uint32_t k = 0xFFFFFFFFu;
+                    uint32_t *ctr = grab + 64u * (xcd + 1u);
+                    if (lane == 0 && __atomic_load_n(ctr, __ATOMIC_RELAXED) < kmax) k = atomicAdd(ctr, 1u);
+                    k = __builtin_amdgcn_readfirstlane(__shfl(k, 0));
+                    if (k < kmax) {
+                        chunk = ((k / G) * 8u + xcd) * G + k % G;
+                        break;
+                    }
+                    xcd = (xcd + 1u) & 7u;
+                    ++tries;
+                }
+                if (chunk == 0xFFFFFFFFu)
+                    drained = true;
+                else
+                    base = chunk * rpw;
+            }
+            if (!drained) cnt = n - base < rpw ? n - base : rpw;
+        }
+        if (drained) {  // overflow slots handed over by tracing waves
+            uint32_t h0 = 0, got = 0, fin = 0;
+            if (lane == 0) {
+                const uint32_t tl0 = ld_agent(tail), tl = tl0 < VHX_OVF_CAP ? tl0 : VHX_OVF_CAP;
+                uint32_t hd = ld_agent(head);
+                while (hd < tl) {
+                    const uint32_t w = tl - hd < s.take ? tl - hd : s.take;
+                    if (__hip_atomic_compare_exchange_strong((gu32 *)head, &hd, hd + w, __ATOMIC_RELAXED,
+                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                        h0 = hd;
+                        got = w;
+                        break;
+                    }
+                }
+                // leave only when no wave holds rays (read first) and every reserved slot is taken; the active count
+                // is looked at on every 8th empty poll only (all waiting waves poll the same lines)
+                if (!got && (spins & 7u) == 0u) {
+                    const uint32_t act = ld_agent(active);
+                    const uint32_t tl1 = ld_agent(tail), hd1 = ld_agent(head);
+                    fin = act == 0u && hd1 >= (tl1 < VHX_OVF_CAP ? tl1 : VHX_OVF_CAP);
+                }
+            }
+            got = __builtin_amdgcn_readfirstlane(__shfl(got, 0));
+            h0 = __builtin_amdgcn_readfirstlane(__shfl(h0, 0));
+            fin = __builtin_amdgcn_readfirstlane(__shfl(fin, 0));
+            if (!got) {
+                if (fin || ++spins >= VHX_SPLIT_SPINS) break;
+                if ((s.diag & 2u) && lane == 0) atomicAdd(s.ctl + 384, 1u);
+                if (!waiting) {  // at most s.max_wait waves wait (pollers of one line slow the whole chip)
+                    uint32_t before = 0;
+                    if (lane == 0) before = atomicAdd(idle, 1u);
+                    before = __builtin_amdgcn_readfirstlane(__shfl(before, 0));
+                    if (before >= s.max_wait) {
+                        if (lane == 0) atomicSub(idle, 1u);
+                        break;
+                    }
+                    waiting = true;
+                }
+                __builtin_amdgcn_s_sleep(32);  // ~2000 cycles between polls (few waves wait: s.max_wait)
+                continue;
+            }
+            if (waiting) {
+                if (lane == 0) atomicSub(idle, 1u);
+                waiting = false;
+            }
+            from_ovf = true;
+            base = h0;
+            cnt = got;
+        }
+        if (lane == 0) atomicAdd(active, 1u);
+        if (lane < cnt) {
+            uint32_t idx = VHX_OVF_SKIP;
+            St4 st;
+            if (from_ovf) {
+                if (!take_slot(s, base + lane, idx, st)) {
+                    atomicOr(s.ctl + 256, 1u);  // a slot that never filled (diagnostics: VHX_DEBUG_PASSES)
+                    idx = VHX_OVF_SKIP;
+                }
+            } else {
+                idx = in[base + lane];
+                const uint4 *sp = q.state + 4ull * idx;
+                st.a = sp[0];
+                st.b = sp[1];
+                st.c = sp[2];
+                st.e = sp[3];
+            }
+            if (idx != VHX_OVF_SKIP) {
+                F3d o, d;
+                const QueueArgs *a = qa;
+                asm volatile("" : "+s"(a));
+                ray_of(a->cam, a->src, idx, o, d);
+                HitOut h;
+                h.bytes = 0;
+                if (trace_split<BD>(t, occ_tab, o, d, h, st, idx, s)) {
+                    const QueueArgs *b = qa;
+                    asm volatile("" : "+s"(b));
+                    if (b->src.kind == 3u)
+                        store_shadow(b->out, idx, h);
+                    else
+                        store(t, b->out, idx, o, h);
+                }
+            }
+        }
+        if (lane == 0) atomicSub(active, 1u);
+    }
+    if (waiting && lane == 0) atomicSub(idle, 1u);
 }
 
 // Scatters rank-gathered tile buffers into framebuffers. Rank r's part of `gathered` holds `planes` planes of
@@ -1035,6 +1302,7 @@ static int finish_out(vhx_ctx *c, HostOut &ho) {
 static void select_schedule(vhx_ctx *c) {
     if (!c->adaptive) {
         c->last_sched = -1;
+        c->split = c->split_force > 0 ? 1u : 0u;
         return;
     }
     bool busy = false;
@@ -1052,6 +1320,7 @@ static void select_schedule(vhx_ctx *c) {
     c->npass = s.npass;
     c->queue_waves = s.queue_waves_per_cu * c->cus;
     c->qorder = s.qorder;
+    c->split = c->split_force >= 0 ? (uint32_t)c->split_force : s.split;
     c->last_sched = busy ? 1 : 0;
 }
 
@@ -1075,6 +1344,10 @@ static int prepare_passes(vhx_ctx *c, uint64_t nout, uint64_t nblocks0, uint32_t
     if (!rc) rc = ensure(c, c->offsets, chunks * 4);
     if (!rc) rc = ensure(c, c->flags, ((nout + 3) & ~3ull));
     if (!rc && c->resume && npass > 1) rc = ensure(c, c->state, nout * 64);
+    if (!rc && c->split && npass > 1 && !c->ovf.ptr) {  // overflow slots of the tail split, zeroed once (epoch 0)
+        rc = ensure(c, c->ovf, (uint64_t)VHX_OVF_CAP * VHX_OVF_STRIDE * 8u);
+        if (!rc) VHX_HIP(c, hipMemsetAsync(c->ovf.ptr, 0, c->ovf.bytes, c->stream));
+    }
     return rc;
 }
 
@@ -1118,6 +1391,13 @@ static void debug_passes(vhx_ctx *c, const char *what) {
     (void)hipMemcpy(v, c->qctl.ptr, sizeof(v), hipMemcpyDeviceToHost);
     fprintf(stderr, "[vhx passes] %-24s counts %u %u %u %u ... %u  grabs %u %u %u %u\n", what, v[0], v[1], v[2], v[3],
             v[7], v[8], v[9], v[10], v[11]);
+    if (c->split) {  // tail split: slots reserved / taken, waves waiting / holding rays, error word
+        uint32_t w[7];
+        for (uint32_t k = 0; k < 7u; ++k)
+            (void)hipMemcpy(&w[k], (uint32_t *)c->qctl.ptr + QCTL_SPLIT + 64u * k, 4, hipMemcpyDeviceToHost);
+        fprintf(stderr, "[vhx passes] %-24s split slots %u taken %u idle %u active %u error %u slot polls failed %u "
+                "waiter polls %u\n", what, w[0], w[1], w[2], w[3], w[4], w[5], w[6]);
+    }
 }
 
 // Chunk lists -> queue `out` with its length at *total: pass-0 style (nchunks_host workgroup chunks of stride 256) or
@@ -1210,8 +1490,28 @@ static int launch_queue_passes(vhx_ctx *c, const DevTree &t, const CamD &cam, co
         const uint32_t qwaves = p == 0 ? c->queue_waves0
                                 : (p + 1 < npass && c->queue_waves_mid ? c->queue_waves_mid : c->queue_waves);
         const unsigned qgrid = (qwaves * 64u + c->qblock - 1) / c->qblock;
-        k_trace_queue<COUNT, BD, MIP><<<qgrid, c->qblock, 0, c->stream>>>(t, qa, in, in_n,
-                                                                         ctl + 16u + QCTL_PASS_WORDS * p, q);
+        bool launched = false;
+        if constexpr (!COUNT && !MIP) {
+            // a lone frame's unbounded last pass over resumed rays: with the tail split (k_trace_queue_split)
+            if (p + 1 == npass && p > 0 && c->split && q.resume && q.state) {
+                SplitQ sq;
+                sq.ovf = (unsigned long long *)c->ovf.ptr;
+                sq.ctl = ctl + QCTL_SPLIT;
+                sq.epoch = ++c->split_epoch == 0u ? ++c->split_epoch : c->split_epoch;  // never 0 (fresh slots)
+                sq.period = c->split_period;
+                sq.min_lanes = c->split_min_lanes;
+                sq.min_idle = c->split_min_idle;
+                sq.take = c->split_take;
+                sq.diag = c->split_diag;
+                sq.max_wait = c->split_max_wait;
+                k_trace_queue_split<BD><<<qgrid, c->qblock, 0, c->stream>>>(t, qa, in, in_n,
+                                                                            ctl + 16u + QCTL_PASS_WORDS * p, q, sq);
+                launched = true;
+            }
+        }
+        if (!launched)
+            k_trace_queue<COUNT, BD, MIP><<<qgrid, c->qblock, 0, c->stream>>>(t, qa, in, in_n,
+                                                                             ctl + 16u + QCTL_PASS_WORDS * p, q);
         debug_passes(c, "queue pass");
         if (p + 1 < npass)
             rc = compact_chunks(c, 0, in_n, q.rpw, q.rpw, (uint32_t *)c->queue[p & 1u].ptr, ctl + p,
@@ -1331,6 +1631,24 @@ int vhx_create(int hip_device, vhx_ctx **out) {
                                                                  : 0u;
             c->sched_busy.qorder = c->sched_idle.qorder = c->qorder;  // both schedules (the rest stays adaptive)
         }
+        const char *psl = getenv("VHX_SPLIT");  // "0" / "1": tail split of the last pass off / on for every trace
+        if (psl && (psl[0] == '0' || psl[0] == '1')) c->split_force = psl[0] - '0';
+        // split tuning "period,min_lanes,min_idle,take" (VHX_SPLIT_TUNE; period a power of two)
+        const char *psw = getenv("VHX_SPLIT_WAIT");
+        if (psw && atoi(psw) > 0) c->split_max_wait = (uint32_t)atoi(psw);
+        const char *psd = getenv("VHX_SPLIT_DIAG");
+        if (psd) c->split_diag = (uint32_t)atoi(psd);
+        const char *pst = getenv("VHX_SPLIT_TUNE");
+        if (pst) {
+            unsigned a = 0, b = 0, d = 0, e = 0;
+            if (sscanf(pst, "%u,%u,%u,%u", &a, &b, &d, &e) == 4 && a && !(a & (a - 1)) && b >= 2 && b <= 64 && d >= 1 &&
+                e >= 1 && e <= 64) {
+                c->split_period = a;
+                c->split_min_lanes = b;
+                c->split_min_idle = d;
+                c->split_take = e;
+            }
+        }
         const char *pqa = getenv("VHX_QXCD_ALL");
         if (pqa && pqa[0] == '1') c->qxcd_all = true;
     }
@@ -1367,7 +1685,7 @@ void vhx_destroy(vhx_ctx *c) {
     c->tree.reset();  // frees the device tree with its last context
     if (c->use_ev) (void)hipEventDestroy(c->use_ev);
     for (DevBuf *b : {&c->scratch, &c->rays, &c->queue[0], &c->queue[1], &c->qctl, &c->tmp, &c->counts, &c->offsets,
-                      &c->flags, &c->qargs, &c->state, &c->upd, &c->prepass_depth})
+                      &c->flags, &c->qargs, &c->state, &c->upd, &c->prepass_depth, &c->ovf})
         if (b->ptr) (void)hipFree(b->ptr);
     for (auto &P : c->pinned) {
         if (P.ptr) (void)hipHostFree(P.ptr);
@@ -1408,6 +1726,21 @@ int vhx_get_pass_budgets(const vhx_ctx *c, uint32_t *budgets, uint32_t *n, int *
     if (budgets)
         for (uint32_t i = 0; i < VHX_MAX_BUDGETS; ++i) budgets[i] = i < *n ? c->budgets[i] : 0u;
     if (sched) *sched = c->last_sched;
+    return VHX_OK;
+}
+
+int vhx_get_split_stats(vhx_ctx *c, uint32_t *handed_over, uint32_t *errors) {
+    if (!c) return VHX_E_INVALID_ARG;
+    uint32_t w[5] = {0, 0, 0, 0, 0};
+    if (c->split && c->split_epoch && c->qctl.ptr) {
+        (void)hipSetDevice(c->device);
+        VHX_STREAM(c);
+        VHX_HIP(c, hipStreamSynchronize(c->stream));
+        for (uint32_t k = 0; k < 5u; ++k)
+            VHX_HIP(c, hipMemcpy(&w[k], (uint32_t *)c->qctl.ptr + QCTL_SPLIT + 64u * k, 4, hipMemcpyDeviceToHost));
+    }
+    if (handed_over) *handed_over = w[0] < VHX_OVF_CAP ? w[0] : VHX_OVF_CAP;
+    if (errors) *errors = w[4];
     return VHX_OK;
 }
 
@@ -1563,6 +1896,13 @@ void vhx::copy_sched(vhx_ctx *c, const vhx_ctx *owner) {
     c->queue_waves_mid = owner->queue_waves_mid;
     c->qxcd = owner->qxcd;
     c->qxcd_all = owner->qxcd_all;
+    c->split_force = owner->split_force;
+    c->split_period = owner->split_period;
+    c->split_min_lanes = owner->split_min_lanes;
+    c->split_min_idle = owner->split_min_idle;
+    c->split_take = owner->split_take;
+    c->split_diag = owner->split_diag;
+    c->split_max_wait = owner->split_max_wait;
     std::memcpy(c->sparse, owner->sparse, sizeof(c->sparse));
     c->prepass = owner->prepass;
     c->prepass_margin = owner->prepass_margin;
