@@ -149,15 +149,18 @@ struct vhx_ctx {
     // Pass 0 at 12 under frames in flight: eight frames 0.645-0.651 ms per bench frame against 0.665-0.670 (8:
     // 0.651-0.661, 16: 0.646-0.657, 24 and 32 slower); the later budgeted passes gained nothing (profiles/r02/sparse*.log)
     uint32_t sparse[VHX_MAX_BUDGETS] = {12u};
-    // tail split of the unbounded last pass (k_trace_queue_split in vhx_device.hip): in force for this trace (the
-    // selected schedule's `split`; off under a fixed schedule), VHX_SPLIT=0/1 forces it either way (-1: not forced);
-    // ovf holds the overflow slots, split_epoch tags this context's frames in them
+    // tail split of the unbounded last pass (k_trace_queue_split in vhx_device.hip): in force for
+    // this trace (the selected schedule's `split`, off in both default schedules: it measured neutral; off under a
+    // fixed schedule), VHX_SPLIT=0/1 forces it either way (-1: not forced); ovf holds the overflow slots, split_epoch
+    // tags this context's frames in them
     uint32_t split = 0;
     int split_force = -1;
     uint32_t split_epoch = 0;
-    uint32_t split_period = 8, split_min_lanes = 2, split_min_idle = 1, split_take = 64;  // SplitQ (VHX_SPLIT_TUNE)
-    uint32_t split_diag = 0;  // SplitQ::diag (VHX_SPLIT_DIAG)
-    uint32_t split_max_wait = 64;  // SplitQ::max_wait (VHX_SPLIT_WAIT)
+    // SplitQ settings (VHX_SPLIT_TUNE = period,min_lanes,min_idle,take; VHX_SPLIT_WAIT; VHX_SPLIT_DIAG): the best of the
+    // lone-frame sweeps (profiles/r03/split/), 1.19-1.22 ms against 1.21-1.25 with the split off
+    uint32_t split_period = 128, split_min_lanes = 2, split_min_idle = 1, split_take = 32;
+    uint32_t split_diag = 0;
+    uint32_t split_max_wait = 32;
     DevBuf ovf;
 };
 

@@ -350,7 +350,7 @@ __device__ __forceinline__ uint32_t flag_bits(const void *src, uint64_t i, uint6
 // the tail split's counters (k_trace_queue_split), each on a 256-byte line: reserved overflow slots, taken slots, waves
 // waiting for work, waves holding rays, error word
 #define QCTL_SPLIT (16u + QCTL_PASS_WORDS * (VHX_MAX_BUDGETS + 1u))
-#define QCTL_WORDS (QCTL_SPLIT + 7u * 64u)
+#define QCTL_WORDS (QCTL_SPLIT + 10u * 64u)
 // Order of the pass-0 queue of a primary frame (vhx_ctx::qorder): W = 0 keeps output-index order (row-major in the
 // framebuffer layout); W > 0 lists the rays tile by tile -- TS x TS pixel tiles (TS = 1 << tsl >= 8), the tiles
 // row-major over the frame (tx per row) or, with mdim > 0, in Morton order over a 2^mdim x 2^mdim grid (tiles outside
@@ -824,7 +824,8 @@ __device__ __forceinline__ bool trace_split(const DevTree &t, const uint64_t *oc
     Trav<false, BD, false> tr;
     tr.begin_resumed(t, o, d, h, st);
     const uint32_t lane = threadIdx.x & 63u;
-    for (uint32_t k = 0;; ++k) {
+    uint32_t k = 0;
+    for (;; ++k) {
         // not before `period` iterations of this wave: a wave that just took handed-over rays first traces them
         // (checking at once made rays bounce from wave to wave, each hop costing more than the iterations it ran)
         const bool chk = ((k + 1u) & (s.period - 1u)) == 0u;
@@ -832,7 +833,7 @@ __device__ __forceinline__ bool trace_split(const DevTree &t, const uint64_t *oc
         if (chk) want = ld_agent(s.ctl + 128);
         tr.step(t, occ_tab, h, VHX_MAX_ITERS);
         if (tr.ex != 0u) break;
-        if (chk && want >= s.min_idle) {
+        if (chk && (int32_t)want >= (int32_t)s.min_idle) {
             const uint64_t act = __ballot(1);
             const uint32_t na = (uint32_t)__popcll(act);
             if (na >= s.min_lanes) {
@@ -840,9 +841,17 @@ __device__ __forceinline__ bool trace_split(const DevTree &t, const uint64_t *oc
                 const uint32_t nk = na >> 1, first = na - nk;
                 const bool go = rank >= first;
                 const uint32_t leader = (uint32_t)__builtin_ctzll(__ballot(go));
-                uint32_t base = 0;
-                if (lane == leader) base = atomicAdd(s.ctl, nk);
+                // book one waiting wave first (a split without a taker parks the rays: measured 1.5-15 ms lone frames
+                // where every tracing wave split as soon as one wave waited); no taker booked, no split
+                uint32_t base = 0xFFFFFFFFu;
+                if (lane == leader) {
+                    if ((int32_t)atomicSub(s.ctl + 128, 1u) > 0)
+                        base = atomicAdd(s.ctl, nk);
+                    else
+                        atomicAdd(s.ctl + 128, 1u);
+                }
                 base = __shfl(base, (int)leader);
+                if (base == 0xFFFFFFFFu) continue;
                 if (go) {
                     const uint32_t slot = base + rank - first;
                     if (base + nk <= VHX_OVF_CAP) {
@@ -854,6 +863,19 @@ __device__ __forceinline__ bool trace_split(const DevTree &t, const uint64_t *oc
                 }
                 if (tr.ex != 0u) break;
             }
+        }
+    }
+    if (s.diag & 2u) {  // diagnostics: ray iterations (sum over lanes) and wave iterations (max) of this call
+        uint32_t sum = k + 1u, mx = k + 1u;
+        for (uint32_t dd = 32; dd > 0; dd >>= 1) {
+            const uint32_t a = __shfl_xor(sum, dd), b = __shfl_xor(mx, dd);
+            const bool live = ((__ballot(1) >> (lane ^ dd)) & 1ull) != 0ull;
+            sum += live ? a : 0u;
+            mx = live && b > mx ? b : mx;
+        }
+        if (lane == (uint32_t)__builtin_ctzll(__ballot(1))) {
+            atomicAdd(s.ctl + 448, sum);
+            atomicAdd(s.ctl + 512, mx);
         }
     }
     if (tr.ex == 5u) return false;
@@ -876,7 +898,8 @@ __global__ void __launch_bounds__(256) VHX_QUEUE_ATTR_SPLIT k_trace_queue_split(
     uint32_t xcd = blockIdx.x & 7u, tries = 0;
     const uint32_t qxcd = (n + rpw - 1) / rpw > gridDim.x * (blockDim.x / 64u) ? q.qxcd : 0u;
     uint32_t *const tail = s.ctl, *const head = s.ctl + 64, *const idle = s.ctl + 128, *const active = s.ctl + 192;
-    bool drained = false, waiting = false;
+    uint32_t *const nwait = s.ctl + 576;
+    bool drained = false, waiting = false, registered = false;
     uint32_t spins = 0;
     for (;;) {
         uint32_t base = 0, cnt = 0;
@@ -939,23 +962,24 @@ __global__ void __launch_bounds__(256) VHX_QUEUE_ATTR_SPLIT k_trace_queue_split(
             if (!got) {
                 if (fin || ++spins >= VHX_SPLIT_SPINS) break;
                 if ((s.diag & 2u) && lane == 0) atomicAdd(s.ctl + 384, 1u);
-                if (!waiting) {  // at most s.max_wait waves wait (pollers of one line slow the whole chip)
-                    uint32_t before = 0;
-                    if (lane == 0) before = atomicAdd(idle, 1u);
-                    before = __builtin_amdgcn_readfirstlane(__shfl(before, 0));
-                    if (before >= s.max_wait) {
-                        if (lane == 0) atomicSub(idle, 1u);
-                        break;
+                if (!waiting) {
+                    if (!registered) {  // at most s.max_wait waves wait (pollers of one line slow the whole chip)
+                        uint32_t before = 0;
+                        if (lane == 0) before = atomicAdd(nwait, 1u);
+                        before = __builtin_amdgcn_readfirstlane(__shfl(before, 0));
+                        if (before >= s.max_wait) {
+                            if (lane == 0) atomicSub(nwait, 1u);
+                            break;
+                        }
+                        registered = true;
                     }
+                    if (lane == 0) atomicAdd(idle, 1u);  // bookable by a tracing wave
                     waiting = true;
                 }
                 __builtin_amdgcn_s_sleep(32);  // ~2000 cycles between polls (few waves wait: s.max_wait)
                 continue;
             }
-            if (waiting) {
-                if (lane == 0) atomicSub(idle, 1u);
-                waiting = false;
-            }
+            waiting = false;  // a tracing wave that handed rays over booked this wave (took it off `idle`)
             from_ovf = true;
             base = h0;
             cnt = got;
@@ -997,6 +1021,7 @@ __global__ void __launch_bounds__(256) VHX_QUEUE_ATTR_SPLIT k_trace_queue_split(
         if (lane == 0) atomicSub(active, 1u);
     }
     if (waiting && lane == 0) atomicSub(idle, 1u);
+    if (registered && lane == 0) atomicSub(nwait, 1u);
 }
 
 // Scatters rank-gathered tile buffers into framebuffers. Rank r's part of `gathered` holds `planes` planes of
@@ -1392,11 +1417,12 @@ static void debug_passes(vhx_ctx *c, const char *what) {
     fprintf(stderr, "[vhx passes] %-24s counts %u %u %u %u ... %u  grabs %u %u %u %u\n", what, v[0], v[1], v[2], v[3],
             v[7], v[8], v[9], v[10], v[11]);
     if (c->split) {  // tail split: slots reserved / taken, waves waiting / holding rays, error word
-        uint32_t w[7];
-        for (uint32_t k = 0; k < 7u; ++k)
+        uint32_t w[9];
+        for (uint32_t k = 0; k < 9u; ++k)
             (void)hipMemcpy(&w[k], (uint32_t *)c->qctl.ptr + QCTL_SPLIT + 64u * k, 4, hipMemcpyDeviceToHost);
         fprintf(stderr, "[vhx passes] %-24s split slots %u taken %u idle %u active %u error %u slot polls failed %u "
-                "waiter polls %u\n", what, w[0], w[1], w[2], w[3], w[4], w[5], w[6]);
+                "waiter polls %u ray iterations %u wave iterations %u\n", what, w[0], w[1], w[2], w[3], w[4], w[5], w[6],
+                w[7], w[8]);
     }
 }
 
