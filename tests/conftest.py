@@ -9,12 +9,12 @@ if ROOT not in sys.path:
 
 # Frames in flight (tests/test_gpu_inflight.py, the bench's configuration): every context stream needs a hardware queue
 # of its own, and HIP reads GPU_MAX_HW_QUEUES once, when it initialises -- so it is raised here, before any test
-# imports torch or loads libvhx (the same rule as bench.py's hw_queues)
+# imports torch or loads libvhx (the same rule as bench.py's hw_queues: F + 4 for the bench's F = 16)
 try:
-    if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 12:
-        os.environ["GPU_MAX_HW_QUEUES"] = "12"
+    if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 20:
+        os.environ["GPU_MAX_HW_QUEUES"] = "20"
 except ValueError:
-    os.environ["GPU_MAX_HW_QUEUES"] = "12"
+    os.environ["GPU_MAX_HW_QUEUES"] = "20"
 
 
 def pytest_configure(config):

@@ -108,14 +108,16 @@ struct vhx_ctx {
     //    at 8 waves per CU (profiles/r03/sched_r03.log, ladder_r03b.log; 4 against 8 queue waves per CU is within noise
     //    at eight frames in flight, 0.562-0.566 against 0.563-0.565 ms, qwaves_r03.log): the queue passes are most of
     //    the frame period (pass_share_r03.log); a finer ladder re-packs the surviving rays into full waves more often,
-    //    and fewer queue waves leave the SIMDs to the other frames' first passes;
+    //    and fewer queue waves leave the SIMDs to the other frames' first passes; 3 queue waves per CU since the bench
+    //    runs sixteen frames in flight (0.478 against 0.484 ms for 4 and 0.489-0.491 for 6, two rounds,
+    //    profiles/r03/inflight/);
     //  * `idle` otherwise (one frame at a time, or frames serialised on one stream): {64} without sparse-wave
     //    abandonment at 8 queue waves per CU -- 1.22 ms for the lone bench frame against 1.54 ms for the busy schedule
     //    run alone (profiles/r03/isolated_r03.log, reentry_r03c/isolated.log; {64, 1024}, {64, 512}, {48, 768} and
     //    three-budget ladders 1.31-1.51 ms, fewer rays per wave in a last pass no better): every extra pass lengthens a
     //    lone frame's critical path.
     bool adaptive = true;
-    Sched sched_busy = {{24u, 72u, 216u, 648u}, 5u, {12u}, 4u, VHX_QORDER_BUSY, 0u};
+    Sched sched_busy = {{24u, 72u, 216u, 648u}, 5u, {12u}, 3u, VHX_QORDER_BUSY, 0u};
     Sched sched_idle = {{64u}, 2u, {0u}, 8u, VHX_QORDER_IDLE, 0u};
     int last_sched = -1;  // the schedule of the last trace: 1 busy, 0 idle, -1 fixed (vhx_get_pass_budgets)
     // the schedule in force (the selected one, or the fixed one)
