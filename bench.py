@@ -92,6 +92,16 @@ def parse():
                         "(vhx_set_node_mips); N = 1, no roofline / CPU leg (keep --size <= 256: O(size^3) inserts)")
     p.add_argument("--no-overlap", action="store_true",
                    help="N>1: gather each frame before tracing the next (default: frame k's gather overlaps k+1)")
+    p.add_argument("--tune", default=None, metavar="SPEC",
+                   help="scheduling knobs of every context (vhx_set_tuning \"key=value;...\", include/vhx.h; results "
+                        "never change): experiments only")
+    p.add_argument("--planes", type=int, choices=(1, 2), default=1,
+                   help="N>1 (vhx_mgpu): planes each rank sends to rank 0 in the timed frames: 1 = RGBA8 (the reference's "
+                        "display output, the rgba8unorm view texture of src/raytracing/bevy/view.rs:269-289), 2 = RGBA8 + "
+                        "f32 depth; the untimed multi-GPU check runs both")
+    p.add_argument("--no-extra", action="store_true",
+                   help="skip the untimed-region extras of an N = 1 line: the `lone` (one frame at a time) and `orbit` "
+                        "(distinct cameras in flight) sub-objects")
     p.add_argument("--root-slots", type=int, default=0,
                    help="N>1 (vhx_mgpu): rank 0's share of the tile slots (R of R+N-1); 0 (default) = measured before "
                         "the warm-up by vhx_mgpu_balance (untimed)")
@@ -203,7 +213,7 @@ def measure_traffic():
     cmd = ([rp, "--pmc"] + counters + ["--kernel-trace", "-f", "csv", "-d", d, "-o", "pmc", "--", sys.executable,
                                        os.path.abspath(__file__)] + sys.argv[1:] +
            ["--steps", "5", "--warmup", "1", "--no-cpu-baseline", "--no-roofline", "--no-pmc",
-            "--no-frame-check"])
+            "--no-frame-check", "--no-extra"])
     env = dict(os.environ, TMPDIR="/tmp")
     env.pop("VHX_BENCH_MGPU1", None)  # the child times the single-GPU path only
     try:
@@ -379,7 +389,7 @@ def main():
     else:
         torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    rt = vhx.Raytracer(local)
+    rt = vhx.Raytracer(local, tune=args.tune)
     # the context's own stream, shared with torch (ExternalStream): the kernels and the events that time them are
     # ordered on it. Every frame in flight traces on its context's own stream; those streams are created back to back
     # so that each gets a hardware queue of its own (GPU_MAX_HW_QUEUES = 4; streams share queues round-robin in
@@ -408,6 +418,7 @@ def main():
             try:
                 mg = M.MgpuRenderer(rt, obj[0], world, rank, tile_size=args.tile, overlap=not args.no_overlap)
                 mg.set_frames_in_flight(min(F, N.VHX_MGPU_MAX_INFLIGHT))
+                mg.set_planes(args.planes)
             except Exception as e:  # noqa: BLE001
                 mgpu_fallback = f"vhx_mgpu on rank {rank}: {e}"
                 mg = None
@@ -481,7 +492,7 @@ def main():
     fb_rgba = fb_depth = None
     if mg is not None and rank == 0:
         fb_rgba = torch.zeros(W * H, dtype=torch.int32, device=dev)
-        fb_depth = torch.zeros(W * H, dtype=torch.float32, device=dev)
+        fb_depth = torch.zeros(W * H, dtype=torch.float32, device=dev) if args.planes == 2 else None
     # frames in flight (single-GPU and torch paths; vhx_mgpu keeps its own): F contexts sharing the tree, F streams,
     # F output sets
     if args.depth_prepass is not None:
@@ -490,6 +501,8 @@ def main():
     if mg is None:
         for _ in range(F - 1):
             r = rt.shared()
+            if args.tune:
+                r.set_tuning(args.tune)
             rts.append(r)
             streams.append(torch.cuda.ExternalStream(r.stream(), device=dev))
     # the pass schedule of every context (vhx_mgpu re-copies the owner context's settings to its frames' contexts)
@@ -607,8 +620,9 @@ def main():
     # isolated launch (one frame at a time, libvhx's own events) after it
     if ev:
         kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-    iso = []
+    iso, iso_wall = [], []
     for _ in range(5):
+        tw0 = time.perf_counter()
         if mg is not None:
             mg.render(cam, fb_rgba, fb_depth)
             iso.append(mg.sync())
@@ -620,8 +634,48 @@ def main():
                 iso = None
                 break
             iso.append(rt.sync())
+        iso_wall.append(time.perf_counter() - tw0)
     kernel_ms_isolated = float(np.median(iso)) if iso else None
     sched_iso = None if mg is not None else rt.pass_budgets()
+    # ---- extras of an N = 1 line (untimed region): the lone frame -- the reference's call shape,
+    # one dispatch per frame (VhxRenderNode::run, src/raytracing/bevy/pipeline/mod.rs:96-155) -- and distinct cameras
+    # in flight (an orbiting view, every frame a different camera)
+    lone = orbit = None
+    if mg is None and world == 1 and not args.shadows and not args.no_extra and iso:
+        lone = {"ms": round(kernel_ms_isolated, 4), "mrays_per_s": round(W * H / kernel_ms_isolated / 1e3, 3),
+                "wall_ms": round(float(np.median(iso_wall)) * 1e3, 4), "frames": len(iso),
+                "schedule": None if sched_iso is None else {"budgets": list(sched_iso[0]), "choice": sched_iso[1]},
+                "basis": "one frame at a time on one context (submit, synchronise): median of 5 device times between "
+                         "libvhx's events around the launch (ms) and of the host wall time of submit + synchronise "
+                         "(wall_ms); the bench camera, after the timed frames"}
+        if not args.orbit and len(rts) > 1:
+            ko, wo, rad = 20, 5, 0.01
+            ocams = [vhx.glass_camera(args.size, W, H, angle=40.0 + k * rad, target=(c, c, c)) for k in range(wo + ko)]
+            seen = {}
+            torch.cuda.synchronize(dev)
+            to0 = None
+            for k in range(wo + ko):
+                if k == wo:
+                    torch.cuda.synchronize(dev)
+                    to0 = time.perf_counter()
+                f = k % len(rts)
+                rts[f].trace_primary(ocams[k], out=outs[f], **trace_kw)
+                seen[f] = ocams[k]
+            torch.cuda.synchronize(dev)
+            o_el = time.perf_counter() - to0
+            # two contexts' last orbit frames against one context tracing the same camera alone
+            o_eq = True
+            for f in sorted(seen)[:2]:
+                ref = rt.trace_primary(seen[f], fields=("rgba", "depth"))
+                for k2 in ("rgba", "depth"):
+                    o_eq = o_eq and bool(np.array_equal(outs[f][k2].cpu().numpy().view(np.uint32),
+                                                        ref[k2].view(np.uint32)))
+            orbit = {"ms_per_frame": round(o_el * 1e3 / ko, 4), "mrays_per_s": round(W * H * ko / o_el / 1e6, 3),
+                     "frames": ko, "warmup": wo, "rad_per_frame": rad, "frames_in_flight": len(rts),
+                     "frames_equal": o_eq,
+                     "basis": f"{ko} timed frames after {wo} warm-up frames, frame k viewing from 40 + {rad}k rad (every "
+                              "frame a distinct camera), submitted like the timed steps and timed between "
+                              "synchronisations; the last frames of two contexts compared with a lone trace"}
     if not ev:
         kernel_ms = kernel_ms_isolated
 
@@ -653,20 +707,37 @@ def main():
         dist.all_gather_object(per_rank, {"rank": rank, "trace_ms": round(tr_ms, 4), "transfer_ms": round(tx_ms, 4),
                                           "rays": int(mg.rays(W, H))})
         if split is not None:
+            split["planes"] = args.planes
+            split["bytes_into_rank0_per_frame"] = int(mg.frame_bytes(W, H))
             split["per_rank"] = per_rank
             split["per_rank_basis"] = ("vhx_mgpu_measure at the timed split, 4 frames one at a time (median): trace = "
                                        "the rank's tile slots, transfer = rank 0 its receives / ranks >= 1 their send")
 
     # ---- multi-GPU check (untimed): the gathered, untiled frame equals rank 0 tracing the whole frame alone -------
     mgpu = None
-    if (world > 1 or mg is not None) and rank == 0:
-        fields = ("rgba", "depth") if mg is not None else ("rgba",)
-        whole = rt.trace_primary(cam, fields=fields)
-        got = (fb_rgba if mg is not None else framebuffer).cpu().numpy().view(np.uint32)
-        eq = bool(np.array_equal(got, whole["rgba"]))
-        if mg is not None:
-            eq = eq and bool(np.array_equal(fb_depth.cpu().numpy().view(np.uint32), whole["depth"].view(np.uint32)))
-        mgpu = {"frame_equal": eq, "fields": list(fields), "pixels": int(W * H)}
+    if world > 1 or mg is not None:
+        whole = None
+        if rank == 0:
+            whole = rt.trace_primary(cam, fields=("rgba", "depth") if mg is not None else ("rgba",))
+            got = (fb_rgba if mg is not None else framebuffer).cpu().numpy().view(np.uint32)
+            eq = bool(np.array_equal(got, whole["rgba"]))
+            fields = ["rgba"]
+            if fb_depth is not None:
+                eq = eq and bool(np.array_equal(fb_depth.cpu().numpy().view(np.uint32), whole["depth"].view(np.uint32)))
+                fields.append("depth")
+            mgpu = {"frame_equal": eq, "fields": fields, "pixels": int(W * H),
+                    "basis": "the gathered, untiled frame of the timed configuration vs rank 0 tracing it alone"}
+        if mg is not None and args.planes == 1:
+            # the two-plane transfer too (collective on every rank): RGBA8 + depth gathered and untiled
+            mg.set_planes(2)
+            fbd2 = torch.zeros(W * H, dtype=torch.float32, device=dev) if rank == 0 else None
+            mg.render(cam, fb_rgba, fbd2)
+            mg.sync()
+            if rank == 0:
+                eq2 = bool(np.array_equal(fb_rgba.cpu().numpy().view(np.uint32), whole["rgba"])) and \
+                    bool(np.array_equal(fbd2.cpu().numpy().view(np.uint32), whole["depth"].view(np.uint32)))
+                mgpu["two_plane_frame_equal"] = eq2
+            mg.set_planes(1)
 
     # ---- roofline: algorithmic bytes of this rank's launch (instrumented kernel, untimed) -------------------------
     roof = None
@@ -787,6 +858,12 @@ def main():
         if frames_check is not None:
             line.update(frames_equal=frames_check["frames_equal"], golden_match=frames_check["golden_match"],
                         frames_check=frames_check)
+        if lone is not None:
+            line["lone"] = lone
+        if orbit is not None:
+            line["orbit"] = orbit
+        if args.tune:
+            line["tune"] = args.tune
         if mgpu is not None:
             line["multi_gpu_check"] = mgpu
         if mgpu_fallback:

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define VHX_ABI_VERSION 3u
+#define VHX_ABI_VERSION 4u
 
 /* ---- error codes ------------------------------------------------------------------------------------------ */
 #define VHX_OK 0
@@ -162,16 +162,23 @@ int vhx_sync(vhx_ctx *ctx, float *last_trace_ms);
  * By default the schedule is adaptive: a trace submitted while another context of the same tree (vhx_create_shared)
  * has a frame in flight on another stream runs the frames-in-flight schedule {24, 72, 216, 648}; otherwise (one frame
  * at a time, or frames serialised on one stream) the lone-frame schedule {64}. vhx_set_pass_budgets fixes the
- * budgets (and ends the adaptive choice; vhx_set_adaptive_schedule(ctx, 1) restores it); the environment overrides
- * VHX_BUDGETS, VHX_SPARSE and VHX_QWAVES fix it likewise. */
+ * budgets (and ends the adaptive choice; vhx_set_adaptive_schedule(ctx, 1) restores it). vhx_set_adaptive_schedule(ctx,
+ * 0) fixes the frames-in-flight schedule whatever the last trace ran. */
 #define VHX_MAX_BUDGETS 6
 int vhx_set_pass_budgets(vhx_ctx *ctx, const uint32_t *budgets, uint32_t n);
 int vhx_set_adaptive_schedule(vhx_ctx *ctx, int on);
 /* The budgets of the context's last trace (or the fixed ones before any), n of them (budgets: VHX_MAX_BUDGETS entries,
  * may be NULL); *schedule (may be NULL) = 1 the frames-in-flight schedule, 0 the lone-frame one, -1 fixed. */
 int vhx_get_pass_budgets(const vhx_ctx *ctx, uint32_t *budgets, uint32_t *n, int *schedule);
+/* Scheduling knobs (no reference counterpart; results never depend on them -- experiments and probes): `spec` is
+ * "key=value[;key=value...]" with keys budgets (list, fixes the schedule), adaptive (0/1), rpw (list: rays per wave of
+ * queue passes 1.., 0 = adaptive), tw, xcdg, resume (0/1), save_from, qblock (64/128/256), qwaves (fixes the schedule),
+ * qwavesm, qwaves0, qxcd, qxcd_all (0/1), sparse (list, fixes the schedule), qorder ("[m]N[z|r]" or 0), split (0/1),
+ * split_wait, split_diag, split_tune ("period,min_lanes,min_idle,take"). The library reads no environment variable for any of them. Unknown keys or
+ * malformed values: VHX_E_INVALID_ARG and nothing is changed. */
+int vhx_set_tuning(vhx_ctx *ctx, const char *spec);
 /* Tail split of the last trace (the lone-frame schedule's unbounded last pass shares its slowest rays out between
- * waves: DESIGN.md section 14.10; VHX_SPLIT=0/1 forces it off / on): synchronises the context's stream and reports the
+ * waves: DESIGN.md section 14.10; vhx_set_tuning "split=0/1" forces it off / on): synchronises the context's stream and reports the
  * rays handed over from one wave to another (*handed_over) and hand-offs that never completed (*errors, always 0
  * unless something is broken). Both 0 when the last trace ran no split pass. Diagnostics; results never depend on it. */
 int vhx_get_split_stats(vhx_ctx *ctx, uint32_t *handed_over, uint32_t *errors);
@@ -324,6 +331,13 @@ int vhx_mgpu_set_root_slots(vhx_mgpu *m, uint32_t root_slots);
  * any output pointer may be NULL. */
 int vhx_mgpu_balance(vhx_mgpu *m, const vhx_camera *cam, uint32_t frames, uint32_t *root_slots, float *trace_ms,
                      float *transfer_ms);
+/* Planes each rank sends to rank 0 (every rank must pass the same value; waits for the frames in flight): 2 (default)
+ * = RGBA8 + f32 depth, 1 = RGBA8 only -- the reference's display output is the rgba8unorm view texture
+ * (src/raytracing/bevy/view.rs:269-289), so a renderer that needs no depth halves rank 0's intake over xGMI. With one
+ * plane rank 0 passes fb_depth = NULL to vhx_mgpu_render. */
+int vhx_mgpu_set_planes(vhx_mgpu *m, uint32_t planes);
+/* Bytes rank 0 receives over xGMI per width x height frame at the current split and plane count. */
+int vhx_mgpu_frame_bytes(const vhx_mgpu *m, uint32_t width, uint32_t height, uint64_t *into_root);
 /* nranks, rank, and the rays this rank traces for a width x height frame (any pointer may be NULL). */
 int vhx_mgpu_info(const vhx_mgpu *m, uint32_t width, uint32_t height, int *nranks, int *rank, uint64_t *rays);
 /* The tile plan of the split, as vhx_mgpu_render deals it (a pure function: no device, no communicator). For N ranks,

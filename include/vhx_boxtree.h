@@ -100,6 +100,10 @@ int vhx_boxtree_switch_mips(vhx_boxtree *tree, int enabled);
 int vhx_boxtree_set_mip_method(vhx_boxtree *tree, uint32_t level, uint32_t method, float threshold);
 int vhx_boxtree_set_mip_color_threshold(vhx_boxtree *tree, uint32_t level, float threshold);
 int vhx_boxtree_recalculate_mips(vhx_boxtree *tree);
+/* Process-wide options of the MIP generation (no reference counterpart; results never depend on them): direct = 1 runs
+ * the direct restatement (get_internal per sample, full palette scans) instead of the exact shortcuts (tests compare the
+ * two); threads caps the leaf-resampling workers (0 = up to 16). */
+int vhx_boxtree_set_mip_options(int direct, int threads);
 /* The root's MIP (sectant 64) or its child's (sectant < 64) at cell (x, y, z) of the brick, as an entry. */
 int vhx_boxtree_sample_root_mip(const vhx_boxtree *tree, uint32_t sectant, uint32_t x, uint32_t y, uint32_t z,
                                 uint32_t *kind, uint32_t *albedo, uint32_t *data);

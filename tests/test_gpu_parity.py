@@ -295,29 +295,27 @@ def test_multipass_schedule_is_bit_identical(gpu, oracle, budgets):
         gpu.set_pass_budgets(DEFAULT_BUDGETS)
 
 
-SCHEDULER_ENVS = [{"VHX_RESUME": "0"},                                   # abandoned rays re-traced from scratch
-                  {"VHX_RPW": "0,0", "VHX_TW": "7"},                      # adaptive rays per wave, few waves
-                  {"VHX_RPW": "0,3", "VHX_TW": "100000", "VHX_QBLOCK": "64"},  # one ray per wave, 1-wave workgroups
-                  {"VHX_QXCD": "0", "VHX_XCDG": "0"},                    # one counter, pass-0 blocks in dispatch order
-                  {"VHX_XCDG": "3"},                                     # odd pass-0 XCD block runs
-                  {"VHX_QXCD": "4"},                                     # shorter runs dealt over the XCDs
-                  {"VHX_QXCD": "1", "VHX_RPW": "0,0", "VHX_TW": "7"},    # ... single chunks, few adaptive waves
-                  {"VHX_SPARSE": "64,64,64"},                            # waves abandon as soon as one lane ends
-                  {"VHX_SPARSE": "0"},                                   # no sparse-wave abandonment
-                  {"VHX_QXCD_ALL": "1", "VHX_QWAVESM": "300"},           # every queue pass dealt over the XCDs
-                  {"VHX_QORDER": "16"},                                  # pass-0 queue in 16x16 tile order
-                  {"VHX_QORDER": "m8"},                                  # ... in Morton order of 8x8 tiles
-                  {"VHX_QORDER": "m32z"},                                # ... every pixel in Morton order
-                  {"VHX_QORDER": "32r"}]                                 # ... 32x32 tiles by rows
+SCHEDULER_TUNES = ["resume=0",                        # abandoned rays re-traced from scratch
+                   "rpw=0,0;tw=7",                    # adaptive rays per wave, few waves
+                   "rpw=0,3;tw=100000;qblock=64",     # one ray per wave, 1-wave workgroups
+                   "qxcd=0;xcdg=0",                   # one counter, pass-0 blocks in dispatch order
+                   "xcdg=3",                          # odd pass-0 XCD block runs
+                   "qxcd=4",                          # shorter runs dealt over the XCDs
+                   "qxcd=1;rpw=0,0;tw=7",             # ... single chunks, few adaptive waves
+                   "sparse=64,64,64",                 # waves abandon as soon as one lane ends
+                   "sparse=0",                        # no sparse-wave abandonment
+                   "qxcd_all=1;qwavesm=300",          # every queue pass dealt over the XCDs
+                   "qorder=16",                       # pass-0 queue in 16x16 tile order
+                   "qorder=m8",                       # ... in Morton order of 8x8 tiles
+                   "qorder=m32z",                     # ... every pixel in Morton order
+                   "qorder=32r"]                      # ... 32x32 tiles by rows
 
 
-@pytest.mark.parametrize("env", SCHEDULER_ENVS, ids=lambda e: "+".join(f"{k}={v}" for k, v in e.items()))
-def test_scheduler_variants_are_bit_identical(oracle, monkeypatch, env):
-    """Scheduler knobs read at context creation (re-trace instead of resume, adaptive rays per wave, queue
-    workgroup size) change only the schedule: results and byte counts stay the oracle's."""
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
-    rt = vhx.Raytracer(0)
+@pytest.mark.parametrize("tune", SCHEDULER_TUNES)
+def test_scheduler_variants_are_bit_identical(oracle, tune):
+    """Scheduler knobs (vhx_set_tuning: re-trace instead of resume, adaptive rays per wave, queue workgroup size, queue
+    orders) change only the schedule: results and byte counts stay the oracle's."""
+    rt = vhx.Raytracer(0, tune=tune)
     try:
         flat = vhx.FlatTree.build_scene(N.VHX_SCENE_LATTICE_CUBE, 256, 4)
         rt.upload(flat)
@@ -328,8 +326,8 @@ def test_scheduler_variants_are_bit_identical(oracle, monkeypatch, env):
         ref_frame = oracle.trace_primary(flat, cam, 0, 0, 160, 96, count_bytes=True)
         for budgets in ((2, 9, 30), (16,), ()):
             rt.set_pass_budgets(budgets)
-            assert_same(rt.trace_rays(o, d, count_bytes=True), ref_rays, f"rays {env} {budgets}")
-            assert_same(rt.trace_primary(cam, count_bytes=True), ref_frame, f"frame {env} {budgets}")
+            assert_same(rt.trace_rays(o, d, count_bytes=True), ref_rays, f"rays {tune} {budgets}")
+            assert_same(rt.trace_primary(cam, count_bytes=True), ref_frame, f"frame {tune} {budgets}")
             full = ref_frame["rgba"].reshape(96, 160)
             for T, R in ((64, 2), (24, 3)):  # tile layout: the pixel stream maps back through the tile numbering
                 tiles_x = (160 + T - 1) // T
@@ -340,7 +338,7 @@ def test_scheduler_variants_are_bit_identical(oracle, monkeypatch, env):
                         tile = r + j * R
                         tx, ty = (tile % tiles_x) * T, (tile // tiles_x) * T
                         want = full[ty:ty + T, tx:tx + T]
-                        assert np.array_equal(part[j, :want.shape[0], :want.shape[1]], want), (env, budgets, T, tile)
+                        assert np.array_equal(part[j, :want.shape[0], :want.shape[1]], want), (tune, budgets, T, tile)
     finally:
         rt.close()
 

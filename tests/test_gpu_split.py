@@ -18,19 +18,14 @@ pytestmark = pytest.mark.gpu
 
 META = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "frames.json")))
 
-# VHX_SPLIT=1 puts the split on every fixed schedule; more queue waves or one-wave workgroups change how many waves
+# split=1 puts the split on every fixed schedule; more queue waves or one-wave workgroups change how many waves
 # wait and how often tracing waves split; few adaptive rays per wave make the main queue itself thin
-SPLIT_ENVS = [{"VHX_SPLIT": "1"},
-              {"VHX_SPLIT": "1", "VHX_QWAVES": "8192"},
-              {"VHX_SPLIT": "1", "VHX_QBLOCK": "64", "VHX_QXCD": "0"},
-              {"VHX_SPLIT": "1", "VHX_RPW": "0,0,0,0", "VHX_TW": "7"}]
+SPLIT_TUNES = ["split=1", "split=1;qwaves=8192", "split=1;qblock=64;qxcd=0", "split=1;rpw=0,0,0,0;tw=7"]
 
 
-@pytest.mark.parametrize("env", SPLIT_ENVS, ids=lambda e: "+".join(f"{k}={v}" for k, v in e.items()))
-def test_split_pass_vs_oracle(oracle, monkeypatch, env):
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
-    rt = vhx.Raytracer(0)
+@pytest.mark.parametrize("tune", SPLIT_TUNES)
+def test_split_pass_vs_oracle(oracle, tune):
+    rt = vhx.Raytracer(0, tune=tune)
     try:
         flat = vhx.FlatTree.build_scene(N.VHX_SCENE_LATTICE_CUBE, 256, 4)
         rt.upload(flat)
@@ -43,12 +38,12 @@ def test_split_pass_vs_oracle(oracle, monkeypatch, env):
         handed = 0
         for budgets in ((64,), (2, 9, 30), (4, 40), (1,)):
             rt.set_pass_budgets(budgets)
-            assert_same(rt.trace_rays(o, d), ref_rays, f"rays {env} {budgets}")
+            assert_same(rt.trace_rays(o, d), ref_rays, f"rays {tune} {budgets}")
             h, err = rt.split_stats()
-            assert err == 0, f"{err} hand-offs never completed ({env} {budgets})"
+            assert err == 0, f"{err} hand-offs never completed ({tune} {budgets})"
             handed += h
             for rep in range(2):  # the second frame reuses the slots under the next epoch
-                assert_same(rt.trace_primary(cam), ref_frame, f"frame {env} {budgets} #{rep}")
+                assert_same(rt.trace_primary(cam), ref_frame, f"frame {tune} {budgets} #{rep}")
                 h, err = rt.split_stats()
                 assert err == 0
                 handed += h
@@ -57,10 +52,9 @@ def test_split_pass_vs_oracle(oracle, monkeypatch, env):
         rt.close()
 
 
-def test_split_shadow_rays_vs_oracle(oracle, monkeypatch):
+def test_split_shadow_rays_vs_oracle(oracle):
     """Shadow rays (config 5) resume through the same split pass."""
-    monkeypatch.setenv("VHX_SPLIT", "1")
-    rt = vhx.Raytracer(0)
+    rt = vhx.Raytracer(0, tune="split=1")
     try:
         size, w, h = 256, 256, 192
         flat = vhx.FlatTree.build_scene(N.VHX_SCENE_LATTICE_CUBE, size, 4)
@@ -83,12 +77,11 @@ def test_split_shadow_rays_vs_oracle(oracle, monkeypatch):
         rt.close()
 
 
-def test_lone_bench_frame_splits_and_matches_golden(monkeypatch):
+def test_lone_bench_frame_splits_and_matches_golden():
     """The adaptive lone frame at the headline size -- 3840x2160 on scene S 1024^3 bd 4, the bench's isolated frame --
     with the split on runs it and equals the golden digests of every field; so does a second frame (next epoch)."""
-    monkeypatch.setenv("VHX_SPLIT", "1")
     name = "c3_1024_bd4_3840x2160"
-    rt = vhx.Raytracer(0)
+    rt = vhx.Raytracer(0, tune="split=1")
     try:
         flat = vhx.FlatTree.build_scene(N.VHX_SCENE_LATTICE_CUBE, 1024, 4)
         rt.upload(flat)

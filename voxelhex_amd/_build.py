@@ -14,6 +14,9 @@ CSRC = os.path.join(HERE, "csrc")
 LIBDIR = os.path.join(HERE, "_lib")
 BUILD = os.path.join(ROOT, "build", "vhx")
 LIB = os.path.join(LIBDIR, "libvhx.so")
+# diagnostic variant builds (never loaded by the package unless VHX_LIB names them): the negative control of the tree-write
+# ordering (tests/test_gpu_tuning.py), with libvhx's waits compiled out
+UNORDERED_LIB = os.path.join(LIBDIR, "libvhx_unordered.so")
 ARCH = os.environ.get("VHX_OFFLOAD_ARCH", "gfx950")
 
 HOST_SRCS = ["boxtree.cpp", "flatten.cpp", "vox.cpp", "stream.cpp"]
@@ -77,6 +80,12 @@ def build(verbose=False, force=False, lib=None, build_dir=None, defines=(), flag
         # -ldl: RCCL is dlopen()ed by vhx_mgpu.hip (no link-time RCCL dependency)
         _run([_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-pthread", "-o", lib] + objs + ["-ldl"], verbose)
     return lib
+
+
+def build_variants(verbose=False, force=False):
+    """The diagnostic variant libraries the GPU tests load in child processes (built here, in-tree, so they travel)."""
+    build(verbose=verbose, force=force, lib=UNORDERED_LIB, build_dir=os.path.join(ROOT, "build", "vhx_unordered"),
+          defines=("VHX_UNORDERED_WRITES=1",))
 
 
 if __name__ == "__main__":

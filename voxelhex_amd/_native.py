@@ -97,6 +97,7 @@ SIGNATURES = [
     ("vhx_set_pass_budgets", c_int, [c_void_p, P(c_u32), c_u32]),
     ("vhx_set_adaptive_schedule", c_int, [c_void_p, c_int]),
     ("vhx_get_pass_budgets", c_int, [c_void_p, P(c_u32), P(c_u32), P(c_int)]),
+    ("vhx_set_tuning", c_int, [c_void_p, ctypes.c_char_p]),
     ("vhx_get_split_stats", c_int, [c_void_p, P(c_u32), P(c_u32)]),
     ("vhx_upload_tree", c_int, [c_void_p, P(TreeDesc)]),
     ("vhx_upload_tree_device", c_int, [c_void_p, P(TreeDesc)]),
@@ -123,11 +124,14 @@ SIGNATURES = [
     ("vhx_mgpu_sync", c_int, [c_void_p, P(c_f32)]),
     ("vhx_mgpu_info", c_int, [c_void_p, c_u32, c_u32, P(c_int), P(c_int), P(c_u64)]),
     ("vhx_mgpu_set_root_slots", c_int, [c_void_p, c_u32]),
+    ("vhx_mgpu_set_planes", c_int, [c_void_p, c_u32]),
+    ("vhx_mgpu_frame_bytes", c_int, [c_void_p, c_u32, c_u32, P(c_u64)]),
     ("vhx_mgpu_balance", c_int, [c_void_p, P(Camera), c_u32, P(c_u32), P(c_f32), P(c_f32)]),
     ("vhx_mgpu_tile_plan", c_int, [c_u32, c_u32, c_u32, c_u32, c_u32, c_u32, P(TilePlan)]),
     ("vhx_mgpu_measure", c_int, [c_void_p, P(Camera), c_u32, P(c_f32), P(c_f32)]),
     ("vhx_mgpu_destroy", None, [c_void_p]),
     ("vhx_boxtree_new", c_int, [c_u32, c_u32, P(c_void_p)]),
+    ("vhx_boxtree_set_mip_options", c_int, [c_int, c_int]),
     ("vhx_boxtree_free", None, [c_void_p]),
     ("vhx_boxtree_set_auto_simplify", c_int, [c_void_p, c_int]),
     ("vhx_boxtree_insert", c_int, [c_void_p, c_u32, c_u32, c_u32, c_u32, c_u32, c_u32]),

@@ -1066,12 +1066,12 @@ static inline float alb_distance(uint32_t x, uint32_t y) {
     return std::sqrt(dr * dr + dg * dg + db * db + da * da);
 }
 
-// VHX_MIP_GENERIC=1 (tests): the leaf resampling through get_internal and the palette matching by a full scan, the
-// direct restatements that leaf_value and mip_palette_match shortcut
-static bool mip_generic() {
-    static const bool g = getenv("VHX_MIP_GENERIC") != nullptr;
-    return g;
-}
+// Process-wide MIP options (vhx_boxtree_set_mip_options; the library reads no environment): `direct` (tests) runs the
+// leaf resampling through get_internal and the palette matching by a full scan, the direct restatements that
+// leaf_value and mip_palette_match shortcut; `threads` caps the leaf-resampling workers (0 = up to 16)
+std::atomic<int> g_mip_direct{0};
+std::atomic<int> g_mip_threads{0};
+static bool mip_generic() { return g_mip_direct.load(std::memory_order_relaxed) != 0; }
 
 // MIPResamplingFunction::execute (iterate.rs:434-560). `sample` returns false for None. PointFilter and Posterize keep
 // their groups in first-seen order where the reference iterates a std HashMap (random order per process): results
@@ -1373,7 +1373,10 @@ void BoxTree::recalculate_mips() {  // mipmap.rs:536-586: depth first, children 
         }
     }
     if (!mip_strategy.enabled) return;
-    const bool tm = getenv("VHX_MIP_TIMING") != nullptr;
+#ifndef VHX_MIP_TIMING
+#define VHX_MIP_TIMING 0  // a diagnostic build prints the phases of recalculate_mips
+#endif
+    const bool tm = VHX_MIP_TIMING != 0;
     auto t0 = std::chrono::steady_clock::now();
     auto lap = [&](const char *what) {
         if (!tm) return;
@@ -1426,7 +1429,7 @@ void BoxTree::recalculate_mips() {  // mipmap.rs:536-586: depth first, children 
                 }
         };
         unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-        if (const char *e = getenv("VHX_MIP_THREADS")) nt = std::max(1, atoi(e));
+        if (const int t = g_mip_threads.load(std::memory_order_relaxed); t > 0) nt = (unsigned)t;
         std::vector<std::thread> pool;
         for (unsigned t = 1; t < nt && (size_t)t * 64 < leaves.size(); ++t) pool.emplace_back(work);
         work();

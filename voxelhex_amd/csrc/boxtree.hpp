@@ -21,6 +21,7 @@
 #pragma once
 
 #include <array>
+#include <atomic>
 #include <deque>
 #include <functional>
 #include <cstddef>
@@ -30,6 +31,11 @@
 #include <vector>
 
 namespace vhx {
+
+// process-wide MIP generation options (vhx_boxtree_set_mip_options, boxtree.cpp)
+extern std::atomic<int> g_mip_direct;
+extern std::atomic<int> g_mip_threads;
+
 
 constexpr uint32_t kChildren = 64;
 constexpr uint32_t kEmpty32 = 0xFFFFFFFFu;

@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <condition_variable>
 #include <cstdint>
 #include <memory>
 #include <mutex>
@@ -36,6 +37,9 @@ struct TreeStore {
     // context (their use_ev), and records write_ev after it; a context's next trace waits for write_ev once per write
     // (write_seq against its seen_write). Contexts register in `users` at creation and leave at destruction.
     std::mutex mu;
+    std::condition_variable cv;  // tracing / writing changed
+    uint32_t tracing = 0;        // traces between trace_begin and trace_end (any thread)
+    uint32_t writing = 0;        // writes between write_begin and write_end
     std::vector<struct vhx_ctx *> users;
     hipEvent_t write_ev = nullptr;
     hipStream_t write_stream = nullptr;
@@ -62,6 +66,7 @@ struct vhx_ctx {
     std::shared_ptr<TreeStore> tree;  // shared by the contexts of one tree
     bool shared = false;              // made by vhx_create_shared: traces only (uploads and updates go to the owner)
     hipEvent_t use_ev = nullptr;      // recorded after every trace submitted on this context (TreeStore ordering)
+    hipStream_t use_stream = nullptr;  // the stream use_ev was last recorded on
     bool use_recorded = false;
     uint64_t seen_write = 0;          // the TreeStore write_seq this context's stream already waits for
     DevBuf scratch, rays;
@@ -213,6 +218,40 @@ int write_end(vhx_ctx *c);
 // before a trace on c's stream: wait for the tree's last write (once per write); after it: record c's use
 int trace_begin(vhx_ctx *c);
 int trace_end(vhx_ctx *c);
+// trace_begin .. trace_end (write_begin .. write_end) as a scope: the end runs on every exit once the begin succeeded,
+// so an error return after the first launch still records the trace's use (or the write) for the ordering
+struct TraceScope {
+    vhx_ctx *c;
+    int rc;
+    bool open;
+    explicit TraceScope(vhx_ctx *ctx) : c(ctx), rc(trace_begin(ctx)), open(true) {}
+    int end() {
+        if (!open) return VHX_OK;
+        open = false;
+        return trace_end(c);
+    }
+    ~TraceScope() {
+        if (open) (void)trace_end(c);
+    }
+    TraceScope(const TraceScope &) = delete;
+    TraceScope &operator=(const TraceScope &) = delete;
+};
+struct WriteScope {
+    vhx_ctx *c;
+    int rc;
+    bool open;
+    explicit WriteScope(vhx_ctx *ctx) : c(ctx), rc(write_begin(ctx)), open(true) {}
+    int end() {
+        if (!open) return VHX_OK;
+        open = false;
+        return write_end(c);
+    }
+    ~WriteScope() {
+        if (open) (void)write_end(c);
+    }
+    WriteScope(const WriteScope &) = delete;
+    WriteScope &operator=(const WriteScope &) = delete;
+};
 // the tree counts as 8 u32 (the message of a device-side tree transfer) and back
 void pack_counts(const vhx_tree_desc &d, uint32_t counts[8]);
 vhx_tree_desc unpack_counts(const uint32_t counts[8]);

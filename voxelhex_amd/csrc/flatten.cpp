@@ -575,6 +575,12 @@ int vhx_boxtree_set_mip_color_threshold(vhx_boxtree *tree, uint32_t level, float
     tree->tree->mip_strategy.color_thresholds[level] = std::clamp(threshold, 0.f, 1.f);
     return VHX_OK;
 }
+int vhx_boxtree_set_mip_options(int direct, int threads) {
+    if (threads < 0 || threads > 256) return VHX_E_INVALID_ARG;
+    g_mip_direct.store(direct ? 1 : 0);
+    g_mip_threads.store(threads);
+    return VHX_OK;
+}
 int vhx_boxtree_recalculate_mips(vhx_boxtree *tree) {
     if (!tree) return VHX_E_INVALID_ARG;
     if (tree->tree->nodes.get(0).content != Content::Nothing) tree->tree->recalculate_mips();

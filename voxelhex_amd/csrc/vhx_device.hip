@@ -1106,19 +1106,27 @@ int vhx::ensure(vhx_ctx *c, DevBuf &b, uint64_t bytes) {
 }
 
 // ---- tree-write ordering (TreeStore): frames in flight on shared contexts and writes through the owner ----------
-// VHX_UNORDERED_WRITES=1 (diagnostics only): no waits either way, the behaviour before round 3, to show that
+// VHX_UNORDERED_WRITES=1 (a diagnostic build only, never the shipped library: voxelhex_amd._build.build(defines=
+// ("VHX_UNORDERED_WRITES=1",), lib=...)): no waits either way, the behaviour before round 3, to show that
 // tests/test_gpu_ordering.py detects the missing ordering
-static bool unordered_writes() {
-    static const bool u = getenv("VHX_UNORDERED_WRITES") != nullptr && getenv("VHX_UNORDERED_WRITES")[0] == '1';
-    return u;
-}
+#ifndef VHX_UNORDERED_WRITES
+#define VHX_UNORDERED_WRITES 0
+#endif
+static constexpr bool unordered_writes() { return VHX_UNORDERED_WRITES != 0; }
 
+// Writes and traces of one tree may come from several host threads (one per context): a write waits until no trace is
+// between trace_begin and trace_end (a trace in submission is not yet visible in its use event), and a trace waits
+// until no write is between write_begin and write_end, so every frame sees the tree as of its submission.
 int vhx::write_begin(vhx_ctx *c) {
-    if (unordered_writes()) return VHX_OK;
     TreeStore &ts = *c->tree;
-    std::lock_guard<std::mutex> lock(ts.mu);
+    std::unique_lock<std::mutex> lock(ts.mu);
+    ts.cv.wait(lock, [&] { return ts.tracing == 0 && ts.writing == 0; });
+    ++ts.writing;
+    if (unordered_writes()) return VHX_OK;
+    // every other context's last submitted trace, whatever stream it went to (waiting on an event of c's own stream is
+    // a no-op, so no stream comparison: a context moved between streams by vhx_set_stream is still waited for)
     for (vhx_ctx *u : ts.users)
-        if (u != c && u->use_recorded && u->stream != c->stream) VHX_HIP(c, hipStreamWaitEvent(c->stream, u->use_ev, 0));
+        if (u != c && u->use_recorded) VHX_HIP(c, hipStreamWaitEvent(c->stream, u->use_ev, 0));
     // a write on another stream than the previous write also follows it (writes are ordered among themselves)
     if (ts.write_seq && ts.write_stream != c->stream) VHX_HIP(c, hipStreamWaitEvent(c->stream, ts.write_ev, 0));
     return VHX_OK;
@@ -1127,6 +1135,9 @@ int vhx::write_begin(vhx_ctx *c) {
 int vhx::write_end(vhx_ctx *c) {
     TreeStore &ts = *c->tree;
     std::lock_guard<std::mutex> lock(ts.mu);
+    ts.writing = ts.writing > 0 ? ts.writing - 1 : 0;
+    ts.cv.notify_all();
+    // recorded on every exit (also after a failed write: the next traces wait for whatever it enqueued)
     if (!ts.write_ev) VHX_HIP(c, hipEventCreateWithFlags(&ts.write_ev, hipEventDisableTiming));
     VHX_HIP(c, hipEventRecord(ts.write_ev, c->stream));
     ts.write_stream = c->stream;
@@ -1136,9 +1147,11 @@ int vhx::write_end(vhx_ctx *c) {
 }
 
 int vhx::trace_begin(vhx_ctx *c) {
-    if (unordered_writes()) return VHX_OK;
     TreeStore &ts = *c->tree;
-    std::lock_guard<std::mutex> lock(ts.mu);
+    std::unique_lock<std::mutex> lock(ts.mu);
+    ts.cv.wait(lock, [&] { return ts.writing == 0; });
+    ++ts.tracing;
+    if (unordered_writes()) return VHX_OK;
     if (c->seen_write != ts.write_seq) {
         if (ts.write_stream != c->stream) VHX_HIP(c, hipStreamWaitEvent(c->stream, ts.write_ev, 0));
         c->seen_write = ts.write_seq;
@@ -1147,9 +1160,13 @@ int vhx::trace_begin(vhx_ctx *c) {
 }
 
 int vhx::trace_end(vhx_ctx *c) {
+    TreeStore &ts = *c->tree;
+    std::lock_guard<std::mutex> lock(ts.mu);  // write_begin reads use_recorded / waits on use_ev
+    ts.tracing = ts.tracing > 0 ? ts.tracing - 1 : 0;
+    ts.cv.notify_all();
     if (!c->use_ev) VHX_HIP(c, hipEventCreateWithFlags(&c->use_ev, hipEventDisableTiming));
-    std::lock_guard<std::mutex> lock(c->tree->mu);  // write_begin reads use_recorded / waits on use_ev
     VHX_HIP(c, hipEventRecord(c->use_ev, c->stream));
+    c->use_stream = c->stream;
     c->use_recorded = true;
     return VHX_OK;
 }
@@ -1334,7 +1351,7 @@ static void select_schedule(vhx_ctx *c) {
     {
         std::lock_guard<std::mutex> lock(c->tree->mu);
         for (vhx_ctx *u : c->tree->users)
-            if (u != c && u->use_recorded && u->stream != c->stream && hipEventQuery(u->use_ev) == hipErrorNotReady) {
+            if (u != c && u->use_recorded && u->use_stream != c->stream && hipEventQuery(u->use_ev) == hipErrorNotReady) {
                 busy = true;
                 break;
             }
@@ -1407,10 +1424,12 @@ static PassQ pass_q(const vhx_ctx *c, uint32_t p, uint32_t npass) {
     return q;
 }
 
-// VHX_DEBUG_PASSES=1: synchronise after every pass step and print the queue counters (diagnostics)
+// VHX_DEBUG_PASSES=1 (a diagnostic build only): synchronise after every pass step and print the queue counters
+#ifndef VHX_DEBUG_PASSES
+#define VHX_DEBUG_PASSES 0
+#endif
 static void debug_passes(vhx_ctx *c, const char *what) {
-    static const bool on = getenv("VHX_DEBUG_PASSES") != nullptr;
-    if (!on || !c->qctl.ptr) return;
+    if (!VHX_DEBUG_PASSES || !c->qctl.ptr) return;
     uint32_t v[16];
     (void)hipStreamSynchronize(c->stream);
     (void)hipMemcpy(v, c->qctl.ptr, sizeof(v), hipMemcpyDeviceToHost);
@@ -1577,106 +1596,15 @@ int vhx_create(int hip_device, vhx_ctx **out) {
     };
     hipError_t e;
     if ((e = hipSetDevice(hip_device)) != hipSuccess) return bail("hipSetDevice", e);
-    // no stream yet: the caller's (vhx_set_stream) or the context's own, created at first use (VHX_STREAM)
+    // no stream yet: the caller's (vhx_set_stream) or the context's own, created at first use (VHX_STREAM). The
+    // library reads no environment: the schedule is the adaptive default until vhx_set_pass_budgets / vhx_set_tuning.
     {
-        const char *pb = getenv("VHX_BUDGETS");  // "32,256" = three passes; "" or "0" = one pass
-        if (pb) {
-            uint32_t b[VHX_MAX_BUDGETS], nb = 0;
-            for (const char *q = pb; *q && nb < VHX_MAX_BUDGETS;) {
-                char *end = nullptr;
-                const unsigned long v = strtoul(q, &end, 10);
-                if (end == q) break;
-                if (v > 0 && v < VHX_MAX_ITERS) b[nb++] = (uint32_t)v;
-                q = *end == ',' ? end + 1 : end;
-            }
-            vhx_set_pass_budgets(c, b, nb);  // fixes the schedule (no adaptive choice)
-        }
-        const char *pa = getenv("VHX_ADAPTIVE");  // "0": the busy schedule always (diagnostics)
-        if (pa && pa[0] == '0') c->adaptive = false;
-        const char *pr = getenv("VHX_RPW");  // rays per wave of the queue passes 1.., e.g. "64,16"
-        if (pr) {
-            uint32_t k = 1;
-            for (const char *q = pr; *q && k < VHX_MAX_BUDGETS + 1;) {
-                char *end = nullptr;
-                const unsigned long v = strtoul(q, &end, 10);
-                if (end == q) break;
-                if (v <= 64) c->rpw[k++] = (uint32_t)v;  // 0 = adaptive
-                q = *end == ',' ? end + 1 : end;
-            }
-        }
-        const char *pt = getenv("VHX_TW");
-        if (pt && atoi(pt) > 0) c->tw = (uint32_t)atoi(pt);
-        const char *pg = getenv("VHX_XCDG");
-        if (pg) c->xcd_group = (uint32_t)atoi(pg);
-        const char *pz = getenv("VHX_RESUME");
-        if (pz && pz[0] == '0') c->resume = false;
-        const char *psf = getenv("VHX_SAVE_FROM");
-        if (psf && atoi(psf) >= 0) c->save_from = (uint32_t)atoi(psf);
-        const char *pq = getenv("VHX_QBLOCK");
-        if (pq && (atoi(pq) == 64 || atoi(pq) == 128)) c->qblock = (uint32_t)atoi(pq);
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, hip_device) == hipSuccess && prop.multiProcessorCount > 0) {
             c->cus = (uint32_t)prop.multiProcessorCount;
             c->queue_blocks = c->cus * 8u;
             c->queue_waves = c->sched_busy.queue_waves_per_cu * c->cus;
         }
-        const char *pw = getenv("VHX_QWAVES");  // after the device default; fixes the schedule
-        if (pw && atoi(pw) > 0) {
-            c->queue_waves = (uint32_t)atoi(pw);
-            c->adaptive = false;
-        }
-        const char *pwm = getenv("VHX_QWAVESM");
-        if (pwm && atoi(pwm) > 0) c->queue_waves_mid = (uint32_t)atoi(pwm);
-        const char *pw0 = getenv("VHX_QWAVES0");
-        if (pw0 && atoi(pw0) > 0) c->queue_waves0 = (uint32_t)atoi(pw0);
-        const char *pqx = getenv("VHX_QXCD");
-        if (pqx && atoi(pqx) >= 0) c->qxcd = (uint32_t)atoi(pqx);
-        const char *psp = getenv("VHX_SPARSE");  // per budgeted pass, e.g. "8,4,4"
-        if (psp) {
-            uint32_t k = 0;
-            for (const char *q = psp; *q && k < VHX_MAX_BUDGETS;) {
-                char *end = nullptr;
-                const unsigned long v = strtoul(q, &end, 10);
-                if (end == q) break;
-                c->sparse[k++] = v <= 64 ? (uint32_t)v : 0u;
-                q = *end == ',' ? end + 1 : end;
-            }
-            c->adaptive = false;  // fixes the schedule
-        }
-        // pass-0 queue order: "[m]N[z|r]": NxN tiles, row-major or (m) in Morton order, inside each tile 8x8 sub-tiles
-        // row-major, (z) every pixel in Morton order or (r) the tile's rows; "0" = output index
-        const char *pqo = getenv("VHX_QORDER");
-        if (pqo) {
-            const bool m = pqo[0] == 'm';
-            char *end = nullptr;
-            const long ts = strtol(pqo + (m ? 1 : 0), &end, 10);
-            const bool z = end && *end == 'z', rows = end && *end == 'r';
-            uint32_t l = 0;
-            while (l < 12u && (1l << l) < ts) ++l;
-            c->qorder = ts >= 8 && ts <= 4096 && (1l << l) == ts ? l | (m ? 16u : 0u) | (z ? 32u : 0u) | (rows ? 64u : 0u)
-                                                                 : 0u;
-            c->sched_busy.qorder = c->sched_idle.qorder = c->qorder;  // both schedules (the rest stays adaptive)
-        }
-        const char *psl = getenv("VHX_SPLIT");  // "0" / "1": tail split of the last pass off / on for every trace
-        if (psl && (psl[0] == '0' || psl[0] == '1')) c->split_force = psl[0] - '0';
-        // split tuning "period,min_lanes,min_idle,take" (VHX_SPLIT_TUNE; period a power of two)
-        const char *psw = getenv("VHX_SPLIT_WAIT");
-        if (psw && atoi(psw) > 0) c->split_max_wait = (uint32_t)atoi(psw);
-        const char *psd = getenv("VHX_SPLIT_DIAG");
-        if (psd) c->split_diag = (uint32_t)atoi(psd);
-        const char *pst = getenv("VHX_SPLIT_TUNE");
-        if (pst) {
-            unsigned a = 0, b = 0, d = 0, e = 0;
-            if (sscanf(pst, "%u,%u,%u,%u", &a, &b, &d, &e) == 4 && a && !(a & (a - 1)) && b >= 2 && b <= 64 && d >= 1 &&
-                e >= 1 && e <= 64) {
-                c->split_period = a;
-                c->split_min_lanes = b;
-                c->split_min_idle = d;
-                c->split_take = e;
-            }
-        }
-        const char *pqa = getenv("VHX_QXCD_ALL");
-        if (pqa && pqa[0] == '1') c->qxcd_all = true;
     }
     if ((e = hipEventCreate(&c->ev0)) != hipSuccess) return bail("hipEventCreate", e);
     if ((e = hipEventCreate(&c->ev1)) != hipSuccess) return bail("hipEventCreate", e);
@@ -1740,8 +1668,162 @@ int vhx_set_pass_budgets(vhx_ctx *c, const uint32_t *budgets, uint32_t n) {
     return VHX_OK;
 }
 
+// vhx_set_tuning: the scheduling knobs of the probes (they used to be environment variables read at vhx_create; the
+// library now reads none). Parsed into a copy of the context first, so a malformed spec changes nothing.
+static bool parse_u32_list(const std::string &v, uint32_t *out, uint32_t cap, uint32_t &n) {
+    n = 0;
+    const char *q = v.c_str();
+    if (!*q) return true;
+    for (;;) {
+        char *end = nullptr;
+        const unsigned long x = strtoul(q, &end, 10);
+        if (end == q || n >= cap || x > 0xFFFFFFFFul) return false;
+        out[n++] = (uint32_t)x;
+        if (*end == '\0') return true;
+        if (*end != ',') return false;
+        q = end + 1;
+    }
+}
+static bool parse_u32(const std::string &v, uint32_t &out) {
+    uint32_t n = 0, x[1];
+    if (!parse_u32_list(v, x, 1, n) || n != 1) return false;
+    out = x[0];
+    return true;
+}
+static int apply_tuning(vhx_ctx *c, const std::string &key, const std::string &val) {
+    uint32_t x = 0, n = 0, l[VHX_MAX_BUDGETS + 1];
+    auto bad = [&]() { return fail(c, VHX_E_INVALID_ARG, ("vhx_set_tuning: bad value for " + key).c_str()); };
+    if (key == "budgets") {  // "" or "0" = one pass
+        if (!parse_u32_list(val, l, VHX_MAX_BUDGETS, n)) return bad();
+        if (n == 1 && l[0] == 0) n = 0;
+        return vhx_set_pass_budgets(c, l, n);
+    } else if (key == "adaptive") {
+        if (!parse_u32(val, x) || x > 1) return bad();
+        return vhx_set_adaptive_schedule(c, (int)x);
+    } else if (key == "rpw") {  // queue passes 1.., 0 = adaptive
+        if (!parse_u32_list(val, l, VHX_MAX_BUDGETS, n)) return bad();
+        for (uint32_t i = 0; i < n; ++i) {
+            if (l[i] > 64) return bad();
+            c->rpw[i + 1] = l[i];
+        }
+    } else if (key == "tw") {
+        if (!parse_u32(val, x) || x == 0) return bad();
+        c->tw = x;
+    } else if (key == "xcdg") {
+        if (!parse_u32(val, x)) return bad();
+        c->xcd_group = x;
+    } else if (key == "resume") {
+        if (!parse_u32(val, x) || x > 1) return bad();
+        c->resume = x != 0;
+    } else if (key == "save_from") {
+        if (!parse_u32(val, x)) return bad();
+        c->save_from = x;
+    } else if (key == "qblock") {
+        if (!parse_u32(val, x) || (x != 64 && x != 128 && x != 256)) return bad();
+        c->qblock = x;
+    } else if (key == "qwaves") {  // fixes the schedule
+        if (!parse_u32(val, x) || x == 0) return bad();
+        if (c->adaptive) vhx_set_adaptive_schedule(c, 0);
+        c->queue_waves = x;
+    } else if (key == "qwavesm") {
+        if (!parse_u32(val, x)) return bad();
+        c->queue_waves_mid = x;
+    } else if (key == "qwaves0") {
+        if (!parse_u32(val, x) || x == 0) return bad();
+        c->queue_waves0 = x;
+    } else if (key == "qxcd") {
+        if (!parse_u32(val, x)) return bad();
+        c->qxcd = x;
+    } else if (key == "qxcd_all") {
+        if (!parse_u32(val, x) || x > 1) return bad();
+        c->qxcd_all = x != 0;
+    } else if (key == "sparse") {  // per budgeted pass; fixes the schedule
+        if (!parse_u32_list(val, l, VHX_MAX_BUDGETS, n)) return bad();
+        for (uint32_t i = 0; i < n; ++i)
+            if (l[i] > 64) return bad();
+        if (c->adaptive) vhx_set_adaptive_schedule(c, 0);
+        for (uint32_t i = 0; i < VHX_MAX_BUDGETS; ++i) c->sparse[i] = i < n ? l[i] : 0u;
+    } else if (key == "qorder") {  // "[m]N[z|r]": NxN tiles, (m) Morton order of the tiles, (z) Morton / (r) rows inside
+        const bool m = !val.empty() && val[0] == 'm';
+        char *end = nullptr;
+        const char *b = val.c_str() + (m ? 1 : 0);
+        const long ts = strtol(b, &end, 10);
+        if (end == b) return bad();
+        const bool z = *end == 'z', rows = *end == 'r';
+        if (*end && !((z || rows) && end[1] == '\0')) return bad();
+        uint32_t lg = 0;
+        while (lg < 12u && (1l << lg) < ts) ++lg;
+        uint32_t code = 0;
+        if (ts != 0) {
+            if (ts < 8 || ts > 4096 || (1l << lg) != ts) return bad();
+            code = lg | (m ? 16u : 0u) | (z ? 32u : 0u) | (rows ? 64u : 0u);
+        }
+        c->qorder = c->sched_busy.qorder = c->sched_idle.qorder = code;  // both schedules (the rest stays adaptive)
+    } else if (key == "split") {
+        if (!parse_u32(val, x) || x > 1) return bad();
+        c->split_force = (int)x;
+    } else if (key == "split_wait") {
+        if (!parse_u32(val, x) || x == 0) return bad();
+        c->split_max_wait = x;
+    } else if (key == "split_diag") {
+        if (!parse_u32(val, x)) return bad();
+        c->split_diag = x;
+    } else if (key == "split_tune") {
+        if (!parse_u32_list(val, l, 4, n) || n != 4) return bad();
+        if (!l[0] || (l[0] & (l[0] - 1)) || l[1] < 2 || l[1] > 64 || l[2] < 1 || l[3] < 1 || l[3] > 64) return bad();
+        c->split_period = l[0];
+        c->split_min_lanes = l[1];
+        c->split_min_idle = l[2];
+        c->split_take = l[3];
+    } else {
+        return fail(c, VHX_E_INVALID_ARG, ("vhx_set_tuning: unknown key " + key).c_str());
+    }
+    return VHX_OK;
+}
+
+int vhx_set_tuning(vhx_ctx *c, const char *spec) {
+    if (!c || !spec) return VHX_E_INVALID_ARG;
+    std::vector<std::pair<std::string, std::string>> kv;
+    for (const char *q = spec; *q;) {
+        const char *e = q;
+        while (*e && *e != ';') ++e;
+        const std::string item(q, e);
+        q = *e ? e + 1 : e;
+        if (item.empty()) continue;
+        const size_t eq = item.find('=');
+        if (eq == std::string::npos || eq == 0) return fail(c, VHX_E_INVALID_ARG, "vhx_set_tuning: expected key=value");
+        kv.emplace_back(item.substr(0, eq), item.substr(eq + 1));
+    }
+    // a dry run on a scratch context first: a malformed spec leaves c unchanged
+    {
+        vhx_ctx dry;
+        copy_sched(&dry, c);
+        for (const auto &p : kv) {
+            const int rc = apply_tuning(&dry, p.first, p.second);
+            if (rc) {
+                c->err = dry.err;
+                return rc;
+            }
+        }
+    }
+    for (const auto &p : kv) {
+        const int rc = apply_tuning(c, p.first, p.second);
+        if (rc) return rc;
+    }
+    return VHX_OK;
+}
+
 int vhx_set_adaptive_schedule(vhx_ctx *c, int on) {
     if (!c) return VHX_E_INVALID_ARG;
+    if (!on && c->adaptive) {  // leaving the adaptive choice: the frames-in-flight schedule, whatever the last trace ran
+        const vhx_ctx::Sched &s = c->sched_busy;
+        std::memcpy(c->budgets, s.budgets, sizeof(c->budgets));
+        std::memcpy(c->sparse, s.sparse, sizeof(c->sparse));
+        c->npass = s.npass;
+        c->queue_waves = s.queue_waves_per_cu * c->cus;
+        c->qorder = s.qorder;
+        c->last_sched = -1;
+    }
     c->adaptive = on != 0;
     return VHX_OK;
 }
@@ -1871,7 +1953,8 @@ int vhx_upload_tree(vhx_ctx *c, const vhx_tree_desc *t) {
             return fail(c, VHX_E_INVALID_ARG, "vhx_upload_tree: null array with non-zero count");
     VHX_HIP(c, hipSetDevice(c->device));
     VHX_STREAM(c);
-    int rc = write_begin(c);  // frames in flight on the tree's other contexts finish reading it first
+    WriteScope ws(c);  // frames in flight on the tree's other contexts finish reading it first
+    int rc = ws.rc;
     if (!rc) rc = alloc_tree(c, t);
     if (rc) return rc;
     for (int id = 0; id < 7; ++id) {
@@ -1879,7 +1962,7 @@ int vhx_upload_tree(vhx_ctx *c, const vhx_tree_desc *t) {
         if (bytes) VHX_HIP(c, hipMemcpyAsync(c->tree->raw[id].ptr, src[id], bytes, hipMemcpyHostToDevice, c->stream));
     }
     if ((rc = finish_upload(c))) return rc;
-    return write_end(c);
+    return ws.end();
 }
 
 }  // extern "C"
@@ -1888,7 +1971,8 @@ int vhx::receive_tree(vhx_ctx *c, const vhx_tree_desc &counts,
                       int (*fill)(void *, void *const[7], const uint64_t[7]), void *arg) {
     VHX_HIP(c, hipSetDevice(c->device));
     VHX_STREAM(c);
-    int rc = write_begin(c);
+    WriteScope ws(c);
+    int rc = ws.rc;
     if (!rc) rc = alloc_tree(c, &counts);
     if (rc) return rc;
     void *dst[7];
@@ -1899,7 +1983,7 @@ int vhx::receive_tree(vhx_ctx *c, const vhx_tree_desc &counts,
     }
     if ((rc = fill(arg, dst, bytes))) return rc;  // the transfers, enqueued on c's stream
     if ((rc = finish_upload(c))) return rc;       // derived layout from the received buffers (synchronises)
-    return write_end(c);
+    return ws.end();
 }
 
 void vhx::copy_sched(vhx_ctx *c, const vhx_ctx *owner) {
@@ -1978,7 +2062,8 @@ int vhx_update_ranges(vhx_ctx *c, const vhx_range *r, uint32_t n) {
     VHX_HIP(c, hipSetDevice(c->device));
     VHX_STREAM(c);
     // the scatter and the derived-state rebuilds write the tree: frames in flight on the other contexts first
-    int rc = write_begin(c);
+    WriteScope ws(c);
+    int rc = ws.rc;
     if (rc) return rc;
     // pinned staging slot (the one used two calls ago: its copy has normally long completed)
     vhx_ctx::Pinned &P = c->pinned[c->pinned_next];
@@ -2079,7 +2164,7 @@ int vhx_update_ranges(vhx_ctx *c, const vhx_range *r, uint32_t n) {
         rc = refresh_child_rec_sel(c, node_lo, node_hi, brick_lo, brick_hi);
     }
     if (rc) return rc;
-    return write_end(c);  // the next trace of every context of the tree waits for this write
+    return ws.end();  // the next trace of every context of the tree waits for this write
 }
 
 int vhx_update_range(vhx_ctx *c, int id, uint64_t off, uint64_t count, const void *src) {
@@ -2102,11 +2187,11 @@ int vhx_read_derived(vhx_ctx *c, int which, uint64_t off, uint64_t count, void *
     const DevBuf &b = which == VHX_DERIVED_NODE_HDR ? c->tree->hdr : c->tree->brick_occ;
     VHX_HIP(c, hipSetDevice(c->device));
     VHX_STREAM(c);
-    int rc = trace_begin(c);  // after the tree's last write
-    if (rc) return rc;
+    TraceScope tscope(c);  // after the tree's last write
+    if (tscope.rc) return tscope.rc;
     VHX_HIP(c, hipMemcpyAsync(dst, (const char *)b.ptr + off * es, count * es, hipMemcpyDeviceToHost, c->stream));
     VHX_HIP(c, hipStreamSynchronize(c->stream));
-    return VHX_OK;
+    return tscope.end();
 }
 
 int vhx_tree_device_bytes(const vhx_ctx *c, uint64_t *bytes) {
@@ -2164,7 +2249,8 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
                                                            : (uint64_t)my_tiles * T * T;
     VHX_HIP(c, hipSetDevice(c->device));
     VHX_STREAM(c);
-    int rc = trace_begin(c);  // after the tree's last write (an update through the owner, on its stream)
+    TraceScope tscope(c);  // after the tree's last write (an update through the owner, on its stream)
+    int rc = tscope.rc;
     if (rc) return rc;
     HostOut ho;
     rc = map_out(c, out, nout, on_device, ho, layout == VHX_LAYOUT_TILES);
@@ -2256,7 +2342,7 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
     c->last_fb_h = layout == VHX_LAYOUT_FRAMEBUFFER ? cam->height : 0u;
     VHX_HIP(c, hipEventRecord(c->ev1, c->stream));
     c->timed = true;
-    if ((rc = trace_end(c))) return rc;  // a later write of the tree waits for this frame
+    if ((rc = tscope.end())) return rc;  // a later write of the tree waits for this frame
     return finish_out(c, ho);
 }
 
@@ -2304,14 +2390,15 @@ int vhx_set_node_mips(vhx_ctx *c, const uint32_t *node_mips, uint32_t count) {
     }
     VHX_HIP(c, hipSetDevice(c->device));
     VHX_STREAM(c);
-    int rc = write_begin(c);  // frames in flight may still read the previous descriptors
+    WriteScope ws(c);  // frames in flight may still read the previous descriptors
+    int rc = ws.rc;
     if (!rc && c->tree->mips.bytes < (uint64_t)count * 4) VHX_HIP(c, hipStreamSynchronize(c->stream));  // regrowth
     if (!rc) rc = ensure(c, c->tree->mips, (uint64_t)count * 4);
     if (rc) return rc;
     VHX_HIP(c, hipMemcpyAsync(c->tree->mips.ptr, node_mips, (uint64_t)count * 4, hipMemcpyHostToDevice, c->stream));
     VHX_HIP(c, hipStreamSynchronize(c->stream));
     c->tree->mips_on = true;
-    return write_end(c);
+    return ws.end();
 }
 
 int vhx_trace_rays(vhx_ctx *c, const float *rays, uint64_t n, const vhx_hits *out, int on_device) {
@@ -2321,7 +2408,8 @@ int vhx_trace_rays(vhx_ctx *c, const float *rays, uint64_t n, const vhx_hits *ou
     if ((n + 255) / 256 > 0x7FFFFFFFull) return fail(c, VHX_E_INVALID_ARG, "too many rays");
     VHX_HIP(c, hipSetDevice(c->device));
     VHX_STREAM(c);
-    int rc = trace_begin(c);
+    TraceScope tscope(c);
+    int rc = tscope.rc;
     if (rc) return rc;
     HostOut ho;
     rc = map_out(c, out, n, on_device, ho);
@@ -2372,7 +2460,7 @@ int vhx_trace_rays(vhx_ctx *c, const float *rays, uint64_t n, const vhx_hits *ou
     VHX_HIP(c, hipGetLastError());
     VHX_HIP(c, hipEventRecord(c->ev1, c->stream));
     c->timed = true;
-    if ((rc = trace_end(c))) return rc;
+    if ((rc = tscope.end())) return rc;
     return finish_out(c, ho);
 }
 
@@ -2405,7 +2493,8 @@ int vhx_trace_shadows(vhx_ctx *c, const float light[3], uint64_t n, const uint32
     }
     VHX_HIP(c, hipSetDevice(c->device));
     VHX_STREAM(c);
-    int rc = trace_begin(c);
+    TraceScope tscope(c);
+    int rc = tscope.rc;
     if (rc) return rc;
     uint32_t npass = 1;
     const uint64_t nb64 = (n + 255) / 256;
@@ -2460,7 +2549,7 @@ int vhx_trace_shadows(vhx_ctx *c, const float light[3], uint64_t n, const uint32
     VHX_HIP(c, hipGetLastError());
     VHX_HIP(c, hipEventRecord(c->ev1, c->stream));
     c->timed = true;
-    return trace_end(c);
+    return tscope.end();
 }
 
 int vhx_untile_frame(vhx_ctx *c, const void *gathered, uint32_t planes, uint32_t ranks, uint32_t tiles_per_rank,

@@ -95,6 +95,9 @@ struct vhx_mgpu {
     int nranks = 1, rank = 0;
     uint32_t T = 64;
     uint32_t R = 1;  // slots of rank 0 (the others own one each)
+    // planes of a slot's part: 2 = [RGBA8 | f32 depth], 1 = RGBA8 only (the reference's display output is the rgba8unorm
+    // view texture, src/raytracing/bevy/view.rs:269-289; depth is optional), equal on every rank (vhx_mgpu_set_planes)
+    uint32_t planes = 2;
     bool overlap = true;
     bool timing = false;  // vhx_mgpu_balance: time rank 0's trace and the transfers of each frame
     hipEvent_t tev[4] = {};  // trace start / end (tracing stream), transfer start / end (communication stream)
@@ -363,6 +366,9 @@ int vhx_mgpu_render(vhx_mgpu *m, const vhx_camera *cam, uint32_t *fb_rgba, float
     if (!m || !cam) return VHX_E_INVALID_ARG;
     vhx_ctx *c = m->ctx;
     if (m->rank == 0 && !fb_rgba && !fb_depth) return fail(c, VHX_E_INVALID_ARG, "vhx_mgpu_render: rank 0 needs a framebuffer");
+    if (m->rank == 0 && m->planes == 1 && (fb_depth || !fb_rgba))
+        return fail(c, VHX_E_INVALID_ARG, "vhx_mgpu_render: one plane (vhx_mgpu_set_planes) carries RGBA only: fb_rgba "
+                                          "and no fb_depth");
     if (!c->tree->uploaded) return fail(c, VHX_E_STATE, "vhx_mgpu_render before the tree is uploaded");
     if (cam->width == 0 || cam->height == 0) return fail(c, VHX_E_INVALID_ARG, "vhx_mgpu_render: empty frame");
     const Rccl &r = rccl();
@@ -372,6 +378,7 @@ int vhx_mgpu_render(vhx_mgpu *m, const vhx_camera *cam, uint32_t *fb_rgba, float
     rank_slots(m, m->rank, first, count);
     const uint32_t V = slots_of(m);
     const uint64_t n_out = (uint64_t)per * m->T * m->T;  // words per plane of one slot's part
+    const uint32_t P = m->planes;
     const uint32_t slot = (uint32_t)(m->k % m->S);
     vhx_ctx *tc = m->k % m->F == 0 ? c : m->extra[m->k % m->F - 1];  // the context tracing this frame
     if (tc != c) copy_sched(tc, c);  // the caller's settings (vhx_set_pass_budgets, ...) go to the owner context
@@ -379,7 +386,7 @@ int vhx_mgpu_render(vhx_mgpu *m, const vhx_camera *cam, uint32_t *fb_rgba, float
     // a slot's buffers are rewritten only after the transfer that read them (stream order on the tracing stream)
     if (m->used[slot]) VHX_HIP(c, hipStreamWaitEvent(tc->stream, m->free_[slot], 0));
     DevBuf &buf = m->rank == 0 ? m->gathered[slot] : m->send[slot];
-    const uint64_t need = n_out * 8 * (m->rank == 0 ? (uint64_t)V : 1u);
+    const uint64_t need = n_out * 4 * P * (m->rank == 0 ? (uint64_t)V : 1u);
     if (buf.bytes < need) {
         int rc = vhx_mgpu_sync(m, nullptr);  // (re)allocation: no frame may still use the old buffers
         if (rc) return rc;
@@ -389,8 +396,8 @@ int vhx_mgpu_render(vhx_mgpu *m, const vhx_camera *cam, uint32_t *fb_rgba, float
     if (m->timing) VHX_HIP(c, hipEventRecord(m->tev[0], tc->stream));
     for (uint32_t s = first; s < first + count && s < ntiles; ++s) {
         vhx_hits h{};
-        h.rgba = parts + 2 * n_out * (s - first);
-        h.depth = (float *)(h.rgba + n_out);
+        h.rgba = parts + P * n_out * (s - first);
+        h.depth = P == 2 ? (float *)(h.rgba + n_out) : nullptr;
         const int rc = vhx_trace_primary(tc, cam, m->T, s, V, VHX_LAYOUT_TILES, &h, 1);
         if (rc) return tc == c ? rc : fail(c, rc, tc->err.c_str());
     }
@@ -407,22 +414,40 @@ int vhx_mgpu_render(vhx_mgpu *m, const vhx_camera *cam, uint32_t *fb_rgba, float
             for (int q = 1; q < m->nranks; ++q) {
                 uint32_t qf, qc;
                 rank_slots(m, q, qf, qc);
-                VHX_NCCL_GROUP(m, r.Recv(parts + 2 * n_out * qf, 2 * n_out, ncclUint32, q, m->comm, m->cstream));
+                VHX_NCCL_GROUP(m, r.Recv(parts + P * n_out * qf, P * n_out, ncclUint32, q, m->comm, m->cstream));
             }
         } else {
-            VHX_NCCL_GROUP(m, r.Send(parts, 2 * n_out, ncclUint32, 0, m->comm, m->cstream));
+            VHX_NCCL_GROUP(m, r.Send(parts, P * n_out, ncclUint32, 0, m->comm, m->cstream));
         }
         VHX_NCCL(m, r.GroupEnd());
     }
     if (m->timing) VHX_HIP(c, hipEventRecord(m->tev[3], m->cstream));
     if (m->rank == 0) {
-        const int rc = launch_untile(c, m->cstream, parts, 2, V, per, m->T, cam->width, cam->height, fb_rgba, fb_depth);
+        const int rc = launch_untile(c, m->cstream, parts, P, V, per, m->T, cam->width, cam->height, fb_rgba, fb_depth);
         if (rc) return rc;
     }
     VHX_HIP(c, hipEventRecord(m->free_[slot], m->cstream));
     m->used[slot] = true;
     ++m->k;
     if (!m->overlap) VHX_HIP(c, hipStreamWaitEvent(tc->stream, m->free_[slot], 0));
+    return VHX_OK;
+}
+
+int vhx_mgpu_set_planes(vhx_mgpu *m, uint32_t planes) {
+    if (!m) return VHX_E_INVALID_ARG;
+    if (planes < 1 || planes > 2) return fail(m->ctx, VHX_E_INVALID_ARG, "vhx_mgpu_set_planes: 1 (RGBA) or 2 (RGBA + depth)");
+    const int rc = vhx_mgpu_sync(m, nullptr);  // no frame may be in flight while the part layout changes
+    if (rc) return rc;
+    m->planes = planes;
+    return VHX_OK;
+}
+
+int vhx_mgpu_frame_bytes(const vhx_mgpu *m, uint32_t W, uint32_t H, uint64_t *into_root) {
+    if (!m || !into_root || W == 0 || H == 0) return VHX_E_INVALID_ARG;
+    uint32_t ntiles, per;
+    tiles_of(m, W, H, ntiles, per);
+    // every rank >= 1 sends its one slot's part: planes x tiles per slot x T^2 words
+    *into_root = (uint64_t)(m->nranks - 1) * m->planes * per * m->T * m->T * 4u;
     return VHX_OK;
 }
 
@@ -448,7 +473,7 @@ static int measure_frames(vhx_mgpu *m, const vhx_camera *cam, uint32_t frames, f
     int rc = VHX_OK;
     if (m->rank == 0) {
         rc = ensure(c, fb, (uint64_t)cam->width * cam->height * 4);
-        if (!rc) rc = ensure(c, fbd, (uint64_t)cam->width * cam->height * 4);
+        if (!rc && m->planes == 2) rc = ensure(c, fbd, (uint64_t)cam->width * cam->height * 4);
     }
     std::vector<float> tr, tx;
     for (uint32_t i = 0; i < frames + 1 && !rc; ++i) {
@@ -506,12 +531,39 @@ int vhx_mgpu_balance(vhx_mgpu *m, const vhx_camera *cam, uint32_t frames, uint32
     if (rc) return rc;
     float a = 0.0f, g = 0.0f;
     const int mrc = measure_frames(m, cam, frames, a, g);
+    // every rank's measurement status to rank 0 (one word per rank, point to point), so that a failure on any rank
+    // makes rank 0 send R = 0 below and every rank fails together
+    if ((rc = ensure(c, m->hdr, 64 + 4u * (uint32_t)m->nranks))) return rc;
+    VHX_STREAM(c);
+    bool all_ok = mrc == VHX_OK;
+    if (m->nranks > 1) {
+        uint32_t *st = (uint32_t *)m->hdr.ptr + 16;
+        const Rccl &r = rccl();
+        if (m->rank != 0) {
+            const uint32_t mine = mrc ? 1u : 0u;
+            VHX_HIP(c, hipMemcpyAsync(st, &mine, 4, hipMemcpyHostToDevice, c->stream));
+        }
+        VHX_NCCL(m, r.GroupStart());
+        if (m->rank == 0) {
+            for (int q = 1; q < m->nranks; ++q) VHX_NCCL_GROUP(m, r.Recv(st + q, 1, ncclUint32, q, m->comm, c->stream));
+        } else {
+            VHX_NCCL_GROUP(m, r.Send(st, 1, ncclUint32, 0, m->comm, c->stream));
+        }
+        VHX_NCCL(m, r.GroupEnd());
+        if (m->rank == 0) {
+            std::vector<uint32_t> all((size_t)m->nranks, 0u);
+            VHX_HIP(c, hipMemcpyAsync(all.data() + 1, st + 1, 4u * (uint32_t)(m->nranks - 1), hipMemcpyDeviceToHost,
+                                      c->stream));
+            VHX_HIP(c, hipStreamSynchronize(c->stream));
+            for (int q = 1; q < m->nranks; ++q) all_ok = all_ok && all[(size_t)q] == 0u;
+        }
+    }
     // rank 0 picks R: with V = R + N - 1 slots a slot's trace and transfer scale by N / V, the frame period is bounded by
     // rank 0's R slots and by the transfers into rank 0 (one slot part per link, concurrent), so it is about
     // N / V * max(R * trace, transfer) with the one-slot figures; the other ranks' single slot never exceeds rank 0's R.
     // A rank whose measurement failed still joins the closing broadcast (rank 0 then sends R = 0: every rank fails)
-    uint32_t best = mrc ? 0u : 1u;
-    if (m->rank == 0 && !mrc) {
+    uint32_t best = all_ok ? 1u : 0u;
+    if (m->rank == 0 && all_ok) {
         const double N = (double)m->nranks;
         double best_t = 0;
         for (uint32_t R = 1; R <= VHX_MGPU_MAX_ROOT_SLOTS; ++R) {
@@ -523,8 +575,6 @@ int vhx_mgpu_balance(vhx_mgpu *m, const vhx_camera *cam, uint32_t frames, uint32
         }
     }
     // every rank takes rank 0's choice (and its two figures)
-    if ((rc = ensure(c, m->hdr, 64))) return rc;
-    VHX_STREAM(c);
     uint32_t msg[3] = {best, 0, 0};
     std::memcpy(&msg[1], &a, 4);
     std::memcpy(&msg[2], &g, 4);
@@ -534,7 +584,7 @@ int vhx_mgpu_balance(vhx_mgpu *m, const vhx_camera *cam, uint32_t frames, uint32
     VHX_HIP(c, hipStreamSynchronize(c->stream));
     if (mrc) return mrc;
     if (msg[0] < 1 || msg[0] > VHX_MGPU_MAX_ROOT_SLOTS)
-        return fail(c, VHX_E_RCCL, "vhx_mgpu_balance: rank 0 reported a failed measurement");
+        return fail(c, VHX_E_RCCL, "vhx_mgpu_balance: the measurement failed on another rank");
     if ((rc = vhx_mgpu_set_root_slots(m, msg[0]))) return rc;
     if (root_slots) *root_slots = msg[0];
     if (trace_ms) std::memcpy(trace_ms, &msg[1], 4);

@@ -5,6 +5,8 @@ contiguous tile-major buffer (VHX_LAYOUT_TILES: the j-th tile of the rank at [j*
 zeros past the frame edge). Rank 0 gathers the buffers (RCCL over xGMI with the nccl backend; gloo on CPU) and
 scatters them into the framebuffer (vhx_untile_rgba on the GPU; untile_numpy is the host restatement used by tests).
 """
+import ctypes
+
 import numpy as np
 
 
@@ -201,6 +203,17 @@ class MgpuRenderer:
         """Collective: rank 0 traces `slots` of the slots + N - 1 tile slots (vhx_mgpu_set_root_slots)."""
         from . import _native as N
         self._check(N.lib().vhx_mgpu_set_root_slots(self._h, slots))
+
+    def set_planes(self, planes):
+        """Planes every rank sends to rank 0 (vhx_mgpu_set_planes): 2 = RGBA8 + depth, 1 = RGBA8 only (rank 0 then
+        renders with fb_depth=None). Every rank must pass the same value."""
+        self._check(N.lib().vhx_mgpu_set_planes(self._h, planes))
+
+    def frame_bytes(self, width, height):
+        """Bytes rank 0 receives over xGMI per frame at the current split and plane count (vhx_mgpu_frame_bytes)."""
+        b = ctypes.c_uint64()
+        self._check(N.lib().vhx_mgpu_frame_bytes(self._h, width, height, ctypes.byref(b)))
+        return b.value
 
     def balance(self, cam, frames=4):
         """Collective: measures rank 0's trace and the transfers into it and picks rank 0's share

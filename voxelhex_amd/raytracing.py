@@ -183,7 +183,8 @@ def _ptr(a):
 class Raytracer:
     """A libvhx context on one HIP device with a tree resident in HBM."""
 
-    def __init__(self, device=0):
+    def __init__(self, device=0, tune=None):
+        """tune: a vhx_set_tuning spec ("key=value;..."), scheduling knobs of experiments (results never change)."""
         lib = N.lib()
         n = ctypes.c_int()
         N.check(lib.vhx_device_count(ctypes.byref(n)))
@@ -194,6 +195,14 @@ class Raytracer:
         self._h = h
         self.device = device
         self._tree = None
+        if tune:
+            self.set_tuning(tune)
+
+    def set_tuning(self, spec):
+        """vhx_set_tuning: scheduling knobs as "key=value;..." (include/vhx.h); a dict is joined the same way."""
+        if isinstance(spec, dict):
+            spec = ";".join(f"{k}={v}" for k, v in spec.items())
+        self._check(N.lib().vhx_set_tuning(self._h, spec.encode()))
 
     def shared(self):
         """vhx_create_shared: another context (its own stream, queues and outputs) tracing this context's tree."""
