@@ -62,6 +62,12 @@ int vhx_stream_set_rates(vhx_stream *stream, uint32_t node_uploads_per_frame, ui
                          uint32_t brick_unload_search_perimeter);
 int vhx_stream_set_viewport(vhx_stream *stream, const float origin[3], float view_distance);
 int vhx_stream_upload(vhx_stream *stream, vhx_stream_stats *stats);
+/* `frames` frames of vhx_stream_upload's decisions (each frame at the reference's per-frame rates, tree changes
+ * first), written to the device as ONE vhx_update_ranges call: one tree version for the `frames` frames a renderer
+ * keeps in flight until its next call (with frames in flight, a write every frame serialises them: every write waits
+ * for the frames before it and every frame for the write). The view after the call equals the view after `frames`
+ * vhx_stream_upload calls; stats sum the frames. frames = 1 is vhx_stream_upload. */
+int vhx_stream_upload_frames(vhx_stream *stream, uint32_t frames, vhx_stream_stats *stats);
 int vhx_stream_resize(vhx_stream *stream);
 int vhx_stream_reload(vhx_stream *stream);
 int vhx_stream_view(const vhx_stream *stream, vhx_tree_desc *out);

@@ -126,6 +126,8 @@ typedef struct {
     uint32_t design, cap;
     uint32_t rpw[NP];    /* rays per wave of queue pass p (0 = 64) */
     uint32_t cost[NB];   /* instructions per wave execution of each block */
+    uint32_t order;      /* queue order of the queue passes: 0 frame rows, 1 64x64 tiles Morton inside ("64z"), 2 bucketed
+                            by the ray's total steps (perfect prediction, sqrt(2) buckets, longest first), 64z inside */
 } cfg_t;
 
 typedef struct {
@@ -343,14 +345,39 @@ static void sim_wave2(const cfg_t *c, int p, lane_t *L, int n, uint32_t budget, 
     }
 }
 
+static uint32_t g_order;
+static uint32_t spread_bits(uint32_t v) {
+    v &= 0xFFFF;
+    v = (v | (v << 8)) & 0x00FF00FF;
+    v = (v | (v << 4)) & 0x0F0F0F0F;
+    v = (v | (v << 2)) & 0x33333333;
+    return (v | (v << 1)) & 0x55555555;
+}
+static uint64_t steps_of(uint32_t ray) {
+    uint64_t st = 0;
+    for (uint64_t i = g_off[ray]; i < g_off[ray + 1]; ++i) st += 1u + g_its[i].nb + g_its[i].na;
+    return st;
+}
+static uint64_t order_key(uint32_t ray) {
+    if (g_order == 0) return ray;
+    const uint32_t x = ray % g_W, y = ray / g_W, tx = (g_W + 63) / 64;
+    const uint64_t tile = (uint64_t)(y / 64) * tx + x / 64;
+    const uint64_t pos = (tile << 12) | (spread_bits(x & 63) | (spread_bits(y & 63) << 1));
+    if (g_order == 1) return pos;
+    const uint64_t st = steps_of(ray);
+    uint32_t b = 0;  /* sqrt(2) buckets: b = floor(2 log2(steps)) */
+    while (b < 63 && (1ull << ((b + 1) / 2)) * ((b + 1) % 2 ? 181ull : 128ull) / 128ull <= st) ++b;
+    return ((uint64_t)(63 - b) << 40) | pos;
+}
 static int cmp_ray(const void *a, const void *b) {
-    const uint32_t x = ((const lane_t *)a)->ray, y = ((const lane_t *)b)->ray;
+    const uint64_t x = order_key(((const lane_t *)a)->ray), y = order_key(((const lane_t *)b)->ray);
     return x < y ? -1 : x > y;
 }
 
 int wavesim_run(const cfg_t *c, stats_t *s) {
     memset(s, 0, sizeof(*s));
     g_cfg = c;
+    g_order = c->order;
     const uint32_t W = g_W, H = g_H;
     const uint64_t n = (uint64_t)W * H;
     lane_t *q = (lane_t *)malloc(n * sizeof(lane_t)), *q2 = (lane_t *)malloc(n * sizeof(lane_t));

@@ -34,7 +34,7 @@ class Stats(ctypes.Structure):
 class Cfg(ctypes.Structure):
     _fields_ = [("budgets", ctypes.c_uint32 * NP), ("npass", ctypes.c_uint32), ("sparse0", ctypes.c_uint32),
                 ("design", ctypes.c_uint32), ("cap", ctypes.c_uint32), ("rpw", ctypes.c_uint32 * NP),
-                ("cost", ctypes.c_uint32 * 16)]
+                ("cost", ctypes.c_uint32 * 16), ("order", ctypes.c_uint32)]
 
 
 def build():
@@ -45,8 +45,9 @@ def build():
     return ctypes.CDLL(LIB)
 
 
-def run(lib, budgets, design, cap, sparse0=12, rpw=()):
+def run(lib, budgets, design, cap, sparse0=12, rpw=(), order=0):
     c = Cfg()
+    c.order = order
     for i, b in enumerate(budgets):
         c.budgets[i] = b
     for i, r in enumerate(rpw):
@@ -88,6 +89,7 @@ def main():
     ap.add_argument("--height", type=int, default=2160)
     ap.add_argument("--budgets", default="24,96,768")
     ap.add_argument("--designs", default="0")
+    ap.add_argument("--orders", default="0", help="queue orders to compare: 0 frame rows, 1 64z tiles, 2 step buckets")
     a = ap.parse_args()
     import time
     import voxelhex_amd as vhx
@@ -101,8 +103,9 @@ def main():
     budgets = tuple(int(b) for b in a.budgets.split(",") if b)
     for d in a.designs.split(","):
         design, _, cap = d.partition(":")
-        s = run(lib, budgets, int(design), int(cap or 0))
-        report(s, f"design {d} budgets {budgets}")
+        for o in a.orders.split(","):
+            s = run(lib, budgets, int(design), int(cap or 0), order=int(o))
+            report(s, f"design {d} budgets {budgets} order {o}")
 
 
 if __name__ == "__main__":

@@ -190,3 +190,55 @@ def test_streamed_mips_stand_in_outside_the_region(oracle):
     s2 = vhx.StreamingView(t2, None, (20.0, 20.0, 20.0), 16.0)
     s2.upload_all()
     assert len(s2.node_mips()) == s2.view().desc.node_count
+
+
+def _view_arrays(s):
+    import ctypes
+    d = s.view().desc
+    n3 = d.brick_dim ** 3
+    out = {}
+    for name, n, dt in (("node_type", d.node_count, np.uint32), ("node_ocbits", d.node_count, np.uint64),
+                        ("node_children", d.node_count * 64, np.uint32), ("voxels", d.brick_count * n3, np.uint32),
+                        ("solid_values", d.solid_count, np.uint32), ("color_palette", d.color_count, np.uint32),
+                        ("data_palette", d.data_count, np.uint32)):
+        ptr = getattr(d, name)
+        nb = n * np.dtype(dt).itemsize
+        out[name] = np.frombuffer((ctypes.c_uint8 * nb).from_address(ptr), dt).copy() if n and ptr else np.zeros(0, dt)
+    return out
+
+
+@pytest.mark.parametrize("batch", [2, 5])
+def test_batched_uploads_equal_single_uploads(batch):
+    """vhx_stream_upload_frames(K) decides exactly what K vhx_stream_upload calls decide (the reference's per-frame
+    rates, tree changes first): after every batch the view mirror equals that of a twin stream uploaded frame by frame,
+    through viewport moves, capacity growth and tree edits between batches."""
+    size, S = 64, 64.0
+    ta, tb = _tree(size, 4), _tree(size, 4)
+    a = vhx.StreamingView(ta, None, (S / 2, S / 2, S / 2), S / 4)
+    b = vhx.StreamingView(tb, None, (S / 2, S / 2, S / 2), S / 4)
+    for s in (a, b):
+        s.set_rates(8, 32, 10)
+    rng_a, rng_b = np.random.default_rng(5), np.random.default_rng(5)
+    for step in range(12):
+        if step in (4, 9):
+            _edit(ta, rng_a, size)
+            _edit(tb, rng_b, size)
+        if step == 6:
+            for s in (a, b):
+                s.set_viewport((0.6 * S, 0.5 * S, 0.5 * S), S)
+        _, grow_a = a.upload(frames=batch)
+        grow_b = False
+        for _ in range(batch):
+            _, g = b.upload()
+            grow_b = grow_b or g
+            if g:
+                break  # a capacity stop ends the batch too
+        assert grow_a == grow_b, step
+        if grow_a:
+            a.resize()
+            b.resize()
+        va, vb = _view_arrays(a), _view_arrays(b)
+        for k in va:
+            assert np.array_equal(va[k], vb[k]), f"batch {batch} step {step}: {k} differs"
+    a.close()
+    b.close()

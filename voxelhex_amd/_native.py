@@ -147,6 +147,7 @@ SIGNATURES = [
     ("vhx_stream_set_rates", c_int, [c_void_p, c_u32, c_u32, c_u32]),
     ("vhx_stream_set_viewport", c_int, [c_void_p, P(c_f32), c_f32]),
     ("vhx_stream_upload", c_int, [c_void_p, c_void_p]),
+    ("vhx_stream_upload_frames", c_int, [c_void_p, c_u32, c_void_p]),
     ("vhx_stream_resize", c_int, [c_void_p]),
     ("vhx_stream_reload", c_int, [c_void_p]),
     ("vhx_stream_view", c_int, [c_void_p, P(TreeDesc)]),

@@ -105,6 +105,7 @@ struct vhx_ctx {
         uint32_t queue_waves_per_cu;         // waves of a queue pass per CU
         uint32_t qorder;                     // order of a primary frame's pass-0 queue (vhx_ctx::qorder below)
         uint32_t split;                      // the unbounded last pass shares its tail rays out (k_trace_queue_split)
+        uint32_t lead;                       // lead blocks: predicted-long blocks first, traced to the end in pass 0
     };
     // Adaptive scheduling (default; vhx_set_pass_budgets or an environment knob fixes the schedule instead): at each
     // trace the context looks at the other contexts of its tree (vhx_create_shared) and picks
@@ -122,8 +123,8 @@ struct vhx_ctx {
     //    three-budget ladders 1.31-1.51 ms, fewer rays per wave in a last pass no better): every extra pass lengthens a
     //    lone frame's critical path.
     bool adaptive = true;
-    Sched sched_busy = {{24u, 72u, 216u, 648u}, 5u, {12u}, 3u, VHX_QORDER_BUSY, 0u};
-    Sched sched_idle = {{64u}, 2u, {0u}, 8u, VHX_QORDER_IDLE, 0u};
+    Sched sched_busy = {{24u, 72u, 216u, 648u}, 5u, {12u}, 3u, VHX_QORDER_BUSY, 0u, 0u};
+    Sched sched_idle = {{64u}, 2u, {0u}, 8u, VHX_QORDER_IDLE, 0u, 1u};
     int last_sched = -1;  // the schedule of the last trace: 1 busy, 0 idle, -1 fixed (vhx_get_pass_budgets)
     // the schedule in force (the selected one, or the fixed one)
     uint32_t budgets[VHX_MAX_BUDGETS] = {24u, 72u, 216u, 648u};
@@ -169,6 +170,16 @@ struct vhx_ctx {
     uint32_t split_diag = 0;
     uint32_t split_max_wait = 32;
     DevBuf ovf;
+    // lead blocks (k_lead_perm in vhx_device.hip): in force for this trace (the selected schedule's
+    // `lead`; tune "lead=0/1" forces it), the step threshold of a lead block, the per-block cost of the last two frames
+    // (recorded into lead_cost[lead_cur], read from the other), pass 0's block order, the frame size lead_cost[lead_cur
+    // ^ 1] belongs to (0: none yet), and the cost buffer of the running trace (its queue passes record into it)
+    uint32_t lead = 0;
+    int lead_force = -1;
+    uint32_t lead_min = 512;
+    DevBuf lead_cost[2], lead_perm;
+    uint32_t lead_cur = 0, lead_w = 0, lead_h = 0;
+    uint32_t *lead_rec = nullptr;
 };
 
 #define VHX_HIP(ctx, call)                                                                                         \

@@ -839,6 +839,40 @@ struct vhx_stream {
         if (!frc && device_valid) frc = sync_device_mips(false);
         return rc ? rc : frc;
     }
+    // K frames of upload decisions (each exactly one upload_frame's: the reference's per-frame rates), written as ONE
+    // vhx_update_ranges: one tree version for the K frames a renderer keeps in flight until the next call. A range's
+    // source points into the host mirror, which a later frame of the batch may overwrite or reallocate (palettes are
+    // reassigned, the solid table grows), so each frame's sources are copied when the frame is decided; the ranges
+    // keep their order, so a later frame's write of the same elements wins, as in K separate calls.
+    std::vector<std::vector<uint8_t>> batch_store;
+    uint64_t batch_bytes = 0, batch_nodes = 0, batch_bricks = 0;
+    int upload_frames(uint32_t K) {
+        std::vector<vhx_range> all;
+        batch_store.clear();
+        batch_bytes = batch_nodes = batch_bricks = 0;
+        int rc = VHX_OK;
+        for (uint32_t k = 0; k < K && !rc; ++k) {
+            frame_writes.clear();
+            rc = collect_frame();
+            batch_bytes += last_bytes;
+            batch_nodes += last_nodes;
+            batch_bricks += last_bricks;
+            for (vhx_range r : frame_writes) {
+                const size_t n = (size_t)r.elem_count * (r.buffer_id == VHX_BUF_NODE_OCBITS ? 8u : 4u);
+                batch_store.emplace_back((const uint8_t *)r.src, (const uint8_t *)r.src + n);
+                r.src = batch_store.back().data();
+                all.push_back(r);
+            }
+        }
+        frame_writes = std::move(all);
+        int frc = flush();  // also after a capacity stop: the frames decided before it are written
+        batch_store.clear();
+        last_bytes = batch_bytes;
+        last_nodes = batch_nodes;
+        last_bricks = batch_bricks;
+        if (!frc && device_valid) frc = sync_device_mips(false);
+        return rc ? rc : frc;
+    }
     int collect_frame() {  // streaming/mod.rs:420-635
         last_nodes = last_bricks = last_bytes = 0;
         if (resize) return VHX_E_CAPACITY;
@@ -974,9 +1008,11 @@ int vhx_stream_set_viewport(vhx_stream *s, const float origin[3], float view_dis
     return VHX_OK;
 }
 
-int vhx_stream_upload(vhx_stream *s, vhx_stream_stats *stats) {
-    if (!s) return VHX_E_INVALID_ARG;
-    const int rc = s->upload_frame();
+int vhx_stream_upload(vhx_stream *s, vhx_stream_stats *stats) { return vhx_stream_upload_frames(s, 1, stats); }
+
+int vhx_stream_upload_frames(vhx_stream *s, uint32_t frames, vhx_stream_stats *stats) {
+    if (!s || frames == 0) return VHX_E_INVALID_ARG;
+    const int rc = frames == 1 ? s->upload_frame() : s->upload_frames(frames);
     if (stats) {
         stats->bytes_written = s->last_bytes;
         stats->nodes_written = s->last_nodes;

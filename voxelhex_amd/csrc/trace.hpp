@@ -110,6 +110,7 @@ struct DevTree {
 
 struct HitOut {
     uint32_t value, cell, vx, vy, vz, bytes;
+    uint32_t iters;  // loop steps of the whole traversal at its end (0 for a ray that misses the root cube)
     float ix, iy, iz, nx, ny, nz;
     bool hit;
 };
@@ -828,6 +829,7 @@ struct Trav {
     }
 
     __device__ __forceinline__ bool end(const DevTree &t, HitOut &h, uint4 *sbase, uint32_t sidx) {
+        h.iters = iters;
         // an abandoned ray's state is the loop state at its exit (saved here, outside the hot loop)
         if (ex == 3u && sbase) save_state(sbase + 4ull * sidx, p, iters, cur, tb, target, count, node, s1, s2, s3);
         if (ex == 1u) {  // the loop left on the hit: node, cur, target and p are those of the probe
@@ -851,6 +853,7 @@ __device__ __forceinline__ bool get_by_ray(const DevTree &t, const uint64_t *occ
                                            bool resume = false, float start = 0.0f, uint32_t sparse = 0) {
     Trav<COUNT, BD, MIP> tr;
     VHX_PROF_BLOCK(pass_of_budget(budget), 10);
+    h.iters = 0;
     if (!tr.template begin<START>(t, o, d, h, sbase, sidx, resume, start)) return true;
     VHX_PROF_BLOCK(pass_of_budget(budget), 11);
     for (;;) {

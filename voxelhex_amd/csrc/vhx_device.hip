@@ -236,6 +236,11 @@ struct PassQ {
     uint32_t xcd_group;  // pass 0: XCD-aware block runs (xcd_block), 0 = dispatch order
     uint32_t qxcd;       // queue passes: runs of this many chunks dealt over the 8 XCDs, one counter each (0 = off)
     uint32_t sparse;     // budgeted passes with saved state: abandon a wave's rays once fewer lanes trace (0 = off)
+    // Lead blocks (a lone frame's schedule, LeadQ below): pass 0 takes its 16x16 blocks in the order of lead_perm
+    // (bit 31 = a lead block: traced to the end in pass 0, unbudgeted), and every ray that ends after more than the
+    // pass-0 budget records its step count in lead_cost[its block] (atomicMax), the prediction of the next frame
+    const uint32_t *lead_perm;
+    uint32_t *lead_cost;
 };
 
 // Rays per wave of a queue pass over n rays: fixed, or (rpw == 0) as many as spread the pass over about `tw` waves.
@@ -525,6 +530,51 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t bid, uint32_t n, uint32_t
     return ((k / G) * 8u + x) * G + k % G;
 }
 
+// Lead blocks of a lone frame. A lone frame is latency-bound: its critical path was pass 0 (~0.40 ms)
+// followed by the slowest chunk of the unbounded tail (~0.8 ms), because a long ray waited for the whole of pass 0 before
+// its tail started. The previous frame on the context records per 16x16 block the step count of its longest ray
+// (lead_cost); k_lead_perm turns it into pass 0's block order: the blocks whose longest ray took >= min_cost steps
+// first (the lead blocks, traced to the end in pass 0: their long tails start at once and overlap the rest of pass 0),
+// then the others; each part keeps the XCD-aware runs of xcd_block. It also zeroes the cost buffer this frame records
+// into. Only the order of the work and the pass that traces a ray change: results are bit-identical for any
+// prediction (a ray's traversal is deterministic).
+// inverse of xcd_block: the dispatch index whose block is r
+__device__ __forceinline__ uint32_t xcd_slot(uint32_t r, uint32_t n, uint32_t G) {
+    if (G == 0u) return r;
+    const uint32_t full = n / (8u * G) * (8u * G);
+    if (r >= full) return r;
+    const uint32_t g = r / G, m = r % G, x = g & 7u, k = (g >> 3) * G + m;
+    return k * 8u + x;
+}
+#define LEAD_THREADS 1024u
+__global__ void __launch_bounds__(LEAD_THREADS) k_lead_perm(const uint32_t *__restrict__ prev, uint32_t *__restrict__ cur,
+                                                           uint32_t n, uint32_t min_cost, uint32_t G,
+                                                           uint32_t *__restrict__ perm) {
+    __shared__ uint32_t s_w[LEAD_THREADS / 64u];
+    const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
+    const uint32_t per = (n + LEAD_THREADS - 1u) / LEAD_THREADS, lo = min(n, t * per), hi = min(n, lo + per);
+    uint32_t cnt = 0;
+    for (uint32_t i = lo; i < hi; ++i) cnt += prev[i] >= min_cost ? 1u : 0u;
+    // exclusive scan of the per-thread counts: waves, then the waves' totals
+    const uint32_t inc = wave_incl_scan(cnt, lane);
+    if (lane == 63u) s_w[wave] = inc;
+    __syncthreads();
+    uint32_t before = 0, nh = 0;
+    for (uint32_t w = 0; w < LEAD_THREADS / 64u; ++w) {
+        before += w < wave ? s_w[w] : 0u;
+        nh += s_w[w];
+    }
+    uint32_t h = before + inc - cnt;  // lead blocks before lo
+    uint32_t l = lo - h;              // other blocks before lo
+    for (uint32_t i = lo; i < hi; ++i) {
+        if (prev[i] >= min_cost)
+            perm[xcd_slot(h++, nh, G)] = i | 0x80000000u;
+        else
+            perm[nh + xcd_slot(l++, n - nh, G)] = i;
+        cur[i] = 0u;
+    }
+}
+
 // occupancy of the traversal kernels (waves per SIMD the register allocation must allow; 0 = the compiler's choice).
 // Default: the queue kernel of brick_dim 1 and 4 fits 96 VGPRs (5 waves per SIMD instead of 4, no spills under the
 // iterative-ilp scheduler of _build.py); brick_dim 2 would spill 4 VGPRs and 8..32 16, so they keep 4 waves (the
@@ -577,7 +627,13 @@ __global__ void __launch_bounds__(256) VHX_PRIMARY_ATTR k_trace_primary(DevTree 
     __shared__ uint64_t occ_tab[OCC_TAB_WORDS];
     fill_occ_tab(occ_tab, t);
     __syncthreads();
-    const uint32_t bid = xcd_block(blockIdx.x, gridDim.x, q.xcd_group);
+    uint32_t bid = xcd_block(blockIdx.x, gridDim.x, q.xcd_group);
+    bool lead = false;  // workgroup-uniform
+    if (q.lead_perm) {
+        const uint32_t e = q.lead_perm[blockIdx.x];
+        bid = e & 0x7FFFFFFFu;
+        lead = (e >> 31) != 0u;
+    }
     const uint32_t j = bid / blocks_per_tile;  // j-th tile of this rank
     const uint32_t sb = bid - j * blocks_per_tile;
     const uint32_t tile = tile_start + j * tile_stride;
@@ -597,18 +653,26 @@ __global__ void __launch_bounds__(256) VHX_PRIMARY_ATTR k_trace_primary(DevTree 
     const uint64_t idx = layout == VHX_LAYOUT_FRAMEBUFFER ? (uint64_t)py * cam.width + px
                                                           : (uint64_t)j * T * T + (uint64_t)ly * T + lx;
     bool done = true;
+    uint32_t steps = 0;
     if (valid) {
         F3d o, d;
         primary_ray(cam, px, py, o, d);
         HitOut h;
         h.bytes = 0;
         const float start = FAST ? prepass_start(fast, px, py) : 0.0f;
-        done = get_by_ray<COUNT, BD, FAST, MIP>(t, occ_tab, o, d, h, q.budget, q.state, (uint32_t)idx, false, start,
-                                                q.sparse);
+        // a lead block's rays run to the end here (started first, their long tails overlap the rest of pass 0)
+        done = get_by_ray<COUNT, BD, FAST, MIP>(t, occ_tab, o, d, h, lead ? VHX_MAX_ITERS : q.budget,
+                                                lead ? nullptr : q.state, (uint32_t)idx, false, start,
+                                                lead ? 0u : q.sparse);
         if (done)
             store(t, out, idx, o, h);
         else if (COUNT && q.state)
             out.bytes[idx] = h.bytes;  // the running count, continued by the pass that resumes the ray
+        steps = done ? h.iters : 0u;
+    }
+    if (lead && q.lead_cost) {  // the block's longest ray (wave maximum, one atomic per wave)
+        for (uint32_t dd = 32; dd > 0; dd >>= 1) steps = max(steps, (uint32_t)__shfl_xor((int)steps, (int)dd));
+        if ((threadIdx.x & 63u) == 0u) atomicMax(q.lead_cost + bid, steps);
     }
     // every entry of the output gets its flag, so the flags need no clearing between frames: in the tile layout
     // every in-tile entry (frame padding included, done = true there); in the framebuffer layout only pixels of the
@@ -726,6 +790,10 @@ __global__ void __launch_bounds__(256) VHX_QUEUE_ATTR k_trace_queue(DevTree t, c
                 store_shadow(b->out, idx, h);
             } else {
                 store(t, b->out, idx, o, h);
+                if (q.lead_cost) {  // a whole framebuffer frame in 16x16 blocks (LeadQ): the ray's block
+                    const uint32_t py = idx / b->cam.width, px = idx - py * b->cam.width;
+                    atomicMax(q.lead_cost + (py >> 4) * b->src.tiles_x + (px >> 4), h.iters);
+                }
             }
         }
         if (q.tmp) {  // this chunk's abandoned rays, in lane order
@@ -1345,6 +1413,7 @@ static void select_schedule(vhx_ctx *c) {
     if (!c->adaptive) {
         c->last_sched = -1;
         c->split = c->split_force > 0 ? 1u : 0u;
+        c->lead = c->lead_force > 0 ? 1u : 0u;
         return;
     }
     bool busy = false;
@@ -1363,6 +1432,7 @@ static void select_schedule(vhx_ctx *c) {
     c->queue_waves = s.queue_waves_per_cu * c->cus;
     c->qorder = s.qorder;
     c->split = c->split_force >= 0 ? (uint32_t)c->split_force : s.split;
+    c->lead = c->lead_force >= 0 ? (uint32_t)c->lead_force : s.lead;
     c->last_sched = busy ? 1 : 0;
 }
 
@@ -1421,6 +1491,8 @@ static PassQ pass_q(const vhx_ctx *c, uint32_t p, uint32_t npass) {
     q.state = c->resume && npass > 1 && p >= c->save_from ? (uint4 *)c->state.ptr : nullptr;
     q.resume = c->resume && p > c->save_from ? 1u : 0u;
     q.sparse = last || !q.state ? 0u : c->sparse[p];
+    q.lead_perm = nullptr;
+    q.lead_cost = p > 0 ? c->lead_rec : nullptr;
     return q;
 }
 
@@ -1639,7 +1711,8 @@ void vhx_destroy(vhx_ctx *c) {
     c->tree.reset();  // frees the device tree with its last context
     if (c->use_ev) (void)hipEventDestroy(c->use_ev);
     for (DevBuf *b : {&c->scratch, &c->rays, &c->queue[0], &c->queue[1], &c->qctl, &c->tmp, &c->counts, &c->offsets,
-                      &c->flags, &c->qargs, &c->state, &c->upd, &c->prepass_depth, &c->ovf})
+                      &c->flags, &c->qargs, &c->state, &c->upd, &c->prepass_depth, &c->ovf, &c->lead_cost[0],
+                      &c->lead_cost[1], &c->lead_perm})
         if (b->ptr) (void)hipFree(b->ptr);
     for (auto &P : c->pinned) {
         if (P.ptr) (void)hipHostFree(P.ptr);
@@ -1762,6 +1835,12 @@ static int apply_tuning(vhx_ctx *c, const std::string &key, const std::string &v
     } else if (key == "split") {
         if (!parse_u32(val, x) || x > 1) return bad();
         c->split_force = (int)x;
+    } else if (key == "lead") {
+        if (!parse_u32(val, x) || x > 1) return bad();
+        c->lead_force = (int)x;
+    } else if (key == "lead_min") {
+        if (!parse_u32(val, x) || x == 0) return bad();
+        c->lead_min = x;
     } else if (key == "split_wait") {
         if (!parse_u32(val, x) || x == 0) return bad();
         c->split_max_wait = x;
@@ -2013,6 +2092,8 @@ void vhx::copy_sched(vhx_ctx *c, const vhx_ctx *owner) {
     c->split_take = owner->split_take;
     c->split_diag = owner->split_diag;
     c->split_max_wait = owner->split_max_wait;
+    c->lead_force = owner->lead_force;
+    c->lead_min = owner->lead_min;
     std::memcpy(c->sparse, owner->sparse, sizeof(c->sparse));
     c->prepass = owner->prepass;
     c->prepass_margin = owner->prepass_margin;
@@ -2304,6 +2385,32 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
     if (npass > 1 && layout == VHX_LAYOUT_FRAMEBUFFER && (tile_start > 0 || tile_stride > 1))
         VHX_HIP(c, hipMemsetAsync(c->flags.ptr, 0, nout, c->stream));
 
+    // lead blocks (a whole framebuffer frame of 16x16 blocks under a multi-pass schedule that selects them): pass 0's
+    // block order from the previous frame's per-block cost, this frame's cost recorded for the next
+    const uint32_t *lead_perm = nullptr;
+    uint32_t *lead_rec = nullptr;
+    if (c->lead && npass > 1 && layout == VHX_LAYOUT_FRAMEBUFFER && T == 16 && tile_start == 0 && tile_stride == 1 &&
+        !c->in_prepass) {
+        const uint64_t bytes = nblocks * 4;
+        const bool fresh = c->lead_cost[0].bytes < bytes || c->lead_cost[1].bytes < bytes;
+        if ((rc = ensure(c, c->lead_cost[0], bytes)) || (rc = ensure(c, c->lead_cost[1], bytes)) ||
+            (rc = ensure(c, c->lead_perm, bytes)))
+            return rc;
+        if (fresh) c->lead_w = c->lead_h = 0;
+        lead_rec = (uint32_t *)c->lead_cost[c->lead_cur].ptr;
+        if (c->lead_w == cam->width && c->lead_h == cam->height) {
+            k_lead_perm<<<1, LEAD_THREADS, 0, c->stream>>>((const uint32_t *)c->lead_cost[c->lead_cur ^ 1u].ptr, lead_rec,
+                                                           (uint32_t)nblocks, c->lead_min, c->xcd_group,
+                                                           (uint32_t *)c->lead_perm.ptr);
+            lead_perm = (const uint32_t *)c->lead_perm.ptr;
+        } else {
+            VHX_HIP(c, hipMemsetAsync(lead_rec, 0, bytes, c->stream));
+        }
+        c->lead_rec = lead_rec;
+        c->lead_cur ^= 1u;
+        c->lead_w = cam->width;
+        c->lead_h = cam->height;
+    }
     const bool count = ho.dev.bytes != nullptr;
     int qrc = VHX_OK;
     // the queue order's frame (c->qorder): the framebuffer layout only. The tile layout's output index is already
@@ -2315,6 +2422,8 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
         constexpr int BD = decltype(bd_tag)::value;
         PassQ q0 = pass_q(c, 0, npass);
         if (npass > 1) q0.flags = (uint8_t *)c->flags.ptr;
+        q0.lead_perm = lead_perm;
+        q0.lead_cost = lead_rec;
         if (t.mips) {  // MIP stand-ins (no byte counting, no depth prepass: refused above)
             k_trace_primary<false, BD, false, true><<<(unsigned)nblocks, 256, 0, c->stream>>>(
                 t, cd, ho.dev, T, tiles_x, tile_start, tile_stride, layout, bpx, bpt, q0);
@@ -2333,7 +2442,9 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
             qrc = launch_queue_passes<false, BD>(c, t, cd, src, ho.dev, 1, npass, nout, nblocks, true, ow, oh);
         }
     };
-    if (!dispatch_bd(c->tree->desc.brick_dim, launch)) return fail(c, VHX_E_INVALID_ARG, "unsupported brick_dim");
+    const bool bd_ok = dispatch_bd(c->tree->desc.brick_dim, launch);
+    c->lead_rec = nullptr;
+    if (!bd_ok) return fail(c, VHX_E_INVALID_ARG, "unsupported brick_dim");
     if (qrc) return qrc;
     VHX_HIP(c, hipGetLastError());
     if (c->in_prepass) return VHX_OK;  // the outer call records the end and copies its outputs

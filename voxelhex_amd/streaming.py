@@ -62,10 +62,14 @@ class StreamingView:
         o = (ctypes.c_float * 3)(*[float(v) for v in origin])
         N.check(N.lib().vhx_stream_set_viewport(self._h, o, float(view_distance)))
 
-    def upload(self):
-        """One frame of uploads; returns (stats dict, needs_resize)."""
+    def upload(self, frames=1):
+        """One frame of uploads (frames > 1: that many frames' uploads written as one batch,
+        vhx_stream_upload_frames); returns (stats dict, needs_resize)."""
         st = StreamStats()
-        rc = N.lib().vhx_stream_upload(self._h, ctypes.byref(st))
+        if frames == 1:
+            rc = N.lib().vhx_stream_upload(self._h, ctypes.byref(st))
+        else:
+            rc = N.lib().vhx_stream_upload_frames(self._h, frames, ctypes.byref(st))
         if rc not in (N.VHX_OK, N.VHX_E_CAPACITY):
             N.check(rc, self._ctx())
         return {f: getattr(st, f) for f in STAT_FIELDS}, rc == N.VHX_E_CAPACITY
