@@ -117,6 +117,13 @@ int vhx_boxtree_flatten_lod(const vhx_boxtree *tree, uint32_t max_depth, vhx_fla
  * without the voxel-by-voxel insert loop (minutes at 1024^3). */
 int vhx_scene_build_lod(uint32_t scene, uint32_t size, uint32_t brick_dim, uint64_t seed, int threads,
                         uint32_t max_depth, vhx_flat **out);
+/* The host BoxTree of vhx_scene_build's image without the voxel-by-voxel insert loop (a 1024^3 tree in seconds instead
+ * of minutes): nodes (pool key = breadth-first index), bricks, occupancy and palettes as vhx_scene_insert builds them,
+ * so vhx_boxtree_flatten gives vhx_scene_build's buffers. Not restored: occlusion bits (they record which siblings
+ * existed when a node became full, an insert-history fact; all clear here, so a stream's upload walk may descend into
+ * nodes the reference would skip) and MIP maps (off; vhx_boxtree_switch_mips builds them). */
+int vhx_scene_build_tree(uint32_t scene, uint32_t size, uint32_t brick_dim, uint64_t seed, int threads,
+                         vhx_boxtree **out);
 int vhx_flat_node_mips(const vhx_flat *flat, const uint32_t **node_mips, uint32_t *count);
 /* Fills *desc with pointers into the flat object (valid until vhx_flat_free). */
 int vhx_flat_desc(const vhx_flat *flat, vhx_tree_desc *desc);

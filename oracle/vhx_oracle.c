@@ -56,6 +56,13 @@ static _Thread_local uint32_t g_ev_n, g_ev_cap;
     do {                                                           \
         if (g_ev && g_ev_n < g_ev_cap) g_ev[g_ev_n++] = (uint8_t)(ch); \
     } while (0)
+/* optional: the node key of every N event (the node the iteration visits), for the queue-order simulations */
+static _Thread_local uint32_t *g_evn;
+static _Thread_local uint32_t g_evn_n, g_evn_cap;
+#define EVN(key)                                                       \
+    do {                                                               \
+        if (g_evn && g_evn_n < g_evn_cap) g_evn[g_evn_n++] = (uint32_t)(key); \
+    } while (0)
 
 typedef struct { float x, y, z; } v3;
 typedef struct { v3 min; float size; } cube;
@@ -375,6 +382,7 @@ static void get_by_ray(const vhx_tree_desc *t, v3 o, v3 d, hit_t *h) {
             if (++iters > VHX_ORACLE_MAX_ITERS) return;
             h->n_node++;
             EV('N');
+            EVN(node);
             uint64_t occ = t->node_ocbits[stack.data[stack.head]];
             uint32_t ntype = t->node_type[node];
             h->bytes += 12;
@@ -731,5 +739,41 @@ int64_t vhx_oracle_ray_events(const vhx_tree_desc *t, const vhx_camera *cam, con
     }
     off[n] = used;
     g_ev = 0;
+    return (int64_t)used;
+}
+
+/* vhx_oracle_ray_events plus the node key of every N event: nodes[noff[i] .. noff[i+1]) for ray i (as many as its N
+ * events); -1 if either capacity was too small. Diagnostics only. */
+int64_t vhx_oracle_ray_events_nodes(const vhx_tree_desc *t, const vhx_camera *cam, const uint32_t *px,
+                                    const uint32_t *py, uint64_t n, uint8_t *buf, uint64_t cap, uint64_t *off,
+                                    uint32_t *nodes, uint64_t ncap, uint64_t *noff) {
+    uint64_t nused = 0;
+    ensure_luts();
+    uint64_t used = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        hit_t hh;
+        v3 o, d;
+        primary_ray(cam, px[i], py[i], &o, &d);
+        g_ev = buf + used;
+        g_ev_n = 0;
+        g_ev_cap = (uint32_t)(cap - used > 0xFFFFFFFFull ? 0xFFFFFFFFull : cap - used);
+        g_evn = nodes + nused;
+        g_evn_n = 0;
+        g_evn_cap = (uint32_t)(ncap - nused > 0xFFFFFFFFull ? 0xFFFFFFFFull : ncap - nused);
+        get_by_ray(t, o, d, &hh);
+        off[i] = used;
+        noff[i] = nused;
+        if (g_ev_n >= g_ev_cap || g_evn_n >= g_evn_cap) {
+            g_ev = 0;
+            g_evn = 0;
+            return -1;
+        }
+        used += g_ev_n;
+        nused += g_evn_n;
+    }
+    off[n] = used;
+    noff[n] = nused;
+    g_ev = 0;
+    g_evn = 0;
     return (int64_t)used;
 }

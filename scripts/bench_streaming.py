@@ -10,7 +10,12 @@ stream) and the trace.
 outputs, the uploads go through the owner, and nothing is synchronised between frames (libvhx orders every write after
 the frames submitted before it and every frame after the writes submitted before it); the figure is the frame period
 (wall time / frames) next to the same loop at F = 1 without per-frame synchronisation.
-usage: bench_streaming.py [frames] [--inflight F]"""
+--batches K1,K2,... (with --inflight F): the uploads of K frames written once every K frames
+(vhx_stream_upload_frames), so that K frames in flight share one tree version; each K runs the same frames of the orbit,
+rounds interleaved.
+--size / --width / --height: the tree (scene S, brick_dim 4; 1024 builds the host tree from the bulk image,
+BoxTree.from_scene) and the frame.
+usage: bench_streaming.py [frames] [--inflight F] [--batches 1,4,8] [--size 1024 --width 3840 --height 2160]"""
 import argparse
 import os
 import sys
@@ -19,6 +24,11 @@ import time
 ap = argparse.ArgumentParser()
 ap.add_argument("frames", nargs="?", type=int, default=200)
 ap.add_argument("--inflight", type=int, default=1)
+ap.add_argument("--batches", default=None)
+ap.add_argument("--size", type=int, default=256)
+ap.add_argument("--width", type=int, default=1920)
+ap.add_argument("--height", type=int, default=1080)
+ap.add_argument("--rounds", type=int, default=2)
 args = ap.parse_args()
 if args.inflight > 1 and int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < args.inflight + 4:
     os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, args.inflight + 4))  # before HIP starts (bench.py's hw_queues)
@@ -31,25 +41,30 @@ import voxelhex_amd as vhx  # noqa: E402
 from voxelhex_amd import _native as N  # noqa: E402
 
 frames = args.frames
-t = vhx.BoxTree(256, 4)
-t.insert_scene(N.VHX_SCENE_LATTICE_CUBE)
+SZ, WD, HT = args.size, args.width, args.height
+if SZ >= 512:
+    t = vhx.BoxTree.from_scene(N.VHX_SCENE_LATTICE_CUBE, SZ, 4, threads=16)
+else:
+    t = vhx.BoxTree(SZ, 4)
+    t.insert_scene(N.VHX_SCENE_LATTICE_CUBE)
 rt = vhx.Raytracer(0)
 stream = torch.cuda.ExternalStream(rt.stream())
 torch.cuda.set_stream(stream)
-S = 256.0
-s = vhx.StreamingView(t, rt, (S / 2, S / 2, S / 2), 64.0)
+S = float(SZ)
+VD = S / 4  # view distance (64 at 256^3)
+s = vhx.StreamingView(t, rt, (S / 2, S / 2, S / 2), VD)
 s.set_rates(25, 50, 10)
 
 
 def view(k):
     a = 2.0 * np.pi * k / frames
-    c = (S / 2 + 60.0 * np.cos(a), S / 2, S / 2 + 60.0 * np.sin(a))
+    c = (S / 2 + 0.234 * S * np.cos(a), S / 2, S / 2 + 0.234 * S * np.sin(a))
     return a, c
 
 
 def outputs():
-    return {"rgba": torch.zeros(1920 * 1080, dtype=torch.int32, device="cuda"),
-            "depth": torch.zeros(1920 * 1080, dtype=torch.float32, device="cuda")}
+    return {"rgba": torch.zeros(WD * HT, dtype=torch.int32, device="cuda"),
+            "depth": torch.zeros(WD * HT, dtype=torch.float32, device="cuda")}
 
 
 q = lambda v: f"median {np.median(v):.3f} p90 {np.percentile(v, 90):.3f} max {np.max(v):.3f}"  # noqa: E731
@@ -59,7 +74,7 @@ if args.inflight <= 1:
     host, dev, trace, written, resizes = [], [], [], [], 0
     for k in range(frames):
         a, c = view(k)
-        s.set_viewport(c, 64.0)
+        s.set_viewport(c, VD)
         e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
         e0.record(stream)
         t0 = time.perf_counter()
@@ -69,7 +84,7 @@ if args.inflight <= 1:
             s.resize()
             resizes += 1
         e1.record(stream)
-        cam = vhx.glass_camera(256, 1920, 1080, angle=40.0 + a, target=c)
+        cam = vhx.glass_camera(SZ, WD, HT, angle=40.0 + a, target=c)
         rt.trace_primary(cam, out=out)
         e2.record(stream)
         written.append(st["bytes_written"])
@@ -93,22 +108,49 @@ else:
         t0 = time.perf_counter()
         for k in range(k0, k0 + frames):
             a, c = view(k)
-            s.set_viewport(c, 64.0)
+            s.set_viewport(c, VD)
             h0 = time.perf_counter()
             _, grow = s.upload()  # through the owner, no host wait
             host.append((time.perf_counter() - h0) * 1e3)
             if grow:
                 s.resize()
                 resizes += 1
-            cam = vhx.glass_camera(256, 1920, 1080, angle=40.0 + a, target=c)
+            cam = vhx.glass_camera(SZ, WD, HT, angle=40.0 + a, target=c)
             ctxs[k % nctx].trace_primary(cam, out=outs[k % nctx])
         torch.cuda.synchronize()
         return (time.perf_counter() - t0) * 1e3 / frames, host, resizes
 
     loop(F, 0)  # warm-up: every context allocates its queues, the view reaches its size
+    if args.batches:
+        def batched(K, k0):
+            t0 = time.perf_counter()
+            resizes = 0
+            for k in range(k0, k0 + frames):
+                a, c = view(k)
+                s.set_viewport(c, VD)
+                if (k - k0) % K == 0:
+                    _, grow = s.upload(frames=K)  # K frames' uploads, one tree version for the next K frames
+                    if grow:
+                        s.resize()
+                        resizes += 1
+                cam = vhx.glass_camera(SZ, WD, HT, angle=40.0 + a, target=c)
+                ctxs[k % F].trace_primary(cam, out=outs[k % F])
+            torch.cuda.synchronize()
+            return (time.perf_counter() - t0) * 1e3 / frames, resizes
+        Ks = [int(x) for x in args.batches.split(",")]
+        res = {K: [] for K in Ks}
+        for rnd in range(args.rounds):
+            for K in Ks:
+                period, resizes = batched(K, frames)  # the same frames of the orbit for every K
+                res[K].append(period)
+                print(f"round {rnd} batch K={K}: {frames} frames on {F} contexts, period {period:.4f} ms per frame "
+                      f"(upload + {WD}x{HT} trace), {resizes} resizes", flush=True)
+        base = min(res[Ks[0]])
+        for K in Ks:
+            print(f"batch K={K}: best period {min(res[K]):.4f} ms per frame = {min(res[K]) / base:.3f} x K={Ks[0]}")
     for nctx in (1, F):
         period, host, resizes = loop(nctx, frames)
-        print(f"frames in flight {nctx}: {frames} frames, period {period:.4f} ms per frame (upload + 1920x1080 trace), "
+        print(f"frames in flight {nctx}: {frames} frames, period {period:.4f} ms per frame (upload + {WD}x{HT} trace), "
               f"producer host ms {q(host)}, {resizes} resizes")
     for r in ctxs[1:]:
         r.close()

@@ -7,14 +7,23 @@ Derived per pass: active lanes per VALU instruction (SQ_THREAD_CYCLES_VALU / SQ_
 wave-instructions per frame, the fraction of wave cycles spent issuing / waiting on dependencies / waiting on memory
 (SQ_ACTIVE_INST_ANY, SQ_WAIT_INST_ANY, SQ_WAIT_ANY over SQ_WAVE_CYCLES; quad-cycle units cancel) and the memory-side
 reads (FETCH_SIZE x 1024 B x 2, the gfx950 correction of scripts/pmc_frame.py).
-usage: pmc_passes.py PROFILE_DIR [OUT_TXT]"""
+--inflight-only (round 4): only frames that ran the frames-in-flight schedule (the most passes
+seen) and come after the first SKIP frames of the run (--skip SKIP: the setup frames that allocate the contexts and the
+warm-up), so that the lone frames of the run (the setup's first frame, the isolated frames after the timed region) do
+not mix into the per-pass figures.
+usage: pmc_passes.py PROFILE_DIR [OUT_TXT] [--inflight-only] [--skip SKIP]"""
 import csv
 import glob
 import os
 import sys
 from collections import defaultdict
 
-d = sys.argv[1]
+args = [a for a in sys.argv[1:] if not a.startswith("--")]
+inflight_only = "--inflight-only" in sys.argv
+skip = int(sys.argv[sys.argv.index("--skip") + 1]) if "--skip" in sys.argv else 0
+if "--skip" in sys.argv:
+    args.remove(str(skip))
+d = args[0]
 sums = defaultdict(lambda: defaultdict(float))  # (run, pass) -> counter -> total
 runs = {}  # run -> (counter names, frames)
 for path in sorted(glob.glob(os.path.join(d, "pmc*_counter_collection.csv"))):
@@ -25,19 +34,21 @@ for path in sorted(glob.glob(os.path.join(d, "pmc*_counter_collection.csv"))):
                             {"name": r["Kernel_Name"].replace("void ", ""), "queue": r["Queue_Id"], "c": defaultdict(float)})
         e["c"][r["Counter_Name"]] += float(r["Counter_Value"])
         names.add(r["Counter_Name"])
-    cur, nf = {}, 0  # queue -> pass index of its latest trace dispatch
+    frames, open_frame = [], {}  # per frame (in dispatch order of its pass 0): its dispatches by pass; queue -> frame
     for k in sorted(disp):
         e = disp[k]
         if e["name"].startswith("k_trace_primary<false"):
-            cur[e["queue"]] = 0
-            nf += 1
-        elif e["name"].startswith("k_trace_queue<false") and e["queue"] in cur:
-            cur[e["queue"]] += 1
-        else:
-            continue
-        for c, v in e["c"].items():
-            sums[(run, cur[e["queue"]])][c] += v
-    runs[run] = (names, nf)
+            open_frame[e["queue"]] = len(frames)
+            frames.append([e])
+        elif e["name"].startswith("k_trace_queue<false") and e["queue"] in open_frame:
+            frames[open_frame[e["queue"]]].append(e)
+    most = max((len(f) for f in frames), default=0)
+    keep = [f for i, f in enumerate(frames) if i >= skip and (not inflight_only or len(f) == most)]
+    for f in keep:
+        for p, e in enumerate(f):
+            for c, v in e["c"].items():
+                sums[(run, p)][c] += v
+    runs[run] = (names, len(keep))
 
 passes = sorted({p for (_, p) in sums})
 
@@ -49,7 +60,9 @@ def per_frame(p, c):
     return None
 
 
-lines = [f"per-pass PMC figures per frame, {os.path.basename(os.path.normpath(d))} (frames per pmc run: "
+lines = [f"per-pass PMC figures per frame, {os.path.basename(os.path.normpath(d))}"
+         + (f" (frames-in-flight schedule only, first {skip} frames skipped)" if inflight_only or skip else "")
+         + " (frames per pmc run: "
          + ", ".join(f"{run} {nf}" for run, (_, nf) in runs.items()) + ")"]
 for p in passes:
     valu, salu = per_frame(p, "SQ_INSTS_VALU"), per_frame(p, "SQ_INSTS_SALU")
@@ -73,5 +86,5 @@ for p in passes:
     lines.append("  " + "  ".join(parts))
 txt = "\n".join(lines)
 print(txt)
-if len(sys.argv) > 2:
-    open(sys.argv[2], "w").write(txt + "\n")
+if len(args) > 1:
+    open(args[1], "w").write(txt + "\n")

@@ -21,13 +21,15 @@
 
 #include "../../include/vhx.h"
 
-int64_t vhx_oracle_ray_events(const vhx_tree_desc *t, const vhx_camera *cam, const uint32_t *px, const uint32_t *py,
-                              uint64_t n, uint8_t *buf, uint64_t cap, uint64_t *off);
+int64_t vhx_oracle_ray_events_nodes(const vhx_tree_desc *t, const vhx_camera *cam, const uint32_t *px,
+                                    const uint32_t *py, uint64_t n, uint8_t *buf, uint64_t cap, uint64_t *off,
+                                    uint32_t *nodes, uint64_t ncap, uint64_t *noff);
 
 #define VHX_MAX_ITERS_SIM (1u << 22)
 
 typedef struct {
     uint8_t probe, nb, pop, push, na, restart;
+    uint32_t node;  /* the node the iteration visits */
 } it_t;
 
 static it_t *g_its;
@@ -51,11 +53,13 @@ int64_t wavesim_build(const vhx_tree_desc *t, const vhx_camera *cam, uint32_t W,
         for (uint32_t x = 0; x < W; ++x) px[x] = x, py[x] = y;
         uint64_t cap = (uint64_t)W * 64;
         uint8_t *buf = NULL;
-        uint64_t *off = (uint64_t *)malloc((W + 1) * 8);
+        uint32_t *nodes = NULL;
+        uint64_t *off = (uint64_t *)malloc((W + 1) * 8), *noff = (uint64_t *)malloc((W + 1) * 8);
         int64_t used;
         for (;;) {
             buf = (uint8_t *)realloc(buf, cap);
-            used = vhx_oracle_ray_events(t, cam, px, py, W, buf, cap, off);
+            nodes = (uint32_t *)realloc(nodes, cap * 4);
+            used = vhx_oracle_ray_events_nodes(t, cam, px, py, W, buf, cap, off, nodes, cap, noff);
             if (used >= 0) break;
             cap *= 4;
         }
@@ -70,7 +74,9 @@ int64_t wavesim_build(const vhx_tree_desc *t, const vhx_camera *cam, uint32_t W,
             for (uint64_t i = off[x]; i < off[x + 1]; ++i) {
                 const uint8_t ch = buf[i];
                 if (ch == 'N') {
-                    cur = &its[k++];
+                    cur = &its[k];
+                    cur->node = nodes[noff[x] + cnt];
+                    ++k;
                     ++cnt;
                 } else if (cur) {
                     switch (ch) {
@@ -88,7 +94,7 @@ int64_t wavesim_build(const vhx_tree_desc *t, const vhx_camera *cam, uint32_t W,
         if (k != nit) bad = 1;
         rows[y] = its;
         row_n[y] = nit;
-        free(px), free(py), free(buf), free(off);
+        free(px), free(py), free(buf), free(off), free(nodes), free(noff);
     }
     if (bad) return -1;
     uint64_t total = 0;
@@ -369,8 +375,26 @@ static uint64_t order_key(uint32_t ray) {
     while (b < 63 && (1ull << ((b + 1) / 2)) * ((b + 1) % 2 ? 181ull : 128ull) / 128ull <= st) ++b;
     return ((uint64_t)(63 - b) << 40) | pos;
 }
+static uint32_t g_mode;
 static int cmp_ray(const void *a, const void *b) {
-    const uint64_t x = order_key(((const lane_t *)a)->ray), y = order_key(((const lane_t *)b)->ray);
+    const lane_t *la = (const lane_t *)a, *lb = (const lane_t *)b;
+    uint64_t x, y;
+    if (g_mode == 3 || g_mode == 4) {
+        g_order = 1;
+        const uint64_t pa = order_key(la->ray), pb = order_key(lb->ray);
+        g_order = g_mode;
+        const uint64_t na = g_its[g_off[la->ray] + la->cur].node, nb = g_its[g_off[lb->ray] + lb->cur].node;
+        if (g_mode == 3) {
+            x = (na << 40) | pa;
+            y = (nb << 40) | pb;
+        } else {  /* tile (pos >> 12), node, Morton inside */
+            x = ((pa >> 12) << 44) | (na << 12) | (pa & 4095);
+            y = ((pb >> 12) << 44) | (nb << 12) | (pb & 4095);
+        }
+    } else {
+        x = order_key(la->ray);
+        y = order_key(lb->ray);
+    }
     return x < y ? -1 : x > y;
 }
 
@@ -378,6 +402,7 @@ int wavesim_run(const cfg_t *c, stats_t *s) {
     memset(s, 0, sizeof(*s));
     g_cfg = c;
     g_order = c->order;
+    g_mode = c->order;
     const uint32_t W = g_W, H = g_H;
     const uint64_t n = (uint64_t)W * H;
     lane_t *q = (lane_t *)malloc(n * sizeof(lane_t)), *q2 = (lane_t *)malloc(n * sizeof(lane_t));

@@ -217,3 +217,96 @@ def test_upload_tree_device_matches_host_upload(oracle):
         assert N.lib().vhx_upload_tree_device(rt._h, ctypes.byref(bad)) == N.VHX_E_INVALID_ARG
     finally:
         rt.close()
+
+
+def _pal_edit(flat):
+    pal = flat.color_palette.copy()
+    pal[1::3] = (pal[1::3] & 0x00FFFFFF) | 0x80000000
+    pal[2::5] &= 0x00FFFFFF  # transparent: their cells become empty (every bitmap is rebuilt)
+    return pal
+
+
+def test_write_waits_for_a_frame_whose_context_changed_stream(oracle):
+    """a shared context traces on its own stream, then is moved onto the owner's stream
+    (vhx_set_stream) before the owner writes. The write must still wait for that frame (recorded on the old stream):
+    the frame shows the tree before the write, the next frame after it."""
+    import torch
+    size, W, H = 256, 1920, 1080
+    base = vhx.FlatTree.build_scene(N.VHX_SCENE_LATTICE_CUBE, size, 4)
+    edited = vhx.FlatTree.build_scene(N.VHX_SCENE_LATTICE_CUBE, size, 4)
+    pal = _pal_edit(base)
+    edited.color_palette[:] = pal
+    cam = vhx.glass_camera(size, W, H, target=(size / 2,) * 3)
+    ref0 = oracle.trace_primary(base, cam, 0, 0, W, H, fields=("value", "rgba", "depth"))
+    ref1 = oracle.trace_primary(edited, cam, 0, 0, W, H, fields=("value", "rgba", "depth"))
+    owner = vhx.Raytracer(0)
+    try:
+        owner.upload(base)
+        sh = owner.shared()
+        sh.stream()  # its own stream
+        dev = torch.device("cuda", 0)
+        o0, o1 = _frame_out(W * H, dev), _frame_out(W * H, dev)
+        torch.cuda.synchronize()
+        for rep in range(3):
+            sh.set_stream(None)
+            sh.trace_primary(cam, out=o0)            # on the shared context's own stream
+            sh.set_stream(owner.stream())            # moved onto the owner's stream before the write
+            owner.update_ranges([(N.VHX_BUF_COLOR_PALETTE, 0, pal if rep % 2 == 0 else base.color_palette)])
+            sh.trace_primary(cam, out=o1)            # after the write, on the owner's stream
+            torch.cuda.synchronize()
+            before, after = (ref0, ref1) if rep % 2 == 0 else (ref1, ref0)
+            _same(_host(o0), before, f"rep {rep}: frame submitted before the write")
+            _same(_host(o1), after, f"rep {rep}: frame submitted after the write")
+        sh.close()
+    finally:
+        owner.close()
+
+
+def test_writes_and_traces_from_two_threads(oracle):
+    """contexts of one tree driven from two host threads -- one thread traces frames on a shared
+    context, the other writes the palette through the owner, alternately. Every frame must show one whole tree version
+    (the one before or the one after a write), never a mix: libvhx holds a write until no trace is being submitted and
+    a trace until no write is."""
+    import threading
+
+    import torch
+    size, W, H = 256, 640, 400
+    base = vhx.FlatTree.build_scene(N.VHX_SCENE_LATTICE_CUBE, size, 4)
+    edited = vhx.FlatTree.build_scene(N.VHX_SCENE_LATTICE_CUBE, size, 4)
+    pal = _pal_edit(base)
+    edited.color_palette[:] = pal
+    cam = vhx.glass_camera(size, W, H, target=(size / 2,) * 3)
+    refs = [oracle.trace_primary(f, cam, 0, 0, W, H, fields=("value", "rgba", "depth")) for f in (base, edited)]
+    owner = vhx.Raytracer(0)
+    try:
+        owner.upload(base)
+        sh = owner.shared()
+        dev = torch.device("cuda", 0)
+        outs = [_frame_out(W * H, dev) for _ in range(24)]
+        torch.cuda.synchronize()
+        errors = []
+
+        def writer():
+            try:
+                for k in range(24):
+                    owner.update_ranges([(N.VHX_BUF_COLOR_PALETTE, 0, pal if k % 2 == 0 else base.color_palette)])
+            except Exception as e:  # noqa: BLE001
+                errors.append(e)
+
+        th = threading.Thread(target=writer)
+        th.start()
+        for o in outs:
+            sh.trace_primary(cam, out=o)
+        th.join()
+        assert not errors, errors
+        torch.cuda.synchronize()
+        seen = set()
+        for k, o in enumerate(outs):
+            h = _host(o)
+            ok = [v for v, r in enumerate(refs) if all(np.array_equal(h[f], r[f].view(np.uint32))
+                                                        for f in ("value", "rgba", "depth"))]
+            assert ok, f"frame {k} shows neither tree version (a torn read)"
+            seen.add(ok[0])
+        sh.close()
+    finally:
+        owner.close()

@@ -6,6 +6,7 @@ inner, as the reference examples and tests do) + vhx_boxtree_flatten, compared b
 import numpy as np
 import pytest
 
+import voxelhex_amd as vhx
 from voxelhex_amd import BoxTree, FlatTree
 from voxelhex_amd import _native as N
 
@@ -66,3 +67,20 @@ def test_bulk_lod_equals_insert_mips(scene, size, bd, depth):
         assert x.shape == y.shape, k
         assert np.array_equal(x, y), k
     assert b.node_mips.size == b.node_type.size and (b.node_mips != N.VHX_EMPTY).any()
+
+
+@pytest.mark.parametrize("scene,size,bd", [(1, 64, 4), (1, 128, 8), (2, 32, 2)])
+def test_scene_build_tree_flattens_like_insert(scene, size, bd):
+    """vhx_scene_build_tree: the host tree of the bulk image flattens to exactly the buffers of the insert loop's tree
+    (and of vhx_scene_build), and keeps working as a tree (get / insert)."""
+    ref = vhx.BoxTree(size, bd)
+    ref.insert_scene(scene)
+    t = vhx.BoxTree.from_scene(scene, size, bd)
+    a, b = ref.flatten(), t.flatten()
+    for name in ("node_type", "node_ocbits", "node_children", "voxels", "solid_values", "color_palette",
+                 "data_palette"):
+        assert np.array_equal(getattr(a, name), getattr(b, name)), name
+    for p in ((0, 0, 0), (size // 2, size // 3, size // 5), (size - 1, size - 1, size - 1)):
+        assert t.get(p) == ref.get(p)
+    t.insert((1, 2, 3), vhx.Albedo(5, 6, 7, 255))
+    assert t.get((1, 2, 3)) == vhx.BoxTreeEntry.Visual(vhx.Albedo(5, 6, 7, 255))

@@ -159,6 +159,7 @@ SIGNATURES = [
     ("vhx_vox_rotation", c_int, [ctypes.c_uint8, P(ctypes.c_int32 * 9)]),
     ("vhx_scene_build", c_int, [c_u32, c_u32, c_u32, c_u64, c_int, P(c_void_p)]),
     ("vhx_scene_build_lod", c_int, [c_u32, c_u32, c_u32, c_u64, c_int, c_u32, P(c_void_p)]),
+    ("vhx_scene_build_tree", c_int, [c_u32, c_u32, c_u32, c_u64, c_int, P(c_void_p)]),
     ("vhx_flat_desc", c_int, [c_void_p, P(TreeDesc)]),
     ("vhx_boxtree_switch_mips", c_int, [c_void_p, c_int]),
     ("vhx_boxtree_set_mip_method", c_int, [c_void_p, c_u32, c_u32, c_f32]),

@@ -304,6 +304,15 @@ class FlatTree:
         return t
 
     @classmethod
+    def from_scene(cls, scene, size, brick_dim, seed=0x5EED, threads=0):
+        """The tree insert_scene builds, from the bulk builder's image (vhx_scene_build_tree: seconds at 1024^3 where the
+        insert loop takes minutes); occlusion bits and MIP maps are not restored (include/vhx_boxtree.h)."""
+        h = ctypes.c_void_p()
+        _tree_check(N.lib().vhx_scene_build_tree(scene, size, brick_dim, seed, threads, ctypes.byref(h)),
+                    f"scene {scene} size {size} brick_dim {brick_dim}")
+        return cls._from_handle(h)
+
+    @classmethod
     def load_vox_file(cls, filename, brick_dimension):
         """BoxTree::load_vox_file (src/convert/magicavoxel.rs:234-265): MagicaVoxel .vox import (C++,
         voxelhex_amd/csrc/vox.cpp). Raises VhxError for unreadable / unsupported files, InvalidPosition for voxels
@@ -367,6 +376,15 @@ class BoxTree:
         t._flat = None
         t._flat_version = -1
         return t
+
+    @classmethod
+    def from_scene(cls, scene, size, brick_dim, seed=0x5EED, threads=0):
+        """The tree insert_scene builds, from the bulk builder's image (vhx_scene_build_tree: seconds at 1024^3 where the
+        insert loop takes minutes); occlusion bits and MIP maps are not restored (include/vhx_boxtree.h)."""
+        h = ctypes.c_void_p()
+        _tree_check(N.lib().vhx_scene_build_tree(scene, size, brick_dim, seed, threads, ctypes.byref(h)),
+                    f"scene {scene} size {size} brick_dim {brick_dim}")
+        return cls._from_handle(h)
 
     @classmethod
     def load_vox_file(cls, filename, brick_dimension):

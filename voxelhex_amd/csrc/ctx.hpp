@@ -177,6 +177,7 @@ struct vhx_ctx {
     uint32_t lead = 0;
     int lead_force = -1;
     uint32_t lead_min = 512;
+    uint32_t lead_cap = 0;  // at most about this many lead blocks (0 = no cap; tune "lead_cap")
     DevBuf lead_cost[2], lead_perm;
     uint32_t lead_cur = 0, lead_w = 0, lead_h = 0;
     uint32_t *lead_rec = nullptr;

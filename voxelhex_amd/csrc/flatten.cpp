@@ -622,6 +622,23 @@ int vhx_scene_build_lod(uint32_t scene, uint32_t size, uint32_t brick_dim, uint6
         return VHX_E_CAPACITY;
     }
 }
+int vhx_scene_build_tree(uint32_t scene, uint32_t size, uint32_t brick_dim, uint64_t seed, int threads,
+                         vhx_boxtree **out) {
+    if (!out || !scene_valid(scene)) return VHX_E_INVALID_ARG;
+    *out = nullptr;
+    try {
+        vhx_flat *full = nullptr;
+        int rc = build_scene(scene, size, brick_dim, seed, threads, &full);
+        if (rc != VHX_OK) return rc;
+        std::unique_ptr<vhx_flat> owned(full);
+        BoxTree *t = tree_of_flat(*full);
+        if (!t) return VHX_E_STATE;
+        *out = new vhx_boxtree{t};
+        return VHX_OK;
+    } catch (const std::bad_alloc &) {
+        return VHX_E_CAPACITY;
+    }
+}
 int vhx_flat_desc(const vhx_flat *f, vhx_tree_desc *d) {
     if (!f || !d) return VHX_E_INVALID_ARG;
     std::memset(d, 0, sizeof(*d));

@@ -547,12 +547,28 @@ __device__ __forceinline__ uint32_t xcd_slot(uint32_t r, uint32_t n, uint32_t G)
     return k * 8u + x;
 }
 #define LEAD_THREADS 1024u
+// cap > 0: at most about cap lead blocks (the threshold is raised to the smallest power of two >= min_cost whose blocks
+// number at most cap), so that the lead blocks leave room for the other blocks in the CUs' workgroup slots
 __global__ void __launch_bounds__(LEAD_THREADS) k_lead_perm(const uint32_t *__restrict__ prev, uint32_t *__restrict__ cur,
-                                                           uint32_t n, uint32_t min_cost, uint32_t G,
+                                                           uint32_t n, uint32_t min_cost, uint32_t cap, uint32_t G,
                                                            uint32_t *__restrict__ perm) {
     __shared__ uint32_t s_w[LEAD_THREADS / 64u];
+    __shared__ uint32_t s_hist[33];
     const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
     const uint32_t per = (n + LEAD_THREADS - 1u) / LEAD_THREADS, lo = min(n, t * per), hi = min(n, lo + per);
+    if (cap) {
+        if (t < 33u) s_hist[t] = 0u;
+        __syncthreads();
+        for (uint32_t i = lo; i < hi; ++i)  // bucket b: cost in [2^(b-1), 2^b), bucket 0: cost 0
+            if (prev[i] >= min_cost) atomicAdd(&s_hist[32u - __clz(prev[i])], 1u);
+        __syncthreads();
+        // the smallest bucket edge e (a power of two) with at most cap blocks at or above it
+        uint32_t above = 0, b = 33u;
+        while (b > 1u && above + s_hist[b - 1u] <= cap) above += s_hist[--b];
+        const uint32_t edge = b >= 33u ? 0xFFFFFFFFu : (b == 0u ? 0u : 1u << (b - 1u));
+        min_cost = max(min_cost, edge);
+        __syncthreads();
+    }
     uint32_t cnt = 0;
     for (uint32_t i = lo; i < hi; ++i) cnt += prev[i] >= min_cost ? 1u : 0u;
     // exclusive scan of the per-thread counts: waves, then the waves' totals
@@ -1841,6 +1857,9 @@ static int apply_tuning(vhx_ctx *c, const std::string &key, const std::string &v
     } else if (key == "lead_min") {
         if (!parse_u32(val, x) || x == 0) return bad();
         c->lead_min = x;
+    } else if (key == "lead_cap") {
+        if (!parse_u32(val, x)) return bad();
+        c->lead_cap = x;
     } else if (key == "split_wait") {
         if (!parse_u32(val, x) || x == 0) return bad();
         c->split_max_wait = x;
@@ -2094,6 +2113,7 @@ void vhx::copy_sched(vhx_ctx *c, const vhx_ctx *owner) {
     c->split_max_wait = owner->split_max_wait;
     c->lead_force = owner->lead_force;
     c->lead_min = owner->lead_min;
+    c->lead_cap = owner->lead_cap;
     std::memcpy(c->sparse, owner->sparse, sizeof(c->sparse));
     c->prepass = owner->prepass;
     c->prepass_margin = owner->prepass_margin;
@@ -2400,7 +2420,7 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
         lead_rec = (uint32_t *)c->lead_cost[c->lead_cur].ptr;
         if (c->lead_w == cam->width && c->lead_h == cam->height) {
             k_lead_perm<<<1, LEAD_THREADS, 0, c->stream>>>((const uint32_t *)c->lead_cost[c->lead_cur ^ 1u].ptr, lead_rec,
-                                                           (uint32_t)nblocks, c->lead_min, c->xcd_group,
+                                                           (uint32_t)nblocks, c->lead_min, c->lead_cap, c->xcd_group,
                                                            (uint32_t *)c->lead_perm.ptr);
             lead_perm = (const uint32_t *)c->lead_perm.ptr;
         } else {
