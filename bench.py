@@ -72,7 +72,7 @@ def parse():
                    help="skip the untimed check of the in-flight frames (frames_equal / golden_match)")
     p.add_argument("--no-pmc", action="store_true",
                    help="skip the rocprofv3 FETCH_SIZE child run (roofline.traffic from profiles/traffic.json)")
-    p.add_argument("--inflight", type=int, default=16,
+    p.add_argument("--inflight", type=int, default=20,
                    help="frames in flight per GPU: F contexts sharing the tree (vhx_create_shared), each on its own "
                         "stream, frame i traced by context i %% F, so a frame's latency-bound long-ray tail overlaps the "
                         "next frame's pass 0 (1 = one frame at a time); GPU_MAX_HW_QUEUES is raised to F + 4 so that every "

@@ -134,6 +134,8 @@ typedef struct {
     uint32_t cost[NB];   /* instructions per wave execution of each block */
     uint32_t order;      /* queue order of the queue passes: 0 frame rows, 1 64x64 tiles Morton inside ("64z"), 2 bucketed
                             by the ray's total steps (perfect prediction, sqrt(2) buckets, longest first), 64z inside */
+    uint32_t nwaves;     /* design 3 / 4: persistent waves of a refill pass */
+    uint32_t seg;        /* order 5: the 64z queue sorted by (node, position) inside segments of `seg` entries */
 } cfg_t;
 
 typedef struct {
@@ -351,6 +353,112 @@ static void sim_wave2(const cfg_t *c, int p, lane_t *L, int n, uint32_t budget, 
     }
 }
 
+/* design 3 (lane refill, persistent waves): a queue pass runs `nw` waves round-robin, one node iteration per turn;
+ * a wave whose empty lanes number at least `refill` (or that holds no ray) takes that many rays from the shared
+ * queue (block 9, one execution per refill, its lanes the rays taken) and goes on; a ray over the pass budget is
+ * abandoned to the next pass, a finished ray frees its lane. Block 14: the per-iteration refill check. */
+static uint64_t g_qpos;
+static void sim_refill_pass(const cfg_t *c, int p, lane_t *q, uint64_t nq, uint32_t budget, uint32_t nw,
+                            uint32_t refill, stats_t *s, lane_t *out, uint64_t *nout) {
+    lane_t *L = (lane_t *)malloc((size_t)nw * 64 * sizeof(lane_t));
+    uint8_t *has = (uint8_t *)calloc((size_t)nw * 64, 1);
+    double *cost = (double *)calloc(nw, sizeof(double));
+    uint32_t *busy = (uint32_t *)calloc(nw, sizeof(uint32_t));
+    g_qpos = 0;
+    uint32_t live = nw;
+    uint8_t *gone = (uint8_t *)calloc(nw, 1);
+    while (live) {
+        for (uint32_t w = 0; w < nw; ++w) {
+            if (gone[w]) continue;
+            lane_t *W = L + (size_t)w * 64;
+            uint8_t *H = has + (size_t)w * 64;
+            const uint32_t empty = 64 - busy[w];
+            if (g_qpos < nq && (empty >= refill || busy[w] == 0)) {
+                uint32_t k = 0;
+                for (int i = 0; i < 64 && g_qpos < nq; ++i)
+                    if (!H[i]) {
+                        W[i] = q[g_qpos++];
+                        W[i].carry = 0;
+                        H[i] = 1;
+                        ++k;
+                    }
+                busy[w] += k;
+                s->rays_in[p] += k;
+                s->waves[p][9] += 1;
+                s->lanes[p][9] += k;
+                cost[w] += c->cost[9];
+            }
+            if (busy[w] == 0) {
+                gone[w] = 1;
+                --live;
+                continue;
+            }
+            /* one node iteration of the wave's rays (design 0 blocks) */
+            g_wave_cost = 0;
+            s->waves[p][14] += 1;
+            s->lanes[p][14] += busy[w];
+            g_wave_cost += c->cost[14];
+            int act[64], na = 0;
+            for (int i = 0; i < 64; ++i)
+                if (H[i]) act[na++] = i;
+            add(s, p, 13, na);
+            const it_t *r[64];
+            uint32_t mb = 0, ma = 0, npr = 0, npop = 0, npush = 0, nws = 0, nres = 0;
+            for (int a = 0; a < na; ++a) {
+                r[a] = &g_its[g_off[W[act[a]].ray] + W[act[a]].cur];
+                if (r[a]->nb > mb) mb = r[a]->nb;
+                npr += r[a]->probe;
+                npop += r[a]->pop;
+                npush += r[a]->push;
+                const uint32_t wk = r[a]->pop ? 1u : r[a]->na;
+                if (r[a]->pop || r[a]->na) ++nws;
+                if (wk > ma) ma = wk;
+                nres += r[a]->restart;
+            }
+            add(s, p, 0, na);
+            if (npr) add(s, p, 1, npr);
+            for (uint32_t t = 0; t < mb; ++t) {
+                uint32_t k = 0;
+                for (int a = 0; a < na; ++a) k += r[a]->nb > t;
+                add(s, p, 2, k);
+            }
+            if (npop) add(s, p, 3, npop);
+            if (npush) add(s, p, 4, npush);
+            if (nws) add(s, p, 5, nws);
+            for (uint32_t t = 0; t < ma; ++t) {
+                uint32_t k = 0;
+                for (int a = 0; a < na; ++a) k += (r[a]->pop ? 1u : r[a]->na) > t;
+                add(s, p, 6, k);
+            }
+            if (nres) add(s, p, 7, nres);
+            for (int a = 0; a < na; ++a) {
+                lane_t *l = &W[act[a]];
+                l->iters += r[a]->nb + r[a]->na;
+                l->cur += 1;
+                const uint32_t nit = (uint32_t)(g_off[l->ray + 1] - g_off[l->ray]);
+                if (l->cur >= nit) {
+                    H[act[a]] = 0;
+                    --busy[w];
+                    continue;
+                }
+                l->iters += 1;
+                if (l->iters > budget) {
+                    H[act[a]] = 0;
+                    --busy[w];
+                    out[(*nout)++] = *l;
+                }
+            }
+            cost[w] += g_wave_cost;
+        }
+    }
+    double mx = 0;
+    for (uint32_t w = 0; w < nw; ++w)
+        if (cost[w] > mx) mx = cost[w];
+    if (mx > s->max_wave[p]) s->max_wave[p] = mx;
+    s->waves_pass[p] += nw;
+    free(L), free(has), free(cost), free(busy), free(gone);
+}
+
 static uint32_t g_order;
 static uint32_t spread_bits(uint32_t v) {
     v &= 0xFFFF;
@@ -379,12 +487,12 @@ static uint32_t g_mode;
 static int cmp_ray(const void *a, const void *b) {
     const lane_t *la = (const lane_t *)a, *lb = (const lane_t *)b;
     uint64_t x, y;
-    if (g_mode == 3 || g_mode == 4) {
+    if (g_mode == 3 || g_mode == 4 || g_mode == 5) {
         g_order = 1;
         const uint64_t pa = order_key(la->ray), pb = order_key(lb->ray);
         g_order = g_mode;
         const uint64_t na = g_its[g_off[la->ray] + la->cur].node, nb = g_its[g_off[lb->ray] + lb->cur].node;
-        if (g_mode == 3) {
+        if (g_mode == 3 || g_mode == 5) {
             x = (na << 40) | pa;
             y = (nb << 40) | pb;
         } else {  /* tile (pos >> 12), node, Morton inside */
@@ -410,6 +518,20 @@ int wavesim_run(const cfg_t *c, stats_t *s) {
     /* pass 0: 8x8-pixel waves (four per 16x16 workgroup, blocks in raster order) */
     const uint32_t bx = (W + 15) / 16, by = (H + 15) / 16;
     const uint32_t b0 = c->npass > 1 ? c->budgets[0] : VHX_MAX_ITERS_SIM;
+    if (c->design == 4) { /* pass 0 as a refill pass over the pixels in wave-tile order */
+        uint64_t np = 0;
+        for (uint32_t b = 0; b < bx * by; ++b)
+            for (uint32_t w = 0; w < 4; ++w)
+                for (uint32_t k = 0; k < 64; ++k) {
+                    const uint32_t x = (b % bx) * 16 + (w & 1) * 8 + (k & 7), y = (b / bx) * 16 + (w >> 1) * 8 + (k >> 3);
+                    if (x >= W || y >= H) continue;
+                    const uint32_t ray = y * W + x;
+                    if (g_off[ray + 1] == g_off[ray]) continue;
+                    q2[np].ray = ray, q2[np].cur = 0, q2[np].iters = 1, q2[np].carry = 0;
+                    ++np;
+                }
+        sim_refill_pass(c, 0, q2, np, b0, c->nwaves, c->cap, s, q, &nq);
+    } else
     for (uint32_t b = 0; b < bx * by; ++b)
         for (uint32_t w = 0; w < 4; ++w) {
             lane_t L[64];
@@ -429,12 +551,28 @@ int wavesim_run(const cfg_t *c, stats_t *s) {
             if (g_wave_cost > s->max_wave[0]) s->max_wave[0] = g_wave_cost;
         }
     for (uint32_t p = 1; p < c->npass; ++p) {
+        if (c->order == 5) { /* 64z order, then each segment of c->seg entries by (node, position) */
+            g_mode = 1;
+            g_order = 1;
+            qsort(q, nq, sizeof(lane_t), cmp_ray);
+            g_mode = 5;
+            for (uint64_t i = 0; i < nq; i += c->seg)
+                qsort(q + i, nq - i < c->seg ? nq - i : c->seg, sizeof(lane_t), cmp_ray);
+        } else
         qsort(q, nq, sizeof(lane_t), cmp_ray); /* frame order (pass 1: flag compaction; later: chunk order) */
         const int last = p + 1 >= c->npass;
         const uint32_t budget = last ? VHX_MAX_ITERS_SIM : c->budgets[p];
         const int slot = (int)p;
         const uint32_t rpw = c->rpw[p] ? c->rpw[p] : 64u;
         uint64_t nq2 = 0;
+        if (c->design >= 3) {
+            sim_refill_pass(c, slot, q, nq, budget, c->nwaves, c->cap, s, q2, &nq2);
+            lane_t *t = q;
+            q = q2;
+            q2 = t;
+            nq = nq2;
+            continue;
+        }
         s->rays_in[slot] += nq;
         for (uint64_t i = 0; i < nq; i += rpw) {
             const int nl = (int)(nq - i < rpw ? nq - i : rpw);

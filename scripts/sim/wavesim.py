@@ -16,9 +16,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 sys.path.insert(0, ROOT)
 LIB = os.path.join(ROOT, "scripts", "sim", "_build", "libwavesim.so")
 BLOCKS = {13: "loop trip", 0: "iteration top", 1: "probe", 2: "brick trip", 8: "post", 3: "pop", 4: "push",
-          5: "walk setup", 6: "advance trip", 7: "restart"}
+          5: "walk setup", 6: "advance trip", 7: "restart", 9: "refill", 14: "refill check"}
 # VALU instructions per wave execution of each block (ISA of the bd-4 queue kernel, round 3)
-COSTS = {13: 15, 0: 25, 1: 55, 2: 28, 8: 15, 3: 30, 4: 40, 5: 20, 6: 28, 7: 55}
+COSTS = {13: 15, 0: 25, 1: 55, 2: 28, 8: 15, 3: 30, 4: 40, 5: 20, 6: 28, 7: 55, 9: 300, 14: 4}
 RAY_SETUP = 250  # ray generation + begin (divisions, square roots) per pass-0 wave
 
 
@@ -34,7 +34,7 @@ class Stats(ctypes.Structure):
 class Cfg(ctypes.Structure):
     _fields_ = [("budgets", ctypes.c_uint32 * NP), ("npass", ctypes.c_uint32), ("sparse0", ctypes.c_uint32),
                 ("design", ctypes.c_uint32), ("cap", ctypes.c_uint32), ("rpw", ctypes.c_uint32 * NP),
-                ("cost", ctypes.c_uint32 * 16), ("order", ctypes.c_uint32)]
+                ("cost", ctypes.c_uint32 * 16), ("order", ctypes.c_uint32), ("nwaves", ctypes.c_uint32), ("seg", ctypes.c_uint32)]
 
 
 def build():
@@ -45,9 +45,11 @@ def build():
     return ctypes.CDLL(LIB)
 
 
-def run(lib, budgets, design, cap, sparse0=12, rpw=(), order=0):
+def run(lib, budgets, design, cap, sparse0=12, rpw=(), order=0, nwaves=768, seg=1024):
     c = Cfg()
+    c.seg = seg
     c.order = order
+    c.nwaves = nwaves
     for i, b in enumerate(budgets):
         c.budgets[i] = b
     for i, r in enumerate(rpw):
@@ -67,7 +69,8 @@ def report(s, label):
     for p in range(NP):
         if not s.waves_pass[p]:
             continue
-        valu = RAY_SETUP * s.waves_pass[p] if p == 0 or s.rays_in[p] else 0
+        refill = s.waves[p][9] > 0  # a refill pass charges its ray setup per refill (block 9)
+        valu = 0 if refill else (RAY_SETUP * s.waves_pass[p] if p == 0 or s.rays_in[p] else 0)
         line = []
         for b, name in BLOCKS.items():
             w, l = s.waves[p][b], s.lanes[p][b]
@@ -89,6 +92,8 @@ def main():
     ap.add_argument("--height", type=int, default=2160)
     ap.add_argument("--budgets", default="24,96,768")
     ap.add_argument("--designs", default="0")
+    ap.add_argument("--seg", type=int, default=1024, help="order 5: segment length of the node sort")
+    ap.add_argument("--nwaves", type=int, default=768, help="persistent waves of a refill pass (designs 3, 4)")
     ap.add_argument("--orders", default="0", help="queue orders to compare: 0 frame rows, 1 64z tiles, 2 step buckets")
     a = ap.parse_args()
     import time
@@ -104,7 +109,7 @@ def main():
     for d in a.designs.split(","):
         design, _, cap = d.partition(":")
         for o in a.orders.split(","):
-            s = run(lib, budgets, int(design), int(cap or 0), order=int(o))
+            s = run(lib, budgets, int(design), int(cap or 0), order=int(o), nwaves=a.nwaves, seg=a.seg)
             report(s, f"design {d} budgets {budgets} order {o}")
 
 

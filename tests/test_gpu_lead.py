@@ -44,10 +44,11 @@ def test_lead_frames_vs_oracle(oracle, tune):
 
 
 def test_lead_bench_frame_matches_golden():
-    """The lone bench frame (3840x2160, scene S 1024^3 bd 4) three times on one context: the first frame records the
-    prediction, the next two lead with it; every field equals the golden digests."""
+    """The lone bench frame (3840x2160, scene S 1024^3 bd 4) three times on one context with lead blocks forced on (off
+    by default): the first frame records the prediction, the next two lead with it; every field equals the golden
+    digests."""
     name = "c3_1024_bd4_3840x2160"
-    rt = vhx.Raytracer(0)
+    rt = vhx.Raytracer(0, tune="lead=1")
     try:
         rt.upload(vhx.FlatTree.build_scene(N.VHX_SCENE_LATTICE_CUBE, 1024, 4))
         cam = vhx.glass_camera(1024, 3840, 2160, target=(512.0,) * 3)

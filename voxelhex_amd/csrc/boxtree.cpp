@@ -111,12 +111,17 @@ std::array<size_t, 3> execute_for_relevant_sectants(const Cube &nb, U3 position_
                      std::fmax((float)position_.z, nb.min.z));
     F3 update_size = sub(add(from_u3(position_), f3((float)update_size_, (float)update_size_, (float)update_size_)), position);
     float cell_size = nb.size / 4.f;
+    // The reference walks the whole update region, which may reach far past the node (the streaming view's include
+    // regions grow by 4x per MIP level): a point past the node's upper bound on an axis fails cube_contains, and so does
+    // every later point on that axis (shifted only grows; position >= nb.min), so the loops stop there. The calls of
+    // `fun` and their order are unchanged.
+    const F3 nmax = f3(nb.min.x + nb.size, nb.min.y + nb.size, nb.min.z + nb.size);
     F3 shifted = position;
-    while (shifted.x <= (position.x + update_size.x)) {
+    while (shifted.x <= (position.x + update_size.x) && shifted.x < nmax.x) {
         shifted.y = position.y;
-        while (shifted.y <= (position.y + update_size.y)) {
+        while (shifted.y <= (position.y + update_size.y) && shifted.y < nmax.y) {
             shifted.z = position.z;
-            while (shifted.z <= (position.z + update_size.z)) {
+            while (shifted.z <= (position.z + update_size.z) && shifted.z < nmax.z) {
                 if (!cube_contains(nb, shifted)) {
                     shifted.z += cell_size;
                     continue;

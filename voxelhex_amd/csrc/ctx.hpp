@@ -124,7 +124,8 @@ struct vhx_ctx {
     //    lone frame's critical path.
     bool adaptive = true;
     Sched sched_busy = {{24u, 72u, 216u, 648u}, 5u, {12u}, 3u, VHX_QORDER_BUSY, 0u, 0u};
-    Sched sched_idle = {{64u}, 2u, {0u}, 8u, VHX_QORDER_IDLE, 0u, 1u};
+    // lead blocks off in both: measured slower for a lone frame (1.66-1.79 against 1.21 ms)
+    Sched sched_idle = {{64u}, 2u, {0u}, 8u, VHX_QORDER_IDLE, 0u, 0u};
     int last_sched = -1;  // the schedule of the last trace: 1 busy, 0 idle, -1 fixed (vhx_get_pass_budgets)
     // the schedule in force (the selected one, or the fixed one)
     uint32_t budgets[VHX_MAX_BUDGETS] = {24u, 72u, 216u, 648u};

@@ -23,6 +23,8 @@
 // (BoxTree::changes, the update trigger of BoxTreeGPUHost::new) and re-uploaded by handle_tree_updates
 // (streaming/mod.rs:35-286) at the start of the next upload frames, before the regular upload queue.
 #include <algorithm>
+#include <atomic>
+#include <thread>
 #include <array>
 #include <cmath>
 #include <cstdint>
@@ -114,7 +116,31 @@ struct vhx_stream {
     std::unordered_map<uint64_t, size_t> brick_by_owner;
     std::unordered_map<size_t, size_t> meta_by_key, key_by_meta;
     std::unordered_map<size_t, std::pair<size_t, uint8_t>> node_index_vs_parent;
-    std::unordered_set<size_t> nodes_to_see;
+    // nodes_to_see (upload_queue.rs: a HashSet of node keys): a set over the pool's dense keys, stamped by generation so
+    // that the per-rebuild clear is O(1); membership and size are what the queue logic reads (no iteration order)
+    struct KeySet {
+        std::vector<uint32_t> stamp;
+        std::vector<size_t> members;
+        uint32_t gen = 1;
+        void clear() {
+            members.clear();
+            if (++gen == 0) {  // wrapped: reset every stamp once
+                std::fill(stamp.begin(), stamp.end(), 0u);
+                gen = 1;
+            }
+        }
+        void insert(size_t k) {
+            if (k >= stamp.size()) stamp.resize(std::max<size_t>(k + 1, stamp.size() * 2), 0u);
+            if (stamp[k] != gen) {
+                stamp[k] = gen;
+                members.push_back(k);
+            }
+        }
+        size_t count(size_t k) const { return k < stamp.size() && stamp[k] == gen ? 1u : 0u; }
+        size_t size() const { return members.size(); }
+        std::vector<size_t>::const_iterator begin() const { return members.begin(); }
+        std::vector<size_t>::const_iterator end() const { return members.end(); }
+    } nodes_to_see;
     // UploadQueueStatus
     std::vector<StackItem> target_node_stack;
     std::vector<Owned> bricks_to_upload;
@@ -126,6 +152,19 @@ struct vhx_stream {
     bool reload = true, resize = false, device_valid = false;
     Cube brick_slot{f3(0.f, 0.f, 0.f), 0.f};
     bool brick_slot_set = false;
+    // A viewport move's upload-queue rebuild (upload_queue.rs:60-142) is deferred to the next upload that reads the queue
+    // and coalesced, the latest request winning: the reference runs it as a background task and keeps only the newest
+    // pending request (bevy/mod.rs:110-155, upload_queue.rs:262-289), so several moves between two uploads (a renderer
+    // keeping K frames in flight on one tree version, vhx_stream_upload_frames) cost one rebuild instead of K.
+    bool rebuild_pending = false;
+    F3 pending_origin{0.f, 0.f, 0.f};
+    float pending_distance = 0.f;
+    void apply_pending_rebuild() {
+        if (!rebuild_pending) return;
+        rebuild_pending = false;
+        rebuild(pending_origin, pending_distance);
+        target_node_stack = node_stack_init();
+    }
     // statistics of the last upload
     uint64_t last_nodes = 0, last_bricks = 0, last_bytes = 0;
     // completion tracking over the cyclic node walk: new work (node adds, brick requests) found in the current and
@@ -258,23 +297,66 @@ struct vhx_stream {
         nodes_to_see.clear();
         bricks_to_upload.clear();
         reload = true;
+        rebuild_pending = false;  // the reload rebuilds at the current viewport
     }
 
     // --------------------------------------------------------------------------------------------- rebuild
-    void add_children_nodes_to_upload_queue(size_t key, Cube nb, uint32_t mip_level, F3 vc, float dist,
-                                            uint32_t min_mip) {  // upload_queue.rs:144-207
-        if (mip_level < min_mip) return;
-        const float include = dist * std::pow(4.f, (float)mip_level - 1.f);
+    // add_children_nodes_to_upload_queue (upload_queue.rs:144-207): every valid child of a relevant sectant joins the
+    // view set, recursively down to min_mip. The walk only reads the tree, and the view set is a set, so subtrees run on
+    // host threads into lists of their own that are merged afterwards: the same set as the serial walk (a 1024^3 tree at
+    // view distance 256 holds 126 k nodes in view).
+    struct ViewItem {
+        size_t key;
+        Cube nb;
+        uint32_t mip;
+    };
+    template <class F>
+    void view_children(const ViewItem &it, F3 vc, float dist, uint32_t min_mip, F &&visit) const {
+        if (it.mip < min_mip) return;
+        const float include = dist * std::pow(4.f, (float)it.mip - 1.f);
         const F3 c = sub(vc, unit(include / 2.f));
         const U3 cbl{round_u32(c.x), round_u32(c.y), round_u32(c.z)};
-        if (node(key).content != Content::Internal) return;
-        execute_for_relevant_sectants(nb, cbl, as_u32(include), [&](U3, U3, uint8_t cs, const Cube &tb) {
+        if (node(it.key).content != Content::Internal) return;
+        execute_for_relevant_sectants(it.nb, cbl, as_u32(include), [&](U3, U3, uint8_t cs, const Cube &tb) {
             size_t ck;
-            if (valid_child(key, cs, ck)) {
-                nodes_to_see.insert(ck);
-                add_children_nodes_to_upload_queue(ck, tb, mip_level - 1, vc, dist, min_mip);
-            }
+            if (valid_child(it.key, cs, ck)) visit(ViewItem{ck, tb, it.mip - 1});
         });
+    }
+    void view_subtree(const ViewItem &it, F3 vc, float dist, uint32_t min_mip, std::vector<size_t> &out) const {
+        view_children(it, vc, dist, min_mip, [&](const ViewItem &ch) {
+            out.push_back(ch.key);
+            view_subtree(ch, vc, dist, min_mip, out);
+        });
+    }
+    void add_children_nodes_to_upload_queue(size_t key, Cube nb, uint32_t mip_level, F3 vc, float dist,
+                                            uint32_t min_mip) {
+        // breadth-first until there are enough subtrees to share out (each level's children join the set here)
+        std::vector<ViewItem> front{ViewItem{key, nb, mip_level}}, next;
+        for (int level = 0; level < 2 && !front.empty() && front.size() < 64; ++level) {
+            next.clear();
+            for (const ViewItem &it : front)
+                view_children(it, vc, dist, min_mip, [&](const ViewItem &ch) {
+                    nodes_to_see.insert(ch.key);
+                    next.push_back(ch);
+                });
+            front.swap(next);
+        }
+        const unsigned nt = (unsigned)std::min<size_t>(
+            front.size(), std::max(1u, std::min(16u, std::thread::hardware_concurrency())));
+        std::vector<std::vector<size_t>> lists(front.size());
+        std::atomic<size_t> at{0};
+        auto work = [&]() {
+            for (size_t i; (i = at.fetch_add(1)) < front.size();) view_subtree(front[i], vc, dist, min_mip, lists[i]);
+        };
+        if (nt <= 1) {
+            work();
+        } else {
+            std::vector<std::thread> pool;
+            for (unsigned k = 0; k < nt; ++k) pool.emplace_back(work);
+            for (auto &th : pool) th.join();
+        }
+        for (const auto &l : lists)
+            for (size_t k : l) nodes_to_see.insert(k);
     }
     void rebuild(F3 center_, float dist) {  // upload_queue.rs:60-142
         nodes_to_see.clear();
@@ -620,6 +702,7 @@ struct vhx_stream {
     // returns false when the view ran out of capacity (re_evaluate_view_size was applied)
     bool process(std::vector<CacheUpdate> &updates) {  // upload_queue.rs:218-404
         if (reload) {
+            rebuild_pending = false;  // superseded: the reload rebuilds at the current viewport
             rebuild(origin, view_distance);
             target_node_stack = node_stack_init();
             reload = false;
@@ -876,6 +959,7 @@ struct vhx_stream {
     int collect_frame() {  // streaming/mod.rs:420-635
         last_nodes = last_bricks = last_bytes = 0;
         if (resize) return VHX_E_CAPACITY;
+        apply_pending_rebuild();
         std::vector<CacheUpdate> updates;
         // streaming::upload (streaming/mod.rs:446-457): a reloading view runs the upload queue; otherwise queued tree
         // changes go first, and the upload queue runs in a frame without any
@@ -997,8 +1081,9 @@ int vhx_stream_set_viewport(vhx_stream *s, const float origin[3], float view_dis
     s->view_distance = view_distance;
     if (moved) {  // bevy/mod.rs:110-155: a rebuild only when the origin leaves its brick slot
         s->upload_range = Cube{sub(o, unit(view_distance / 2.f)), view_distance};
-        s->rebuild(o, view_distance);
-        s->target_node_stack = s->node_stack_init();
+        s->rebuild_pending = true;  // run by the next upload (apply_pending_rebuild)
+        s->pending_origin = o;
+        s->pending_distance = view_distance;
         const float bd = (float)s->tree->brick_dim;  // Cube::brick_slot_for, spatial/raytracing/mod.rs:65-70
         s->brick_slot = Cube{f3(o.x - std::fabs(std::fmod(o.x, bd)), o.y - std::fabs(std::fmod(o.y, bd)),
                                 o.z - std::fabs(std::fmod(o.z, bd))),
