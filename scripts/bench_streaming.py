@@ -94,7 +94,7 @@ if args.inflight <= 1:
     print(f"{frames} frames, {resizes} resizes, bytes written per frame median {int(np.median(written))} max {max(written)}")
     print(f"producer host ms (vhx_stream_upload): {q(host)}")
     print(f"ranged writes device ms (update batch on the stream): {q(dev)}")
-    print(f"trace 1920x1080 of the view ms: {q(trace)}")
+    print(f"trace {WD}x{HT} of the view ms: {q(trace)}")
 else:
     F = args.inflight
     ctxs = [rt] + [rt.shared() for _ in range(F - 1)]
