@@ -596,6 +596,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step(True)
+    submit_s = time.perf_counter() - t0  # host time to submit the K steps (the GPU runs behind it)
     drain()  # the last frame's gather and untile are inside the timed region
     if world > 1:
         dist.barrier()
@@ -831,6 +832,7 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": "f32",
             "frames_in_flight": F, "gpu_max_hw_queues": queues,
+            "host_submit_ms_per_step": round(submit_s * 1e3 / args.steps, 4),
             "pass_budgets": args.budgets if args.budgets is not None else ("one pass" if args.mip_lod is not None
                                                                            else "library default (adaptive)"),
             "schedule": None if sched_timed is None else {

@@ -308,7 +308,10 @@ SCHEDULER_TUNES = ["resume=0",                        # abandoned rays re-traced
                    "qorder=16",                       # pass-0 queue in 16x16 tile order
                    "qorder=m8",                       # ... in Morton order of 8x8 tiles
                    "qorder=m32z",                     # ... every pixel in Morton order
-                   "qorder=32r"]                      # ... 32x32 tiles by rows
+                   "qorder=32r",                      # ... 32x32 tiles by rows
+                   "qsort=0",                         # queue passes without the segment node sort
+                   "qsort=256;rpw=0,0;tw=7",          # short sorted segments, few adaptive waves
+                   "qsort=2048;resume=0"]             # the longest segments; re-traced rays (no state: no sort)
 
 
 @pytest.mark.parametrize("tune", SCHEDULER_TUNES)

@@ -58,7 +58,7 @@ def test_set_tuning_validates_and_applies():
         rt.set_tuning("budgets=16,128;qorder=32r")
         assert rt.pass_budgets() == ((16, 128), "fixed")
         for bad in ("nokey=1", "budgets=3,2", "qblock=100", "qorder=12", "rpw=65", "split_tune=3,2,1,1", "adaptive",
-                    "budgets=1;bogus=2", "sparse=1,x"):
+                    "budgets=1;bogus=2", "sparse=1,x", "qsort=100", "qsort=4096", "qsort=768"):
             with pytest.raises(Exception):
                 rt.set_tuning(bad)
             assert rt.pass_budgets() == ((16, 128), "fixed"), bad  # a refused spec changes nothing

@@ -55,6 +55,14 @@ struct TreeStore {
 // (its critical path is its slowest chunk, and 2-D clusters gather the longest rays into fewer, longer chunks).
 #define VHX_QORDER_BUSY 38u
 #define VHX_QORDER_IDLE 0u
+// Queue passes of the frames-in-flight schedule: every segment of VHX_QSORT_BUSY consecutive queue entries sorted by the
+// node each ray's saved state stands at (k_sort_segments in vhx_device.hip), so that a wave's rays start
+// at the same node; 0 = off. Off by default: 2-7 % fewer VALU instructions per frame, but no faster (0.527-0.564 against
+// 0.526-0.536 ms per bench frame over five sort variants, profiles/r04/qsort/); tune "qsort=N" turns it on
+#ifndef VHX_QSORT_BUSY
+#define VHX_QSORT_BUSY 0u
+#endif
+#define VHX_QSORT_MAX 2048u
 
 struct vhx_ctx {
     int device = 0;
@@ -106,6 +114,7 @@ struct vhx_ctx {
         uint32_t qorder;                     // order of a primary frame's pass-0 queue (vhx_ctx::qorder below)
         uint32_t split;                      // the unbounded last pass shares its tail rays out (k_trace_queue_split)
         uint32_t lead;                       // lead blocks: predicted-long blocks first, traced to the end in pass 0
+        uint32_t qsort;                      // queue passes: segments of this many queue entries sorted by saved node
     };
     // Adaptive scheduling (default; vhx_set_pass_budgets or an environment knob fixes the schedule instead): at each
     // trace the context looks at the other contexts of its tree (vhx_create_shared) and picks
@@ -123,9 +132,9 @@ struct vhx_ctx {
     //    three-budget ladders 1.31-1.51 ms, fewer rays per wave in a last pass no better): every extra pass lengthens a
     //    lone frame's critical path.
     bool adaptive = true;
-    Sched sched_busy = {{24u, 72u, 216u, 648u}, 5u, {12u}, 3u, VHX_QORDER_BUSY, 0u, 0u};
+    Sched sched_busy = {{24u, 72u, 216u, 648u}, 5u, {12u}, 3u, VHX_QORDER_BUSY, 0u, 0u, VHX_QSORT_BUSY};
     // lead blocks off in both: measured slower for a lone frame (1.66-1.79 against 1.21 ms)
-    Sched sched_idle = {{64u}, 2u, {0u}, 8u, VHX_QORDER_IDLE, 0u, 0u};
+    Sched sched_idle = {{64u}, 2u, {0u}, 8u, VHX_QORDER_IDLE, 0u, 0u, 0u};
     int last_sched = -1;  // the schedule of the last trace: 1 busy, 0 idle, -1 fixed (vhx_get_pass_budgets)
     // the schedule in force (the selected one, or the fixed one)
     uint32_t budgets[VHX_MAX_BUDGETS] = {24u, 72u, 216u, 648u};
@@ -177,6 +186,11 @@ struct vhx_ctx {
     // ^ 1] belongs to (0: none yet), and the cost buffer of the running trace (its queue passes record into it)
     uint32_t lead = 0;
     int lead_force = -1;
+    // segment node sort of the queue passes (Sched::qsort): in force for this trace; tune "qsort=N" forces it (-1: not)
+    uint32_t qsort = 0;
+    int qsort_force = -1;
+    uint32_t qsort_passes = 0xFEu;   // bit p: the queue of pass p is sorted (tune "qsortp")
+    uint32_t qsort_blocks = 2048u;   // workgroups of a sort launch, striding over the segments (tune "qsortb")
     uint32_t lead_min = 512;
     uint32_t lead_cap = 0;  // at most about this many lead blocks (0 = no cap; tune "lead_cap")
     DevBuf lead_cost[2], lead_perm;

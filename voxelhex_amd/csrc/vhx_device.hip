@@ -477,6 +477,49 @@ __global__ void __launch_bounds__(256) k_gather_chunks(const uint32_t *__restric
     }
 }
 
+// Segment node sort of a queue pass's input: every segment of `seg` consecutive entries (a power of two
+// <= VHX_QSORT_MAX) is reordered by the node each ray's saved state stands at (the NodeStack top, state word 12), ties
+// in queue order, so that a wave's 64 rays start their first node iteration together and at the same node loads, while
+// the segments keep the queue's 2-D order. Bitonic sort of {node, position} keys in LDS; the queue length is read on the
+// device, and the workgroups stride over its segments. Only the order of the queue changes, never a result.
+#define QSORT_THREADS 256u
+__global__ void __launch_bounds__(QSORT_THREADS) k_sort_segments(uint32_t *__restrict__ q, const uint32_t *n_ptr,
+                                                                 const uint32_t *__restrict__ state, uint32_t seg) {
+    __shared__ unsigned long long key[VHX_QSORT_MAX];
+    __shared__ uint32_t val[VHX_QSORT_MAX];
+    const uint32_t n = *n_ptr, t = threadIdx.x;
+    for (uint64_t base = (uint64_t)blockIdx.x * seg; base < n; base += (uint64_t)gridDim.x * seg) {
+        const uint32_t cnt = (uint32_t)min<uint64_t>(seg, n - base);
+        for (uint32_t i = t; i < seg; i += QSORT_THREADS) {
+            uint32_t v = 0;
+            unsigned long long k = ~0ull;  // past the queue's end: sorts last, never written back
+            if (i < cnt) {
+                v = q[base + i];
+                k = ((unsigned long long)state[16ull * v + 12u] << 32) | i;
+            }
+            key[i] = k;
+            val[i] = v;
+        }
+        __syncthreads();
+        for (uint32_t k = 2; k <= seg; k <<= 1)
+            for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+                for (uint32_t i = t; i < seg; i += QSORT_THREADS) {
+                    const uint32_t l = i ^ j;
+                    if (l > i) {
+                        const unsigned long long a = key[i], b = key[l];
+                        if ((a > b) == ((i & k) == 0u)) {
+                            key[i] = b;
+                            key[l] = a;
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+        for (uint32_t i = t; i < cnt; i += QSORT_THREADS) q[base + i] = val[(uint32_t)key[i]];
+        __syncthreads();
+    }
+}
+
 // Where a queued output index comes from: a primary-ray frame (framebuffer or tile layout) or an explicit ray batch.
 struct RaySrc {
     uint32_t kind;  // 0 framebuffer, 1 tiles, 2 explicit rays, 3 shadow rays from hit records
@@ -1430,6 +1473,7 @@ static void select_schedule(vhx_ctx *c) {
         c->last_sched = -1;
         c->split = c->split_force > 0 ? 1u : 0u;
         c->lead = c->lead_force > 0 ? 1u : 0u;
+        c->qsort = c->qsort_force >= 0 ? (uint32_t)c->qsort_force : c->sched_busy.qsort;  // a fixed schedule: the busy one's
         return;
     }
     bool busy = false;
@@ -1449,6 +1493,7 @@ static void select_schedule(vhx_ctx *c) {
     c->qorder = s.qorder;
     c->split = c->split_force >= 0 ? (uint32_t)c->split_force : s.split;
     c->lead = c->lead_force >= 0 ? (uint32_t)c->lead_force : s.lead;
+    c->qsort = c->qsort_force >= 0 ? (uint32_t)c->qsort_force : s.qsort;
     c->last_sched = busy ? 1 : 0;
 }
 
@@ -1549,6 +1594,19 @@ static int compact_chunks(vhx_ctx *c, uint32_t nchunks_host, const uint32_t *n_i
     return VHX_OK;
 }
 
+// k_sort_segments over the queue of pass p (its length at *n_dev, at most nmax entries) when the schedule sorts and the
+// rays of that pass resume from saved state (the node is read there)
+static int sort_segments(vhx_ctx *c, uint32_t p, uint32_t npass, uint32_t *queue, const uint32_t *n_dev, uint64_t nmax) {
+    const PassQ q = pass_q(c, p, npass);
+    if (!c->qsort || !q.resume || !q.state || p >= 32u || !((c->qsort_passes >> p) & 1u)) return VHX_OK;
+    const uint64_t segs = (nmax + c->qsort - 1) / c->qsort;
+    const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(segs, c->qsort_blocks));
+    k_sort_segments<<<grid, QSORT_THREADS, 0, c->stream>>>(queue, n_dev, (const uint32_t *)q.state, c->qsort);
+    VHX_HIP(c, hipGetLastError());
+    debug_passes(c, "sorted segments");
+    return VHX_OK;
+}
+
 // The FlagOrder of code `qorder` for a W x H framebuffer frame (W = 0 or qorder = 0: output-index order) and the
 // number of positions its compaction scans (npos: in / out)
 static FlagOrder flag_order(uint32_t qorder, uint32_t W, uint32_t H, uint64_t &npos) {
@@ -1588,6 +1646,7 @@ static int launch_queue_passes(vhx_ctx *c, const DevTree &t, const CamD &cam, co
             k_emit_flags<false><<<nb, 256, 0, c->stream>>>(flags, npos, offsets, (uint32_t *)c->queue[0].ptr, ord);
             VHX_HIP(c, hipGetLastError());
             debug_passes(c, "compacted flags");
+            if ((rc = sort_segments(c, 1, npass, (uint32_t *)c->queue[0].ptr, ctl, nout))) return rc;
         } else {
             rc = compact_chunks(c, (uint32_t)nblocks0, nullptr, 256, 256, (uint32_t *)c->queue[0].ptr, ctl, nblocks0);
         }
@@ -1646,9 +1705,11 @@ static int launch_queue_passes(vhx_ctx *c, const DevTree &t, const CamD &cam, co
             k_trace_queue<COUNT, BD, MIP><<<qgrid, c->qblock, 0, c->stream>>>(t, qa, in, in_n,
                                                                              ctl + 16u + QCTL_PASS_WORDS * p, q);
         debug_passes(c, "queue pass");
-        if (p + 1 < npass)
+        if (p + 1 < npass) {
             rc = compact_chunks(c, 0, in_n, q.rpw, q.rpw, (uint32_t *)c->queue[p & 1u].ptr, ctl + p,
                                 q.rpw ? (nout + q.rpw - 1) / q.rpw : nout);
+            if (!rc) rc = sort_segments(c, p + 1, npass, (uint32_t *)c->queue[p & 1u].ptr, ctl + p, nout);
+        }
     }
     return rc;
 }
@@ -1854,6 +1915,15 @@ static int apply_tuning(vhx_ctx *c, const std::string &key, const std::string &v
     } else if (key == "lead") {
         if (!parse_u32(val, x) || x > 1) return bad();
         c->lead_force = (int)x;
+    } else if (key == "qsort") {  // segment length of the queue passes' node sort: 0 = off, else 256 .. VHX_QSORT_MAX
+        if (!parse_u32(val, x) || (x && (x < 256 || x > VHX_QSORT_MAX || (x & (x - 1))))) return bad();
+        c->qsort_force = (int)x;
+    } else if (key == "qsortp") {  // bit mask of the queue passes whose input is sorted
+        if (!parse_u32(val, x)) return bad();
+        c->qsort_passes = x;
+    } else if (key == "qsortb") {
+        if (!parse_u32(val, x) || x == 0) return bad();
+        c->qsort_blocks = x;
     } else if (key == "lead_min") {
         if (!parse_u32(val, x) || x == 0) return bad();
         c->lead_min = x;
@@ -2112,6 +2182,9 @@ void vhx::copy_sched(vhx_ctx *c, const vhx_ctx *owner) {
     c->split_diag = owner->split_diag;
     c->split_max_wait = owner->split_max_wait;
     c->lead_force = owner->lead_force;
+    c->qsort_force = owner->qsort_force;
+    c->qsort_passes = owner->qsort_passes;
+    c->qsort_blocks = owner->qsort_blocks;
     c->lead_min = owner->lead_min;
     c->lead_cap = owner->lead_cap;
     std::memcpy(c->sparse, owner->sparse, sizeof(c->sparse));
