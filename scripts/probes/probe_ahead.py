@@ -1,7 +1,7 @@
 """Lone-frame latency (one frame at a time, synchronised; libvhx's events, like bench.py's `lone`) of the bench frame
-for each vhx_set_tuning spec on the command line (lead blocks), interleaved over REPS rounds so that
+for each vhx_set_tuning spec on the command line (the ahead stream), interleaved over REPS rounds so that
 box drift hits every spec alike; also a lone orbiting frame (the prediction comes from the previous, different view).
-usage: probe_lead.py "lead=0" "lead=1;lead_min=512" ..."""
+usage: probe_ahead.py "ahead=0" "ahead=1;ahead_min=512" ..."""
 import os
 import sys
 

@@ -63,6 +63,10 @@ struct TreeStore {
 #define VHX_QSORT_BUSY 0u
 #endif
 #define VHX_QSORT_MAX 2048u
+// the ahead stream in the lone-frame schedule (tune "ahead=0/1" forces it either way)
+#ifndef VHX_AHEAD_IDLE
+#define VHX_AHEAD_IDLE 0u
+#endif
 
 struct vhx_ctx {
     int device = 0;
@@ -113,7 +117,7 @@ struct vhx_ctx {
         uint32_t queue_waves_per_cu;         // waves of a queue pass per CU
         uint32_t qorder;                     // order of a primary frame's pass-0 queue (vhx_ctx::qorder below)
         uint32_t split;                      // the unbounded last pass shares its tail rays out (k_trace_queue_split)
-        uint32_t lead;                       // lead blocks: predicted-long blocks first, traced to the end in pass 0
+        uint32_t ahead;                      // the ahead stream: a lone frame's predicted-long rays traced first, aside
         uint32_t qsort;                      // queue passes: segments of this many queue entries sorted by saved node
     };
     // Adaptive scheduling (default; vhx_set_pass_budgets or an environment knob fixes the schedule instead): at each
@@ -133,8 +137,7 @@ struct vhx_ctx {
     //    lone frame's critical path.
     bool adaptive = true;
     Sched sched_busy = {{24u, 72u, 216u, 648u}, 5u, {12u}, 3u, VHX_QORDER_BUSY, 0u, 0u, VHX_QSORT_BUSY};
-    // lead blocks off in both: measured slower for a lone frame (1.66-1.79 against 1.21 ms)
-    Sched sched_idle = {{64u}, 2u, {0u}, 8u, VHX_QORDER_IDLE, 0u, 0u, 0u};
+    Sched sched_idle = {{64u}, 2u, {0u}, 8u, VHX_QORDER_IDLE, 0u, VHX_AHEAD_IDLE, 0u};
     int last_sched = -1;  // the schedule of the last trace: 1 busy, 0 idle, -1 fixed (vhx_get_pass_budgets)
     // the schedule in force (the selected one, or the fixed one)
     uint32_t budgets[VHX_MAX_BUDGETS] = {24u, 72u, 216u, 648u};
@@ -180,22 +183,27 @@ struct vhx_ctx {
     uint32_t split_diag = 0;
     uint32_t split_max_wait = 32;
     DevBuf ovf;
-    // lead blocks (k_lead_perm in vhx_device.hip): in force for this trace (the selected schedule's
-    // `lead`; tune "lead=0/1" forces it), the step threshold of a lead block, the per-block cost of the last two frames
-    // (recorded into lead_cost[lead_cur], read from the other), pass 0's block order, the frame size lead_cost[lead_cur
-    // ^ 1] belongs to (0: none yet), and the cost buffer of the running trace (its queue passes record into it)
-    uint32_t lead = 0;
-    int lead_force = -1;
+    // the ahead stream of a lone frame (k_ahead_pick in vhx_device.hip): in force for this trace (the
+    // selected schedule's `ahead`; tune "ahead" forces it), a predicted-long ray's step threshold (ahead_min), the most
+    // rays listed (ahead_cap), rays per wave of the ahead pass (ahead_rpw), the per-pixel step counts the queue passes
+    // record (ahead_cost, of the ahead_w x ahead_h frame last traced with it; 0 x 0: no prediction), the list, the cost
+    // buffer of the running trace, the second stream and the events that fork it off and join it back
+    uint32_t ahead = 0;
+    int ahead_force = -1;
+    uint32_t ahead_min = 256;
+    uint32_t ahead_cap = 16384;
+    uint32_t ahead_rpw = 8;
+    uint32_t ahead_prio = 1;  // the ahead pass's waves at the highest issue priority (s_setprio; tune "ahead_prio")
+    DevBuf ahead_cost, ahead_list;
+    uint32_t ahead_w = 0, ahead_h = 0;
+    uint32_t *ahead_rec = nullptr;
+    hipStream_t aux_stream = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     // segment node sort of the queue passes (Sched::qsort): in force for this trace; tune "qsort=N" forces it (-1: not)
     uint32_t qsort = 0;
     int qsort_force = -1;
     uint32_t qsort_passes = 0xFEu;   // bit p: the queue of pass p is sorted (tune "qsortp")
     uint32_t qsort_blocks = 2048u;   // workgroups of a sort launch, striding over the segments (tune "qsortb")
-    uint32_t lead_min = 512;
-    uint32_t lead_cap = 0;  // at most about this many lead blocks (0 = no cap; tune "lead_cap")
-    DevBuf lead_cost[2], lead_perm;
-    uint32_t lead_cur = 0, lead_w = 0, lead_h = 0;
-    uint32_t *lead_rec = nullptr;
 };
 
 #define VHX_HIP(ctx, call)                                                                                         \

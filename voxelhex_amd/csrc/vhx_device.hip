@@ -236,11 +236,13 @@ struct PassQ {
     uint32_t xcd_group;  // pass 0: XCD-aware block runs (xcd_block), 0 = dispatch order
     uint32_t qxcd;       // queue passes: runs of this many chunks dealt over the 8 XCDs, one counter each (0 = off)
     uint32_t sparse;     // budgeted passes with saved state: abandon a wave's rays once fewer lanes trace (0 = off)
-    // Lead blocks (a lone frame's schedule, LeadQ below): pass 0 takes its 16x16 blocks in the order of lead_perm
-    // (bit 31 = a lead block: traced to the end in pass 0, unbudgeted), and every ray that ends after more than the
-    // pass-0 budget records its step count in lead_cost[its block] (atomicMax), the prediction of the next frame
-    const uint32_t *lead_perm;
-    uint32_t *lead_cost;
+    // The ahead stream of a lone frame: pass 0 skips the pixels whose flag is VHX_FLAG_AHEAD (their
+    // rays are traced on the context's second stream, from the list k_ahead_pick made), and a queue pass that finishes a
+    // framebuffer ray records its step count in cost[idx], the prediction of the next frame
+    const uint8_t *skip;
+    uint32_t *cost;
+    uint32_t in_cap;  // queue passes: at most this many input entries (0: all *in_n of them)
+    uint32_t prio;    // queue passes: the waves' issue priority within their SIMD (s_setprio; 0 = the default)
 };
 
 // Rays per wave of a queue pass over n rays: fixed, or (rpw == 0) as many as spread the pass over about `tw` waves.
@@ -340,7 +342,7 @@ __device__ __forceinline__ uint32_t flag_bits(const void *src, uint64_t i, uint6
         }
     } else {
         for (uint64_t k = i; k < n && k < i + 4; ++k) {
-            const bool f = HITS ? ((const uint32_t *)src)[k] != VHX_EMPTY : ((const uint8_t *)src)[k] != 0;
+            const bool f = HITS ? ((const uint32_t *)src)[k] != VHX_EMPTY : (((const uint8_t *)src)[k] & 1u) != 0;
             if (f) bits |= 1u << (k - i);
         }
     }
@@ -355,7 +357,10 @@ __device__ __forceinline__ uint32_t flag_bits(const void *src, uint64_t i, uint6
 // the tail split's counters (k_trace_queue_split), each on a 256-byte line: reserved overflow slots, taken slots, waves
 // waiting for work, waves holding rays, error word
 #define QCTL_SPLIT (16u + QCTL_PASS_WORDS * (VHX_MAX_BUDGETS + 1u))
-#define QCTL_WORDS (QCTL_SPLIT + 10u * 64u)
+// the ahead stream's list length and grab counter (zeroed by the frame that uses them, never by the compaction, which
+// runs while the ahead pass may still be grabbing)
+#define QCTL_AHEAD (QCTL_SPLIT + 10u * 64u)
+#define QCTL_WORDS (QCTL_AHEAD + 3u * 64u)
 // Order of the pass-0 queue of a primary frame (vhx_ctx::qorder): W = 0 keeps output-index order (row-major in the
 // framebuffer layout); W > 0 lists the rays tile by tile -- TS x TS pixel tiles (TS = 1 << tsl >= 8), the tiles
 // row-major over the frame (tx per row) or, with mdim > 0, in Morton order over a 2^mdim x 2^mdim grid (tiles outside
@@ -408,7 +413,8 @@ __device__ __forceinline__ uint32_t order_bits(const void *src, const FlagOrder 
         uint32_t px, py;
         if (!order_pixel(o, k + j, px, py)) continue;
         const uint64_t i = (uint64_t)py * o.W + px;
-        if (HITS ? ((const uint32_t *)src)[i] != VHX_EMPTY : ((const uint8_t *)src)[i] != 0) bits |= 1u << j;
+        // a pass-0 flag byte: bit 0 = abandoned (VHX_FLAG_AHEAD pixels are traced elsewhere)
+        if (HITS ? ((const uint32_t *)src)[i] != VHX_EMPTY : (((const uint8_t *)src)[i] & 1u) != 0) bits |= 1u << j;
     }
     return bits;
 }
@@ -423,7 +429,7 @@ __global__ void __launch_bounds__(256) k_count_flags(const void *__restrict__ sr
                                                      uint64_t nclear = 0) {
     __shared__ uint32_t s_cnt[4];
     if (blockIdx.x == 0)
-        for (uint32_t w = threadIdx.x; w < QCTL_WORDS - 16u; w += blockDim.x) zero[w] = 0u;
+        for (uint32_t w = threadIdx.x; w < QCTL_AHEAD - 16u; w += blockDim.x) zero[w] = 0u;
     const uint64_t i = ((uint64_t)blockIdx.x * 256u + threadIdx.x) * 4u;
     if (clear)
         for (uint64_t k = i; k < nclear && k < i + 4u; ++k) clear[k] = 0u;
@@ -573,65 +579,62 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t bid, uint32_t n, uint32_t
     return ((k / G) * 8u + x) * G + k % G;
 }
 
-// Lead blocks of a lone frame. A lone frame is latency-bound: its critical path was pass 0 (~0.40 ms)
-// followed by the slowest chunk of the unbounded tail (~0.8 ms), because a long ray waited for the whole of pass 0 before
-// its tail started. The previous frame on the context records per 16x16 block the step count of its longest ray
-// (lead_cost); k_lead_perm turns it into pass 0's block order: the blocks whose longest ray took >= min_cost steps
-// first (the lead blocks, traced to the end in pass 0: their long tails start at once and overlap the rest of pass 0),
-// then the others; each part keeps the XCD-aware runs of xcd_block. It also zeroes the cost buffer this frame records
-// into. Only the order of the work and the pass that traces a ray change: results are bit-identical for any
-// prediction (a ray's traversal is deterministic).
-// inverse of xcd_block: the dispatch index whose block is r
-__device__ __forceinline__ uint32_t xcd_slot(uint32_t r, uint32_t n, uint32_t G) {
-    if (G == 0u) return r;
-    const uint32_t full = n / (8u * G) * (8u * G);
-    if (r >= full) return r;
-    const uint32_t g = r / G, m = r % G, x = g & 7u, k = (g >> 3) * G + m;
-    return k * 8u + x;
+// The ahead stream of a lone frame. A lone frame is latency-bound: its critical path is pass 0
+// (~0.40 ms) followed by the slowest chunk of the unbounded pass (~0.8 ms), because its longest rays wait for all of
+// pass 0 before their tails start. The queue passes of a lone frame record every finished ray's step count (cost);
+// before the next frame's pass 0, k_ahead_pick lists the pixels whose ray took >= min_steps steps in the previous frame
+// (at most cap of them, appended in any order) and marks them VHX_FLAG_AHEAD in the flags pass 0 writes anyway. The
+// context's second stream traces that list from scratch, unbudgeted and a few rays per wave, starting at once, while pass
+// 0 skips those pixels (leaves them marked: not queued, and predicted again) and the rest of the frame runs as before;
+// the frame ends when both streams have. Only which pass and stream trace a ray change: results are bit-identical for
+// any prediction (a ray's traversal is deterministic), and a ray's cost is its traversal's step count wherever it ran.
+#define VHX_FLAG_AHEAD 2u
+// ctl (QCTL_AHEAD): [0] list length, [64] grab counter of the ahead pass, [128 ..] 33 histogram buckets of the
+// candidates' step counts (bucket b: [2^(b-1), 2^b), by the highest set bit)
+__device__ __forceinline__ bool ahead_candidate(uint32_t f, uint32_t cost, uint32_t min_steps) {
+    return (f & 3u) != 0u && cost >= min_steps;  // abandoned in pass 0 (1) or ahead (2) last frame, and long
 }
-#define LEAD_THREADS 1024u
-// cap > 0: at most about cap lead blocks (the threshold is raised to the smallest power of two >= min_cost whose blocks
-// number at most cap), so that the lead blocks leave room for the other blocks in the CUs' workgroup slots
-__global__ void __launch_bounds__(LEAD_THREADS) k_lead_perm(const uint32_t *__restrict__ prev, uint32_t *__restrict__ cur,
-                                                           uint32_t n, uint32_t min_cost, uint32_t cap, uint32_t G,
-                                                           uint32_t *__restrict__ perm) {
-    __shared__ uint32_t s_w[LEAD_THREADS / 64u];
-    __shared__ uint32_t s_hist[33];
-    const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
-    const uint32_t per = (n + LEAD_THREADS - 1u) / LEAD_THREADS, lo = min(n, t * per), hi = min(n, lo + per);
-    if (cap) {
-        if (t < 33u) s_hist[t] = 0u;
-        __syncthreads();
-        for (uint32_t i = lo; i < hi; ++i)  // bucket b: cost in [2^(b-1), 2^b), bucket 0: cost 0
-            if (prev[i] >= min_cost) atomicAdd(&s_hist[32u - __clz(prev[i])], 1u);
-        __syncthreads();
-        // the smallest bucket edge e (a power of two) with at most cap blocks at or above it
-        uint32_t above = 0, b = 33u;
-        while (b > 1u && above + s_hist[b - 1u] <= cap) above += s_hist[--b];
-        const uint32_t edge = b >= 33u ? 0xFFFFFFFFu : (b == 0u ? 0u : 1u << (b - 1u));
-        min_cost = max(min_cost, edge);
-        __syncthreads();
-    }
-    uint32_t cnt = 0;
-    for (uint32_t i = lo; i < hi; ++i) cnt += prev[i] >= min_cost ? 1u : 0u;
-    // exclusive scan of the per-thread counts: waves, then the waves' totals
-    const uint32_t inc = wave_incl_scan(cnt, lane);
-    if (lane == 63u) s_w[wave] = inc;
+__global__ void __launch_bounds__(256) k_ahead_hist(const uint8_t *__restrict__ flags, const uint32_t *__restrict__ cost,
+                                                    uint64_t n, uint32_t min_steps, uint32_t *__restrict__ ctl) {
+    __shared__ uint32_t s_h[33];
+    if (threadIdx.x < 33u) s_h[threadIdx.x] = 0u;
     __syncthreads();
-    uint32_t before = 0, nh = 0;
-    for (uint32_t w = 0; w < LEAD_THREADS / 64u; ++w) {
-        before += w < wave ? s_w[w] : 0u;
-        nh += s_w[w];
+    const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    if (i < n && ahead_candidate(flags[i], cost[i], min_steps)) atomicAdd(&s_h[32u - __clz(cost[i])], 1u);
+    __syncthreads();
+    if (threadIdx.x < 33u && s_h[threadIdx.x]) atomicAdd(ctl + 128u + threadIdx.x, s_h[threadIdx.x]);
+}
+// Lists the candidates whose step count is at or above the smallest power-of-two edge (>= min_steps) with at most cap
+// candidates at or above it: the longest rays, whatever the order of the appends; marks them, unmarks the others.
+__global__ void __launch_bounds__(256) k_ahead_pick(uint8_t *__restrict__ flags, const uint32_t *__restrict__ cost,
+                                                    uint64_t n, uint32_t min_steps, uint32_t cap,
+                                                    uint32_t *__restrict__ list, uint32_t *__restrict__ ctl) {
+    __shared__ uint32_t s_edge;
+    if (threadIdx.x == 0) {
+        uint32_t above = 0, b = 33u;
+        while (b > 1u && above + ctl[128u + b - 1u] <= cap) above += ctl[128u + --b];
+        s_edge = max(min_steps, b >= 33u ? 0xFFFFFFFFu : (b <= 1u ? 0u : 1u << (b - 1u)));
     }
-    uint32_t h = before + inc - cnt;  // lead blocks before lo
-    uint32_t l = lo - h;              // other blocks before lo
-    for (uint32_t i = lo; i < hi; ++i) {
-        if (prev[i] >= min_cost)
-            perm[xcd_slot(h++, nh, G)] = i | 0x80000000u;
-        else
-            perm[nh + xcd_slot(l++, n - nh, G)] = i;
-        cur[i] = 0u;
+    __syncthreads();
+    const uint32_t edge = s_edge;
+    const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t f = 0;
+    bool want = false;
+    if (i < n) {
+        f = flags[i];
+        want = ahead_candidate(f, cost[i], edge);
     }
+    const uint64_t m = __ballot(want);
+    const uint32_t first = (uint32_t)__builtin_ctzll(m | (1ull << 63));
+    uint32_t base = 0;
+    if (lane == first && m) base = atomicAdd(ctl, (uint32_t)__popcll(m));
+    base = __shfl(base, (int)first);
+    const uint32_t slot = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+    const bool ahead = want && slot < cap;
+    if (ahead) list[slot] = (uint32_t)i;
+    if (i < n && (ahead ? f != VHX_FLAG_AHEAD : f == VHX_FLAG_AHEAD))
+        flags[i] = ahead ? (uint8_t)VHX_FLAG_AHEAD : (uint8_t)0;  // pass 0 traces every pixel not marked
 }
 
 // occupancy of the traversal kernels (waves per SIMD the register allocation must allow; 0 = the compiler's choice).
@@ -686,13 +689,7 @@ __global__ void __launch_bounds__(256) VHX_PRIMARY_ATTR k_trace_primary(DevTree 
     __shared__ uint64_t occ_tab[OCC_TAB_WORDS];
     fill_occ_tab(occ_tab, t);
     __syncthreads();
-    uint32_t bid = xcd_block(blockIdx.x, gridDim.x, q.xcd_group);
-    bool lead = false;  // workgroup-uniform
-    if (q.lead_perm) {
-        const uint32_t e = q.lead_perm[blockIdx.x];
-        bid = e & 0x7FFFFFFFu;
-        lead = (e >> 31) != 0u;
-    }
+    const uint32_t bid = xcd_block(blockIdx.x, gridDim.x, q.xcd_group);
     const uint32_t j = bid / blocks_per_tile;  // j-th tile of this rank
     const uint32_t sb = bid - j * blocks_per_tile;
     const uint32_t tile = tile_start + j * tile_stride;
@@ -712,31 +709,26 @@ __global__ void __launch_bounds__(256) VHX_PRIMARY_ATTR k_trace_primary(DevTree 
     const uint64_t idx = layout == VHX_LAYOUT_FRAMEBUFFER ? (uint64_t)py * cam.width + px
                                                           : (uint64_t)j * T * T + (uint64_t)ly * T + lx;
     bool done = true;
-    uint32_t steps = 0;
-    if (valid) {
+    // a pixel of the ahead list (its ray traced on the context's second stream) keeps its mark and is not traced here
+    const bool ahead = q.skip && valid && q.skip[idx] == VHX_FLAG_AHEAD;
+    if (valid && !ahead) {
         F3d o, d;
         primary_ray(cam, px, py, o, d);
         HitOut h;
         h.bytes = 0;
         const float start = FAST ? prepass_start(fast, px, py) : 0.0f;
-        // a lead block's rays run to the end here (started first, their long tails overlap the rest of pass 0)
-        done = get_by_ray<COUNT, BD, FAST, MIP>(t, occ_tab, o, d, h, lead ? VHX_MAX_ITERS : q.budget,
-                                                lead ? nullptr : q.state, (uint32_t)idx, false, start,
-                                                lead ? 0u : q.sparse);
+        done = get_by_ray<COUNT, BD, FAST, MIP>(t, occ_tab, o, d, h, q.budget, q.state, (uint32_t)idx, false, start,
+                                                q.sparse);
         if (done)
             store(t, out, idx, o, h);
         else if (COUNT && q.state)
             out.bytes[idx] = h.bytes;  // the running count, continued by the pass that resumes the ray
-        steps = done ? h.iters : 0u;
-    }
-    if (lead && q.lead_cost) {  // the block's longest ray (wave maximum, one atomic per wave)
-        for (uint32_t dd = 32; dd > 0; dd >>= 1) steps = max(steps, (uint32_t)__shfl_xor((int)steps, (int)dd));
-        if ((threadIdx.x & 63u) == 0u) atomicMax(q.lead_cost + bid, steps);
     }
     // every entry of the output gets its flag, so the flags need no clearing between frames: in the tile layout
     // every in-tile entry (frame padding included, done = true there); in the framebuffer layout only pixels of the
     // frame (a lane past the frame edge has no entry of its own: its idx aliases the next row or runs past the end)
-    if (q.flags && (layout == VHX_LAYOUT_FRAMEBUFFER ? valid : (lx < T && ly < T))) q.flags[idx] = done ? 0 : 1;
+    if (q.flags && (layout == VHX_LAYOUT_FRAMEBUFFER ? valid : (lx < T && ly < T)))
+        q.flags[idx] = ahead ? (uint8_t)VHX_FLAG_AHEAD : (done ? 0 : 1);
 }
 
 template <bool COUNT, int BD, bool MIP = false>
@@ -789,7 +781,9 @@ __global__ void __launch_bounds__(256) VHX_QUEUE_ATTR k_trace_queue(DevTree t, c
     fill_occ_tab(occ_tab, t);
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t n = *in_n;
+    // the ahead pass: its few long rays issue before the waves of the pass 0 they run beside (wave-uniform)
+    if (q.prio) __builtin_amdgcn_s_setprio(3);
+    const uint32_t n = q.in_cap ? min(*in_n, q.in_cap) : *in_n;
     const uint32_t rpw = pass_rpw(q.rpw, q.tw, n);
     // q.qxcd = G > 0: chunk runs of G are dealt round-robin over the XCDs (blockIdx % 8 runs on one XCD and shares
     // its L2), each XCD's waves take its runs in order from their own counter (grab[64 (x + 1)]) and move on to the next
@@ -849,10 +843,7 @@ __global__ void __launch_bounds__(256) VHX_QUEUE_ATTR k_trace_queue(DevTree t, c
                 store_shadow(b->out, idx, h);
             } else {
                 store(t, b->out, idx, o, h);
-                if (q.lead_cost) {  // a whole framebuffer frame in 16x16 blocks (LeadQ): the ray's block
-                    const uint32_t py = idx / b->cam.width, px = idx - py * b->cam.width;
-                    atomicMax(q.lead_cost + (py >> 4) * b->src.tiles_x + (px >> 4), h.iters);
-                }
+                if (q.cost) q.cost[idx] = h.iters;  // a lone framebuffer frame: the next frame's prediction
             }
         }
         if (q.tmp) {  // this chunk's abandoned rays, in lane order
@@ -1472,7 +1463,7 @@ static void select_schedule(vhx_ctx *c) {
     if (!c->adaptive) {
         c->last_sched = -1;
         c->split = c->split_force > 0 ? 1u : 0u;
-        c->lead = c->lead_force > 0 ? 1u : 0u;
+        c->ahead = c->ahead_force > 0 ? 1u : 0u;
         c->qsort = c->qsort_force >= 0 ? (uint32_t)c->qsort_force : c->sched_busy.qsort;  // a fixed schedule: the busy one's
         return;
     }
@@ -1492,7 +1483,7 @@ static void select_schedule(vhx_ctx *c) {
     c->queue_waves = s.queue_waves_per_cu * c->cus;
     c->qorder = s.qorder;
     c->split = c->split_force >= 0 ? (uint32_t)c->split_force : s.split;
-    c->lead = c->lead_force >= 0 ? (uint32_t)c->lead_force : s.lead;
+    c->ahead = c->ahead_force >= 0 ? (uint32_t)c->ahead_force : s.ahead;
     c->qsort = c->qsort_force >= 0 ? (uint32_t)c->qsort_force : s.qsort;
     c->last_sched = busy ? 1 : 0;
 }
@@ -1552,8 +1543,10 @@ static PassQ pass_q(const vhx_ctx *c, uint32_t p, uint32_t npass) {
     q.state = c->resume && npass > 1 && p >= c->save_from ? (uint4 *)c->state.ptr : nullptr;
     q.resume = c->resume && p > c->save_from ? 1u : 0u;
     q.sparse = last || !q.state ? 0u : c->sparse[p];
-    q.lead_perm = nullptr;
-    q.lead_cost = p > 0 ? c->lead_rec : nullptr;
+    q.skip = nullptr;
+    q.cost = p > 0 && last ? c->ahead_rec : nullptr;  // the unbounded pass finishes the rays over the pass-0 budget
+    q.in_cap = 0;
+    q.prio = 0;
     return q;
 }
 
@@ -1624,6 +1617,27 @@ static FlagOrder flag_order(uint32_t qorder, uint32_t W, uint32_t H, uint64_t &n
     return ord;
 }
 
+// The QueueArgs slot of a frame (camera, ray source, outputs) on c's stream. They rarely change between frames: the
+// device copy is rewritten only when they do.
+static int put_qargs(vhx_ctx *c, const CamD &cam, const RaySrc &src, const OutD &o, QueueArgs *&qa) {
+    const uint32_t slot = src.kind == 3u ? 1u : 0u;  // a shadow frame alternates with its primary frame
+    qa = (QueueArgs *)c->qargs.ptr + slot;
+    QueueArgs a;
+    std::memset(&a, 0, sizeof(a));  // padding included, for the comparison
+    a.cam = cam;
+    a.src = src;
+    a.out = o;
+    const uint8_t *ab = (const uint8_t *)&a;
+    if (c->qargs_host_ptr[slot] != c->qargs.ptr || c->qargs_host[slot].size() != sizeof(a) ||
+        std::memcmp(c->qargs_host[slot].data(), ab, sizeof(a)) != 0) {
+        k_put_queue_args<<<1, 64, 0, c->stream>>>(a, qa);
+        VHX_HIP(c, hipGetLastError());
+        c->qargs_host[slot].assign(ab, ab + sizeof(a));
+        c->qargs_host_ptr[slot] = c->qargs.ptr;
+    }
+    return VHX_OK;
+}
+
 // Queue passes first..npass-1: pass p re-traces the queue of pass p-1 (pass 0's queue, for first == 0, is the list
 // in queue[1] with its length in qctl[7]); what exceeds its budget is listed per chunk and compacted into the next
 // pass's queue. For first == 1, pass 0 (a grid kernel of nblocks0 workgroups) has just run and is compacted first.
@@ -1651,24 +1665,8 @@ static int launch_queue_passes(vhx_ctx *c, const DevTree &t, const CamD &cam, co
             rc = compact_chunks(c, (uint32_t)nblocks0, nullptr, 256, 256, (uint32_t *)c->queue[0].ptr, ctl, nblocks0);
         }
     }
-    const uint32_t slot = src.kind == 3u ? 1u : 0u;  // a shadow frame alternates with its primary frame
-    QueueArgs *qa = (QueueArgs *)c->qargs.ptr + slot;
-    if (first < npass) {
-        // camera, ray source and outputs rarely change between frames: the device copy is rewritten only when they do
-        QueueArgs a;
-        std::memset(&a, 0, sizeof(a));  // padding included, for the comparison
-        a.cam = cam;
-        a.src = src;
-        a.out = o;
-        const uint8_t *ab = (const uint8_t *)&a;
-        if (c->qargs_host_ptr[slot] != c->qargs.ptr || c->qargs_host[slot].size() != sizeof(a) ||
-            std::memcmp(c->qargs_host[slot].data(), ab, sizeof(a)) != 0) {
-            k_put_queue_args<<<1, 64, 0, c->stream>>>(a, qa);
-            VHX_HIP(c, hipGetLastError());
-            c->qargs_host[slot].assign(ab, ab + sizeof(a));
-            c->qargs_host_ptr[slot] = c->qargs.ptr;
-        }
-    }
+    QueueArgs *qa = nullptr;
+    if (first < npass && (rc = put_qargs(c, cam, src, o, qa))) return rc;
 #ifdef VHX_PROBE_PASSES  // diagnostic builds only: run the first VHX_PROBE_PASSES passes (the frame is incomplete)
     const uint32_t np_run = std::min<uint32_t>(npass, VHX_PROBE_PASSES);
 #else
@@ -1712,6 +1710,50 @@ static int launch_queue_passes(vhx_ctx *c, const DevTree &t, const CamD &cam, co
         }
     }
     return rc;
+}
+
+// The ahead stream's fork, on c's stream before pass 0: k_ahead_pick lists the previous frame's long
+// rays (their flags marked VHX_FLAG_AHEAD), then the second stream traces them from scratch, unbudgeted, ahead_rpw rays
+// per wave, into the frame's outputs and records their step counts; ev_join marks its end.
+template <int BD>
+static int fork_ahead(vhx_ctx *c, const DevTree &t, const CamD &cam, const RaySrc &src, const OutD &o, uint64_t nout,
+                      bool count) {
+    uint32_t *ctl = (uint32_t *)c->qctl.ptr;
+    VHX_HIP(c, hipMemsetAsync(ctl + QCTL_AHEAD, 0, 3u * 64u * sizeof(uint32_t), c->stream));
+    const unsigned nb = (unsigned)((nout + 255) / 256);
+    k_ahead_hist<<<nb, 256, 0, c->stream>>>((const uint8_t *)c->flags.ptr, (const uint32_t *)c->ahead_cost.ptr, nout,
+                                            c->ahead_min, ctl + QCTL_AHEAD);
+    k_ahead_pick<<<nb, 256, 0, c->stream>>>((uint8_t *)c->flags.ptr, (const uint32_t *)c->ahead_cost.ptr, nout,
+                                            c->ahead_min, c->ahead_cap, (uint32_t *)c->ahead_list.ptr,
+                                            ctl + QCTL_AHEAD);
+    VHX_HIP(c, hipGetLastError());
+    QueueArgs *qa = nullptr;
+    int rc = put_qargs(c, cam, src, o, qa);
+    if (rc) return rc;
+    VHX_HIP(c, hipEventRecord(c->ev_fork, c->stream));
+    VHX_HIP(c, hipStreamWaitEvent(c->aux_stream, c->ev_fork, 0));
+    PassQ q{};
+    q.budget = VHX_MAX_ITERS;
+    q.rpw = c->ahead_rpw;
+    q.tw = c->tw;
+    q.counts = (uint32_t *)c->counts.ptr;  // unused: the unbounded pass lists nothing
+    q.cost = (uint32_t *)c->ahead_cost.ptr;
+    q.in_cap = c->ahead_cap;
+    q.prio = c->ahead_prio;
+    const uint32_t waves = std::min<uint32_t>(2048u, (c->ahead_cap + c->ahead_rpw - 1) / c->ahead_rpw);
+    const unsigned grid = (waves * 64u + 255u) / 256u;
+    const uint32_t *list = (const uint32_t *)c->ahead_list.ptr;
+    if (t.mips)
+        k_trace_queue<false, BD, true><<<grid, 256, 0, c->aux_stream>>>(t, qa, list, ctl + QCTL_AHEAD,
+                                                                        ctl + QCTL_AHEAD + 64u, q);
+    else if (count)
+        k_trace_queue<true, BD><<<grid, 256, 0, c->aux_stream>>>(t, qa, list, ctl + QCTL_AHEAD, ctl + QCTL_AHEAD + 64u, q);
+    else
+        k_trace_queue<false, BD><<<grid, 256, 0, c->aux_stream>>>(t, qa, list, ctl + QCTL_AHEAD, ctl + QCTL_AHEAD + 64u,
+                                                                  q);
+    VHX_HIP(c, hipGetLastError());
+    VHX_HIP(c, hipEventRecord(c->ev_join, c->aux_stream));
+    return VHX_OK;
 }
 
 // ------------------------------------------------------------------------------------------------ C ABI
@@ -1788,8 +1830,8 @@ void vhx_destroy(vhx_ctx *c) {
     c->tree.reset();  // frees the device tree with its last context
     if (c->use_ev) (void)hipEventDestroy(c->use_ev);
     for (DevBuf *b : {&c->scratch, &c->rays, &c->queue[0], &c->queue[1], &c->qctl, &c->tmp, &c->counts, &c->offsets,
-                      &c->flags, &c->qargs, &c->state, &c->upd, &c->prepass_depth, &c->ovf, &c->lead_cost[0],
-                      &c->lead_cost[1], &c->lead_perm})
+                      &c->flags, &c->qargs, &c->state, &c->upd, &c->prepass_depth, &c->ovf, &c->ahead_cost,
+                      &c->ahead_list})
         if (b->ptr) (void)hipFree(b->ptr);
     for (auto &P : c->pinned) {
         if (P.ptr) (void)hipHostFree(P.ptr);
@@ -1798,6 +1840,9 @@ void vhx_destroy(vhx_ctx *c) {
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    if (c->aux_stream) (void)hipStreamDestroy(c->aux_stream);
+    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+    if (c->ev_join) (void)hipEventDestroy(c->ev_join);
     delete c;
 }
 
@@ -1912,9 +1957,9 @@ static int apply_tuning(vhx_ctx *c, const std::string &key, const std::string &v
     } else if (key == "split") {
         if (!parse_u32(val, x) || x > 1) return bad();
         c->split_force = (int)x;
-    } else if (key == "lead") {
+    } else if (key == "ahead") {
         if (!parse_u32(val, x) || x > 1) return bad();
-        c->lead_force = (int)x;
+        c->ahead_force = (int)x;
     } else if (key == "qsort") {  // segment length of the queue passes' node sort: 0 = off, else 256 .. VHX_QSORT_MAX
         if (!parse_u32(val, x) || (x && (x < 256 || x > VHX_QSORT_MAX || (x & (x - 1))))) return bad();
         c->qsort_force = (int)x;
@@ -1924,12 +1969,18 @@ static int apply_tuning(vhx_ctx *c, const std::string &key, const std::string &v
     } else if (key == "qsortb") {
         if (!parse_u32(val, x) || x == 0) return bad();
         c->qsort_blocks = x;
-    } else if (key == "lead_min") {
+    } else if (key == "ahead_min") {
         if (!parse_u32(val, x) || x == 0) return bad();
-        c->lead_min = x;
-    } else if (key == "lead_cap") {
-        if (!parse_u32(val, x)) return bad();
-        c->lead_cap = x;
+        c->ahead_min = x;
+    } else if (key == "ahead_cap") {
+        if (!parse_u32(val, x) || x == 0 || x > (1u << 24)) return bad();
+        c->ahead_cap = x;
+    } else if (key == "ahead_prio") {
+        if (!parse_u32(val, x) || x > 1) return bad();
+        c->ahead_prio = x;
+    } else if (key == "ahead_rpw") {
+        if (!parse_u32(val, x) || x == 0 || x > 64) return bad();
+        c->ahead_rpw = x;
     } else if (key == "split_wait") {
         if (!parse_u32(val, x) || x == 0) return bad();
         c->split_max_wait = x;
@@ -2181,12 +2232,14 @@ void vhx::copy_sched(vhx_ctx *c, const vhx_ctx *owner) {
     c->split_take = owner->split_take;
     c->split_diag = owner->split_diag;
     c->split_max_wait = owner->split_max_wait;
-    c->lead_force = owner->lead_force;
+    c->ahead_force = owner->ahead_force;
     c->qsort_force = owner->qsort_force;
     c->qsort_passes = owner->qsort_passes;
     c->qsort_blocks = owner->qsort_blocks;
-    c->lead_min = owner->lead_min;
-    c->lead_cap = owner->lead_cap;
+    c->ahead_min = owner->ahead_min;
+    c->ahead_cap = owner->ahead_cap;
+    c->ahead_rpw = owner->ahead_rpw;
+    c->ahead_prio = owner->ahead_prio;
     std::memcpy(c->sparse, owner->sparse, sizeof(c->sparse));
     c->prepass = owner->prepass;
     c->prepass_margin = owner->prepass_margin;
@@ -2478,32 +2531,36 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
     if (npass > 1 && layout == VHX_LAYOUT_FRAMEBUFFER && (tile_start > 0 || tile_stride > 1))
         VHX_HIP(c, hipMemsetAsync(c->flags.ptr, 0, nout, c->stream));
 
-    // lead blocks (a whole framebuffer frame of 16x16 blocks under a multi-pass schedule that selects them): pass 0's
-    // block order from the previous frame's per-block cost, this frame's cost recorded for the next
-    const uint32_t *lead_perm = nullptr;
-    uint32_t *lead_rec = nullptr;
-    if (c->lead && npass > 1 && layout == VHX_LAYOUT_FRAMEBUFFER && T == 16 && tile_start == 0 && tile_stride == 1 &&
-        !c->in_prepass) {
-        const uint64_t bytes = nblocks * 4;
-        const bool fresh = c->lead_cost[0].bytes < bytes || c->lead_cost[1].bytes < bytes;
-        if ((rc = ensure(c, c->lead_cost[0], bytes)) || (rc = ensure(c, c->lead_cost[1], bytes)) ||
-            (rc = ensure(c, c->lead_perm, bytes)))
+    // the ahead stream (a lone framebuffer frame under a multi-pass schedule that selects it; not in the approximate
+    // prepass mode, whose rays start elsewhere): the previous frame's long rays listed and traced on the second stream
+    const bool ahead = c->ahead && npass > 1 && layout == VHX_LAYOUT_FRAMEBUFFER && tile_start == 0 && tile_stride == 1 &&
+                       !c->in_prepass && !fast;
+    bool predicted = false;
+    if (ahead) {
+        const bool fresh = c->ahead_cost.bytes < nout * 4;
+        if ((rc = ensure(c, c->ahead_cost, nout * 4)) || (rc = ensure(c, c->ahead_list, (uint64_t)c->ahead_cap * 4)))
             return rc;
-        if (fresh) c->lead_w = c->lead_h = 0;
-        lead_rec = (uint32_t *)c->lead_cost[c->lead_cur].ptr;
-        if (c->lead_w == cam->width && c->lead_h == cam->height) {
-            k_lead_perm<<<1, LEAD_THREADS, 0, c->stream>>>((const uint32_t *)c->lead_cost[c->lead_cur ^ 1u].ptr, lead_rec,
-                                                           (uint32_t)nblocks, c->lead_min, c->lead_cap, c->xcd_group,
-                                                           (uint32_t *)c->lead_perm.ptr);
-            lead_perm = (const uint32_t *)c->lead_perm.ptr;
-        } else {
-            VHX_HIP(c, hipMemsetAsync(lead_rec, 0, bytes, c->stream));
+        if (fresh) c->ahead_w = c->ahead_h = 0;
+        predicted = c->ahead_w == cam->width && c->ahead_h == cam->height;
+        if (!c->aux_stream) {  // the highest stream priority: the ahead pass's workgroups dispatch before pass 0's
+            int lo = 0, hi = 0;
+            VHX_HIP(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
+            VHX_HIP(c, hipStreamCreateWithPriority(&c->aux_stream, hipStreamNonBlocking, hi));
         }
-        c->lead_rec = lead_rec;
-        c->lead_cur ^= 1u;
-        c->lead_w = cam->width;
-        c->lead_h = cam->height;
+        if (!c->ev_fork) VHX_HIP(c, hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
+        if (!c->ev_join) VHX_HIP(c, hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
+        c->ahead_rec = (uint32_t *)c->ahead_cost.ptr;  // this frame's queue passes record the next prediction
     }
+    c->ahead_w = ahead ? cam->width : 0u;  // a frame without it leaves no prediction (its flags mean something else)
+    c->ahead_h = ahead ? cam->height : 0u;
+    // the main stream waits for the ahead pass on every exit after the fork (before the trace's use is recorded)
+    struct JoinGuard {
+        vhx_ctx *c;
+        bool armed = false;
+        ~JoinGuard() {
+            if (armed) (void)hipStreamWaitEvent(c->stream, c->ev_join, 0);
+        }
+    } join{c};
     const bool count = ho.dev.bytes != nullptr;
     int qrc = VHX_OK;
     // the queue order's frame (c->qorder): the framebuffer layout only. The tile layout's output index is already
@@ -2515,8 +2572,11 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
         constexpr int BD = decltype(bd_tag)::value;
         PassQ q0 = pass_q(c, 0, npass);
         if (npass > 1) q0.flags = (uint8_t *)c->flags.ptr;
-        q0.lead_perm = lead_perm;
-        q0.lead_cost = lead_rec;
+        if (predicted) {
+            if ((qrc = fork_ahead<BD>(c, t, cd, src, ho.dev, nout, count))) return;
+            join.armed = true;
+            q0.skip = (const uint8_t *)c->flags.ptr;
+        }
         if (t.mips) {  // MIP stand-ins (no byte counting, no depth prepass: refused above)
             k_trace_primary<false, BD, false, true><<<(unsigned)nblocks, 256, 0, c->stream>>>(
                 t, cd, ho.dev, T, tiles_x, tile_start, tile_stride, layout, bpx, bpt, q0);
@@ -2536,7 +2596,7 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
         }
     };
     const bool bd_ok = dispatch_bd(c->tree->desc.brick_dim, launch);
-    c->lead_rec = nullptr;
+    c->ahead_rec = nullptr;
     if (!bd_ok) return fail(c, VHX_E_INVALID_ARG, "unsupported brick_dim");
     if (qrc) return qrc;
     VHX_HIP(c, hipGetLastError());
@@ -2544,6 +2604,10 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
     // a shadow trace of this frame's hit records lists them in the same tile order (vhx_trace_shadows)
     c->last_fb_w = layout == VHX_LAYOUT_FRAMEBUFFER ? cam->width : 0u;
     c->last_fb_h = layout == VHX_LAYOUT_FRAMEBUFFER ? cam->height : 0u;
+    if (join.armed) {
+        join.armed = false;
+        VHX_HIP(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
+    }
     VHX_HIP(c, hipEventRecord(c->ev1, c->stream));
     c->timed = true;
     if ((rc = tscope.end())) return rc;  // a later write of the tree waits for this frame
