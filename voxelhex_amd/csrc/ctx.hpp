@@ -63,6 +63,10 @@ struct TreeStore {
 #define VHX_QSORT_BUSY 0u
 #endif
 #define VHX_QSORT_MAX 2048u
+// the one-launch frame (k_trace_frame) in the lone-frame schedule (tune "one=0/1" forces it)
+#ifndef VHX_ONE_IDLE
+#define VHX_ONE_IDLE 0u
+#endif
 // the ahead stream in the lone-frame schedule (tune "ahead=0/1" forces it either way)
 #ifndef VHX_AHEAD_IDLE
 #define VHX_AHEAD_IDLE 0u
@@ -119,6 +123,7 @@ struct vhx_ctx {
         uint32_t split;                      // the unbounded last pass shares its tail rays out (k_trace_queue_split)
         uint32_t ahead;                      // the ahead stream: a lone frame's predicted-long rays traced first, aside
         uint32_t qsort;                      // queue passes: segments of this many queue entries sorted by saved node
+        uint32_t one;                        // a framebuffer frame's pass ladder in one persistent launch (k_trace_frame)
     };
     // Adaptive scheduling (default; vhx_set_pass_budgets or an environment knob fixes the schedule instead): at each
     // trace the context looks at the other contexts of its tree (vhx_create_shared) and picks
@@ -136,8 +141,8 @@ struct vhx_ctx {
     //    three-budget ladders 1.31-1.51 ms, fewer rays per wave in a last pass no better): every extra pass lengthens a
     //    lone frame's critical path.
     bool adaptive = true;
-    Sched sched_busy = {{24u, 72u, 216u, 648u}, 5u, {12u}, 3u, VHX_QORDER_BUSY, 0u, 0u, VHX_QSORT_BUSY};
-    Sched sched_idle = {{64u}, 2u, {0u}, 8u, VHX_QORDER_IDLE, 0u, VHX_AHEAD_IDLE, 0u};
+    Sched sched_busy = {{24u, 72u, 216u, 648u}, 5u, {12u}, 3u, VHX_QORDER_BUSY, 0u, 0u, VHX_QSORT_BUSY, 0u};
+    Sched sched_idle = {{64u}, 2u, {0u}, 8u, VHX_QORDER_IDLE, 0u, VHX_AHEAD_IDLE, 0u, VHX_ONE_IDLE};
     int last_sched = -1;  // the schedule of the last trace: 1 busy, 0 idle, -1 fixed (vhx_get_pass_budgets)
     // the schedule in force (the selected one, or the fixed one)
     uint32_t budgets[VHX_MAX_BUDGETS] = {24u, 72u, 216u, 648u};
@@ -199,6 +204,12 @@ struct vhx_ctx {
     uint32_t *ahead_rec = nullptr;
     hipStream_t aux_stream = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    // the one-launch frame (Sched::one): in force for this trace, forced by tune "one" (-1: not), its counters and
+    // queue slots, and the epoch that tags this context's frames in them (never 0: the slots start zeroed)
+    uint32_t one = 0;
+    int one_force = -1;
+    DevBuf fq_ctl, fq_slots;
+    uint32_t fq_epoch = 0;
     // segment node sort of the queue passes (Sched::qsort): in force for this trace; tune "qsort=N" forces it (-1: not)
     uint32_t qsort = 0;
     int qsort_force = -1;

@@ -1142,6 +1142,277 @@ __global__ void __launch_bounds__(256) VHX_QUEUE_ATTR_SPLIT k_trace_queue_split(
     if (registered && lane == 0) atomicSub(nwait, 1u);
 }
 
+// ------------------------------------------------------------------------------------------------ one-launch frame
+// k_trace_frame: a primary framebuffer frame's whole pass ladder in ONE persistent launch, so that no
+// pass waits for the end of the one before it. Every wave loops: it takes a full chunk of 64 rays from the deepest
+// pass queue that has one (the oldest rays first), else an 8x8 pixel tile of pass 0, else -- after a few idle polls --
+// a partial chunk; it traces them to the pass budget and appends the rays it abandons, each with its loop state, to the
+// next pass's queue.
+// Every hand-off stays inside one XCD: the tiles are dealt to the XCDs in runs of FQ_RUN (XCC_ID, read in the kernel),
+// and each XCD has its own counters and queues, so a ray abandoned on an XCD is resumed there. Within one XCD's L2 a
+// hand-off needs no fence and no write-through: the producer stores the slot's 64 B of state with plain stores (they
+// stay in that L2), waits for them (vmcnt(0)), then stores the slot's {output index, frame epoch} word; the consumer
+// polls that word and reads the state with sc1 loads (L2-served, past its CU's L1). The counters are XCD-local atomics
+// (workgroup scope: executed in that L2) read by sc1 loads. (Cross-XCD forms -- agent-scope granules -- measured 30-110
+// ms per frame: every granule a fabric write) A wave leaves when its XCD's tiles are all traced,
+// its queues drained and no wave there traces a budgeted pass (the rays of the unbounded last pass finish where they
+// are); every poll loop is bounded (an error word, which the parity tests would show). Results are the reference's: a
+// ray's traversal is deterministic and its state is handed over whole (Trav::packed / begin_resumed).
+#define VHX_FRAME_PASSES (VHX_MAX_BUDGETS + 1u)
+#define FQ_RUN 16u               // consecutive 8x8 tiles per XCD run
+#define FQ_SLOT 5u               // uint4 per queue slot: the 4 of Trav::packed, then {output index, epoch, 0, 0}
+#define FQ_LINE 64u              // counter stride (256 B: one line each)
+#define FQ_XWORDS (FQ_LINE * (3u + 3u * VHX_FRAME_PASSES))  // one XCD's counters
+#define FQ_WORDS (8u * FQ_XWORDS + FQ_LINE)                  // eight XCDs, then the error word
+#define VHX_FRAME_SPINS (1u << 18)  // idle polls before a wave gives up (sets the error word)
+struct FrameQ {
+    uint32_t *ctl;                      // FQ_WORDS counters, zeroed before the launch
+    uint4 *slots;                       // queues of passes 1 .. npass-1 of every XCD
+    uint64_t capx;                      // slots per (XCD, pass) queue: every ray of the XCD's tiles
+    uint32_t budget[VHX_FRAME_PASSES];  // step budget of pass p (VHX_MAX_ITERS: the last)
+    uint32_t npass, epoch, ntiles, tiles_x, sparse0;
+};
+__global__ void k_put_frameq(FrameQ f, FrameQ *dst) {
+    if (threadIdx.x == 0) *dst = f;
+}
+// an XCD's counters: [0] tile counter, [1] tiles traced, [2] waves started, then res / head / active of each pass
+__device__ __forceinline__ uint32_t *fq_x(const FrameQ &f, uint32_t x, uint32_t k) { return f.ctl + x * FQ_XWORDS + FQ_LINE * k; }
+__device__ __forceinline__ uint32_t *fq_res(const FrameQ &f, uint32_t x, uint32_t p) { return fq_x(f, x, 3u + p); }
+__device__ __forceinline__ uint32_t *fq_head(const FrameQ &f, uint32_t x, uint32_t p) {
+    return fq_x(f, x, 3u + VHX_FRAME_PASSES + p);
+}
+__device__ __forceinline__ uint32_t *fq_active(const FrameQ &f, uint32_t x, uint32_t p) {
+    return fq_x(f, x, 3u + 2u * VHX_FRAME_PASSES + p);
+}
+__device__ __forceinline__ uint32_t *fq_err(const FrameQ &f) { return f.ctl + 8u * FQ_XWORDS; }
+__device__ __forceinline__ uint4 *fq_slot(const FrameQ &f, uint32_t x, uint32_t p, uint32_t slot) {
+    return f.slots + ((uint64_t)(x * (VHX_FRAME_PASSES - 1u) + (p - 1u)) * f.capx + slot) * FQ_SLOT;
+}
+// XCD-local counter atomics: executed in the XCD's L2, which every CU of the XCD shares
+__device__ __forceinline__ uint32_t xadd(uint32_t *p, uint32_t v) {
+    return __hip_atomic_fetch_add((gu32 *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ bool xcas(uint32_t *p, uint32_t &expected, uint32_t desired) {
+    return __hip_atomic_compare_exchange_strong((gu32 *)p, &expected, desired, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ unsigned long long ld2_l2(const void *p) {  // sc1: past this CU's L1, from the XCD's L2
+    return __hip_atomic_load((const gu64 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void fq_publish(uint4 *sl, uint32_t idx, uint32_t epoch, const St4 &st) {
+    sl[0] = st.a;
+    sl[1] = st.b;
+    sl[2] = st.c;
+    sl[3] = st.e;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the state in the XCD's L2 before the word that publishes it
+    sl[4] = make_uint4(idx, epoch, 0u, 0u);
+}
+// polls a slot its producer has reserved until it carries this frame's epoch; false after VHX_FRAME_SPINS polls
+__device__ __forceinline__ bool fq_take(const uint4 *sl, uint32_t epoch, uint32_t &idx, St4 &st) {
+    for (uint32_t spins = 0; spins < VHX_FRAME_SPINS; ++spins) {
+        const unsigned long long w = ld2_l2(sl + 4);
+        if ((uint32_t)(w >> 32) == epoch) {
+            idx = (uint32_t)w;
+            uint32_t v[16];
+#pragma unroll
+            for (uint32_t k = 0; k < 8u; ++k) {
+                const unsigned long long x = ld2_l2((const unsigned long long *)sl + k);
+                v[2 * k] = (uint32_t)x;
+                v[2 * k + 1] = (uint32_t)(x >> 32);
+            }
+            st.a = make_uint4(v[0], v[1], v[2], v[3]);
+            st.b = make_uint4(v[4], v[5], v[6], v[7]);
+            st.c = make_uint4(v[8], v[9], v[10], v[11]);
+            st.e = make_uint4(v[12], v[13], v[14], v[15]);
+            return true;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    return false;
+}
+// One ray of a k_trace_frame work unit, get_by_ray's shape with the state in registers: a fresh ray, or a resumed one
+// from its handed-over state `in`; traced to `budget` (pass 0: with sparse-wave abandonment). false: abandoned, its loop
+// state in `out`; true: finished, h filled.
+template <int BD>
+__device__ __forceinline__ bool trace_unit(const DevTree &t, const uint64_t *occ_tab, F3d o, F3d d, HitOut &h,
+                                           uint32_t budget, uint32_t sparse, bool resumed, const St4 &in, St4 &out) {
+    Trav<false, BD, false> tr;
+    h.iters = 0;
+    if (resumed)
+        tr.begin_resumed(t, o, d, h, in);
+    else if (!tr.begin(t, o, d, h, nullptr, 0, false))
+        return true;
+    for (;;) {
+        tr.step(t, occ_tab, h, budget);
+        if (tr.ex != 0u) break;
+        if (sparse && (uint32_t)__popcll(__ballot(1)) < sparse) {
+            tr.ex = 3u;
+            break;
+        }
+    }
+    if (tr.ex == 3u) {
+        out = tr.packed();
+        return false;
+    }
+    tr.end(t, h, nullptr, 0);
+    return true;
+}
+
+// 4 waves per SIMD (128 VGPRs, a few spills outside the walk loops): the hand-offs' state in and out of registers does
+// not fit the queue kernel's 96 (5 waves: 220 B of scratch per lane)
+template <int BD>
+#ifndef VHX_FRAME_WPE
+#define VHX_FRAME_WPE 4
+#endif
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VHX_FRAME_WPE)))
+k_trace_frame(DevTree t, const QueueArgs *qa, const FrameQ *fq) {
+    __shared__ uint64_t occ_tab[OCC_TAB_WORDS];
+    fill_occ_tab(occ_tab, t);
+    __syncthreads();  // the only barrier: the waves of a workgroup go their own ways from here
+    const uint32_t lane = threadIdx.x & 63u;
+    // the frame's queue description is read through a pointer laundered at each use (FQ_AT): loads of it hoisted to
+    // the kernel's start would be held across the traversal
+#define FQ_AT(f)                   \
+    const FrameQ *f##_p = fq;       \
+    asm volatile("" : "+s"(f##_p)); \
+    const FrameQ &f = *f##_p
+    uint32_t xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    const uint32_t x = xcc & 7u;
+    uint32_t ntx;  // this XCD's tiles: runs x, x + 8, ... of FQ_RUN tiles
+    {
+        FQ_AT(f);
+        const uint32_t runs = (f.ntiles + FQ_RUN - 1u) / FQ_RUN;
+        const uint32_t myruns = runs > x ? (runs - x + 7u) / 8u : 0u;
+        ntx = myruns * FQ_RUN;
+        if (myruns && (runs - 1u) % 8u == x) ntx -= runs * FQ_RUN - f.ntiles;  // the frame's last run is short
+        if (lane == 0) xadd(fq_x(f, x, 2), 1u);
+    }
+    uint32_t idle = 0;
+    bool tiles_left = true;
+    for (;;) {
+        // ---- the next work unit (one lane decides, the wave follows): pass wp, first entry / tile wb, wc rays
+        int32_t wp = -1;
+        uint32_t wb = 0, wc = 0, quit = 0;
+        if (lane == 0) {
+            FQ_AT(f);
+            const uint32_t P = f.npass;
+            const uint32_t want = idle >= 6u ? 1u : (64u >> idle);  // full chunks first, partial ones once idle
+            for (int32_t p = (int32_t)P - 1; p >= 1 && wp < 0; --p) {
+                uint32_t *hp = fq_head(f, x, (uint32_t)p);
+                uint32_t h = (uint32_t)ld2_l2(hp);
+                for (uint32_t tries = 0; tries < 4u; ++tries) {
+                    const uint32_t r = (uint32_t)ld2_l2(fq_res(f, x, (uint32_t)p));
+                    if (r <= h || r - h < want) break;
+                    const uint32_t n = r - h < 64u ? r - h : 64u;
+                    if (xcas(hp, h, h + n)) {
+                        wp = p;
+                        wb = h;
+                        wc = n;
+                        break;
+                    }
+                }
+            }
+            if (wp < 0 && tiles_left) {
+                const uint32_t k = xadd(fq_x(f, x, 0), 1u);
+                if (k < ntx) {
+                    wp = 0;
+                    wb = ((k / FQ_RUN) * 8u + x) * FQ_RUN + k % FQ_RUN;
+                    wc = 64u;
+                } else {
+                    tiles_left = false;
+                }
+            }
+            if (wp > 0) {
+                xadd(fq_active(f, x, (uint32_t)wp), 1u);
+            } else if (wp < 0) {
+                // nothing more can come on this XCD: its tiles traced, its queues drained, no wave in a budgeted
+                // queue pass (the rays of the last pass still tracing append nothing)
+                bool fin = (uint32_t)ld2_l2(fq_x(f, x, 1)) >= ntx;
+                for (uint32_t p = 1; p + 1 < P && fin; ++p) fin = (uint32_t)ld2_l2(fq_active(f, x, p)) == 0u;
+                for (uint32_t p = 1; p < P && fin; ++p)
+                    fin = (uint32_t)ld2_l2(fq_head(f, x, p)) >= (uint32_t)ld2_l2(fq_res(f, x, p));
+                quit = fin ? 1u : 0u;
+            }
+        }
+        wp = (int32_t)__builtin_amdgcn_readfirstlane(__shfl(wp, 0));
+        if (wp < 0) {
+            quit = __builtin_amdgcn_readfirstlane(__shfl(quit, 0));
+            if (quit) break;
+            if (++idle >= VHX_FRAME_SPINS) {
+                FQ_AT(f);
+                if (lane == 0) atomicOr(fq_err(f), 1u);
+                break;
+            }
+            // back off (the idle waves of an XCD poll its counter lines): ~1, then ~4, then ~16 us between polls
+            const uint32_t naps = idle < 4u ? 1u : (idle < 8u ? 4u : 16u);
+            for (uint32_t i = 0; i < naps; ++i) __builtin_amdgcn_s_sleep(32);
+            continue;
+        }
+        idle = 0;
+        wb = __builtin_amdgcn_readfirstlane(__shfl(wb, 0));
+        wc = __builtin_amdgcn_readfirstlane(__shfl(wc, 0));
+        const QueueArgs *a = qa;
+        asm volatile("" : "+s"(a));  // read where used (not held in scalar registers across the traversal)
+        const uint32_t W = a->cam.width, H = a->cam.height;
+        // ---- its rays: a pass-0 tile, or queued rays with their saved state
+        bool have = false;
+        uint32_t idx = 0, px = 0, py = 0;
+        St4 st;
+        if (wp == 0) {
+            FQ_AT(f);
+            px = (wb % f.tiles_x) * 8u + (lane & 7u);
+            py = (wb / f.tiles_x) * 8u + (lane >> 3);
+            have = px < W && py < H;
+            idx = py * W + px;
+        } else if (lane < wc) {
+            FQ_AT(f);
+            have = fq_take(fq_slot(f, x, (uint32_t)wp, wb + lane), f.epoch, idx, st);
+            if (!have) atomicOr(fq_err(f), 2u);  // a reserved slot that never filled: the ray is lost (parity fails)
+            py = idx / W;
+            px = idx - py * W;
+        }
+        // ---- trace to the pass budget; the rays over it go to the next pass's queue (it holds a slot for every ray)
+        F3d o, d;
+        HitOut h;
+        h.bytes = 0;
+        bool fin = true;
+        St4 out;
+        if (have) {
+            primary_ray(a->cam, px, py, o, d);
+            uint32_t budget, sparse;
+            {
+                FQ_AT(g);
+                budget = g.budget[wp];
+                sparse = wp == 0 ? g.sparse0 : 0u;
+            }
+            fin = trace_unit<BD>(t, occ_tab, o, d, h, budget, sparse, wp > 0, st, out);
+        }
+        const uint64_t m = __ballot(!fin);
+        if (m) {
+            const uint32_t first = (uint32_t)__builtin_ctzll(m);
+            uint32_t base = 0;
+            FQ_AT(g);
+            if (lane == first) base = xadd(fq_res(g, x, (uint32_t)wp + 1u), (uint32_t)__popcll(m));
+            base = __shfl(base, (int)first);
+            if (!fin)
+                fq_publish(fq_slot(g, x, (uint32_t)wp + 1u, base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))),
+                           idx, g.epoch, out);
+        }
+        if (have && fin) {
+            const QueueArgs *b = qa;
+            asm volatile("" : "+s"(b));  // the outputs' pointers loaded here, not held across the traversal
+            store(t, b->out, idx, o, h);
+        }
+        if (lane == 0) {
+            FQ_AT(g);
+            // a unit is done once its rays are stored or queued (the publishes above waited for their stores)
+            xadd(wp > 0 ? fq_active(g, x, (uint32_t)wp) : fq_x(g, x, 1), wp > 0 ? 0xFFFFFFFFu : 1u);
+        }
+    }
+#undef FQ_AT
+}
+
 // Scatters rank-gathered tile buffers into framebuffers. Rank r's part of `gathered` holds `planes` planes of
 // tiles_per_rank*T*T words each (plane 0 RGBA8, plane 1 f32 depth bits), rank r traced tiles r, r + ranks, ...
 __global__ void __launch_bounds__(256) k_untile_planes(const uint32_t *__restrict__ gathered, uint32_t planes,
@@ -1465,6 +1736,7 @@ static void select_schedule(vhx_ctx *c) {
         c->split = c->split_force > 0 ? 1u : 0u;
         c->ahead = c->ahead_force > 0 ? 1u : 0u;
         c->qsort = c->qsort_force >= 0 ? (uint32_t)c->qsort_force : c->sched_busy.qsort;  // a fixed schedule: the busy one's
+        c->one = c->one_force > 0 ? 1u : 0u;
         return;
     }
     bool busy = false;
@@ -1485,6 +1757,7 @@ static void select_schedule(vhx_ctx *c) {
     c->split = c->split_force >= 0 ? (uint32_t)c->split_force : s.split;
     c->ahead = c->ahead_force >= 0 ? (uint32_t)c->ahead_force : s.ahead;
     c->qsort = c->qsort_force >= 0 ? (uint32_t)c->qsort_force : s.qsort;
+    c->one = c->one_force >= 0 ? (uint32_t)c->one_force : s.one;
     c->last_sched = busy ? 1 : 0;
 }
 
@@ -1712,6 +1985,43 @@ static int launch_queue_passes(vhx_ctx *c, const DevTree &t, const CamD &cam, co
     return rc;
 }
 
+// k_trace_frame for a whole framebuffer frame: the pass ladder of the schedule in force, per XCD and
+// pass a queue slot for every ray of the XCD's tiles (80 B each: 4 GB for a 3840x2160 frame, of a context that traces
+// one-launch frames), the counters zeroed on c's stream, one workgroup per resident slot (four per CU).
+template <int BD>
+static int launch_frame(vhx_ctx *c, const DevTree &t, const CamD &cam, const RaySrc &src, const OutD &o, uint64_t nout,
+                        uint32_t npass) {
+    FrameQ f{};
+    f.npass = std::min<uint32_t>(npass, VHX_FRAME_PASSES);
+    for (uint32_t p = 0; p < f.npass; ++p) f.budget[p] = p + 1 < f.npass ? c->budgets[p] : VHX_MAX_ITERS;
+    f.sparse0 = c->sparse[0];
+    f.tiles_x = (cam.width + 7u) / 8u;
+    f.ntiles = f.tiles_x * ((cam.height + 7u) / 8u);
+    const uint64_t runs = (f.ntiles + FQ_RUN - 1u) / FQ_RUN;
+    f.capx = (runs + 7u) / 8u * FQ_RUN * 64u;  // every ray of an XCD's tiles
+    const uint64_t slot_bytes = 8ull * (VHX_FRAME_PASSES - 1u) * f.capx * FQ_SLOT * sizeof(uint4);
+    (void)nout;
+    const bool fresh = c->fq_slots.bytes < slot_bytes;
+    int rc = ensure(c, c->fq_slots, slot_bytes);
+    if (!rc) rc = ensure(c, c->fq_ctl, FQ_WORDS * sizeof(uint32_t) + sizeof(FrameQ));  // counters, then the FrameQ
+    if (rc) return rc;
+    if (fresh) {  // a new allocation holds no epoch of this context's frames: tags from 1 again
+        VHX_HIP(c, hipMemsetAsync(c->fq_slots.ptr, 0, c->fq_slots.bytes, c->stream));
+        c->fq_epoch = 0;
+    }
+    f.epoch = ++c->fq_epoch == 0u ? ++c->fq_epoch : c->fq_epoch;
+    f.ctl = (uint32_t *)c->fq_ctl.ptr;
+    f.slots = (uint4 *)c->fq_slots.ptr;
+    VHX_HIP(c, hipMemsetAsync(c->fq_ctl.ptr, 0, FQ_WORDS * sizeof(uint32_t), c->stream));
+    QueueArgs *qa = nullptr;
+    if ((rc = put_qargs(c, cam, src, o, qa))) return rc;
+    FrameQ *fd = (FrameQ *)((uint8_t *)c->fq_ctl.ptr + FQ_WORDS * sizeof(uint32_t));
+    k_put_frameq<<<1, 64, 0, c->stream>>>(f, fd);
+    k_trace_frame<BD><<<c->cus * VHX_FRAME_WPE, 256, 0, c->stream>>>(t, qa, fd);
+    VHX_HIP(c, hipGetLastError());
+    return VHX_OK;
+}
+
 // The ahead stream's fork, on c's stream before pass 0: k_ahead_pick lists the previous frame's long
 // rays (their flags marked VHX_FLAG_AHEAD), then the second stream traces them from scratch, unbudgeted, ahead_rpw rays
 // per wave, into the frame's outputs and records their step counts; ev_join marks its end.
@@ -1831,7 +2141,7 @@ void vhx_destroy(vhx_ctx *c) {
     if (c->use_ev) (void)hipEventDestroy(c->use_ev);
     for (DevBuf *b : {&c->scratch, &c->rays, &c->queue[0], &c->queue[1], &c->qctl, &c->tmp, &c->counts, &c->offsets,
                       &c->flags, &c->qargs, &c->state, &c->upd, &c->prepass_depth, &c->ovf, &c->ahead_cost,
-                      &c->ahead_list})
+                      &c->ahead_list, &c->fq_ctl, &c->fq_slots})
         if (b->ptr) (void)hipFree(b->ptr);
     for (auto &P : c->pinned) {
         if (P.ptr) (void)hipHostFree(P.ptr);
@@ -1963,6 +2273,9 @@ static int apply_tuning(vhx_ctx *c, const std::string &key, const std::string &v
     } else if (key == "qsort") {  // segment length of the queue passes' node sort: 0 = off, else 256 .. VHX_QSORT_MAX
         if (!parse_u32(val, x) || (x && (x < 256 || x > VHX_QSORT_MAX || (x & (x - 1))))) return bad();
         c->qsort_force = (int)x;
+    } else if (key == "one") {
+        if (!parse_u32(val, x) || x > 1) return bad();
+        c->one_force = (int)x;
     } else if (key == "qsortp") {  // bit mask of the queue passes whose input is sorted
         if (!parse_u32(val, x)) return bad();
         c->qsort_passes = x;
@@ -2234,6 +2547,7 @@ void vhx::copy_sched(vhx_ctx *c, const vhx_ctx *owner) {
     c->split_max_wait = owner->split_max_wait;
     c->ahead_force = owner->ahead_force;
     c->qsort_force = owner->qsort_force;
+    c->one_force = owner->one_force;
     c->qsort_passes = owner->qsort_passes;
     c->qsort_blocks = owner->qsort_blocks;
     c->ahead_min = owner->ahead_min;
@@ -2563,6 +2877,10 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
     } join{c};
     const bool count = ho.dev.bytes != nullptr;
     int qrc = VHX_OK;
+    // the one-launch frame: a whole framebuffer frame under a multi-pass schedule that selects it (not with byte
+    // counting, node MIPs or the approximate prepass mode, which keep the per-pass launches)
+    const bool one = c->one && npass > 1 && layout == VHX_LAYOUT_FRAMEBUFFER && tile_start == 0 && tile_stride == 1 &&
+                     !count && !t.mips && !fast && !c->in_prepass && !ahead;
     // the queue order's frame (c->qorder): the framebuffer layout only. The tile layout's output index is already
     // tile-major with T-wide rows inside a tile (config 4 on one rank, 64x64 tiles: 2.019-2.025 ms per frame in that
     // order against 2.071-2.074 with the tiles re-ordered Morton inside, profiles/r03/qorder/mgpu1_*.log)
@@ -2570,6 +2888,10 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
     const uint32_t oh = cam->height;
     auto launch = [&](auto bd_tag) {
         constexpr int BD = decltype(bd_tag)::value;
+        if (one) {  // the whole ladder in one persistent launch
+            qrc = launch_frame<BD>(c, t, cd, src, ho.dev, nout, npass);
+            return;
+        }
         PassQ q0 = pass_q(c, 0, npass);
         if (npass > 1) q0.flags = (uint8_t *)c->flags.ptr;
         if (predicted) {
