@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define VHX_ABI_VERSION 4u
+#define VHX_ABI_VERSION 5u
 
 /* ---- error codes ------------------------------------------------------------------------------------------ */
 #define VHX_OK 0
@@ -173,19 +173,11 @@ int vhx_get_pass_budgets(const vhx_ctx *ctx, uint32_t *budgets, uint32_t *n, int
 /* Scheduling knobs (no reference counterpart; results never depend on them -- experiments and probes): `spec` is
  * "key=value[;key=value...]" with keys budgets (list, fixes the schedule), adaptive (0/1), rpw (list: rays per wave of
  * queue passes 1.., 0 = adaptive), tw, xcdg, resume (0/1), save_from, qblock (64/128/256), qwaves (fixes the schedule),
- * qwavesm, qwaves0, qxcd, qxcd_all (0/1), sparse (list, fixes the schedule), qorder ("[m]N[z|r]" or 0), split (0/1),
- * split_wait, split_diag, split_tune ("period,min_lanes,min_idle,take"), ahead (0/1: the ahead stream of a lone frame, on in the
- * lone-frame schedule), ahead_min (steps), ahead_cap (rays), ahead_rpw (1..64), qsort (0 or 256..2048: segment node
- * sort of the queue passes, §15.3), qsortp (pass mask), qsortb (workgroups). The library reads no environment variable for any of
- * them. Unknown keys or malformed values: VHX_E_INVALID_ARG and nothing is changed.
- * The ahead stream runs part of a lone framebuffer frame on a second stream of the context: the frame still starts and
- * ends on the context's stream (its events, and the ordering against tree writes, cover both). */
+ * qwavesm, qwaves0, qxcd, qxcd_all (0/1), sparse (list, fixes the schedule), qorder ("[m]N[z|r]" or 0), qsort (0 or
+ * 256..2048: segment node sort of the queue passes), qsortp (pass mask), qsortb (workgroups). The
+ * library reads no environment variable for any of them. Unknown keys or malformed values:
+ * VHX_E_INVALID_ARG and nothing is changed. */
 int vhx_set_tuning(vhx_ctx *ctx, const char *spec);
-/* Tail split of the last trace (the lone-frame schedule's unbounded last pass shares its slowest rays out between
- * waves: DESIGN.md section 14.10; vhx_set_tuning "split=0/1" forces it off / on): synchronises the context's stream and reports the
- * rays handed over from one wave to another (*handed_over) and hand-offs that never completed (*errors, always 0
- * unless something is broken). Both 0 when the last trace ran no split pass. Diagnostics; results never depend on it. */
-int vhx_get_split_stats(vhx_ctx *ctx, uint32_t *handed_over, uint32_t *errors);
 
 /* Tree upload ----------------------------------------------------------------------------------------------- */
 /* Copies the flattened tree to HBM (full residency) and builds the device-side layout. */

@@ -1,7 +1,7 @@
 """Lone-frame latency (one frame at a time, synchronised; libvhx's events, like bench.py's `lone`) of the bench frame
-for each vhx_set_tuning spec on the command line (the ahead stream), interleaved over REPS rounds so that
-box drift hits every spec alike; also a lone orbiting frame (the prediction comes from the previous, different view).
-usage: probe_ahead.py "ahead=0" "ahead=1;ahead_min=512" ..."""
+for each vhx_set_tuning spec on the command line, interleaved over REPS rounds so that box drift hits
+every spec alike; also a lone orbiting frame (every frame a different view).
+usage: probe_lone.py "" "budgets=64,1024" ..."""
 import os
 import sys
 

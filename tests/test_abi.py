@@ -39,7 +39,7 @@ def test_integration_binds_every_declared_function():
 
 
 def test_abi_version_and_struct_sizes():
-    assert N.lib().vhx_abi_version() == 4
+    assert N.lib().vhx_abi_version() == 5
     assert ctypes.sizeof(N.TreeDesc) == 8 * 4 + 7 * 8
     assert ctypes.sizeof(N.Camera) == 4 * 4 + 4 * 12 + 8 + 64
     assert ctypes.sizeof(N.Hits) == 8 * 8

@@ -98,7 +98,6 @@ SIGNATURES = [
     ("vhx_set_adaptive_schedule", c_int, [c_void_p, c_int]),
     ("vhx_get_pass_budgets", c_int, [c_void_p, P(c_u32), P(c_u32), P(c_int)]),
     ("vhx_set_tuning", c_int, [c_void_p, ctypes.c_char_p]),
-    ("vhx_get_split_stats", c_int, [c_void_p, P(c_u32), P(c_u32)]),
     ("vhx_upload_tree", c_int, [c_void_p, P(TreeDesc)]),
     ("vhx_upload_tree_device", c_int, [c_void_p, P(TreeDesc)]),
     ("vhx_set_node_mips", c_int, [c_void_p, c_void_p, c_u32]),

@@ -63,14 +63,6 @@ struct TreeStore {
 #define VHX_QSORT_BUSY 0u
 #endif
 #define VHX_QSORT_MAX 2048u
-// the one-launch frame (k_trace_frame) in the lone-frame schedule (tune "one=0/1" forces it)
-#ifndef VHX_ONE_IDLE
-#define VHX_ONE_IDLE 0u
-#endif
-// the ahead stream in the lone-frame schedule (tune "ahead=0/1" forces it either way)
-#ifndef VHX_AHEAD_IDLE
-#define VHX_AHEAD_IDLE 0u
-#endif
 
 struct vhx_ctx {
     int device = 0;
@@ -120,10 +112,7 @@ struct vhx_ctx {
         uint32_t sparse[VHX_MAX_BUDGETS];    // abandon a wave's rays once fewer lanes still trace (0 = off)
         uint32_t queue_waves_per_cu;         // waves of a queue pass per CU
         uint32_t qorder;                     // order of a primary frame's pass-0 queue (vhx_ctx::qorder below)
-        uint32_t split;                      // the unbounded last pass shares its tail rays out (k_trace_queue_split)
-        uint32_t ahead;                      // the ahead stream: a lone frame's predicted-long rays traced first, aside
         uint32_t qsort;                      // queue passes: segments of this many queue entries sorted by saved node
-        uint32_t one;                        // a framebuffer frame's pass ladder in one persistent launch (k_trace_frame)
     };
     // Adaptive scheduling (default; vhx_set_pass_budgets or an environment knob fixes the schedule instead): at each
     // trace the context looks at the other contexts of its tree (vhx_create_shared) and picks
@@ -141,8 +130,8 @@ struct vhx_ctx {
     //    three-budget ladders 1.31-1.51 ms, fewer rays per wave in a last pass no better): every extra pass lengthens a
     //    lone frame's critical path.
     bool adaptive = true;
-    Sched sched_busy = {{24u, 72u, 216u, 648u}, 5u, {12u}, 3u, VHX_QORDER_BUSY, 0u, 0u, VHX_QSORT_BUSY, 0u};
-    Sched sched_idle = {{64u}, 2u, {0u}, 8u, VHX_QORDER_IDLE, 0u, VHX_AHEAD_IDLE, 0u, VHX_ONE_IDLE};
+    Sched sched_busy = {{24u, 72u, 216u, 648u}, 5u, {12u}, 3u, VHX_QORDER_BUSY, VHX_QSORT_BUSY};
+    Sched sched_idle = {{64u}, 2u, {0u}, 8u, VHX_QORDER_IDLE, 0u};
     int last_sched = -1;  // the schedule of the last trace: 1 busy, 0 idle, -1 fixed (vhx_get_pass_budgets)
     // the schedule in force (the selected one, or the fixed one)
     uint32_t budgets[VHX_MAX_BUDGETS] = {24u, 72u, 216u, 648u};
@@ -175,41 +164,6 @@ struct vhx_ctx {
     // Pass 0 at 12 under frames in flight: eight frames 0.645-0.651 ms per bench frame against 0.665-0.670 (8:
     // 0.651-0.661, 16: 0.646-0.657, 24 and 32 slower); the later budgeted passes gained nothing (profiles/r02/sparse*.log)
     uint32_t sparse[VHX_MAX_BUDGETS] = {12u};
-    // tail split of the unbounded last pass (k_trace_queue_split in vhx_device.hip): in force for
-    // this trace (the selected schedule's `split`, off in both default schedules: it measured neutral; off under a
-    // fixed schedule), VHX_SPLIT=0/1 forces it either way (-1: not forced); ovf holds the overflow slots, split_epoch
-    // tags this context's frames in them
-    uint32_t split = 0;
-    int split_force = -1;
-    uint32_t split_epoch = 0;
-    // SplitQ settings (VHX_SPLIT_TUNE = period,min_lanes,min_idle,take; VHX_SPLIT_WAIT; VHX_SPLIT_DIAG): the best of the
-    // lone-frame sweeps (profiles/r03/split/), 1.19-1.22 ms against 1.21-1.25 with the split off
-    uint32_t split_period = 128, split_min_lanes = 2, split_min_idle = 1, split_take = 32;
-    uint32_t split_diag = 0;
-    uint32_t split_max_wait = 32;
-    DevBuf ovf;
-    // the ahead stream of a lone frame (k_ahead_pick in vhx_device.hip): in force for this trace (the
-    // selected schedule's `ahead`; tune "ahead" forces it), a predicted-long ray's step threshold (ahead_min), the most
-    // rays listed (ahead_cap), rays per wave of the ahead pass (ahead_rpw), the per-pixel step counts the queue passes
-    // record (ahead_cost, of the ahead_w x ahead_h frame last traced with it; 0 x 0: no prediction), the list, the cost
-    // buffer of the running trace, the second stream and the events that fork it off and join it back
-    uint32_t ahead = 0;
-    int ahead_force = -1;
-    uint32_t ahead_min = 256;
-    uint32_t ahead_cap = 16384;
-    uint32_t ahead_rpw = 8;
-    uint32_t ahead_prio = 1;  // the ahead pass's waves at the highest issue priority (s_setprio; tune "ahead_prio")
-    DevBuf ahead_cost, ahead_list;
-    uint32_t ahead_w = 0, ahead_h = 0;
-    uint32_t *ahead_rec = nullptr;
-    hipStream_t aux_stream = nullptr;
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-    // the one-launch frame (Sched::one): in force for this trace, forced by tune "one" (-1: not), its counters and
-    // queue slots, and the epoch that tags this context's frames in them (never 0: the slots start zeroed)
-    uint32_t one = 0;
-    int one_force = -1;
-    DevBuf fq_ctl, fq_slots;
-    uint32_t fq_epoch = 0;
     // segment node sort of the queue passes (Sched::qsort): in force for this trace; tune "qsort=N" forces it (-1: not)
     uint32_t qsort = 0;
     int qsort_force = -1;

@@ -236,13 +236,6 @@ struct PassQ {
     uint32_t xcd_group;  // pass 0: XCD-aware block runs (xcd_block), 0 = dispatch order
     uint32_t qxcd;       // queue passes: runs of this many chunks dealt over the 8 XCDs, one counter each (0 = off)
     uint32_t sparse;     // budgeted passes with saved state: abandon a wave's rays once fewer lanes trace (0 = off)
-    // The ahead stream of a lone frame: pass 0 skips the pixels whose flag is VHX_FLAG_AHEAD (their
-    // rays are traced on the context's second stream, from the list k_ahead_pick made), and a queue pass that finishes a
-    // framebuffer ray records its step count in cost[idx], the prediction of the next frame
-    const uint8_t *skip;
-    uint32_t *cost;
-    uint32_t in_cap;  // queue passes: at most this many input entries (0: all *in_n of them)
-    uint32_t prio;    // queue passes: the waves' issue priority within their SIMD (s_setprio; 0 = the default)
 };
 
 // Rays per wave of a queue pass over n rays: fixed, or (rpw == 0) as many as spread the pass over about `tw` waves.
@@ -354,13 +347,7 @@ __device__ __forceinline__ uint32_t flag_bits(const void *src, uint64_t i, uint6
 // one line, the drain of a budgeted pass over many short chunks, every wave probing every exhausted counter, took 2.5 -
 // 3.6 times as long as with one counter: DESIGN.md §3)
 #define QCTL_PASS_WORDS (9u * 64u)
-// the tail split's counters (k_trace_queue_split), each on a 256-byte line: reserved overflow slots, taken slots, waves
-// waiting for work, waves holding rays, error word
-#define QCTL_SPLIT (16u + QCTL_PASS_WORDS * (VHX_MAX_BUDGETS + 1u))
-// the ahead stream's list length and grab counter (zeroed by the frame that uses them, never by the compaction, which
-// runs while the ahead pass may still be grabbing)
-#define QCTL_AHEAD (QCTL_SPLIT + 10u * 64u)
-#define QCTL_WORDS (QCTL_AHEAD + 3u * 64u)
+#define QCTL_WORDS (16u + QCTL_PASS_WORDS * (VHX_MAX_BUDGETS + 1u))
 // Order of the pass-0 queue of a primary frame (vhx_ctx::qorder): W = 0 keeps output-index order (row-major in the
 // framebuffer layout); W > 0 lists the rays tile by tile -- TS x TS pixel tiles (TS = 1 << tsl >= 8), the tiles
 // row-major over the frame (tx per row) or, with mdim > 0, in Morton order over a 2^mdim x 2^mdim grid (tiles outside
@@ -413,7 +400,7 @@ __device__ __forceinline__ uint32_t order_bits(const void *src, const FlagOrder 
         uint32_t px, py;
         if (!order_pixel(o, k + j, px, py)) continue;
         const uint64_t i = (uint64_t)py * o.W + px;
-        // a pass-0 flag byte: bit 0 = abandoned (VHX_FLAG_AHEAD pixels are traced elsewhere)
+        // a pass-0 flag byte: 1 = abandoned
         if (HITS ? ((const uint32_t *)src)[i] != VHX_EMPTY : (((const uint8_t *)src)[i] & 1u) != 0) bits |= 1u << j;
     }
     return bits;
@@ -429,7 +416,7 @@ __global__ void __launch_bounds__(256) k_count_flags(const void *__restrict__ sr
                                                      uint64_t nclear = 0) {
     __shared__ uint32_t s_cnt[4];
     if (blockIdx.x == 0)
-        for (uint32_t w = threadIdx.x; w < QCTL_AHEAD - 16u; w += blockDim.x) zero[w] = 0u;
+        for (uint32_t w = threadIdx.x; w < QCTL_WORDS - 16u; w += blockDim.x) zero[w] = 0u;
     const uint64_t i = ((uint64_t)blockIdx.x * 256u + threadIdx.x) * 4u;
     if (clear)
         for (uint64_t k = i; k < nclear && k < i + 4u; ++k) clear[k] = 0u;
@@ -579,64 +566,6 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t bid, uint32_t n, uint32_t
     return ((k / G) * 8u + x) * G + k % G;
 }
 
-// The ahead stream of a lone frame. A lone frame is latency-bound: its critical path is pass 0
-// (~0.40 ms) followed by the slowest chunk of the unbounded pass (~0.8 ms), because its longest rays wait for all of
-// pass 0 before their tails start. The queue passes of a lone frame record every finished ray's step count (cost);
-// before the next frame's pass 0, k_ahead_pick lists the pixels whose ray took >= min_steps steps in the previous frame
-// (at most cap of them, appended in any order) and marks them VHX_FLAG_AHEAD in the flags pass 0 writes anyway. The
-// context's second stream traces that list from scratch, unbudgeted and a few rays per wave, starting at once, while pass
-// 0 skips those pixels (leaves them marked: not queued, and predicted again) and the rest of the frame runs as before;
-// the frame ends when both streams have. Only which pass and stream trace a ray change: results are bit-identical for
-// any prediction (a ray's traversal is deterministic), and a ray's cost is its traversal's step count wherever it ran.
-#define VHX_FLAG_AHEAD 2u
-// ctl (QCTL_AHEAD): [0] list length, [64] grab counter of the ahead pass, [128 ..] 33 histogram buckets of the
-// candidates' step counts (bucket b: [2^(b-1), 2^b), by the highest set bit)
-__device__ __forceinline__ bool ahead_candidate(uint32_t f, uint32_t cost, uint32_t min_steps) {
-    return (f & 3u) != 0u && cost >= min_steps;  // abandoned in pass 0 (1) or ahead (2) last frame, and long
-}
-__global__ void __launch_bounds__(256) k_ahead_hist(const uint8_t *__restrict__ flags, const uint32_t *__restrict__ cost,
-                                                    uint64_t n, uint32_t min_steps, uint32_t *__restrict__ ctl) {
-    __shared__ uint32_t s_h[33];
-    if (threadIdx.x < 33u) s_h[threadIdx.x] = 0u;
-    __syncthreads();
-    const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
-    if (i < n && ahead_candidate(flags[i], cost[i], min_steps)) atomicAdd(&s_h[32u - __clz(cost[i])], 1u);
-    __syncthreads();
-    if (threadIdx.x < 33u && s_h[threadIdx.x]) atomicAdd(ctl + 128u + threadIdx.x, s_h[threadIdx.x]);
-}
-// Lists the candidates whose step count is at or above the smallest power-of-two edge (>= min_steps) with at most cap
-// candidates at or above it: the longest rays, whatever the order of the appends; marks them, unmarks the others.
-__global__ void __launch_bounds__(256) k_ahead_pick(uint8_t *__restrict__ flags, const uint32_t *__restrict__ cost,
-                                                    uint64_t n, uint32_t min_steps, uint32_t cap,
-                                                    uint32_t *__restrict__ list, uint32_t *__restrict__ ctl) {
-    __shared__ uint32_t s_edge;
-    if (threadIdx.x == 0) {
-        uint32_t above = 0, b = 33u;
-        while (b > 1u && above + ctl[128u + b - 1u] <= cap) above += ctl[128u + --b];
-        s_edge = max(min_steps, b >= 33u ? 0xFFFFFFFFu : (b <= 1u ? 0u : 1u << (b - 1u)));
-    }
-    __syncthreads();
-    const uint32_t edge = s_edge;
-    const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
-    const uint32_t lane = threadIdx.x & 63u;
-    uint32_t f = 0;
-    bool want = false;
-    if (i < n) {
-        f = flags[i];
-        want = ahead_candidate(f, cost[i], edge);
-    }
-    const uint64_t m = __ballot(want);
-    const uint32_t first = (uint32_t)__builtin_ctzll(m | (1ull << 63));
-    uint32_t base = 0;
-    if (lane == first && m) base = atomicAdd(ctl, (uint32_t)__popcll(m));
-    base = __shfl(base, (int)first);
-    const uint32_t slot = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-    const bool ahead = want && slot < cap;
-    if (ahead) list[slot] = (uint32_t)i;
-    if (i < n && (ahead ? f != VHX_FLAG_AHEAD : f == VHX_FLAG_AHEAD))
-        flags[i] = ahead ? (uint8_t)VHX_FLAG_AHEAD : (uint8_t)0;  // pass 0 traces every pixel not marked
-}
-
 // occupancy of the traversal kernels (waves per SIMD the register allocation must allow; 0 = the compiler's choice).
 // Default: the queue kernel of brick_dim 1 and 4 fits 96 VGPRs (5 waves per SIMD instead of 4, no spills under the
 // iterative-ilp scheduler of _build.py); brick_dim 2 would spill 4 VGPRs and 8..32 16, so they keep 4 waves (the
@@ -655,8 +584,6 @@ __global__ void __launch_bounds__(256) k_ahead_pick(uint8_t *__restrict__ flags,
 #else
 #define VHX_QUEUE_ATTR __attribute__((amdgpu_waves_per_eu(!COUNT && (BD == 1 || BD == 4) ? 5 : 4)))
 #endif
-// the split pass runs 8 waves per CU (2 per SIMD): no occupancy bound for the register allocation
-#define VHX_QUEUE_ATTR_SPLIT
 #if VHX_PRIMARY_WPE > 0
 #define VHX_PRIMARY_ATTR __attribute__((amdgpu_waves_per_eu(VHX_PRIMARY_WPE)))
 #else
@@ -709,9 +636,7 @@ __global__ void __launch_bounds__(256) VHX_PRIMARY_ATTR k_trace_primary(DevTree 
     const uint64_t idx = layout == VHX_LAYOUT_FRAMEBUFFER ? (uint64_t)py * cam.width + px
                                                           : (uint64_t)j * T * T + (uint64_t)ly * T + lx;
     bool done = true;
-    // a pixel of the ahead list (its ray traced on the context's second stream) keeps its mark and is not traced here
-    const bool ahead = q.skip && valid && q.skip[idx] == VHX_FLAG_AHEAD;
-    if (valid && !ahead) {
+    if (valid) {
         F3d o, d;
         primary_ray(cam, px, py, o, d);
         HitOut h;
@@ -728,7 +653,7 @@ __global__ void __launch_bounds__(256) VHX_PRIMARY_ATTR k_trace_primary(DevTree 
     // every in-tile entry (frame padding included, done = true there); in the framebuffer layout only pixels of the
     // frame (a lane past the frame edge has no entry of its own: its idx aliases the next row or runs past the end)
     if (q.flags && (layout == VHX_LAYOUT_FRAMEBUFFER ? valid : (lx < T && ly < T)))
-        q.flags[idx] = ahead ? (uint8_t)VHX_FLAG_AHEAD : (done ? 0 : 1);
+        q.flags[idx] = done ? 0 : 1;
 }
 
 template <bool COUNT, int BD, bool MIP = false>
@@ -781,9 +706,7 @@ __global__ void __launch_bounds__(256) VHX_QUEUE_ATTR k_trace_queue(DevTree t, c
     fill_occ_tab(occ_tab, t);
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u;
-    // the ahead pass: its few long rays issue before the waves of the pass 0 they run beside (wave-uniform)
-    if (q.prio) __builtin_amdgcn_s_setprio(3);
-    const uint32_t n = q.in_cap ? min(*in_n, q.in_cap) : *in_n;
+    const uint32_t n = *in_n;
     const uint32_t rpw = pass_rpw(q.rpw, q.tw, n);
     // q.qxcd = G > 0: chunk runs of G are dealt round-robin over the XCDs (blockIdx % 8 runs on one XCD and shares
     // its L2), each XCD's waves take its runs in order from their own counter (grab[64 (x + 1)]) and move on to the next
@@ -843,7 +766,6 @@ __global__ void __launch_bounds__(256) VHX_QUEUE_ATTR k_trace_queue(DevTree t, c
                 store_shadow(b->out, idx, h);
             } else {
                 store(t, b->out, idx, o, h);
-                if (q.cost) q.cost[idx] = h.iters;  // a lone framebuffer frame: the next frame's prediction
             }
         }
         if (q.tmp) {  // this chunk's abandoned rays, in lane order
@@ -853,564 +775,6 @@ __global__ void __launch_bounds__(256) VHX_QUEUE_ATTR k_trace_queue(DevTree t, c
             if (lane == 0) q.counts[chunk] = (uint32_t)__popcll(m);
         }
     }
-}
-
-// ------------------------------------------------------------------------------------------------ tail split
-// A lone frame's unbounded last pass ends on its slowest chunks: 64 neighbouring long rays in one wave, which runs the
-// union of their divergent paths while the rest of the GPU has gone idle (bench frame: the last pass is 0.83-0.86 of
-// the 1.22 ms; the 256 longest rays take 1.05 ms at 64 per wave and 0.56 ms at one per wave). k_trace_queue_split runs
-// that pass with work sharing: a wave that finds the queue drained waits for work (the `idle` count), and a tracing
-// wave that sees idle waves hands the upper half of its still-tracing rays over -- their loop state, packed as
-// save_state would, goes to overflow slots -- and goes on with the lower half; waiting waves take the slots (up to 64
-// at a time) and resume the rays, splitting again while other waves wait. Results are the same (a ray's traversal is
-// deterministic and its state is handed over whole); only which wave runs which iterations changes.
-//
-// Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility, form R2: the data is the flag): every word of a slot is
-// an 8-byte granule {tag = the frame's epoch, value} written by ONE agent-scope atomic store (sc1) and read by
-// agent-scope atomic loads until every tag matches; no fences. Epochs count per context from 1 and the slots are
-// zeroed when allocated, so a slot of an earlier frame never matches. Termination needs no barrier: a wave leaves only
-// when the queue is drained, no slot is left untaken and no wave holds rays; a wave that hands rays over keeps looking
-// for slots itself before it can leave, so no slot is ever orphaned, whatever the other waves do. Every wait is
-// bounded (VHX_SPLIT_SPINS; a slot that never fills sets the error word and its ray is dropped, which the parity tests
-// would show).
-#define VHX_OVF_CAP 65536u   // overflow slots per context (a frame hands over fewer: the tail is a few thousand rays)
-#define VHX_OVF_STRIDE 32u   // granules per slot (17 used: output index + 16 state words); 256 B
-#define VHX_OVF_SKIP 0xFFFFFFFFu
-#define VHX_SPLIT_SPINS (1u << 20)
-typedef __attribute__((address_space(1))) uint32_t gu32;
-typedef __attribute__((address_space(1))) unsigned long long gu64;
-struct SplitQ {
-    unsigned long long *ovf;  // VHX_OVF_CAP slots of VHX_OVF_STRIDE granules
-    uint32_t *ctl;            // qctl + QCTL_SPLIT
-    uint32_t epoch;
-    uint32_t period;     // a tracing wave looks at the idle count every `period` iterations (a power of two)
-    uint32_t min_lanes;  // ... and splits only with at least this many rays still tracing
-    uint32_t min_idle;   // ... and at least this many waves waiting
-    uint32_t take;       // a waiting wave takes up to this many slots at a time
-    uint32_t diag;       // bit 0: poll slots by atomic read-modify-write (fetch_or 0); bit 1: count polls (ctl[320], [384])
-    uint32_t max_wait;   // at most this many waves wait for slots; the others leave once the queue is drained
-};
-__device__ __forceinline__ uint32_t ld_agent(const uint32_t *p) {
-    return __hip_atomic_load((gu32 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void put_granule(unsigned long long *g, uint32_t epoch, uint32_t v) {
-    __hip_atomic_store((gu64 *)g, ((unsigned long long)epoch << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void publish_slot(const SplitQ &s, uint32_t slot, uint32_t idx, const St4 &st) {
-    unsigned long long *g = s.ovf + (uint64_t)slot * VHX_OVF_STRIDE;
-    const uint32_t w[16] = {st.a.x, st.a.y, st.a.z, st.a.w, st.b.x, st.b.y, st.b.z, st.b.w,
-                            st.c.x, st.c.y, st.c.z, st.c.w, st.e.x, st.e.y, st.e.z, st.e.w};
-    put_granule(g, s.epoch, idx);
-#pragma unroll
-    for (uint32_t k = 0; k < 16u; ++k) put_granule(g + 1 + k, s.epoch, w[k]);
-}
-// polls one slot until all 17 granules carry this frame's epoch; false after VHX_SPLIT_SPINS polls
-__device__ __forceinline__ bool take_slot(const SplitQ &s, uint32_t slot, uint32_t &idx, St4 &st) {
-    unsigned long long *g = s.ovf + (uint64_t)slot * VHX_OVF_STRIDE;
-    uint32_t w[17];
-    for (uint32_t spins = 0; spins < VHX_SPLIT_SPINS; ++spins) {
-        bool ok = true;
-#pragma unroll
-        for (uint32_t k = 0; k < 17u; ++k) {
-            const unsigned long long x =
-                (s.diag & 1u) ? __hip_atomic_fetch_or((gu64 *)(g + k), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                              : __hip_atomic_load((const gu64 *)(g + k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            w[k] = (uint32_t)x;
-            ok &= (uint32_t)(x >> 32) == s.epoch;
-        }
-        if ((s.diag & 2u) && !ok) atomicAdd(s.ctl + 320, 1u);
-        if (ok) {
-            idx = w[0];
-            st.a = make_uint4(w[1], w[2], w[3], w[4]);
-            st.b = make_uint4(w[5], w[6], w[7], w[8]);
-            st.c = make_uint4(w[9], w[10], w[11], w[12]);
-            st.e = make_uint4(w[13], w[14], w[15], w[16]);
-            return true;
-        }
-        __builtin_amdgcn_s_sleep(1);
-    }
-    return false;
-}
-
-// One resumed ray of the split pass, unbounded. Every s.period-th iteration of the wave reads the idle count (issued
-// before the iteration's node loads, used after them); with at least s.min_idle waves waiting and s.min_lanes rays
-// still tracing, the upper half of them (in lane order: the wave's rays stay spatial neighbours) is handed over. Returns false when this lane's
-// ray was handed over, true when it finished here (h filled).
-template <int BD>
-__device__ __forceinline__ bool trace_split(const DevTree &t, const uint64_t *occ_tab, F3d o, F3d d, HitOut &h,
-                                            const St4 &st, uint32_t idx, const SplitQ &s) {
-    Trav<false, BD, false> tr;
-    tr.begin_resumed(t, o, d, h, st);
-    const uint32_t lane = threadIdx.x & 63u;
-    uint32_t k = 0;
-    for (;; ++k) {
-        // not before `period` iterations of this wave: a wave that just took handed-over rays first traces them
-        // (checking at once made rays bounce from wave to wave, each hop costing more than the iterations it ran)
-        const bool chk = ((k + 1u) & (s.period - 1u)) == 0u;
-        uint32_t want = 0;
-        if (chk) want = ld_agent(s.ctl + 128);
-        tr.step(t, occ_tab, h, VHX_MAX_ITERS);
-        if (tr.ex != 0u) break;
-        if (chk && (int32_t)want >= (int32_t)s.min_idle) {
-            const uint64_t act = __ballot(1);
-            const uint32_t na = (uint32_t)__popcll(act);
-            if (na >= s.min_lanes) {
-                const uint32_t rank = (uint32_t)__popcll(act & ((1ull << lane) - 1ull));
-                const uint32_t nk = na >> 1, first = na - nk;
-                const bool go = rank >= first;
-                const uint32_t leader = (uint32_t)__builtin_ctzll(__ballot(go));
-                // book one waiting wave first (a split without a taker parks the rays: measured 1.5-15 ms lone frames
-                // where every tracing wave split as soon as one wave waited); no taker booked, no split
-                uint32_t base = 0xFFFFFFFFu;
-                if (lane == leader) {
-                    if ((int32_t)atomicSub(s.ctl + 128, 1u) > 0)
-                        base = atomicAdd(s.ctl, nk);
-                    else
-                        atomicAdd(s.ctl + 128, 1u);
-                }
-                base = __shfl(base, (int)leader);
-                if (base == 0xFFFFFFFFu) continue;
-                if (go) {
-                    const uint32_t slot = base + rank - first;
-                    if (base + nk <= VHX_OVF_CAP) {
-                        publish_slot(s, slot, idx, tr.packed());
-                        tr.ex = 5u;  // handed over
-                    } else if (slot < VHX_OVF_CAP) {
-                        publish_slot(s, slot, VHX_OVF_SKIP, tr.packed());  // no room: a skip entry, the ray stays
-                    }
-                }
-                if (tr.ex != 0u) break;
-            }
-        }
-    }
-    if (s.diag & 2u) {  // diagnostics: ray iterations (sum over lanes) and wave iterations (max) of this call
-        uint32_t sum = k + 1u, mx = k + 1u;
-        for (uint32_t dd = 32; dd > 0; dd >>= 1) {
-            const uint32_t a = __shfl_xor(sum, dd), b = __shfl_xor(mx, dd);
-            const bool live = ((__ballot(1) >> (lane ^ dd)) & 1ull) != 0ull;
-            sum += live ? a : 0u;
-            mx = live && b > mx ? b : mx;
-        }
-        if (lane == (uint32_t)__builtin_ctzll(__ballot(1))) {
-            atomicAdd(s.ctl + 448, sum);
-            atomicAdd(s.ctl + 512, mx);
-        }
-    }
-    if (tr.ex == 5u) return false;
-    tr.end(t, h, nullptr, 0);
-    return true;
-}
-
-// The unbounded last pass of a lone frame with the tail split (q.state holds every queued ray's saved state).
-template <int BD>
-__global__ void __launch_bounds__(256) VHX_QUEUE_ATTR_SPLIT k_trace_queue_split(DevTree t, const QueueArgs *qa,
-                                                                                const uint32_t *__restrict__ in,
-                                                                                const uint32_t *in_n, uint32_t *grab,
-                                                                                PassQ q, SplitQ s) {
-    __shared__ uint64_t occ_tab[OCC_TAB_WORDS];
-    fill_occ_tab(occ_tab, t);
-    __syncthreads();
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t n = *in_n;
-    const uint32_t rpw = pass_rpw(q.rpw, q.tw, n);
-    uint32_t xcd = blockIdx.x & 7u, tries = 0;
-    const uint32_t qxcd = (n + rpw - 1) / rpw > gridDim.x * (blockDim.x / 64u) ? q.qxcd : 0u;
-    uint32_t *const tail = s.ctl, *const head = s.ctl + 64, *const idle = s.ctl + 128, *const active = s.ctl + 192;
-    uint32_t *const nwait = s.ctl + 576;
-    bool drained = false, waiting = false, registered = false;
-    uint32_t spins = 0;
-    for (;;) {
-        uint32_t base = 0, cnt = 0;
-        bool from_ovf = false;
-        if (!drained) {  // the pass's queue, as k_trace_queue takes it
-            if (qxcd == 0u) {
-                if (lane == 0) base = atomicAdd(grab, rpw);
-                base = __shfl(base, 0);
-                if (base >= n) drained = true;
-            } else {
-                const uint32_t G = qxcd;
-                const uint32_t nch = (n + rpw - 1) / rpw, nfull = nch / G, rem = nch % G;
-                uint32_t chunk = 0xFFFFFFFFu;
-                while (tries < 8u) {
-                    const uint32_t kmax = (nfull > xcd ? (nfull - xcd + 7u) / 8u : 0u) * G +
-                                          (rem > 0u && nfull % 8u == xcd ? rem : 0u);
-                    uint32_t k = 0xFFFFFFFFu;
-                    uint32_t *ctr = grab + 64u * (xcd + 1u);
-                    if (lane == 0 && __atomic_load_n(ctr, __ATOMIC_RELAXED) < kmax) k = atomicAdd(ctr, 1u);
-                    k = __builtin_amdgcn_readfirstlane(__shfl(k, 0));
-                    if (k < kmax) {
-                        chunk = ((k / G) * 8u + xcd) * G + k % G;
-                        break;
-                    }
-                    xcd = (xcd + 1u) & 7u;
-                    ++tries;
-                }
-                if (chunk == 0xFFFFFFFFu)
-                    drained = true;
-                else
-                    base = chunk * rpw;
-            }
-            if (!drained) cnt = n - base < rpw ? n - base : rpw;
-        }
-        if (drained) {  // overflow slots handed over by tracing waves
-            uint32_t h0 = 0, got = 0, fin = 0;
-            if (lane == 0) {
-                const uint32_t tl0 = ld_agent(tail), tl = tl0 < VHX_OVF_CAP ? tl0 : VHX_OVF_CAP;
-                uint32_t hd = ld_agent(head);
-                while (hd < tl) {
-                    const uint32_t w = tl - hd < s.take ? tl - hd : s.take;
-                    if (__hip_atomic_compare_exchange_strong((gu32 *)head, &hd, hd + w, __ATOMIC_RELAXED,
-                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-                        h0 = hd;
-                        got = w;
-                        break;
-                    }
-                }
-                // leave only when no wave holds rays (read first) and every reserved slot is taken; the active count
-                // is looked at on every 8th empty poll only (all waiting waves poll the same lines)
-                if (!got && (spins & 7u) == 0u) {
-                    const uint32_t act = ld_agent(active);
-                    const uint32_t tl1 = ld_agent(tail), hd1 = ld_agent(head);
-                    fin = act == 0u && hd1 >= (tl1 < VHX_OVF_CAP ? tl1 : VHX_OVF_CAP);
-                }
-            }
-            got = __builtin_amdgcn_readfirstlane(__shfl(got, 0));
-            h0 = __builtin_amdgcn_readfirstlane(__shfl(h0, 0));
-            fin = __builtin_amdgcn_readfirstlane(__shfl(fin, 0));
-            if (!got) {
-                if (fin || ++spins >= VHX_SPLIT_SPINS) break;
-                if ((s.diag & 2u) && lane == 0) atomicAdd(s.ctl + 384, 1u);
-                if (!waiting) {
-                    if (!registered) {  // at most s.max_wait waves wait (pollers of one line slow the whole chip)
-                        uint32_t before = 0;
-                        if (lane == 0) before = atomicAdd(nwait, 1u);
-                        before = __builtin_amdgcn_readfirstlane(__shfl(before, 0));
-                        if (before >= s.max_wait) {
-                            if (lane == 0) atomicSub(nwait, 1u);
-                            break;
-                        }
-                        registered = true;
-                    }
-                    if (lane == 0) atomicAdd(idle, 1u);  // bookable by a tracing wave
-                    waiting = true;
-                }
-                __builtin_amdgcn_s_sleep(32);  // ~2000 cycles between polls (few waves wait: s.max_wait)
-                continue;
-            }
-            waiting = false;  // a tracing wave that handed rays over booked this wave (took it off `idle`)
-            from_ovf = true;
-            base = h0;
-            cnt = got;
-        }
-        if (lane == 0) atomicAdd(active, 1u);
-        if (lane < cnt) {
-            uint32_t idx = VHX_OVF_SKIP;
-            St4 st;
-            if (from_ovf) {
-                if (!take_slot(s, base + lane, idx, st)) {
-                    atomicOr(s.ctl + 256, 1u);  // a slot that never filled (diagnostics: VHX_DEBUG_PASSES)
-                    idx = VHX_OVF_SKIP;
-                }
-            } else {
-                idx = in[base + lane];
-                const uint4 *sp = q.state + 4ull * idx;
-                st.a = sp[0];
-                st.b = sp[1];
-                st.c = sp[2];
-                st.e = sp[3];
-            }
-            if (idx != VHX_OVF_SKIP) {
-                F3d o, d;
-                const QueueArgs *a = qa;
-                asm volatile("" : "+s"(a));
-                ray_of(a->cam, a->src, idx, o, d);
-                HitOut h;
-                h.bytes = 0;
-                if (trace_split<BD>(t, occ_tab, o, d, h, st, idx, s)) {
-                    const QueueArgs *b = qa;
-                    asm volatile("" : "+s"(b));
-                    if (b->src.kind == 3u)
-                        store_shadow(b->out, idx, h);
-                    else
-                        store(t, b->out, idx, o, h);
-                }
-            }
-        }
-        if (lane == 0) atomicSub(active, 1u);
-    }
-    if (waiting && lane == 0) atomicSub(idle, 1u);
-    if (registered && lane == 0) atomicSub(nwait, 1u);
-}
-
-// ------------------------------------------------------------------------------------------------ one-launch frame
-// k_trace_frame: a primary framebuffer frame's whole pass ladder in ONE persistent launch, so that no
-// pass waits for the end of the one before it. Every wave loops: it takes a full chunk of 64 rays from the deepest
-// pass queue that has one (the oldest rays first), else an 8x8 pixel tile of pass 0, else -- after a few idle polls --
-// a partial chunk; it traces them to the pass budget and appends the rays it abandons, each with its loop state, to the
-// next pass's queue.
-// Every hand-off stays inside one XCD: the tiles are dealt to the XCDs in runs of FQ_RUN (XCC_ID, read in the kernel),
-// and each XCD has its own counters and queues, so a ray abandoned on an XCD is resumed there. Within one XCD's L2 a
-// hand-off needs no fence and no write-through: the producer stores the slot's 64 B of state with plain stores (they
-// stay in that L2), waits for them (vmcnt(0)), then stores the slot's {output index, frame epoch} word; the consumer
-// polls that word and reads the state with sc1 loads (L2-served, past its CU's L1). The counters are XCD-local atomics
-// (workgroup scope: executed in that L2) read by sc1 loads. (Cross-XCD forms -- agent-scope granules -- measured 30-110
-// ms per frame: every granule a fabric write) A wave leaves when its XCD's tiles are all traced,
-// its queues drained and no wave there traces a budgeted pass (the rays of the unbounded last pass finish where they
-// are); every poll loop is bounded (an error word, which the parity tests would show). Results are the reference's: a
-// ray's traversal is deterministic and its state is handed over whole (Trav::packed / begin_resumed).
-#define VHX_FRAME_PASSES (VHX_MAX_BUDGETS + 1u)
-#define FQ_RUN 16u               // consecutive 8x8 tiles per XCD run
-#define FQ_SLOT 5u               // uint4 per queue slot: the 4 of Trav::packed, then {output index, epoch, 0, 0}
-#define FQ_LINE 64u              // counter stride (256 B: one line each)
-#define FQ_XWORDS (FQ_LINE * (3u + 3u * VHX_FRAME_PASSES))  // one XCD's counters
-#define FQ_WORDS (8u * FQ_XWORDS + FQ_LINE)                  // eight XCDs, then the error word
-#define VHX_FRAME_SPINS (1u << 18)  // idle polls before a wave gives up (sets the error word)
-struct FrameQ {
-    uint32_t *ctl;                      // FQ_WORDS counters, zeroed before the launch
-    uint4 *slots;                       // queues of passes 1 .. npass-1 of every XCD
-    uint64_t capx;                      // slots per (XCD, pass) queue: every ray of the XCD's tiles
-    uint32_t budget[VHX_FRAME_PASSES];  // step budget of pass p (VHX_MAX_ITERS: the last)
-    uint32_t npass, epoch, ntiles, tiles_x, sparse0;
-};
-__global__ void k_put_frameq(FrameQ f, FrameQ *dst) {
-    if (threadIdx.x == 0) *dst = f;
-}
-// an XCD's counters: [0] tile counter, [1] tiles traced, [2] waves started, then res / head / active of each pass
-__device__ __forceinline__ uint32_t *fq_x(const FrameQ &f, uint32_t x, uint32_t k) { return f.ctl + x * FQ_XWORDS + FQ_LINE * k; }
-__device__ __forceinline__ uint32_t *fq_res(const FrameQ &f, uint32_t x, uint32_t p) { return fq_x(f, x, 3u + p); }
-__device__ __forceinline__ uint32_t *fq_head(const FrameQ &f, uint32_t x, uint32_t p) {
-    return fq_x(f, x, 3u + VHX_FRAME_PASSES + p);
-}
-__device__ __forceinline__ uint32_t *fq_active(const FrameQ &f, uint32_t x, uint32_t p) {
-    return fq_x(f, x, 3u + 2u * VHX_FRAME_PASSES + p);
-}
-__device__ __forceinline__ uint32_t *fq_err(const FrameQ &f) { return f.ctl + 8u * FQ_XWORDS; }
-__device__ __forceinline__ uint4 *fq_slot(const FrameQ &f, uint32_t x, uint32_t p, uint32_t slot) {
-    return f.slots + ((uint64_t)(x * (VHX_FRAME_PASSES - 1u) + (p - 1u)) * f.capx + slot) * FQ_SLOT;
-}
-// XCD-local counter atomics: executed in the XCD's L2, which every CU of the XCD shares
-__device__ __forceinline__ uint32_t xadd(uint32_t *p, uint32_t v) {
-    return __hip_atomic_fetch_add((gu32 *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ bool xcas(uint32_t *p, uint32_t &expected, uint32_t desired) {
-    return __hip_atomic_compare_exchange_strong((gu32 *)p, &expected, desired, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ unsigned long long ld2_l2(const void *p) {  // sc1: past this CU's L1, from the XCD's L2
-    return __hip_atomic_load((const gu64 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void fq_publish(uint4 *sl, uint32_t idx, uint32_t epoch, const St4 &st) {
-    sl[0] = st.a;
-    sl[1] = st.b;
-    sl[2] = st.c;
-    sl[3] = st.e;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the state in the XCD's L2 before the word that publishes it
-    sl[4] = make_uint4(idx, epoch, 0u, 0u);
-}
-// polls a slot its producer has reserved until it carries this frame's epoch; false after VHX_FRAME_SPINS polls
-__device__ __forceinline__ bool fq_take(const uint4 *sl, uint32_t epoch, uint32_t &idx, St4 &st) {
-    for (uint32_t spins = 0; spins < VHX_FRAME_SPINS; ++spins) {
-        const unsigned long long w = ld2_l2(sl + 4);
-        if ((uint32_t)(w >> 32) == epoch) {
-            idx = (uint32_t)w;
-            uint32_t v[16];
-#pragma unroll
-            for (uint32_t k = 0; k < 8u; ++k) {
-                const unsigned long long x = ld2_l2((const unsigned long long *)sl + k);
-                v[2 * k] = (uint32_t)x;
-                v[2 * k + 1] = (uint32_t)(x >> 32);
-            }
-            st.a = make_uint4(v[0], v[1], v[2], v[3]);
-            st.b = make_uint4(v[4], v[5], v[6], v[7]);
-            st.c = make_uint4(v[8], v[9], v[10], v[11]);
-            st.e = make_uint4(v[12], v[13], v[14], v[15]);
-            return true;
-        }
-        __builtin_amdgcn_s_sleep(1);
-    }
-    return false;
-}
-// One ray of a k_trace_frame work unit, get_by_ray's shape with the state in registers: a fresh ray, or a resumed one
-// from its handed-over state `in`; traced to `budget` (pass 0: with sparse-wave abandonment). false: abandoned, its loop
-// state in `out`; true: finished, h filled.
-template <int BD>
-__device__ __forceinline__ bool trace_unit(const DevTree &t, const uint64_t *occ_tab, F3d o, F3d d, HitOut &h,
-                                           uint32_t budget, uint32_t sparse, bool resumed, const St4 &in, St4 &out) {
-    Trav<false, BD, false> tr;
-    h.iters = 0;
-    if (resumed)
-        tr.begin_resumed(t, o, d, h, in);
-    else if (!tr.begin(t, o, d, h, nullptr, 0, false))
-        return true;
-    for (;;) {
-        tr.step(t, occ_tab, h, budget);
-        if (tr.ex != 0u) break;
-        if (sparse && (uint32_t)__popcll(__ballot(1)) < sparse) {
-            tr.ex = 3u;
-            break;
-        }
-    }
-    if (tr.ex == 3u) {
-        out = tr.packed();
-        return false;
-    }
-    tr.end(t, h, nullptr, 0);
-    return true;
-}
-
-// 4 waves per SIMD (128 VGPRs, a few spills outside the walk loops): the hand-offs' state in and out of registers does
-// not fit the queue kernel's 96 (5 waves: 220 B of scratch per lane)
-template <int BD>
-#ifndef VHX_FRAME_WPE
-#define VHX_FRAME_WPE 4
-#endif
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VHX_FRAME_WPE)))
-k_trace_frame(DevTree t, const QueueArgs *qa, const FrameQ *fq) {
-    __shared__ uint64_t occ_tab[OCC_TAB_WORDS];
-    fill_occ_tab(occ_tab, t);
-    __syncthreads();  // the only barrier: the waves of a workgroup go their own ways from here
-    const uint32_t lane = threadIdx.x & 63u;
-    // the frame's queue description is read through a pointer laundered at each use (FQ_AT): loads of it hoisted to
-    // the kernel's start would be held across the traversal
-#define FQ_AT(f)                   \
-    const FrameQ *f##_p = fq;       \
-    asm volatile("" : "+s"(f##_p)); \
-    const FrameQ &f = *f##_p
-    uint32_t xcc;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    const uint32_t x = xcc & 7u;
-    uint32_t ntx;  // this XCD's tiles: runs x, x + 8, ... of FQ_RUN tiles
-    {
-        FQ_AT(f);
-        const uint32_t runs = (f.ntiles + FQ_RUN - 1u) / FQ_RUN;
-        const uint32_t myruns = runs > x ? (runs - x + 7u) / 8u : 0u;
-        ntx = myruns * FQ_RUN;
-        if (myruns && (runs - 1u) % 8u == x) ntx -= runs * FQ_RUN - f.ntiles;  // the frame's last run is short
-        if (lane == 0) xadd(fq_x(f, x, 2), 1u);
-    }
-    uint32_t idle = 0;
-    bool tiles_left = true;
-    for (;;) {
-        // ---- the next work unit (one lane decides, the wave follows): pass wp, first entry / tile wb, wc rays
-        int32_t wp = -1;
-        uint32_t wb = 0, wc = 0, quit = 0;
-        if (lane == 0) {
-            FQ_AT(f);
-            const uint32_t P = f.npass;
-            const uint32_t want = idle >= 6u ? 1u : (64u >> idle);  // full chunks first, partial ones once idle
-            for (int32_t p = (int32_t)P - 1; p >= 1 && wp < 0; --p) {
-                uint32_t *hp = fq_head(f, x, (uint32_t)p);
-                uint32_t h = (uint32_t)ld2_l2(hp);
-                for (uint32_t tries = 0; tries < 4u; ++tries) {
-                    const uint32_t r = (uint32_t)ld2_l2(fq_res(f, x, (uint32_t)p));
-                    if (r <= h || r - h < want) break;
-                    const uint32_t n = r - h < 64u ? r - h : 64u;
-                    if (xcas(hp, h, h + n)) {
-                        wp = p;
-                        wb = h;
-                        wc = n;
-                        break;
-                    }
-                }
-            }
-            if (wp < 0 && tiles_left) {
-                const uint32_t k = xadd(fq_x(f, x, 0), 1u);
-                if (k < ntx) {
-                    wp = 0;
-                    wb = ((k / FQ_RUN) * 8u + x) * FQ_RUN + k % FQ_RUN;
-                    wc = 64u;
-                } else {
-                    tiles_left = false;
-                }
-            }
-            if (wp > 0) {
-                xadd(fq_active(f, x, (uint32_t)wp), 1u);
-            } else if (wp < 0) {
-                // nothing more can come on this XCD: its tiles traced, its queues drained, no wave in a budgeted
-                // queue pass (the rays of the last pass still tracing append nothing)
-                bool fin = (uint32_t)ld2_l2(fq_x(f, x, 1)) >= ntx;
-                for (uint32_t p = 1; p + 1 < P && fin; ++p) fin = (uint32_t)ld2_l2(fq_active(f, x, p)) == 0u;
-                for (uint32_t p = 1; p < P && fin; ++p)
-                    fin = (uint32_t)ld2_l2(fq_head(f, x, p)) >= (uint32_t)ld2_l2(fq_res(f, x, p));
-                quit = fin ? 1u : 0u;
-            }
-        }
-        wp = (int32_t)__builtin_amdgcn_readfirstlane(__shfl(wp, 0));
-        if (wp < 0) {
-            quit = __builtin_amdgcn_readfirstlane(__shfl(quit, 0));
-            if (quit) break;
-            if (++idle >= VHX_FRAME_SPINS) {
-                FQ_AT(f);
-                if (lane == 0) atomicOr(fq_err(f), 1u);
-                break;
-            }
-            // back off (the idle waves of an XCD poll its counter lines): ~1, then ~4, then ~16 us between polls
-            const uint32_t naps = idle < 4u ? 1u : (idle < 8u ? 4u : 16u);
-            for (uint32_t i = 0; i < naps; ++i) __builtin_amdgcn_s_sleep(32);
-            continue;
-        }
-        idle = 0;
-        wb = __builtin_amdgcn_readfirstlane(__shfl(wb, 0));
-        wc = __builtin_amdgcn_readfirstlane(__shfl(wc, 0));
-        const QueueArgs *a = qa;
-        asm volatile("" : "+s"(a));  // read where used (not held in scalar registers across the traversal)
-        const uint32_t W = a->cam.width, H = a->cam.height;
-        // ---- its rays: a pass-0 tile, or queued rays with their saved state
-        bool have = false;
-        uint32_t idx = 0, px = 0, py = 0;
-        St4 st;
-        if (wp == 0) {
-            FQ_AT(f);
-            px = (wb % f.tiles_x) * 8u + (lane & 7u);
-            py = (wb / f.tiles_x) * 8u + (lane >> 3);
-            have = px < W && py < H;
-            idx = py * W + px;
-        } else if (lane < wc) {
-            FQ_AT(f);
-            have = fq_take(fq_slot(f, x, (uint32_t)wp, wb + lane), f.epoch, idx, st);
-            if (!have) atomicOr(fq_err(f), 2u);  // a reserved slot that never filled: the ray is lost (parity fails)
-            py = idx / W;
-            px = idx - py * W;
-        }
-        // ---- trace to the pass budget; the rays over it go to the next pass's queue (it holds a slot for every ray)
-        F3d o, d;
-        HitOut h;
-        h.bytes = 0;
-        bool fin = true;
-        St4 out;
-        if (have) {
-            primary_ray(a->cam, px, py, o, d);
-            uint32_t budget, sparse;
-            {
-                FQ_AT(g);
-                budget = g.budget[wp];
-                sparse = wp == 0 ? g.sparse0 : 0u;
-            }
-            fin = trace_unit<BD>(t, occ_tab, o, d, h, budget, sparse, wp > 0, st, out);
-        }
-        const uint64_t m = __ballot(!fin);
-        if (m) {
-            const uint32_t first = (uint32_t)__builtin_ctzll(m);
-            uint32_t base = 0;
-            FQ_AT(g);
-            if (lane == first) base = xadd(fq_res(g, x, (uint32_t)wp + 1u), (uint32_t)__popcll(m));
-            base = __shfl(base, (int)first);
-            if (!fin)
-                fq_publish(fq_slot(g, x, (uint32_t)wp + 1u, base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))),
-                           idx, g.epoch, out);
-        }
-        if (have && fin) {
-            const QueueArgs *b = qa;
-            asm volatile("" : "+s"(b));  // the outputs' pointers loaded here, not held across the traversal
-            store(t, b->out, idx, o, h);
-        }
-        if (lane == 0) {
-            FQ_AT(g);
-            // a unit is done once its rays are stored or queued (the publishes above waited for their stores)
-            xadd(wp > 0 ? fq_active(g, x, (uint32_t)wp) : fq_x(g, x, 1), wp > 0 ? 0xFFFFFFFFu : 1u);
-        }
-    }
-#undef FQ_AT
 }
 
 // Scatters rank-gathered tile buffers into framebuffers. Rank r's part of `gathered` holds `planes` planes of
@@ -1733,10 +1097,7 @@ static int finish_out(vhx_ctx *c, HostOut &ho) {
 static void select_schedule(vhx_ctx *c) {
     if (!c->adaptive) {
         c->last_sched = -1;
-        c->split = c->split_force > 0 ? 1u : 0u;
-        c->ahead = c->ahead_force > 0 ? 1u : 0u;
         c->qsort = c->qsort_force >= 0 ? (uint32_t)c->qsort_force : c->sched_busy.qsort;  // a fixed schedule: the busy one's
-        c->one = c->one_force > 0 ? 1u : 0u;
         return;
     }
     bool busy = false;
@@ -1754,10 +1115,7 @@ static void select_schedule(vhx_ctx *c) {
     c->npass = s.npass;
     c->queue_waves = s.queue_waves_per_cu * c->cus;
     c->qorder = s.qorder;
-    c->split = c->split_force >= 0 ? (uint32_t)c->split_force : s.split;
-    c->ahead = c->ahead_force >= 0 ? (uint32_t)c->ahead_force : s.ahead;
     c->qsort = c->qsort_force >= 0 ? (uint32_t)c->qsort_force : s.qsort;
-    c->one = c->one_force >= 0 ? (uint32_t)c->one_force : s.one;
     c->last_sched = busy ? 1 : 0;
 }
 
@@ -1781,10 +1139,6 @@ static int prepare_passes(vhx_ctx *c, uint64_t nout, uint64_t nblocks0, uint32_t
     if (!rc) rc = ensure(c, c->offsets, chunks * 4);
     if (!rc) rc = ensure(c, c->flags, ((nout + 3) & ~3ull));
     if (!rc && c->resume && npass > 1) rc = ensure(c, c->state, nout * 64);
-    if (!rc && c->split && npass > 1 && !c->ovf.ptr) {  // overflow slots of the tail split, zeroed once (epoch 0)
-        rc = ensure(c, c->ovf, (uint64_t)VHX_OVF_CAP * VHX_OVF_STRIDE * 8u);
-        if (!rc) VHX_HIP(c, hipMemsetAsync(c->ovf.ptr, 0, c->ovf.bytes, c->stream));
-    }
     return rc;
 }
 
@@ -1816,10 +1170,6 @@ static PassQ pass_q(const vhx_ctx *c, uint32_t p, uint32_t npass) {
     q.state = c->resume && npass > 1 && p >= c->save_from ? (uint4 *)c->state.ptr : nullptr;
     q.resume = c->resume && p > c->save_from ? 1u : 0u;
     q.sparse = last || !q.state ? 0u : c->sparse[p];
-    q.skip = nullptr;
-    q.cost = p > 0 && last ? c->ahead_rec : nullptr;  // the unbounded pass finishes the rays over the pass-0 budget
-    q.in_cap = 0;
-    q.prio = 0;
     return q;
 }
 
@@ -1834,14 +1184,6 @@ static void debug_passes(vhx_ctx *c, const char *what) {
     (void)hipMemcpy(v, c->qctl.ptr, sizeof(v), hipMemcpyDeviceToHost);
     fprintf(stderr, "[vhx passes] %-24s counts %u %u %u %u ... %u  grabs %u %u %u %u\n", what, v[0], v[1], v[2], v[3],
             v[7], v[8], v[9], v[10], v[11]);
-    if (c->split) {  // tail split: slots reserved / taken, waves waiting / holding rays, error word
-        uint32_t w[9];
-        for (uint32_t k = 0; k < 9u; ++k)
-            (void)hipMemcpy(&w[k], (uint32_t *)c->qctl.ptr + QCTL_SPLIT + 64u * k, 4, hipMemcpyDeviceToHost);
-        fprintf(stderr, "[vhx passes] %-24s split slots %u taken %u idle %u active %u error %u slot polls failed %u "
-                "waiter polls %u ray iterations %u wave iterations %u\n", what, w[0], w[1], w[2], w[3], w[4], w[5], w[6],
-                w[7], w[8]);
-    }
 }
 
 // Chunk lists -> queue `out` with its length at *total: pass-0 style (nchunks_host workgroup chunks of stride 256) or
@@ -1953,28 +1295,8 @@ static int launch_queue_passes(vhx_ctx *c, const DevTree &t, const CamD &cam, co
         const uint32_t qwaves = p == 0 ? c->queue_waves0
                                 : (p + 1 < npass && c->queue_waves_mid ? c->queue_waves_mid : c->queue_waves);
         const unsigned qgrid = (qwaves * 64u + c->qblock - 1) / c->qblock;
-        bool launched = false;
-        if constexpr (!COUNT && !MIP) {
-            // a lone frame's unbounded last pass over resumed rays: with the tail split (k_trace_queue_split)
-            if (p + 1 == npass && p > 0 && c->split && q.resume && q.state) {
-                SplitQ sq;
-                sq.ovf = (unsigned long long *)c->ovf.ptr;
-                sq.ctl = ctl + QCTL_SPLIT;
-                sq.epoch = ++c->split_epoch == 0u ? ++c->split_epoch : c->split_epoch;  // never 0 (fresh slots)
-                sq.period = c->split_period;
-                sq.min_lanes = c->split_min_lanes;
-                sq.min_idle = c->split_min_idle;
-                sq.take = c->split_take;
-                sq.diag = c->split_diag;
-                sq.max_wait = c->split_max_wait;
-                k_trace_queue_split<BD><<<qgrid, c->qblock, 0, c->stream>>>(t, qa, in, in_n,
-                                                                            ctl + 16u + QCTL_PASS_WORDS * p, q, sq);
-                launched = true;
-            }
-        }
-        if (!launched)
-            k_trace_queue<COUNT, BD, MIP><<<qgrid, c->qblock, 0, c->stream>>>(t, qa, in, in_n,
-                                                                             ctl + 16u + QCTL_PASS_WORDS * p, q);
+        k_trace_queue<COUNT, BD, MIP><<<qgrid, c->qblock, 0, c->stream>>>(t, qa, in, in_n,
+                                                                         ctl + 16u + QCTL_PASS_WORDS * p, q);
         debug_passes(c, "queue pass");
         if (p + 1 < npass) {
             rc = compact_chunks(c, 0, in_n, q.rpw, q.rpw, (uint32_t *)c->queue[p & 1u].ptr, ctl + p,
@@ -1983,87 +1305,6 @@ static int launch_queue_passes(vhx_ctx *c, const DevTree &t, const CamD &cam, co
         }
     }
     return rc;
-}
-
-// k_trace_frame for a whole framebuffer frame: the pass ladder of the schedule in force, per XCD and
-// pass a queue slot for every ray of the XCD's tiles (80 B each: 4 GB for a 3840x2160 frame, of a context that traces
-// one-launch frames), the counters zeroed on c's stream, one workgroup per resident slot (four per CU).
-template <int BD>
-static int launch_frame(vhx_ctx *c, const DevTree &t, const CamD &cam, const RaySrc &src, const OutD &o, uint64_t nout,
-                        uint32_t npass) {
-    FrameQ f{};
-    f.npass = std::min<uint32_t>(npass, VHX_FRAME_PASSES);
-    for (uint32_t p = 0; p < f.npass; ++p) f.budget[p] = p + 1 < f.npass ? c->budgets[p] : VHX_MAX_ITERS;
-    f.sparse0 = c->sparse[0];
-    f.tiles_x = (cam.width + 7u) / 8u;
-    f.ntiles = f.tiles_x * ((cam.height + 7u) / 8u);
-    const uint64_t runs = (f.ntiles + FQ_RUN - 1u) / FQ_RUN;
-    f.capx = (runs + 7u) / 8u * FQ_RUN * 64u;  // every ray of an XCD's tiles
-    const uint64_t slot_bytes = 8ull * (VHX_FRAME_PASSES - 1u) * f.capx * FQ_SLOT * sizeof(uint4);
-    (void)nout;
-    const bool fresh = c->fq_slots.bytes < slot_bytes;
-    int rc = ensure(c, c->fq_slots, slot_bytes);
-    if (!rc) rc = ensure(c, c->fq_ctl, FQ_WORDS * sizeof(uint32_t) + sizeof(FrameQ));  // counters, then the FrameQ
-    if (rc) return rc;
-    if (fresh) {  // a new allocation holds no epoch of this context's frames: tags from 1 again
-        VHX_HIP(c, hipMemsetAsync(c->fq_slots.ptr, 0, c->fq_slots.bytes, c->stream));
-        c->fq_epoch = 0;
-    }
-    f.epoch = ++c->fq_epoch == 0u ? ++c->fq_epoch : c->fq_epoch;
-    f.ctl = (uint32_t *)c->fq_ctl.ptr;
-    f.slots = (uint4 *)c->fq_slots.ptr;
-    VHX_HIP(c, hipMemsetAsync(c->fq_ctl.ptr, 0, FQ_WORDS * sizeof(uint32_t), c->stream));
-    QueueArgs *qa = nullptr;
-    if ((rc = put_qargs(c, cam, src, o, qa))) return rc;
-    FrameQ *fd = (FrameQ *)((uint8_t *)c->fq_ctl.ptr + FQ_WORDS * sizeof(uint32_t));
-    k_put_frameq<<<1, 64, 0, c->stream>>>(f, fd);
-    k_trace_frame<BD><<<c->cus * VHX_FRAME_WPE, 256, 0, c->stream>>>(t, qa, fd);
-    VHX_HIP(c, hipGetLastError());
-    return VHX_OK;
-}
-
-// The ahead stream's fork, on c's stream before pass 0: k_ahead_pick lists the previous frame's long
-// rays (their flags marked VHX_FLAG_AHEAD), then the second stream traces them from scratch, unbudgeted, ahead_rpw rays
-// per wave, into the frame's outputs and records their step counts; ev_join marks its end.
-template <int BD>
-static int fork_ahead(vhx_ctx *c, const DevTree &t, const CamD &cam, const RaySrc &src, const OutD &o, uint64_t nout,
-                      bool count) {
-    uint32_t *ctl = (uint32_t *)c->qctl.ptr;
-    VHX_HIP(c, hipMemsetAsync(ctl + QCTL_AHEAD, 0, 3u * 64u * sizeof(uint32_t), c->stream));
-    const unsigned nb = (unsigned)((nout + 255) / 256);
-    k_ahead_hist<<<nb, 256, 0, c->stream>>>((const uint8_t *)c->flags.ptr, (const uint32_t *)c->ahead_cost.ptr, nout,
-                                            c->ahead_min, ctl + QCTL_AHEAD);
-    k_ahead_pick<<<nb, 256, 0, c->stream>>>((uint8_t *)c->flags.ptr, (const uint32_t *)c->ahead_cost.ptr, nout,
-                                            c->ahead_min, c->ahead_cap, (uint32_t *)c->ahead_list.ptr,
-                                            ctl + QCTL_AHEAD);
-    VHX_HIP(c, hipGetLastError());
-    QueueArgs *qa = nullptr;
-    int rc = put_qargs(c, cam, src, o, qa);
-    if (rc) return rc;
-    VHX_HIP(c, hipEventRecord(c->ev_fork, c->stream));
-    VHX_HIP(c, hipStreamWaitEvent(c->aux_stream, c->ev_fork, 0));
-    PassQ q{};
-    q.budget = VHX_MAX_ITERS;
-    q.rpw = c->ahead_rpw;
-    q.tw = c->tw;
-    q.counts = (uint32_t *)c->counts.ptr;  // unused: the unbounded pass lists nothing
-    q.cost = (uint32_t *)c->ahead_cost.ptr;
-    q.in_cap = c->ahead_cap;
-    q.prio = c->ahead_prio;
-    const uint32_t waves = std::min<uint32_t>(2048u, (c->ahead_cap + c->ahead_rpw - 1) / c->ahead_rpw);
-    const unsigned grid = (waves * 64u + 255u) / 256u;
-    const uint32_t *list = (const uint32_t *)c->ahead_list.ptr;
-    if (t.mips)
-        k_trace_queue<false, BD, true><<<grid, 256, 0, c->aux_stream>>>(t, qa, list, ctl + QCTL_AHEAD,
-                                                                        ctl + QCTL_AHEAD + 64u, q);
-    else if (count)
-        k_trace_queue<true, BD><<<grid, 256, 0, c->aux_stream>>>(t, qa, list, ctl + QCTL_AHEAD, ctl + QCTL_AHEAD + 64u, q);
-    else
-        k_trace_queue<false, BD><<<grid, 256, 0, c->aux_stream>>>(t, qa, list, ctl + QCTL_AHEAD, ctl + QCTL_AHEAD + 64u,
-                                                                  q);
-    VHX_HIP(c, hipGetLastError());
-    VHX_HIP(c, hipEventRecord(c->ev_join, c->aux_stream));
-    return VHX_OK;
 }
 
 // ------------------------------------------------------------------------------------------------ C ABI
@@ -2140,8 +1381,7 @@ void vhx_destroy(vhx_ctx *c) {
     c->tree.reset();  // frees the device tree with its last context
     if (c->use_ev) (void)hipEventDestroy(c->use_ev);
     for (DevBuf *b : {&c->scratch, &c->rays, &c->queue[0], &c->queue[1], &c->qctl, &c->tmp, &c->counts, &c->offsets,
-                      &c->flags, &c->qargs, &c->state, &c->upd, &c->prepass_depth, &c->ovf, &c->ahead_cost,
-                      &c->ahead_list, &c->fq_ctl, &c->fq_slots})
+                      &c->flags, &c->qargs, &c->state, &c->upd, &c->prepass_depth})
         if (b->ptr) (void)hipFree(b->ptr);
     for (auto &P : c->pinned) {
         if (P.ptr) (void)hipHostFree(P.ptr);
@@ -2150,9 +1390,6 @@ void vhx_destroy(vhx_ctx *c) {
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
-    if (c->aux_stream) (void)hipStreamDestroy(c->aux_stream);
-    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
-    if (c->ev_join) (void)hipEventDestroy(c->ev_join);
     delete c;
 }
 
@@ -2264,50 +1501,16 @@ static int apply_tuning(vhx_ctx *c, const std::string &key, const std::string &v
             code = lg | (m ? 16u : 0u) | (z ? 32u : 0u) | (rows ? 64u : 0u);
         }
         c->qorder = c->sched_busy.qorder = c->sched_idle.qorder = code;  // both schedules (the rest stays adaptive)
-    } else if (key == "split") {
-        if (!parse_u32(val, x) || x > 1) return bad();
-        c->split_force = (int)x;
-    } else if (key == "ahead") {
-        if (!parse_u32(val, x) || x > 1) return bad();
-        c->ahead_force = (int)x;
-    } else if (key == "qsort") {  // segment length of the queue passes' node sort: 0 = off, else 256 .. VHX_QSORT_MAX
+        } else if (key == "qsort") {  // segment length of the queue passes' node sort: 0 = off, else 256 .. VHX_QSORT_MAX
         if (!parse_u32(val, x) || (x && (x < 256 || x > VHX_QSORT_MAX || (x & (x - 1))))) return bad();
         c->qsort_force = (int)x;
-    } else if (key == "one") {
-        if (!parse_u32(val, x) || x > 1) return bad();
-        c->one_force = (int)x;
-    } else if (key == "qsortp") {  // bit mask of the queue passes whose input is sorted
+        } else if (key == "qsortp") {  // bit mask of the queue passes whose input is sorted
         if (!parse_u32(val, x)) return bad();
         c->qsort_passes = x;
     } else if (key == "qsortb") {
         if (!parse_u32(val, x) || x == 0) return bad();
         c->qsort_blocks = x;
-    } else if (key == "ahead_min") {
-        if (!parse_u32(val, x) || x == 0) return bad();
-        c->ahead_min = x;
-    } else if (key == "ahead_cap") {
-        if (!parse_u32(val, x) || x == 0 || x > (1u << 24)) return bad();
-        c->ahead_cap = x;
-    } else if (key == "ahead_prio") {
-        if (!parse_u32(val, x) || x > 1) return bad();
-        c->ahead_prio = x;
-    } else if (key == "ahead_rpw") {
-        if (!parse_u32(val, x) || x == 0 || x > 64) return bad();
-        c->ahead_rpw = x;
-    } else if (key == "split_wait") {
-        if (!parse_u32(val, x) || x == 0) return bad();
-        c->split_max_wait = x;
-    } else if (key == "split_diag") {
-        if (!parse_u32(val, x)) return bad();
-        c->split_diag = x;
-    } else if (key == "split_tune") {
-        if (!parse_u32_list(val, l, 4, n) || n != 4) return bad();
-        if (!l[0] || (l[0] & (l[0] - 1)) || l[1] < 2 || l[1] > 64 || l[2] < 1 || l[3] < 1 || l[3] > 64) return bad();
-        c->split_period = l[0];
-        c->split_min_lanes = l[1];
-        c->split_min_idle = l[2];
-        c->split_take = l[3];
-    } else {
+        } else {
         return fail(c, VHX_E_INVALID_ARG, ("vhx_set_tuning: unknown key " + key).c_str());
     }
     return VHX_OK;
@@ -2366,21 +1569,6 @@ int vhx_get_pass_budgets(const vhx_ctx *c, uint32_t *budgets, uint32_t *n, int *
     if (budgets)
         for (uint32_t i = 0; i < VHX_MAX_BUDGETS; ++i) budgets[i] = i < *n ? c->budgets[i] : 0u;
     if (sched) *sched = c->last_sched;
-    return VHX_OK;
-}
-
-int vhx_get_split_stats(vhx_ctx *c, uint32_t *handed_over, uint32_t *errors) {
-    if (!c) return VHX_E_INVALID_ARG;
-    uint32_t w[5] = {0, 0, 0, 0, 0};
-    if (c->split && c->split_epoch && c->qctl.ptr) {
-        (void)hipSetDevice(c->device);
-        VHX_STREAM(c);
-        VHX_HIP(c, hipStreamSynchronize(c->stream));
-        for (uint32_t k = 0; k < 5u; ++k)
-            VHX_HIP(c, hipMemcpy(&w[k], (uint32_t *)c->qctl.ptr + QCTL_SPLIT + 64u * k, 4, hipMemcpyDeviceToHost));
-    }
-    if (handed_over) *handed_over = w[0] < VHX_OVF_CAP ? w[0] : VHX_OVF_CAP;
-    if (errors) *errors = w[4];
     return VHX_OK;
 }
 
@@ -2538,22 +1726,9 @@ void vhx::copy_sched(vhx_ctx *c, const vhx_ctx *owner) {
     c->queue_waves_mid = owner->queue_waves_mid;
     c->qxcd = owner->qxcd;
     c->qxcd_all = owner->qxcd_all;
-    c->split_force = owner->split_force;
-    c->split_period = owner->split_period;
-    c->split_min_lanes = owner->split_min_lanes;
-    c->split_min_idle = owner->split_min_idle;
-    c->split_take = owner->split_take;
-    c->split_diag = owner->split_diag;
-    c->split_max_wait = owner->split_max_wait;
-    c->ahead_force = owner->ahead_force;
     c->qsort_force = owner->qsort_force;
-    c->one_force = owner->one_force;
     c->qsort_passes = owner->qsort_passes;
     c->qsort_blocks = owner->qsort_blocks;
-    c->ahead_min = owner->ahead_min;
-    c->ahead_cap = owner->ahead_cap;
-    c->ahead_rpw = owner->ahead_rpw;
-    c->ahead_prio = owner->ahead_prio;
     std::memcpy(c->sparse, owner->sparse, sizeof(c->sparse));
     c->prepass = owner->prepass;
     c->prepass_margin = owner->prepass_margin;
@@ -2845,42 +2020,8 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
     if (npass > 1 && layout == VHX_LAYOUT_FRAMEBUFFER && (tile_start > 0 || tile_stride > 1))
         VHX_HIP(c, hipMemsetAsync(c->flags.ptr, 0, nout, c->stream));
 
-    // the ahead stream (a lone framebuffer frame under a multi-pass schedule that selects it; not in the approximate
-    // prepass mode, whose rays start elsewhere): the previous frame's long rays listed and traced on the second stream
-    const bool ahead = c->ahead && npass > 1 && layout == VHX_LAYOUT_FRAMEBUFFER && tile_start == 0 && tile_stride == 1 &&
-                       !c->in_prepass && !fast;
-    bool predicted = false;
-    if (ahead) {
-        const bool fresh = c->ahead_cost.bytes < nout * 4;
-        if ((rc = ensure(c, c->ahead_cost, nout * 4)) || (rc = ensure(c, c->ahead_list, (uint64_t)c->ahead_cap * 4)))
-            return rc;
-        if (fresh) c->ahead_w = c->ahead_h = 0;
-        predicted = c->ahead_w == cam->width && c->ahead_h == cam->height;
-        if (!c->aux_stream) {  // the highest stream priority: the ahead pass's workgroups dispatch before pass 0's
-            int lo = 0, hi = 0;
-            VHX_HIP(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
-            VHX_HIP(c, hipStreamCreateWithPriority(&c->aux_stream, hipStreamNonBlocking, hi));
-        }
-        if (!c->ev_fork) VHX_HIP(c, hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
-        if (!c->ev_join) VHX_HIP(c, hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
-        c->ahead_rec = (uint32_t *)c->ahead_cost.ptr;  // this frame's queue passes record the next prediction
-    }
-    c->ahead_w = ahead ? cam->width : 0u;  // a frame without it leaves no prediction (its flags mean something else)
-    c->ahead_h = ahead ? cam->height : 0u;
-    // the main stream waits for the ahead pass on every exit after the fork (before the trace's use is recorded)
-    struct JoinGuard {
-        vhx_ctx *c;
-        bool armed = false;
-        ~JoinGuard() {
-            if (armed) (void)hipStreamWaitEvent(c->stream, c->ev_join, 0);
-        }
-    } join{c};
     const bool count = ho.dev.bytes != nullptr;
     int qrc = VHX_OK;
-    // the one-launch frame: a whole framebuffer frame under a multi-pass schedule that selects it (not with byte
-    // counting, node MIPs or the approximate prepass mode, which keep the per-pass launches)
-    const bool one = c->one && npass > 1 && layout == VHX_LAYOUT_FRAMEBUFFER && tile_start == 0 && tile_stride == 1 &&
-                     !count && !t.mips && !fast && !c->in_prepass && !ahead;
     // the queue order's frame (c->qorder): the framebuffer layout only. The tile layout's output index is already
     // tile-major with T-wide rows inside a tile (config 4 on one rank, 64x64 tiles: 2.019-2.025 ms per frame in that
     // order against 2.071-2.074 with the tiles re-ordered Morton inside, profiles/r03/qorder/mgpu1_*.log)
@@ -2888,17 +2029,8 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
     const uint32_t oh = cam->height;
     auto launch = [&](auto bd_tag) {
         constexpr int BD = decltype(bd_tag)::value;
-        if (one) {  // the whole ladder in one persistent launch
-            qrc = launch_frame<BD>(c, t, cd, src, ho.dev, nout, npass);
-            return;
-        }
         PassQ q0 = pass_q(c, 0, npass);
         if (npass > 1) q0.flags = (uint8_t *)c->flags.ptr;
-        if (predicted) {
-            if ((qrc = fork_ahead<BD>(c, t, cd, src, ho.dev, nout, count))) return;
-            join.armed = true;
-            q0.skip = (const uint8_t *)c->flags.ptr;
-        }
         if (t.mips) {  // MIP stand-ins (no byte counting, no depth prepass: refused above)
             k_trace_primary<false, BD, false, true><<<(unsigned)nblocks, 256, 0, c->stream>>>(
                 t, cd, ho.dev, T, tiles_x, tile_start, tile_stride, layout, bpx, bpt, q0);
@@ -2918,7 +2050,6 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
         }
     };
     const bool bd_ok = dispatch_bd(c->tree->desc.brick_dim, launch);
-    c->ahead_rec = nullptr;
     if (!bd_ok) return fail(c, VHX_E_INVALID_ARG, "unsupported brick_dim");
     if (qrc) return qrc;
     VHX_HIP(c, hipGetLastError());
@@ -2926,10 +2057,6 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
     // a shadow trace of this frame's hit records lists them in the same tile order (vhx_trace_shadows)
     c->last_fb_w = layout == VHX_LAYOUT_FRAMEBUFFER ? cam->width : 0u;
     c->last_fb_h = layout == VHX_LAYOUT_FRAMEBUFFER ? cam->height : 0u;
-    if (join.armed) {
-        join.armed = false;
-        VHX_HIP(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
-    }
     VHX_HIP(c, hipEventRecord(c->ev1, c->stream));
     c->timed = true;
     if ((rc = tscope.end())) return rc;  // a later write of the tree waits for this frame

@@ -298,12 +298,6 @@ class Raytracer:
         self._check(N.lib().vhx_get_pass_budgets(self._h, b, ctypes.byref(n), ctypes.byref(sched)))
         return tuple(b[:n.value]), {1: "busy", 0: "idle"}.get(sched.value, "fixed")
 
-    def split_stats(self):
-        """(rays handed over between waves, failed hand-offs) by the tail split of the last trace (synchronises)."""
-        h, e = ctypes.c_uint32(), ctypes.c_uint32()
-        self._check(N.lib().vhx_get_split_stats(self._h, ctypes.byref(h), ctypes.byref(e)))
-        return h.value, e.value
-
     def sync(self):
         ms = ctypes.c_float()
         self._check(N.lib().vhx_sync(self._h, ctypes.byref(ms)))
