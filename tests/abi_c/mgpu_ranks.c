@@ -9,9 +9,11 @@
  *   TREE_FILE  the consumer.c tree file (tree + camera A);  CAMB_FILE  raw vhx_camera bytes of camera B
  *   ROOT_SLOTS R (MODE "balance": chosen by vhx_mgpu_balance instead)
  *   FRAMES     frames rendered, alternating camera A and B (A first), every one submitted without waiting
- *   MODE       "plain" | "balance"
+ *   MODE       "plain" | "balance" | "rgba" (plain with one plane: vhx_mgpu_set_planes(m, 1) on every rank, rank 0
+ *              passes fb_depth = NULL, so its depth framebuffers keep their 0xAB fill)
  *   OUT_FILE   rank 0's framebuffers after the last frame of each camera: rgbaA | depthA | rgbaB | depthB
- * prints one line per rank (rays, measured trace / transfer ms) and "root_slots R", then "ok"; exit 1 on failure. */
+ * prints one line per rank (rays, measured trace / transfer ms, bytes into rank 0 per frame) and "root_slots R", then
+ * "ok"; exit 1 on failure. */
 #define _POSIX_C_SOURCE 200809L
 #include <hip/hip_runtime_api.h>
 #include <pthread.h>
@@ -27,7 +29,7 @@
 static vhx_tree_desc g_tree;
 static vhx_camera g_cam[2];
 static uint8_t g_id[VHX_MGPU_ID_BYTES];
-static int g_n, g_R, g_F, g_overlap, g_frames, g_balance;
+static int g_n, g_R, g_F, g_overlap, g_frames, g_balance, g_rgba;
 static const char *g_out;
 
 typedef struct {
@@ -37,6 +39,7 @@ typedef struct {
     uint64_t rays;
     float trace_ms, xfer_ms;
     uint32_t R;
+    uint64_t root_bytes;
 } rank_state;
 
 #define RCHECK(call)                                                                                              \
@@ -61,6 +64,7 @@ static void *rank_main(void *arg) {
     RCHECK(vhx_mgpu_set_frames_in_flight(m, (uint32_t)g_F));
     RCHECK(vhx_mgpu_set_overlap(m, g_overlap));
     RCHECK(vhx_mgpu_broadcast_tree(m, s->rank == 0 ? &g_tree : NULL));
+    if (g_rgba) RCHECK(vhx_mgpu_set_planes(m, 1));
     if (g_balance) {
         RCHECK(vhx_mgpu_balance(m, &g_cam[0], 3, &s->R, NULL, NULL));
     } else {
@@ -77,9 +81,10 @@ static void *rank_main(void *arg) {
             }
     /* every frame submitted back to back: frames in flight on F contexts, gathers overlapping the next traces */
     for (int k = 0; k < g_frames; ++k)
-        RCHECK(vhx_mgpu_render(m, &g_cam[k & 1], (uint32_t *)fb[k & 1], (float *)fbd[k & 1]));
+        RCHECK(vhx_mgpu_render(m, &g_cam[k & 1], (uint32_t *)fb[k & 1], g_rgba ? NULL : (float *)fbd[k & 1]));
     RCHECK(vhx_mgpu_sync(m, NULL));
     RCHECK(vhx_mgpu_info(m, g_cam[0].width, g_cam[0].height, NULL, NULL, &s->rays));
+    RCHECK(vhx_mgpu_frame_bytes(m, g_cam[0].width, g_cam[0].height, &s->root_bytes));
     RCHECK(vhx_mgpu_measure(m, &g_cam[0], 2, &s->trace_ms, &s->xfer_ms));
     if (s->rank == 0) {
         host = (uint32_t *)malloc(16 * n);
@@ -132,6 +137,7 @@ int main(int argc, char **argv) {
     g_overlap = atoi(argv[7]);
     g_frames = atoi(argv[8]);
     g_balance = strcmp(argv[9], "balance") == 0;
+    g_rgba = strcmp(argv[9], "rgba") == 0;
     if (g_n < 1 || g_n > MAX_RANKS || g_frames < 2) return 1;
     FILE *f = fopen(argv[1], "rb");
     char magic[4];
@@ -190,8 +196,9 @@ int main(int argc, char **argv) {
     uint64_t rays = 0;
     for (int r = 0; r < g_n; ++r) {
         pthread_join(th[r], NULL);
-        printf("rank %d rc %d rays %llu trace_ms %.4f transfer_ms %.4f R %u %s\n", r, st[r].rc,
-               (unsigned long long)st[r].rays, st[r].trace_ms, st[r].xfer_ms, st[r].R, st[r].err);
+        printf("rank %d rc %d rays %llu trace_ms %.4f transfer_ms %.4f R %u root_bytes %llu %s\n", r, st[r].rc,
+               (unsigned long long)st[r].rays, st[r].trace_ms, st[r].xfer_ms, st[r].R,
+               (unsigned long long)st[r].root_bytes, st[r].err);
         bad |= st[r].rc != 0 || st[r].R != st[0].R;
         rays += st[r].rays;
     }

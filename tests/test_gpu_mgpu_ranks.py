@@ -17,6 +17,7 @@ import numpy as np
 import pytest
 
 import voxelhex_amd as vhx
+from voxelhex_amd.multigpu import tile_plan
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BUILD = os.path.join(ROOT, "tests", "abi_c", "_build")
@@ -70,6 +71,8 @@ def scene(tmp_path_factory, oracle):
     (8, 3, 1, 1, 4, "plain"),
     (2, 1, 2, 1, 4, "balance"),
     (3, 1, 1, 1, 4, "balance"),
+    (2, 1, 1, 1, 4, "rgba"),
+    (8, 3, 2, 1, 5, "rgba"),
 ])
 def test_ranks_frames_equal_golden_and_oracle(scene, nranks, root_slots, inflight, overlap, frames, mode):
     _build()
@@ -88,7 +91,16 @@ def test_ranks_frames_equal_golden_and_oracle(scene, nranks, root_slots, infligh
     fb = np.fromfile(out, np.uint32).reshape(4, n)
     sha = scene["meta"]["sha256"]
     assert hashlib.sha256(fb[0].tobytes()).hexdigest() == sha["rgba"], "camera A rgba differs from golden"
-    assert hashlib.sha256(fb[1].tobytes()).hexdigest() == sha["depth"], "camera A depth differs from golden"
     ref = scene["ref_b"]
     assert np.array_equal(fb[2], ref["rgba"].view(np.uint32)), "camera B rgba differs from the oracle"
+    # bytes into rank 0 per frame (vhx_mgpu_frame_bytes, every rank reports the same): the other N - 1 slots' parts,
+    # one plane of 32-bit words per tile entry in RGBA-only mode, two otherwise
+    root_bytes = {int(line.split("root_bytes ")[1].split()[0]) for line in r.stdout.splitlines() if "root_bytes" in line}
+    plan = tile_plan(nranks, R, 64, W, H, 0)
+    planes = 1 if mode == "rgba" else 2
+    assert root_bytes == {(nranks - 1) * plan["tiles_per_slot"] * 64 * 64 * 4 * planes}, root_bytes
+    if mode == "rgba":  # no depth plane crossed: rank 0's depth framebuffers keep their fill
+        assert (fb[1] == 0xABABABAB).all() and (fb[3] == 0xABABABAB).all()
+        return
+    assert hashlib.sha256(fb[1].tobytes()).hexdigest() == sha["depth"], "camera A depth differs from golden"
     assert np.array_equal(fb[3], ref["depth"].view(np.uint32)), "camera B depth differs from the oracle"
