@@ -327,7 +327,9 @@ int vhx_mgpu_set_root_slots(vhx_mgpu *m, uint32_t root_slots);
  * any output pointer may be NULL. */
 int vhx_mgpu_balance(vhx_mgpu *m, const vhx_camera *cam, uint32_t frames, uint32_t *root_slots, float *trace_ms,
                      float *transfer_ms);
-/* Planes each rank sends to rank 0 (every rank must pass the same value; waits for the frames in flight): 2 (default)
+/* Collective: planes each rank sends to rank 0 (waits for the frames in flight; the ranks agree on the value over the
+ * communicator, and when they passed different values every rank fails with VHX_E_INVALID_ARG and keeps its old
+ * count): 2 (default)
  * = RGBA8 + f32 depth, 1 = RGBA8 only -- the reference's display output is the rgba8unorm view texture
  * (src/raytracing/bevy/view.rs:269-289), so a renderer that needs no depth halves rank 0's intake over xGMI. With one
  * plane rank 0 passes fb_depth = NULL to vhx_mgpu_render. */

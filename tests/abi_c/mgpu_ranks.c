@@ -10,7 +10,8 @@
  *   ROOT_SLOTS R (MODE "balance": chosen by vhx_mgpu_balance instead)
  *   FRAMES     frames rendered, alternating camera A and B (A first), every one submitted without waiting
  *   MODE       "plain" | "balance" | "rgba" (plain with one plane: vhx_mgpu_set_planes(m, 1) on every rank, rank 0
- *              passes fb_depth = NULL, so its depth framebuffers keep their 0xAB fill)
+ *              passes fb_depth = NULL, so its depth framebuffers keep their 0xAB fill; first a set_planes call with
+ *              different counts on rank 0 and the others, which every rank must refuse)
  *   OUT_FILE   rank 0's framebuffers after the last frame of each camera: rgbaA | depthA | rgbaB | depthB
  * prints one line per rank (rays, measured trace / transfer ms, bytes into rank 0 per frame) and "root_slots R", then
  * "ok"; exit 1 on failure. */
@@ -64,7 +65,16 @@ static void *rank_main(void *arg) {
     RCHECK(vhx_mgpu_set_frames_in_flight(m, (uint32_t)g_F));
     RCHECK(vhx_mgpu_set_overlap(m, g_overlap));
     RCHECK(vhx_mgpu_broadcast_tree(m, s->rank == 0 ? &g_tree : NULL));
-    if (g_rgba) RCHECK(vhx_mgpu_set_planes(m, 1));
+    if (g_rgba) {
+        /* a disagreement first (rank 0 asks for one plane, the others for two): every rank is refused alike */
+        const int drc = vhx_mgpu_set_planes(m, s->rank == 0 ? 1u : 2u);
+        if (drc != VHX_E_INVALID_ARG) {
+            snprintf(s->err, sizeof(s->err), "set_planes with different counts returned %d", drc);
+            s->rc = -1;
+            goto done;
+        }
+        RCHECK(vhx_mgpu_set_planes(m, 1));
+    }
     if (g_balance) {
         RCHECK(vhx_mgpu_balance(m, &g_cam[0], 3, &s->R, NULL, NULL));
     } else {

@@ -114,7 +114,7 @@ struct vhx_ctx {
         uint32_t qorder;                     // order of a primary frame's pass-0 queue (vhx_ctx::qorder below)
         uint32_t qsort;                      // queue passes: segments of this many queue entries sorted by saved node
     };
-    // Adaptive scheduling (default; vhx_set_pass_budgets or an environment knob fixes the schedule instead): at each
+    // Adaptive scheduling (default; vhx_set_pass_budgets or a tuning key fixes the schedule instead): at each
     // trace the context looks at the other contexts of its tree (vhx_create_shared) and picks
     //  * `busy` when any of them still has a frame in flight on another stream: {24, 72, 216, 648} with 4 queue waves per
     //    CU -- the bench frame at eight frames in flight 0.561-0.567 ms against 0.593-0.598 for round 2's {24, 96, 768}
@@ -136,31 +136,31 @@ struct vhx_ctx {
     // the schedule in force (the selected one, or the fixed one)
     uint32_t budgets[VHX_MAX_BUDGETS] = {24u, 72u, 216u, 648u};
     uint32_t npass = 5;
-    uint32_t rpw[VHX_MAX_BUDGETS + 1] = {64u, 64u, 64u, 64u, 64u, 64u, 64u};  // rays per wave of each pass (VHX_RPW="64,16" style override; 0 = adaptive)
-    uint32_t tw = 1024;            // adaptive rays per wave: target waves per queue pass (VHX_TW)
-    bool resume = true;            // abandoned rays continue from saved state (VHX_RESUME=0: re-traced from scratch)
+    uint32_t rpw[VHX_MAX_BUDGETS + 1] = {64u, 64u, 64u, 64u, 64u, 64u, 64u};  // rays per wave of each pass (tune "rpw=64,16" style override; 0 = adaptive)
+    uint32_t tw = 1024;            // adaptive rays per wave: target waves per queue pass (tune "tw")
+    bool resume = true;            // abandoned rays continue from saved state (tune "resume=0": re-traced from scratch)
     // passes before save_from keep no state: the rays they abandon are traced again from scratch by pass save_from,
-    // which saves (VHX_SAVE_FROM; 0 = every budgeted pass saves)
+    // which saves (tune "save_from"; 0 = every budgeted pass saves)
     uint32_t save_from = 0;
-    uint32_t xcd_group = 16;       // pass-0 XCD-aware block runs (VHX_XCDG; 0 = dispatch order)
-    uint32_t qblock = 256;         // threads per workgroup of a queue pass (VHX_QBLOCK=64: one wave per workgroup)
+    uint32_t xcd_group = 16;       // pass-0 XCD-aware block runs (tune "xcdg"; 0 = dispatch order)
+    uint32_t qblock = 256;         // threads per workgroup of a queue pass (tune "qblock=64": one wave per workgroup)
     uint32_t queue_blocks = 2048;  // workgroups of a queue pass (CUs x resident workgroups)
-    // waves of a queue pass (VHX_QWAVES; the schedule's per-CU figure times the CUs). One frame at a time, 8 per CU:
+    // waves of a queue pass (tune "qwaves"; the schedule's per-CU figure times the CUs). One frame at a time, 8 per CU:
     // round 1's tail pass (148 k rays, 2316 chunks of 64) took 1.55 ms/frame at 2048 waves against 1.62 at 8192 and
     // 1.82 at 1024 (fewer busy waves per CU at the start of the pass, while every chunk still starts at once); with
     // frames in flight 4 per CU (equal within noise there; profiles/r03/qwaves_r03.log)
     uint32_t queue_waves = 1024;
     uint32_t cus = 256;            // compute units of the device (the adaptive schedules' queue waves are per CU)
-    uint32_t queue_waves0 = 8192;  // waves of a first queue pass over fresh rays (VHX_QWAVES0)
-    uint32_t queue_waves_mid = 0;  // waves of a budgeted queue pass after the first (VHX_QWAVESM; 0 = queue_waves)
-    uint32_t qxcd = 16;            // queue passes: XCD-dealt chunk runs (VHX_QXCD = run length, 0 = one counter)
-    bool qxcd_all = false;         // deal every queue pass, not only the last (VHX_QXCD_ALL=1, diagnostics)
-    // pass-0 queue of a framebuffer frame (the schedule's, or VHX_QORDER = "[m]N[z]"): 0 output-index order; else
+    uint32_t queue_waves0 = 8192;  // waves of a first queue pass over fresh rays (tune "qwaves0")
+    uint32_t queue_waves_mid = 0;  // waves of a budgeted queue pass after the first (tune "qwavesm"; 0 = queue_waves)
+    uint32_t qxcd = 16;            // queue passes: XCD-dealt chunk runs (tune "qxcd" = run length, 0 = one counter)
+    bool qxcd_all = false;         // deal every queue pass, not only the last (tune "qxcd_all=1", diagnostics)
+    // pass-0 queue of a framebuffer frame (the schedule's, or tune "qorder=[m]N[z|r]"): 0 output-index order; else
     // log2 of the tile size (bits 0-3), bit 4 Morton order of the tiles, bit 5 Morton order of the pixels inside a tile
     // (FlagOrder in vhx_device.hip)
     uint32_t qorder = VHX_QORDER_BUSY;
     uint32_t last_fb_w = 0, last_fb_h = 0;  // the last primary framebuffer frame traced on this context
-    // budgeted passes: a wave abandons its rays once fewer than sparse[p] lanes still trace (VHX_SPARSE="8,4,4").
+    // budgeted passes: a wave abandons its rays once fewer than sparse[p] lanes still trace (tune "sparse=8,4,4").
     // Pass 0 at 12 under frames in flight: eight frames 0.645-0.651 ms per bench frame against 0.665-0.670 (8:
     // 0.651-0.661, 16: 0.646-0.657, 24 and 32 slower); the later budgeted passes gained nothing (profiles/r02/sparse*.log)
     uint32_t sparse[VHX_MAX_BUDGETS] = {12u};

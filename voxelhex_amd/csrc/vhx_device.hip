@@ -1160,7 +1160,7 @@ static PassQ pass_q(const vhx_ctx *c, uint32_t p, uint32_t npass) {
     q.tw = c->tw;
     q.xcd_group = c->xcd_group;
     // the unbounded last pass only: dealing the budgeted passes too measured the same (shadow frames 2.90 against
-    // 2.87 ms, primary frames equal) once the XCD counters had cache lines of their own; VHX_QXCD_ALL=1 deals every
+    // 2.87 ms, primary frames equal) once the XCD counters had cache lines of their own; tune "qxcd_all=1" deals every
     // queue pass (diagnostics)
     q.qxcd = last || c->qxcd_all ? c->qxcd : 0u;
     q.tmp = last ? nullptr : (uint32_t *)c->tmp.ptr;

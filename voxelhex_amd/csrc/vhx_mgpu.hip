@@ -433,11 +433,53 @@ int vhx_mgpu_render(vhx_mgpu *m, const vhx_camera *cam, uint32_t *fb_rgba, float
     return VHX_OK;
 }
 
+// Collective agreement on one word: every rank sends `value` to rank 0 (point to point), rank 0 broadcasts it back if
+// all ranks sent the same, else VHX_MGPU_DISAGREE, so every rank sees the same outcome.
+#define VHX_MGPU_DISAGREE 0xFFFFFFFFu
+static int agree_u32(vhx_mgpu *m, uint32_t value, uint32_t &agreed) {
+    agreed = value;
+    if (m->nranks < 2) return VHX_OK;
+    vhx_ctx *c = m->ctx;
+    int rc = ensure(c, m->hdr, 64 + 4u * (uint32_t)m->nranks);
+    if (rc) return rc;
+    VHX_STREAM(c);
+    uint32_t *w = (uint32_t *)m->hdr.ptr + 16;
+    const Rccl &r = rccl();
+    VHX_HIP(c, hipMemcpyAsync(w + m->rank, &value, 4, hipMemcpyHostToDevice, c->stream));
+    VHX_NCCL(m, r.GroupStart());
+    if (m->rank == 0) {
+        for (int q = 1; q < m->nranks; ++q) VHX_NCCL_GROUP(m, r.Recv(w + q, 1, ncclUint32, q, m->comm, c->stream));
+    } else {
+        VHX_NCCL_GROUP(m, r.Send(w + m->rank, 1, ncclUint32, 0, m->comm, c->stream));
+    }
+    VHX_NCCL(m, r.GroupEnd());
+    uint32_t out = value;
+    if (m->rank == 0) {
+        std::vector<uint32_t> all((size_t)m->nranks, 0u);
+        VHX_HIP(c, hipMemcpyAsync(all.data(), w, 4u * (uint32_t)m->nranks, hipMemcpyDeviceToHost, c->stream));
+        VHX_HIP(c, hipStreamSynchronize(c->stream));
+        for (int q = 1; q < m->nranks; ++q)
+            if (all[(size_t)q] != value) out = VHX_MGPU_DISAGREE;
+        VHX_HIP(c, hipMemcpyAsync(m->hdr.ptr, &out, 4, hipMemcpyHostToDevice, c->stream));
+    }
+    VHX_NCCL(m, r.Broadcast(m->hdr.ptr, m->hdr.ptr, 1, ncclUint32, 0, m->comm, c->stream));
+    VHX_HIP(c, hipMemcpyAsync(&out, m->hdr.ptr, 4, hipMemcpyDeviceToHost, c->stream));
+    VHX_HIP(c, hipStreamSynchronize(c->stream));
+    agreed = out;
+    return VHX_OK;
+}
+
 int vhx_mgpu_set_planes(vhx_mgpu *m, uint32_t planes) {
     if (!m) return VHX_E_INVALID_ARG;
-    if (planes < 1 || planes > 2) return fail(m->ctx, VHX_E_INVALID_ARG, "vhx_mgpu_set_planes: 1 (RGBA) or 2 (RGBA + depth)");
-    const int rc = vhx_mgpu_sync(m, nullptr);  // no frame may be in flight while the part layout changes
+    // an out-of-range value still joins the agreement (as a disagreement), so that no rank is left waiting in it
+    const bool ok = planes >= 1 && planes <= 2;
+    int rc = vhx_mgpu_sync(m, nullptr);  // no frame may be in flight while the part layout changes
     if (rc) return rc;
+    uint32_t agreed = 0;
+    if ((rc = agree_u32(m, ok ? planes : VHX_MGPU_DISAGREE, agreed))) return rc;
+    if (!ok) return fail(m->ctx, VHX_E_INVALID_ARG, "vhx_mgpu_set_planes: 1 (RGBA) or 2 (RGBA + depth)");
+    if (agreed != planes)
+        return fail(m->ctx, VHX_E_INVALID_ARG, "vhx_mgpu_set_planes: the ranks passed different plane counts");
     m->planes = planes;
     return VHX_OK;
 }
