@@ -104,43 +104,7 @@ static inline bool pix_data_is_some(uint32_t v) { return pix_data_index(v) != 0x
 using SectantFn = std::function<void(U3, U3, uint8_t, const Cube &)>;
 std::array<size_t, 3> execute_for_relevant_sectants(const Cube &nb, U3 position_, uint32_t update_size_,
                                                     const SectantFn &fun) {
-    if ((float)position_.x > nb.min.x + nb.size || (float)position_.y > nb.min.y + nb.size ||
-        (float)position_.z > nb.min.z + nb.size)
-        return {0, 0, 0};
-    F3 position = f3(std::fmax((float)position_.x, nb.min.x), std::fmax((float)position_.y, nb.min.y),
-                     std::fmax((float)position_.z, nb.min.z));
-    F3 update_size = sub(add(from_u3(position_), f3((float)update_size_, (float)update_size_, (float)update_size_)), position);
-    float cell_size = nb.size / 4.f;
-    // The reference walks the whole update region, which may reach far past the node (the streaming view's include
-    // regions grow by 4x per MIP level): a point past the node's upper bound on an axis fails cube_contains, and so does
-    // every later point on that axis (shifted only grows; position >= nb.min), so the loops stop there. The calls of
-    // `fun` and their order are unchanged.
-    const F3 nmax = f3(nb.min.x + nb.size, nb.min.y + nb.size, nb.min.z + nb.size);
-    F3 shifted = position;
-    while (shifted.x <= (position.x + update_size.x) && shifted.x < nmax.x) {
-        shifted.y = position.y;
-        while (shifted.y <= (position.y + update_size.y) && shifted.y < nmax.y) {
-            shifted.z = position.z;
-            while (shifted.z <= (position.z + update_size.z) && shifted.z < nmax.z) {
-                if (!cube_contains(nb, shifted)) {
-                    shifted.z += cell_size;
-                    continue;
-                }
-                uint8_t s = sectant_for(nb, shifted);
-                Cube tb = child_bounds_for(nb, s);
-                tb = Cube{floor3(tb.min), std::ceil(tb.size)};
-                F3 pit = f3(std::fmax(position.x, tb.min.x), std::fmax(position.y, tb.min.y), std::fmax(position.z, tb.min.z));
-                F3 remains = sub(add(position, update_size), pit);
-                F3 uit = sub(add(tb.min, f3(tb.size, tb.size, tb.size)), pit);
-                uit = f3(std::fmin(uit.x, remains.x), std::fmin(uit.y, remains.y), std::fmin(uit.z, remains.z));
-                if (0.f < uit.x && 0.f < uit.y && 0.f < uit.z) fun(round_u3(pit), round_u3(uit), s, tb);
-                shifted.z += cell_size;
-            }
-            shifted.y += cell_size;
-        }
-        shifted.x += cell_size;
-    }
-    return {as_usize(std::round(update_size.x)), as_usize(std::round(update_size.y)), as_usize(std::round(update_size.z))};
+    return relevant_sectants(nb, position_, update_size_, fun);  // boxtree.hpp
 }
 
 // ---------------------------------------------------------------------------------------------- ObjectPool

@@ -21,6 +21,7 @@
 #pragma once
 
 #include <array>
+#include <cmath>
 #include <atomic>
 #include <deque>
 #include <functional>
@@ -213,6 +214,72 @@ uint8_t step_sectant_i(uint8_t s, int dx, int dy, int dz);
 // execute_for_relevant_sectants (src/boxtree/iterate.rs:40-121)
 std::array<size_t, 3> execute_for_relevant_sectants(const Cube &nb, U3 position, uint32_t update_size,
                                                     const std::function<void(U3, U3, uint8_t, const Cube &)> &fun);
+
+namespace sect {  // the scalar conversions relevant_sectants needs (Rust `as` casts: saturating, NaN -> 0)
+inline uint32_t as_u32(float f) {
+    if (std::isnan(f) || f <= 0.f) return 0;
+    if (f >= 4294967296.0f) return 0xFFFFFFFFu;
+    return (uint32_t)f;
+}
+inline size_t as_usize(float f) {
+    if (std::isnan(f) || f <= 0.f) return 0;
+    if (f >= 18446744073709551616.0f) return SIZE_MAX;
+    return (size_t)f;
+}
+}  // namespace sect
+
+// The body of execute_for_relevant_sectants as a template over the callback, so that a hot caller (the streaming view
+// walk, stream.cpp) calls `fun` inline instead of through std::function; execute_for_relevant_sectants forwards here.
+// The reference walks the whole update region, which may reach far past the node (the streaming view's include regions
+// grow by 4x per MIP level): a point past the node's upper bound on an axis fails cube_contains, and so does every
+// later point on that axis (shifted only grows; position >= nb.min), so the loops stop there. The calls of `fun` and
+// their order are the reference's.
+template <class Fn>
+inline std::array<size_t, 3> relevant_sectants(const Cube &nb, U3 position_, uint32_t update_size_, Fn &&fun) {
+    const float nx = nb.min.x + nb.size, ny = nb.min.y + nb.size, nz = nb.min.z + nb.size;
+    if ((float)position_.x > nx || (float)position_.y > ny || (float)position_.z > nz) return {0, 0, 0};
+    const F3 position{std::fmax((float)position_.x, nb.min.x), std::fmax((float)position_.y, nb.min.y),
+                      std::fmax((float)position_.z, nb.min.z)};
+    const float us = (float)update_size_;
+    const F3 update_size{((float)position_.x + us) - position.x, ((float)position_.y + us) - position.y,
+                         ((float)position_.z + us) - position.z};
+    const float cell_size = nb.size / 4.f;
+    const F3 end{position.x + update_size.x, position.y + update_size.y, position.z + update_size.z};
+    F3 shifted = position;
+    while (shifted.x <= end.x && shifted.x < nx) {
+        shifted.y = position.y;
+        while (shifted.y <= end.y && shifted.y < ny) {
+            shifted.z = position.z;
+            while (shifted.z <= end.z && shifted.z < nz) {
+                // cube_contains (src/spatial/mod.rs:54-61)
+                if (!(shifted.x >= nb.min.x && shifted.y >= nb.min.y && shifted.z >= nb.min.z && shifted.x < nx &&
+                      shifted.y < ny && shifted.z < nz)) {
+                    shifted.z += cell_size;
+                    continue;
+                }
+                const uint8_t s = offset_sectant(F3{shifted.x - nb.min.x, shifted.y - nb.min.y, shifted.z - nb.min.z},
+                                                 nb.size);  // Cube::sectant_for
+                Cube tb = child_bounds_for(nb, s);
+                tb = Cube{F3{std::floor(tb.min.x), std::floor(tb.min.y), std::floor(tb.min.z)}, std::ceil(tb.size)};
+                const F3 pit{std::fmax(position.x, tb.min.x), std::fmax(position.y, tb.min.y),
+                             std::fmax(position.z, tb.min.z)};
+                const F3 remains{end.x - pit.x, end.y - pit.y, end.z - pit.z};
+                const F3 uit{std::fmin((tb.min.x + tb.size) - pit.x, remains.x),
+                             std::fmin((tb.min.y + tb.size) - pit.y, remains.y),
+                             std::fmin((tb.min.z + tb.size) - pit.z, remains.z)};
+                if (0.f < uit.x && 0.f < uit.y && 0.f < uit.z)
+                    fun(U3{sect::as_u32(std::round(pit.x)), sect::as_u32(std::round(pit.y)), sect::as_u32(std::round(pit.z))},
+                        U3{sect::as_u32(std::round(uit.x)), sect::as_u32(std::round(uit.y)), sect::as_u32(std::round(uit.z))},
+                        s, tb);
+                shifted.z += cell_size;
+            }
+            shifted.y += cell_size;
+        }
+        shifted.x += cell_size;
+    }
+    return {sect::as_usize(std::round(update_size.x)), sect::as_usize(std::round(update_size.y)),
+            sect::as_usize(std::round(update_size.z))};
+}
 
 }  // namespace vhx
 

@@ -115,6 +115,17 @@ struct vhx_stream {
     std::unordered_map<size_t, Owned> brick_by_index;
     std::unordered_map<uint64_t, size_t> brick_by_owner;
     std::unordered_map<size_t, size_t> meta_by_key, key_by_meta;
+    // meta_by_key's keys as a dense flag per pool key (kept with it by meta_insert / reset_targets): the upload stats
+    // count the nodes to see that are not resident with one pass over the set instead of a hash lookup per node
+    std::vector<uint8_t> resident_key;
+    void set_resident(size_t key, bool on) {
+        if (key >= resident_key.size()) {
+            if (!on) return;
+            resident_key.resize(std::max<size_t>(key + 1, resident_key.size() * 2), 0u);
+        }
+        resident_key[key] = on ? 1u : 0u;
+    }
+    bool is_resident(size_t key) const { return key < resident_key.size() && resident_key[key] != 0u; }
     std::unordered_map<size_t, std::pair<size_t, uint8_t>> node_index_vs_parent;
     // nodes_to_see (upload_queue.rs: a HashSet of node keys): a set over the pool's dense keys, stamped by generation so
     // that the per-rebuild clear is O(1); membership and size are what the queue logic reads (no iteration order)
@@ -211,9 +222,13 @@ struct vhx_stream {
         auto a = meta_by_key.find(key);
         if (a != meta_by_key.end()) key_by_meta.erase(a->second);
         auto b = key_by_meta.find(meta);
-        if (b != key_by_meta.end()) meta_by_key.erase(b->second);
+        if (b != key_by_meta.end()) {
+            meta_by_key.erase(b->second);
+            set_resident(b->second, false);
+        }
         meta_by_key[key] = meta;
         key_by_meta[meta] = key;
+        set_resident(key, true);
     }
 
     // ------------------------------------------------------------------------------------------ node MIPs
@@ -293,6 +308,7 @@ struct vhx_stream {
         brick_by_owner.clear();
         meta_by_key.clear();
         key_by_meta.clear();
+        std::fill(resident_key.begin(), resident_key.end(), 0u);
         node_index_vs_parent.clear();
         nodes_to_see.clear();
         bricks_to_upload.clear();
@@ -317,7 +333,7 @@ struct vhx_stream {
         const F3 c = sub(vc, unit(include / 2.f));
         const U3 cbl{round_u32(c.x), round_u32(c.y), round_u32(c.z)};
         if (node(it.key).content != Content::Internal) return;
-        execute_for_relevant_sectants(it.nb, cbl, as_u32(include), [&](U3, U3, uint8_t cs, const Cube &tb) {
+        relevant_sectants(it.nb, cbl, as_u32(include), [&](U3, U3, uint8_t cs, const Cube &tb) {
             size_t ck;
             if (valid_child(it.key, cs, ck)) visit(ViewItem{ck, tb, it.mip - 1});
         });
@@ -343,16 +359,20 @@ struct vhx_stream {
         }
         const unsigned nt = (unsigned)std::min<size_t>(
             front.size(), std::max(1u, std::min(16u, std::thread::hardware_concurrency())));
-        std::vector<std::vector<size_t>> lists(front.size());
+        // each thread collects into a vector of its own, handed over at its end (per-subtree vectors side by side had
+        // their headers share cache lines between threads: every push_back bounced a line)
+        std::vector<std::vector<size_t>> lists(std::max(1u, nt));
         std::atomic<size_t> at{0};
-        auto work = [&]() {
-            for (size_t i; (i = at.fetch_add(1)) < front.size();) view_subtree(front[i], vc, dist, min_mip, lists[i]);
+        auto work = [&](unsigned k) {
+            std::vector<size_t> mine;
+            for (size_t i; (i = at.fetch_add(1)) < front.size();) view_subtree(front[i], vc, dist, min_mip, mine);
+            lists[k] = std::move(mine);
         };
         if (nt <= 1) {
-            work();
+            work(0);
         } else {
             std::vector<std::thread> pool;
-            for (unsigned k = 0; k < nt; ++k) pool.emplace_back(work);
+            for (unsigned k = 0; k < nt; ++k) pool.emplace_back(work, k);
             for (auto &th : pool) th.join();
         }
         for (const auto &l : lists)
@@ -623,7 +643,7 @@ struct vhx_stream {
                 if (!owner_has(o)) res.push_back(o);
             }
         } else if (n.content == Content::Leaf) {
-            execute_for_relevant_sectants(nb, vbl, as_u32(dist), [&](U3, U3, uint8_t cs, const Cube &tb) {
+            relevant_sectants(nb, vbl, as_u32(dist), [&](U3, U3, uint8_t cs, const Cube &tb) {
                 if (n.bricks[cs].kind != BrickKind::Parted) return;
                 Owned o;
                 o.kind = 1;
@@ -1108,7 +1128,7 @@ int vhx_stream_upload_frames(vhx_stream *s, uint32_t frames, vhx_stream_stats *s
         stats->bricks_in_view = s->bricks_in_view;
         stats->nodes_to_see = s->nodes_to_see.size();
         uint64_t missing = 0;
-        for (size_t k : s->nodes_to_see) missing += s->meta_by_key.count(k) ? 0u : 1u;
+        for (size_t k : s->nodes_to_see) missing += s->is_resident(k) ? 0u : 1u;
         stats->pending = missing + s->bricks_to_upload.size() + s->tree->changes.size() +
                          (s->last_cycle_work == 0 ? 0u : 1u);
     }
