@@ -590,39 +590,6 @@ struct Trav {
         return true;
     }
 
-    // begin() of a resumed ray whose saved state is already in registers (the words save_state writes; the tail split
-    // of k_trace_queue_split hands rays over that way)
-    __device__ __forceinline__ void begin_resumed(const DevTree &t, F3d o, F3d d, HitOut &h, const St4 &s) {
-        h.hit = false;
-        ray_setup(r, o, d);
-        {
-            const F3d od = vadd(mk(1.0f, 1.0f, 1.0f), d);
-            dir_idx = (uint32_t)(od.x >= 1.0f) + (uint32_t)(od.z >= 1.0f) * 2u + (uint32_t)(od.y >= 1.0f) * 4u;
-        }
-        tsize = (float)t.size;
-        ex = 0;
-        hdesc = 0;
-        hflat = 0;
-        p = mk(__uint_as_float(s.a.x), __uint_as_float(s.a.y), __uint_as_float(s.a.z));
-        iters = s.a.w;
-        cur.min = mk(__uint_as_float(s.b.x), __uint_as_float(s.b.y), __uint_as_float(s.b.z));
-        cur.size = __uint_as_float(s.b.w & 0xFF800000u);
-        target = s.b.w & 0x7Fu;
-        count = (s.b.w >> 8) & 7u;
-        tb.min = mk(__uint_as_float(s.c.x), __uint_as_float(s.c.y), __uint_as_float(s.c.z));
-        tb.size = __uint_as_float(s.c.w);
-        node = s.e.x;
-        s1 = s.e.y;
-        s2 = s.e.z;
-        s3 = s.e.w;
-        ray_scale_factors(r);
-        tbok = 0u;
-    }
-    // the loop state as save_state would write it
-    __device__ __forceinline__ St4 packed() const {
-        return pack_state(p, iters, cur, tb, target, count, node, s1, s2, s3);
-    }
-
     __device__ __forceinline__ void step(const DevTree &t, const uint64_t *occ_tab, HitOut &h, uint32_t budget) {
         // the child slot is read by both the leaf probe and the push: issue it with the header load so the
         // iteration waits for one memory latency instead of two (with brick_dim <= 4 the child record also carries
