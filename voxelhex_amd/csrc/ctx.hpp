@@ -62,6 +62,11 @@ struct TreeStore {
 #ifndef VHX_QSORT_BUSY
 #define VHX_QSORT_BUSY 0u
 #endif
+// ... and of the lone-frame schedule's unbounded pass: segments of 256 (the lone bench frame 1.19 against 1.22 ms in two
+// runs, the orbiting lone frame unchanged; 512 / 1024 / 2048 no faster or slower: profiles/r04/final_check/lone_qsort*.log)
+#ifndef VHX_QSORT_IDLE
+#define VHX_QSORT_IDLE 256u
+#endif
 #define VHX_QSORT_MAX 2048u
 
 struct vhx_ctx {
@@ -131,7 +136,7 @@ struct vhx_ctx {
     //    lone frame's critical path.
     bool adaptive = true;
     Sched sched_busy = {{24u, 72u, 216u, 648u}, 5u, {12u}, 3u, VHX_QORDER_BUSY, VHX_QSORT_BUSY};
-    Sched sched_idle = {{64u}, 2u, {0u}, 8u, VHX_QORDER_IDLE, 0u};
+    Sched sched_idle = {{64u}, 2u, {0u}, 8u, VHX_QORDER_IDLE, VHX_QSORT_IDLE};
     int last_sched = -1;  // the schedule of the last trace: 1 busy, 0 idle, -1 fixed (vhx_get_pass_budgets)
     // the schedule in force (the selected one, or the fixed one)
     uint32_t budgets[VHX_MAX_BUDGETS] = {24u, 72u, 216u, 648u};

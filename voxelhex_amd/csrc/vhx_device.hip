@@ -1501,16 +1501,16 @@ static int apply_tuning(vhx_ctx *c, const std::string &key, const std::string &v
             code = lg | (m ? 16u : 0u) | (z ? 32u : 0u) | (rows ? 64u : 0u);
         }
         c->qorder = c->sched_busy.qorder = c->sched_idle.qorder = code;  // both schedules (the rest stays adaptive)
-        } else if (key == "qsort") {  // segment length of the queue passes' node sort: 0 = off, else 256 .. VHX_QSORT_MAX
+    } else if (key == "qsort") {  // segment length of the queue passes' node sort: 0 = off, else 256 .. VHX_QSORT_MAX
         if (!parse_u32(val, x) || (x && (x < 256 || x > VHX_QSORT_MAX || (x & (x - 1))))) return bad();
         c->qsort_force = (int)x;
-        } else if (key == "qsortp") {  // bit mask of the queue passes whose input is sorted
+    } else if (key == "qsortp") {  // bit mask of the queue passes whose input is sorted
         if (!parse_u32(val, x)) return bad();
         c->qsort_passes = x;
     } else if (key == "qsortb") {
         if (!parse_u32(val, x) || x == 0) return bad();
         c->qsort_blocks = x;
-        } else {
+    } else {
         return fail(c, VHX_E_INVALID_ARG, ("vhx_set_tuning: unknown key " + key).c_str());
     }
     return VHX_OK;
