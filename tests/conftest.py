@@ -38,6 +38,11 @@ def oracle():
 
 @pytest.fixture(scope="session")
 def gpu():
+    # torch's HIP runtime first, then libvhx's: the order every full-suite run has had (a subset run once saw torch
+    # find no device when libvhx had initialised the GPU first, after the loopback rank subprocesses)
+    import torch
+    if torch.cuda.is_available():
+        torch.cuda.init()
     from voxelhex_amd import Raytracer
     rt = Raytracer(0)
     yield rt
