@@ -38,8 +38,9 @@ def oracle():
 
 @pytest.fixture(scope="session")
 def gpu():
-    # torch's HIP runtime first, then libvhx's: the order every full-suite run has had (a subset run once saw torch
-    # find no device when libvhx had initialised the GPU first, after the loopback rank subprocesses)
+    # torch's HIP runtime first, then libvhx's: the order of every full-suite run. (A run of only the loopback rank
+    # tests followed by this fixture has seen no HIP device in this process once those subprocesses had used the GPU
+    # first; in the full suite the process initialises the GPU long before them.)
     import torch
     if torch.cuda.is_available():
         torch.cuda.init()
