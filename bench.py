@@ -418,7 +418,6 @@ def main():
             try:
                 mg = M.MgpuRenderer(rt, obj[0], world, rank, tile_size=args.tile, overlap=not args.no_overlap)
                 mg.set_frames_in_flight(min(F, N.VHX_MGPU_MAX_INFLIGHT))
-                mg.set_planes(args.planes)
             except Exception as e:  # noqa: BLE001
                 mgpu_fallback = f"vhx_mgpu on rank {rank}: {e}"
                 mg = None
@@ -435,6 +434,10 @@ def main():
             dist.destroy_process_group()
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
             F = 1
+        else:
+            # collective (the ranks agree on the plane count over the communicator): only once every rank has its
+            # renderer, so that no rank waits in it for one that fell back
+            mg.set_planes(args.planes)
 
     # the tree: built on the host (rank 0 only when it is broadcast over RCCL), uploaded to HBM
     t0 = time.time()
