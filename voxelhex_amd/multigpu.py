@@ -206,7 +206,8 @@ class MgpuRenderer:
 
     def set_planes(self, planes):
         """Planes every rank sends to rank 0 (vhx_mgpu_set_planes): 2 = RGBA8 + depth, 1 = RGBA8 only (rank 0 then
-        renders with fb_depth=None). Every rank must pass the same value."""
+        renders with fb_depth=None). Collective: every rank calls it; the ranks agree on the value over the
+        communicator, and if they passed different values every rank raises and keeps its previous count."""
         self._check(N.lib().vhx_mgpu_set_planes(self._h, planes))
 
     def frame_bytes(self, width, height):
