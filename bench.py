@@ -197,14 +197,17 @@ def parse_pmc_dir(d):
             "lanes": lanes}
 
 
-def measure_traffic():
+def measure_traffic(busy_only=False, tune=None):
     """Memory-side read bytes per frame, measured now: this bench (same arguments, 5 timed + 1 warm-up frames, no
     roofline / CPU leg) under `rocprofv3 --pmc FETCH_SIZE --kernel-trace` as a child process, FETCH_SIZE summed over
     the frame kernels and divided by the pass-0 dispatches, x1024 B and x2 (gfx950: FETCH_SIZE derives from
     TCC_EA0_RDREQ and reads half the bytes; /opt/skills/guides/MI355X_MICROARCH.md, HBM section; Infinity-Cache hits
     included, an upper bound of HBM bytes). The same pass (one --pmc run: 3 TCC + 3 SQ counters) collects
     SQ_INSTS_VALU, SQ_THREAD_CYCLES_VALU and SQ_ACTIVE_INST_VALU for the issue side. Returns a dict (bytes,
-    valu, active lanes per VALU instruction per trace kernel, frames) or None (no profiler, a failure or 120 s)."""
+    valu, active lanes per VALU instruction per trace kernel, frames) or None (no profiler, a failure or 120 s).
+    busy_only: every frame of the child runs the frames-in-flight schedule (vhx_set_tuning "adaptive=0", after any
+    --tune of this run), the schedule of the timed frames; otherwise its setup frames (one per context, each alone)
+    would run the lone-frame schedule and their counters would mix into the per-frame figures."""
     rp = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
     if not os.path.exists(rp):
         return None
@@ -213,7 +216,8 @@ def measure_traffic():
     cmd = ([rp, "--pmc"] + counters + ["--kernel-trace", "-f", "csv", "-d", d, "-o", "pmc", "--", sys.executable,
                                        os.path.abspath(__file__)] + sys.argv[1:] +
            ["--steps", "5", "--warmup", "1", "--no-cpu-baseline", "--no-roofline", "--no-pmc",
-            "--no-frame-check", "--no-extra"])
+            "--no-frame-check", "--no-extra"] +
+           (["--tune", (tune + ";" if tune else "") + "adaptive=0"] if busy_only else []))
     env = dict(os.environ, TMPDIR="/tmp")
     env.pop("VHX_BENCH_MGPU1", None)  # the child times the single-GPU path only
     try:
@@ -759,7 +763,8 @@ def main():
         tr = pmc_traffic(workload)
         measured = None
         if world == 1 and rank == 0 and not args.no_pmc and mg is None:
-            measured = measure_traffic()
+            # the timed frames run the frames-in-flight schedule whenever F > 1 and the schedule is adaptive
+            measured = measure_traffic(busy_only=F > 1 and budgets is None, tune=args.tune)
         roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5),
                 "basis": ("algorithmic bytes of one frame's launch / the frame period (wall time per frame with "
@@ -770,7 +775,9 @@ def main():
                 round(launch_bytes / (kernel_ms_isolated * 1e-3) / 1e9, 2),
                 "traffic": measured["bytes"] if measured else (None if tr is None else tr["read_bytes_per_launch"]),
                 "traffic_source": (f"measured in this run: rocprofv3 --pmc FETCH_SIZE child run of this workload "
-                                   f"(x1024 B, x2 gfx950), frame kernels / frames ({measured['frames']})") if measured else
+                                   f"(x1024 B, x2 gfx950), frame kernels / frames ({measured['frames']})"
+                                   + ("; every child frame on the timed frames' schedule (frames in flight)"
+                                      if F > 1 and budgets is None else "")) if measured else
                                   (None if tr is None else tr["source"] + " (committed profile)"),
                 "traffic_committed": None if tr is None else tr["read_bytes_per_launch"],
                 "kernel": "vhx_trace_primary launch = k_trace_primary (pass 0, step budget) + k_trace_queue "
@@ -786,7 +793,9 @@ def main():
             iss = {"valu_wave_instructions_per_frame": measured["valu"], "useful_lane_frac": round(measured["useful"], 4),
                    "active_lanes_per_valu": measured["lanes"], "peak_valu_wave_instructions_per_s": 1024 * 2.4e9 / 2,
                    "source": "measured in this run: rocprofv3 --pmc SQ_INSTS_VALU, SQ_THREAD_CYCLES_VALU / "
-                             f"SQ_ACTIVE_INST_VALU (same child run), frame kernels / frames ({measured['frames']})"}
+                             f"SQ_ACTIVE_INST_VALU (same child run), frame kernels / frames ({measured['frames']})"
+                             + ("; every child frame on the timed frames' schedule (frames in flight)"
+                                if F > 1 and budgets is None else "")}
         elif tr is not None and "issue" in tr:
             iss = dict(tr["issue"], source=tr["issue"]["source"] + " (committed profile)")
         if iss is not None:
