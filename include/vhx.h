@@ -134,7 +134,10 @@ typedef struct vhx_ctx vhx_ctx;
 
 /* Library / device ------------------------------------------------------------------------------------------ */
 uint32_t vhx_abi_version(void);
+/* The number of HIP devices visible to the process (0 on a host without a GPU). VHX_E_HIP when the HIP runtime fails
+ * to answer for another reason; vhx_device_error() then names the hipError_t (thread-local text, "" after a success). */
 int vhx_device_count(int *count);
+const char *vhx_device_error(void);
 int vhx_create(int hip_device, vhx_ctx **out);
 /* A further context on the owner's device that traces the owner's uploaded tree (no second copy in HBM): one context
  * per frame in flight. Each context has its own stream, ray queues and outputs, so frame k+1's trace runs while frame

@@ -109,6 +109,50 @@ def test_mgpu_balance_one_rank(config4):
         rt.close()
 
 
+def test_mgpu_planes_and_frame_bytes_through_python(config4):
+    """MgpuRenderer.set_planes / frame_bytes (the calls bench.py makes on every rank of the vhx_mgpu path) through the
+    Python wrapper: RGBA-only frames (fb_depth None) equal the oracle, rank 0 receives no bytes at N = 1, and a plane
+    count other than 1 or 2 is refused."""
+    import torch
+    flat, cam, ref = config4
+    rt = vhx.Raytracer(0)
+    try:
+        m = M.MgpuRenderer(rt, M.mgpu_unique_id(), 1, 0, tile_size=T4)
+        m.broadcast_tree(flat)
+        m.set_planes(1)
+        assert m.frame_bytes(W4, H4) == 0  # one rank: nothing crosses a link
+        rgba = torch.zeros(W4 * H4, dtype=torch.int32, device="cuda")
+        m.render(cam, rgba, None)
+        m.sync()
+        assert np.array_equal(rgba.cpu().numpy().view(np.uint32), ref["rgba"])
+        m.set_planes(2)
+        assert m.frame_bytes(W4, H4) == 0
+        with pytest.raises(N.VhxError):
+            m.set_planes(3)
+        m.close()
+    finally:
+        rt.close()
+
+
+def test_bench_mgpu_path_one_rank():
+    """bench.py's vhx_mgpu path end to end (VHX_BENCH_MGPU1=1: gloo setup, RCCL id exchange, renderer, set_planes,
+    balance, tree broadcast, timed frames, frame_bytes, the untimed multi-GPU check) on a small workload; the line
+    reports the gathered frame equal to a lone trace in both plane counts."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, VHX_BENCH_MGPU1="1", MASTER_ADDR="127.0.0.1", MASTER_PORT="29541")
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--size", "64", "--width", "512", "--height", "256",
+           "--steps", "3", "--warmup", "1", "--inflight", "2", "--no-cpu-baseline", "--no-pmc", "--no-extra"]
+    p = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-4000:]
+    line = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+    assert line["multi_gpu_check"]["frame_equal"] and line["multi_gpu_check"]["two_plane_frame_equal"]
+    assert line["mgpu_split"]["bytes_into_rank0_per_frame"] == 0 and "mgpu_fallback" not in line
+
+
 def test_mgpu_argument_errors(gpu):
     import ctypes
     flat = vhx.FlatTree.build_scene(N.VHX_SCENE_LATTICE_CUBE, 64, 4)

@@ -87,6 +87,7 @@ class Hits(ctypes.Structure):
 SIGNATURES = [
     ("vhx_abi_version", c_u32, []),
     ("vhx_device_count", c_int, [P(c_int)]),
+    ("vhx_device_error", ctypes.c_char_p, []),
     ("vhx_create", c_int, [c_int, P(c_void_p)]),
     ("vhx_create_shared", c_int, [c_void_p, P(c_void_p)]),
     ("vhx_destroy", None, [c_void_p]),

@@ -13,6 +13,7 @@
 #include <atomic>
 #include <climits>
 #include <cstdint>
+#include <system_error>
 #include <thread>
 
 #include "../../include/vhx_boxtree.h"
@@ -1400,7 +1401,13 @@ void BoxTree::recalculate_mips() {  // mipmap.rs:536-586: depth first, children 
         unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
         if (const int t = g_mip_threads.load(std::memory_order_relaxed); t > 0) nt = (unsigned)t;
         std::vector<std::thread> pool;
-        for (unsigned t = 1; t < nt && (size_t)t * 64 < leaves.size(); ++t) pool.emplace_back(work);
+        for (unsigned t = 1; t < nt && (size_t)t * 64 < leaves.size(); ++t) {
+            try {  // a thread that cannot be created is missing: the shared queue is finished by the others
+                pool.emplace_back(work);
+            } catch (const std::system_error &) {
+                break;
+            }
+        }
         work();
         for (auto &th : pool) th.join();
     }

@@ -40,6 +40,7 @@ struct TreeStore {
     std::condition_variable cv;  // tracing / writing changed
     uint32_t tracing = 0;        // traces between trace_begin and trace_end (any thread)
     uint32_t writing = 0;        // writes between write_begin and write_end
+    uint32_t writers_waiting = 0;  // writes blocked in write_begin (new traces wait for them: no writer starvation)
     std::vector<struct vhx_ctx *> users;
     hipEvent_t write_ev = nullptr;
     hipStream_t write_stream = nullptr;

@@ -18,6 +18,7 @@
 #include <deque>
 #include <memory>
 #include <new>
+#include <system_error>
 #include <thread>
 #include <unordered_map>
 #include <unordered_set>
@@ -54,15 +55,24 @@ static void parallel_for(int64_t n, int threads, F &&f) {
         return;
     }
     std::atomic<int64_t> next{0};
+    auto worker = [&] {
+        for (;;) {
+            int64_t i = next.fetch_add(1);
+            if (i >= n) break;
+            f(i);
+        }
+    };
+    // the calling thread is one of the workers; a helper that cannot be created (std::system_error) is missing and the
+    // shared counter lets the others finish, so no exception crosses the C ABI
     std::vector<std::thread> pool;
-    for (int t = 0; t < threads; ++t)
-        pool.emplace_back([&] {
-            for (;;) {
-                int64_t i = next.fetch_add(1);
-                if (i >= n) break;
-                f(i);
-            }
-        });
+    for (int t = 1; t < threads; ++t) {
+        try {
+            pool.emplace_back(worker);
+        } catch (const std::system_error &) {
+            break;
+        }
+    }
+    worker();
     for (auto &th : pool) th.join();
 }
 

@@ -24,6 +24,7 @@
 // (streaming/mod.rs:35-286) at the start of the next upload frames, before the regular upload queue.
 #include <algorithm>
 #include <atomic>
+#include <system_error>
 #include <thread>
 #include <array>
 #include <cmath>
@@ -371,8 +372,18 @@ struct vhx_stream {
         if (nt <= 1) {
             work(0);
         } else {
+            // threads 1..nt-1 help the calling thread, which takes part itself (slot 0); a thread that cannot be created
+            // (std::system_error under a thread limit) is simply missing: the work queue is shared, so the threads that
+            // exist finish it, and no exception crosses the C ABI
             std::vector<std::thread> pool;
-            for (unsigned k = 0; k < nt; ++k) pool.emplace_back(work, k);
+            for (unsigned k = 1; k < nt; ++k) {
+                try {
+                    pool.emplace_back(work, k);
+                } catch (const std::system_error &) {
+                    break;
+                }
+            }
+            work(0);
             for (auto &th : pool) th.join();
         }
         for (const auto &l : lists)

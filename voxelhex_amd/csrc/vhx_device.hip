@@ -956,7 +956,11 @@ static constexpr bool unordered_writes() { return VHX_UNORDERED_WRITES != 0; }
 int vhx::write_begin(vhx_ctx *c) {
     TreeStore &ts = *c->tree;
     std::unique_lock<std::mutex> lock(ts.mu);
+    // a waiting writer holds off traces that have not begun yet (trace_begin waits while writers_waiting > 0), so that
+    // a stream of back-to-back traces from other threads cannot keep `tracing` above 0 forever
+    ++ts.writers_waiting;
     ts.cv.wait(lock, [&] { return ts.tracing == 0 && ts.writing == 0; });
+    --ts.writers_waiting;
     ++ts.writing;
     if (unordered_writes()) return VHX_OK;
     // every other context's last submitted trace, whatever stream it went to (waiting on an event of c's own stream is
@@ -985,7 +989,7 @@ int vhx::write_end(vhx_ctx *c) {
 int vhx::trace_begin(vhx_ctx *c) {
     TreeStore &ts = *c->tree;
     std::unique_lock<std::mutex> lock(ts.mu);
-    ts.cv.wait(lock, [&] { return ts.writing == 0; });
+    ts.cv.wait(lock, [&] { return ts.writing == 0 && ts.writers_waiting == 0; });
     ++ts.tracing;
     if (unordered_writes()) return VHX_OK;
     if (c->seen_write != ts.write_seq) {
@@ -1407,13 +1411,26 @@ extern "C" {
 
 uint32_t vhx_abi_version(void) { return VHX_ABI_VERSION; }
 
+// The HIP runtime's answer, with its error: hipGetDeviceCount failing for any reason other than "no device" is
+// VHX_E_HIP (count 0) and its text is kept for vhx_device_error (there is no context to hold it), instead of a silent
+// count of 0 (a process that lost the device must say why)
+static thread_local std::string g_device_err;
 int vhx_device_count(int *count) {
     if (!count) return VHX_E_INVALID_ARG;
     int n = 0;
-    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    const hipError_t e = hipGetDeviceCount(&n);
+    if (e == hipErrorNoDevice) n = 0;  // no GPU visible: a count of 0, not an error (a CPU-only host)
+    else if (e != hipSuccess) {
+        g_device_err = std::string("hipGetDeviceCount: ") + hipGetErrorName(e) + ": " + hipGetErrorString(e);
+        *count = 0;
+        return VHX_E_HIP;
+    }
+    g_device_err.clear();
     *count = n;
     return VHX_OK;
 }
+
+const char *vhx_device_error(void) { return g_device_err.c_str(); }
 
 int vhx_create(int hip_device, vhx_ctx **out) {
     if (!out) return VHX_E_INVALID_ARG;
@@ -2192,8 +2209,14 @@ int vhx_set_node_mips(vhx_ctx *c, const uint32_t *node_mips, uint32_t count) {
     if (!c) return VHX_E_INVALID_ARG;
     if (c->shared) return fail(c, VHX_E_STATE, "vhx_set_node_mips on a shared context: set them through the owner");
     if (!node_mips) {
+        // switching MIPs off is a tree write too: frames in flight finish with the descriptors they started with, and
+        // traces on other host threads see the switch in submission order (TreeStore ordering)
+        VHX_HIP(c, hipSetDevice(c->device));
+        VHX_STREAM(c);
+        WriteScope ws(c);
+        if (ws.rc) return ws.rc;
         c->tree->mips_on = false;
-        return VHX_OK;
+        return ws.end();
     }
     if (!c->tree->uploaded) return fail(c, VHX_E_STATE, "vhx_set_node_mips: no tree uploaded");
     const vhx_tree_desc &d = c->tree->desc;

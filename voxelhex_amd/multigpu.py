@@ -9,6 +9,8 @@ import ctypes
 
 import numpy as np
 
+from . import _native as N
+
 
 def tile_grid(width, height, T):
     return (width + T - 1) // T, (height + T - 1) // T
@@ -37,8 +39,6 @@ def rank_rays(width, height, T, rank, world):
 def tile_plan(nranks, root_slots, T, width, height, rank):
     """vhx_mgpu_tile_plan (the C deal vhx_mgpu_render uses; pure, no device): dict with tiles_x, tiles_y, tiles, slots,
     tiles_per_slot, first_slot, slot_count."""
-    import ctypes
-    from . import _native as N
     p = N.TilePlan()
     rc = N.lib().vhx_mgpu_tile_plan(nranks, root_slots, T, width, height, rank, ctypes.byref(p))
     if rc != N.VHX_OK:
@@ -143,8 +143,6 @@ def gather_to_root(local, world, rank, dist):
 
 def mgpu_unique_id():
     """vhx_mgpu_unique_id: rank 0's RCCL communicator id (128 bytes) to send to every rank out of band."""
-    import ctypes
-    from . import _native as N
     buf = (ctypes.c_uint8 * N.VHX_MGPU_ID_BYTES)()
     N.check(N.lib().vhx_mgpu_unique_id(buf))
     return bytes(buf)
@@ -157,8 +155,6 @@ class MgpuRenderer:
     rank 0 (exchange them with e.g. torch.distributed.broadcast_object_list over gloo)."""
 
     def __init__(self, raytracer, uid, world, rank, tile_size=64, overlap=True):
-        import ctypes
-        from . import _native as N
         self.rt, self.world, self.rank, self.T = raytracer, world, rank, tile_size
         idbuf = (ctypes.c_uint8 * N.VHX_MGPU_ID_BYTES).from_buffer_copy(uid)
         h = ctypes.c_void_p()
@@ -170,38 +166,29 @@ class MgpuRenderer:
         return self.rt._check(rc)
 
     def set_overlap(self, on):
-        from . import _native as N
         self._check(N.lib().vhx_mgpu_set_overlap(self._h, 1 if on else 0))
 
     def set_frames_in_flight(self, frames):
-        from . import _native as N
         self._check(N.lib().vhx_mgpu_set_frames_in_flight(self._h, frames))
 
     def broadcast_tree(self, flat=None):
         """Rank 0 passes the FlatTree, the other ranks None (collective)."""
-        import ctypes
-        from . import _native as N
         desc = ctypes.byref(flat.desc) if flat is not None else None
         self._check(N.lib().vhx_mgpu_broadcast_tree(self._h, desc))
         self.rt._tree = flat
 
     def render(self, cam, fb_rgba=None, fb_depth=None):
         """Collective; rank 0 passes device framebuffers (torch tensors of width*height int32 / float32)."""
-        import ctypes
-        from . import _native as N
         p = lambda t: ctypes.c_void_p(None if t is None else t.data_ptr())
         self._check(N.lib().vhx_mgpu_render(self._h, ctypes.byref(cam), p(fb_rgba), p(fb_depth)))
 
     def sync(self):
-        import ctypes
-        from . import _native as N
         ms = ctypes.c_float()
         self._check(N.lib().vhx_mgpu_sync(self._h, ctypes.byref(ms)))
         return ms.value
 
     def set_root_slots(self, slots):
         """Collective: rank 0 traces `slots` of the slots + N - 1 tile slots (vhx_mgpu_set_root_slots)."""
-        from . import _native as N
         self._check(N.lib().vhx_mgpu_set_root_slots(self._h, slots))
 
     def set_planes(self, planes):
@@ -219,8 +206,6 @@ class MgpuRenderer:
     def balance(self, cam, frames=4):
         """Collective: measures rank 0's trace and the transfers into it and picks rank 0's share
         (vhx_mgpu_balance); returns (root_slots, trace_ms, transfer_ms)."""
-        import ctypes
-        from . import _native as N
         r, a, g = ctypes.c_uint32(), ctypes.c_float(), ctypes.c_float()
         self._check(N.lib().vhx_mgpu_balance(self._h, ctypes.byref(cam), frames, ctypes.byref(r), ctypes.byref(a),
                                              ctypes.byref(g)))
@@ -229,21 +214,16 @@ class MgpuRenderer:
     def measure(self, cam, frames=4):
         """Collective: this rank's median trace and transfer device times (ms) at the current split, frames rendered
         one at a time (vhx_mgpu_measure)."""
-        import ctypes
-        from . import _native as N
         a, g = ctypes.c_float(), ctypes.c_float()
         self._check(N.lib().vhx_mgpu_measure(self._h, ctypes.byref(cam), frames, ctypes.byref(a), ctypes.byref(g)))
         return a.value, g.value
 
     def rays(self, width, height):
-        import ctypes
-        from . import _native as N
         n = ctypes.c_uint64()
         self._check(N.lib().vhx_mgpu_info(self._h, width, height, None, None, ctypes.byref(n)))
         return n.value
 
     def close(self):
-        from . import _native as N
         if getattr(self, "_h", None) and self._h.value:
             N.lib().vhx_mgpu_destroy(self._h)
             self._h = None

@@ -187,7 +187,9 @@ class Raytracer:
         """tune: a vhx_set_tuning spec ("key=value;..."), scheduling knobs of experiments (results never change)."""
         lib = N.lib()
         n = ctypes.c_int()
-        N.check(lib.vhx_device_count(ctypes.byref(n)))
+        rc = lib.vhx_device_count(ctypes.byref(n))
+        if rc != N.VHX_OK:
+            raise N.VhxError(rc, "vhx_device_count: " + (lib.vhx_device_error() or b"").decode())
         if n.value == 0:
             raise RuntimeError("voxelhex_amd: no HIP device is visible (the raytracer has no CPU fallback)")
         h = ctypes.c_void_p()
