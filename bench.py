@@ -168,7 +168,7 @@ def pmc_traffic(workload):
     return None if e is None else e
 
 
-FRAME_KERNELS = ("k_trace_primary<false", "k_trace_queue<false", "k_trace_refill<", "k_count_flags", "k_scan_counts", "k_emit_flags",
+FRAME_KERNELS = ("k_trace_primary<false", "k_trace_queue<false", "k_count_flags", "k_scan_counts", "k_emit_flags",
                  "k_gather_chunks", "k_put_queue_args")
 
 

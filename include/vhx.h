@@ -177,8 +177,7 @@ int vhx_get_pass_budgets(const vhx_ctx *ctx, uint32_t *budgets, uint32_t *n, int
  * "key=value[;key=value...]" with keys budgets (list, fixes the schedule), adaptive (0/1), rpw (list: rays per wave of
  * queue passes 1.., 0 = adaptive), tw, xcdg, resume (0/1), save_from, qblock (64/128/256), qwaves (fixes the schedule),
  * qwavesm, qwaves0, qxcd, qxcd_all (0/1), sparse (list, fixes the schedule), qorder ("[m]N[z|r]" or 0), qsort (0 or
- * 256..2048: segment node sort of the queue passes), qsortp (pass mask), qsortb (workgroups), refill (0..64:
- * lane refill of the unbounded last pass at that many idle lanes, 0 = off). The
+ * 256..2048: segment node sort of the queue passes), qsortp (pass mask), qsortb (workgroups). The
  * library reads no environment variable for any of them. Unknown keys or malformed values:
  * VHX_E_INVALID_ARG and nothing is changed. */
 int vhx_set_tuning(vhx_ctx *ctx, const char *spec);

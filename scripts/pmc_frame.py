@@ -19,7 +19,7 @@ import os
 import sys
 from collections import defaultdict
 
-FRAME_KERNELS = ("k_trace_primary<false", "k_trace_queue<false", "k_trace_refill<", "k_count_flags", "k_scan_counts", "k_emit_flags",
+FRAME_KERNELS = ("k_trace_primary<false", "k_trace_queue<false", "k_count_flags", "k_scan_counts", "k_emit_flags",
                  "k_gather_chunks", "k_put_queue_args")
 PEAK_VALU_WAVE_INSTR_PER_S = 1024 * 2.4e9 / 2
 

@@ -40,7 +40,7 @@ for path in sorted(glob.glob(os.path.join(d, "pmc*_counter_collection.csv"))):
         if e["name"].startswith("k_trace_primary<false"):
             open_frame[e["queue"]] = len(frames)
             frames.append([e])
-        elif e["name"].startswith(("k_trace_queue<false", "k_trace_refill<")) and e["queue"] in open_frame:
+        elif e["name"].startswith("k_trace_queue<false") and e["queue"] in open_frame:
             frames[open_frame[e["queue"]]].append(e)
     most = max((len(f) for f in frames), default=0)
     keep = [f for i, f in enumerate(frames) if i >= skip and (not inflight_only or len(f) == most)]

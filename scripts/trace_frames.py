@@ -12,7 +12,7 @@ from collections import defaultdict
 
 rows = list(csv.DictReader(open(sys.argv[1])))
 skip, steps = int(sys.argv[2]), int(sys.argv[3])
-frame_k = ("k_trace_primary<false", "k_trace_queue<false", "k_trace_refill<", "k_count_flags", "k_scan_counts", "k_emit_flags",
+frame_k = ("k_trace_primary<false", "k_trace_queue<false", "k_count_flags", "k_scan_counts", "k_emit_flags",
            "k_gather_chunks", "k_put_queue_args")
 ks = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"].replace("void ", ""))
             for r in rows)

@@ -103,7 +103,7 @@ def test_random_rays_vs_oracle(gpu, oracle, scene, size, bd):
 def test_degenerate_directions_vs_oracle(gpu, oracle):
     """Rays whose distances are NaN or infinite (zero, NaN and infinite direction components, from inside and outside
     the tree): the reference loops until the iteration bound and reports a miss where such a ray stops making progress;
-    so do the kernels (a VHX_WALK_PROGRESS build ends it as a miss at once), and a ray that runs past the bound inside a
+    so do the kernels, and a ray that runs past the bound inside a
     budgeted pass must not be resumed; the same result in every field, for every pass schedule."""
     flat = vhx.FlatTree.build_scene(N.VHX_SCENE_LATTICE_CUBE, 64, 4)
     gpu.upload(flat)

@@ -68,10 +68,6 @@ struct TreeStore {
 #ifndef VHX_QSORT_IDLE
 #define VHX_QSORT_IDLE 256u
 #endif
-// lane refill of the lone-frame schedule's unbounded pass (k_trace_refill in vhx_device.hip; tune "refill=k")
-#ifndef VHX_REFILL_IDLE
-#define VHX_REFILL_IDLE 0u
-#endif
 #define VHX_QSORT_MAX 2048u
 
 struct vhx_ctx {
@@ -123,7 +119,6 @@ struct vhx_ctx {
         uint32_t queue_waves_per_cu;         // waves of a queue pass per CU
         uint32_t qorder;                     // order of a primary frame's pass-0 queue (vhx_ctx::qorder below)
         uint32_t qsort;                      // queue passes: segments of this many queue entries sorted by saved node
-        uint32_t refill;                     // unbounded last pass: lane refill at this many idle lanes (0 = off)
     };
     // Adaptive scheduling (default; vhx_set_pass_budgets or a tuning key fixes the schedule instead): at each
     // trace the context looks at the other contexts of its tree (vhx_create_shared) and picks
@@ -141,8 +136,8 @@ struct vhx_ctx {
     //    three-budget ladders 1.31-1.51 ms, fewer rays per wave in a last pass no better): every extra pass lengthens a
     //    lone frame's critical path.
     bool adaptive = true;
-    Sched sched_busy = {{24u, 72u, 216u, 648u}, 5u, {12u}, 3u, VHX_QORDER_BUSY, VHX_QSORT_BUSY, 0u};
-    Sched sched_idle = {{64u}, 2u, {0u}, 8u, VHX_QORDER_IDLE, VHX_QSORT_IDLE, VHX_REFILL_IDLE};
+    Sched sched_busy = {{24u, 72u, 216u, 648u}, 5u, {12u}, 3u, VHX_QORDER_BUSY, VHX_QSORT_BUSY};
+    Sched sched_idle = {{64u}, 2u, {0u}, 8u, VHX_QORDER_IDLE, VHX_QSORT_IDLE};
     int last_sched = -1;  // the schedule of the last trace: 1 busy, 0 idle, -1 fixed (vhx_get_pass_budgets)
     // the schedule in force (the selected one, or the fixed one)
     uint32_t budgets[VHX_MAX_BUDGETS] = {24u, 72u, 216u, 648u};
@@ -180,9 +175,6 @@ struct vhx_ctx {
     int qsort_force = -1;
     uint32_t qsort_passes = 0xFEu;   // bit p: the queue of pass p is sorted (tune "qsortp")
     uint32_t qsort_blocks = 2048u;   // workgroups of a sort launch, striding over the segments (tune "qsortb")
-    // lane refill of the unbounded last pass (Sched::refill): in force for this trace; tune "refill=k" forces it (-1: not)
-    uint32_t refill = 0;
-    int refill_force = -1;
 };
 
 #define VHX_HIP(ctx, call)                                                                                         \

@@ -50,39 +50,6 @@ __device__ unsigned long long g_prof[5 * 16 * 2];
     do {                         \
     } while (0)
 #endif
-// Perturbation builds (diagnostics, scripts/probes/probe_perturb.sh): VHX_PERTURB_VALU / _SALU = N adds N dependent
-// dummy VALU / SALU instructions to every walk trip, to measure what bounds the frame (a VALU-issue-bound frame slows in
-// proportion to the VALU instructions added).
-#ifndef VHX_PERTURB_VALU
-#define VHX_PERTURB_VALU 0
-#endif
-#ifndef VHX_PERTURB_SALU
-#define VHX_PERTURB_SALU 0
-#endif
-__device__ __forceinline__ void perturb_trip() {
-#if VHX_PERTURB_VALU
-    {
-        float x = 0.0f;
-#pragma unroll
-        for (int i = 0; i < VHX_PERTURB_VALU; ++i) asm volatile("v_add_f32 %0, %0, %0" : "+v"(x));
-    }
-#endif
-#if VHX_PERTURB_SALU
-    {
-        uint32_t x = 0;
-#pragma unroll
-        for (int i = 0; i < VHX_PERTURB_SALU; ++i) asm volatile("s_add_u32 %0, %0, 1" : "+s"(x) : : "scc");
-    }
-#endif
-}
-// VHX_WALK_PROGRESS (experiment, default 0): in builds without byte counting the walk loops end a ray that makes no
-// progress (no axis stepped: NaN distances) as a miss, where the reference loops until the iteration bound and then
-// reports a miss (the same result), instead of testing the bound in every trip; the pass budget counts the walk's axis
-// steps. Two VALU instructions fewer per trip, but 3 more VGPRs in pass 0 (73: 6 waves per SIMD instead of 7): the bench
-// frame took 0.597 against 0.583 ms (profiles/r03/variants_r03d.txt), so it stays off.
-#ifndef VHX_WALK_PROGRESS
-#define VHX_WALK_PROGRESS 0
-#endif
 // pass slots of the default schedule {24, 72, 216, 648} (round 2's {24, 96, 768} uses slots 0, 1, 3, 4)
 __device__ __forceinline__ uint32_t pass_of_budget(uint32_t b) {
     return b >= VHX_MAX_ITERS ? 4u : (b <= 24u ? 0u : (b <= 96u ? 1u : (b <= 256u ? 2u : 3u)));
@@ -312,9 +279,7 @@ __device__ __forceinline__ void fill_hit(HitOut &h, uint32_t v, uint32_t cell, F
 // traversal loop (finish_hit), so the loop carries two registers for it instead of a dozen.
 template <bool COUNT, int BD>
 __device__ __forceinline__ bool probe_brick(const DevTree &t, const RayD &r, F3d &p, uint32_t desc, uint64_t cocc,
-                                            CubeD bb, HitOut &h, uint32_t &iters, int32_t &hflat, bool &stuck,
-                                            uint32_t pp = 0) {
-    constexpr bool PROG = !COUNT && VHX_WALK_PROGRESS;
+                                            CubeD bb, HitOut &h, uint32_t &iters, int32_t &hflat, uint32_t pp = 0) {
     // one branch (a Parted brick's walk); Empty and Solid (cpu.rs:249-260) resolve by selects. VHX_EMPTY has the
     // Solid bit set, so "Parted" is simply the bit clear.
     const bool solid = (desc & VHX_SOLID_BIT) != 0u && desc != VHX_EMPTY;
@@ -362,11 +327,9 @@ __device__ __forceinline__ bool probe_brick(const DevTree &t, const RayD &r, F3d
                            fz = spos(r.sg.z) ? 0u : BD - 1u;
             const uint32_t F = fx + fy * BD + fz * (BD * BD);
             uint32_t jx = (uint32_t)ix ^ fx, jy = (uint32_t)iy ^ fy, jz = (uint32_t)iz ^ fz;
-            const uint32_t js0 = jx + jy + jz;
             for (;;) {
                 VHX_PROF_BLOCK(pp, 2);
-                perturb_trip();
-                if (!PROG) ++iters;
+                ++iters;
                 // dda_step_to_next_sibling (cpu.rs:104-132) on the cell {cmin, unit}
                 const F2 sxy = (exy - pxy) * sfxy;
                 const float dx = __builtin_fabsf(sxy.x), dy = __builtin_fabsf(sxy.y),
@@ -397,14 +360,8 @@ __device__ __forceinline__ bool probe_brick(const DevTree &t, const RayD &r, F3d
                 // the bound only ends a ray whose steps make no progress (a zero or NaN direction); at the bound the
                 // oracle tests the cell it stepped into and stops before the next step, like this exit
                 static_assert(VHX_MAX_ITERS == (1u << 22), "bound test below");
-                if (PROG) {
-                    stuck = !(mx || my || mz);  // no axis stepped: the ray cannot make progress (VHX_WALK_PROGRESS)
-                    if ((oob | bit) != 0u || stuck) break;
-                } else if ((oob | bit | (iters >> 22)) != 0u) {
-                    break;
-                }
+                if ((oob | bit | (iters >> 22)) != 0u) break;
             }
-            if (PROG) iters += jx + jy + jz - js0;  // the walk's axis steps (the pass budget only schedules)
             // hit = the exit test, recomputed once from the final cell instead of carrying the loop's booleans out of
             // it (opaque copies keep the compiler from reusing the in-loop values, which costs mask bookkeeping per
             // cell)
@@ -446,18 +403,9 @@ constexpr OccTab make_occ_tab() {
     return t;
 }
 __constant__ OccTab g_occ_tab = make_occ_tab();
-// VHX_LDS_ROOT (experiment): the root's header and its 64 child records are copied into LDS after the
-// occupancy table (OCC_TAB_WORDS words in all), and node iterations at the root read them there
-#ifndef VHX_LDS_ROOT
-#define VHX_LDS_ROOT 0
-#endif
-#define OCC_TAB_WORDS (512u + (VHX_LDS_ROOT ? 2u + 64u * 2u : 0u))
-__device__ __forceinline__ void fill_occ_tab(uint64_t *occ_tab, const DevTree &t) {
+#define OCC_TAB_WORDS 512u
+__device__ __forceinline__ void fill_occ_tab(uint64_t *occ_tab) {
     for (uint32_t i = threadIdx.x; i < 512u; i += blockDim.x) occ_tab[i] = g_occ_tab.v[i];
-    if (VHX_LDS_ROOT && t.child_rec) {
-        uint4 *root = (uint4 *)(occ_tab + 512);
-        for (uint32_t i = threadIdx.x; i < 65u; i += blockDim.x) root[i] = i == 0 ? t.hdr[0] : t.child_rec[i - 1];
-    }
 }
 
 // Saved traversal state of a ray abandoned at a pass budget (multi-pass scheduling): everything the loop below
@@ -597,13 +545,7 @@ struct Trav {
         uint4 lh;
         uint32_t slot;
         uint64_t cocc = 0;
-        if (VHX_LDS_ROOT && Brick<BD>::WORDS == 1 && node == 0u) {
-            const uint4 *root = (const uint4 *)(occ_tab + 512);
-            lh = root[0];
-            const uint4 cr = root[1u + (target & 63u)];
-            slot = cr.x;
-            cocc = ((uint64_t)cr.z << 32) | (uint64_t)cr.y;
-        } else if (Brick<BD>::WORDS == 1) {
+        if (Brick<BD>::WORDS == 1) {
             lh = t.hdr[node];
             const uint4 cr = t.child_rec[(uint64_t)node * 64u + (target & 63u)];
             slot = cr.x;
@@ -631,8 +573,7 @@ struct Trav {
             hdesc = Brick<BD>::WORDS == 1 || !uniform ? slot : t.children[(uint64_t)node * 64u];
             CubeD bb = uniform ? cur : tb;
             if (!uniform && tbok == 0u) bb = child_bounds(cur, target);
-            bool stuck = false;
-            ex = probe_brick<COUNT, BD>(t, r, p, hdesc, cocc, bb, h, iters, hflat, stuck, pp) ? 1u : (stuck ? 2u : 0u);
+            ex = probe_brick<COUNT, BD>(t, r, p, hdesc, cocc, bb, h, iters, hflat, pp) ? 1u : 0u;
         }
         // MIP stand-in (viewport_render.wgsl:438-454, probe_MIP 328-364): the target sectant is occupied but its child
         // entry is absent (a view that does not hold it). The node's MIP brick is traced over the node's cube from a
@@ -651,14 +592,11 @@ struct Trav {
                         Brick<BD>::WORDS == 1 && (mdesc & VHX_SOLID_BIT) == 0u ? t.brick_occ[mdesc] : 0ull;
                     F3d pm = p;
                     int32_t mflat;
-                    bool stuck = false;
-                    if (probe_brick<COUNT, BD>(t, r, pm, mdesc, mocc, cur, h, iters, mflat, stuck)) {
+                    if (probe_brick<COUNT, BD>(t, r, pm, mdesc, mocc, cur, h, iters, mflat)) {
                         p = pm;
                         hdesc = mdesc;
                         hflat = mflat;
                         ex = 4u;
-                    } else if (stuck) {
-                        ex = 2u;
                     }
                 }
             }
@@ -732,13 +670,9 @@ struct Trav {
                 const F2 sgsxy = mk2(sgs.x, sgs.y), sfxy = r.sfxy, dxy = r.dxy;
                 F2 pxy = mk2(p.x, p.y);
                 float pz = p.z;
-                constexpr bool PROG = !COUNT && VHX_WALK_PROGRESS;
-                const uint32_t js0 = jx + jy + jz;
-                bool stuck = false;
                 for (;;) {
                     VHX_PROF_BLOCK(pp, 6);
-                    perturb_trip();
-                    if (!PROG) ++iters;
+                    ++iters;
                     const F2 sxy = (exy - pxy) * sfxy;
                     const float dx = __builtin_fabsf(sxy.x), dy = __builtin_fabsf(sxy.y),
                                 dz = __builtin_fabsf((ez - pz) * r.sfz);
@@ -755,21 +689,14 @@ struct Trav {
                     const uint32_t oob = (jx | jy | jz) & ~3u;  // non-zero iff the walk left the node
                     const uint32_t tg = (jx + jy * 4u + jz * 16u) ^ F;
                     const uint32_t bit = (uint32_t)(wocc >> (tg & 63u)) & 1u;
-                    if (PROG) {
-                        stuck = !(mx || my || mz);  // no progress: a miss (VHX_WALK_PROGRESS)
-                        if ((oob | bit) != 0u || stuck) break;
-                    } else if ((oob | bit | ((iters - 1u) >> 22)) != 0u) {
-                        break;  // left | occupied | iters > 2^22
-                    }
+                    if ((oob | bit | ((iters - 1u) >> 22)) != 0u) break;  // left | occupied | iters > 2^22
                 }
-                if (PROG && !pop) iters += jx + jy + jz - js0;
                 p = mk(pxy.x, pxy.y, pz);
                 asm volatile("" : "+v"(jx), "+v"(jy), "+v"(jz));
                 target = (jx | jy | jz) < 4u ? (jx + jy * 4u + jz * 16u) ^ F : 64u;
                 tb.min = mk(exy.x - usg.x, exy.y - usg.y, ez - usg.z);  // exact: undoes the exact e = tb.min + usg
-                if (PROG && stuck) ex = 2u;
                 if (pop) {
-                    if (!PROG) iters -= 1u;  // POP's step is not one of the walk's steps
+                    iters -= 1u;  // POP's step is not one of the walk's steps
                     tbok = 1u;
                     if (count == 0) {
                         VHX_PROF_BLOCK(pp, 7);

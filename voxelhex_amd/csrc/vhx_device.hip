@@ -566,38 +566,11 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t bid, uint32_t n, uint32_t
     return ((k / G) * 8u + x) * G + k % G;
 }
 
-// occupancy of the traversal kernels (waves per SIMD the register allocation must allow; 0 = the compiler's choice).
-// Default: the queue kernel of brick_dim 1 and 4 fits 96 VGPRs (5 waves per SIMD instead of 4, no spills under the
-// iterative-ilp scheduler of _build.py); brick_dim 2 would spill 4 VGPRs and 8..32 16, so they keep 4 waves (the
-// minimum of 4 compiles to the same code as no attribute)
-#ifndef VHX_QUEUE_WPE
-#define VHX_QUEUE_WPE 0
-#endif
-#ifndef VHX_WAVE_TILE
-#define VHX_WAVE_TILE 0  // pass-0 pixel footprint of a wave (experiment knob, see k_trace_primary)
-#endif
-#ifndef VHX_PRIMARY_WPE
-#define VHX_PRIMARY_WPE 0
-#endif
-#if VHX_QUEUE_WPE > 0
-#define VHX_QUEUE_ATTR __attribute__((amdgpu_waves_per_eu(VHX_QUEUE_WPE)))
-#else
+// occupancy of the queue kernel (waves per SIMD the register allocation must allow): the queue kernel of brick_dim 1
+// and 4 fits 96 VGPRs (5 waves per SIMD instead of 4, no spills under the iterative-ilp scheduler of _build.py);
+// brick_dim 2 would spill 4 VGPRs and 8..32 16, so they keep 4 waves (the minimum of 4 compiles to the same code as no
+// attribute)
 #define VHX_QUEUE_ATTR __attribute__((amdgpu_waves_per_eu(!COUNT && (BD == 1 || BD == 4) ? 5 : 4)))
-#endif
-// the refill kernel: its register allocation bound (waves per SIMD; 0 = the compiler's choice)
-#ifndef VHX_REFILL_WPE
-#define VHX_REFILL_WPE 4
-#endif
-#if VHX_REFILL_WPE > 0
-#define VHX_QUEUE_ATTR_REFILL __attribute__((amdgpu_waves_per_eu(VHX_REFILL_WPE)))
-#else
-#define VHX_QUEUE_ATTR_REFILL
-#endif
-#if VHX_PRIMARY_WPE > 0
-#define VHX_PRIMARY_ATTR __attribute__((amdgpu_waves_per_eu(VHX_PRIMARY_WPE)))
-#else
-#define VHX_PRIMARY_ATTR
-#endif
 
 // One workgroup = 256 lanes = a 16x16 pixel block made of four 8x8 wave tiles (wave64-coherent ray bundles, the
 // 8x8 footprint of the reference's @workgroup_size(8, 8, 1)). Blocks are dealt tile by tile.
@@ -618,28 +591,21 @@ __device__ __forceinline__ float prepass_start(const FastD &f, uint32_t px, uint
 }
 
 template <bool COUNT, int BD, bool FAST = false, bool MIP = false>
-__global__ void __launch_bounds__(256) VHX_PRIMARY_ATTR k_trace_primary(DevTree t, CamD cam, OutD out, uint32_t T, uint32_t tiles_x,
+__global__ void __launch_bounds__(256) k_trace_primary(DevTree t, CamD cam, OutD out, uint32_t T, uint32_t tiles_x,
                                                        uint32_t tile_start, uint32_t tile_stride, uint32_t layout,
                                                        uint32_t blocks_per_tile_x, uint32_t blocks_per_tile,
                                                        PassQ q, FastD fast = FastD{}) {
     __shared__ uint64_t occ_tab[OCC_TAB_WORDS];
-    fill_occ_tab(occ_tab, t);
+    fill_occ_tab(occ_tab);
     __syncthreads();
     const uint32_t bid = xcd_block(blockIdx.x, gridDim.x, q.xcd_group);
     const uint32_t j = bid / blocks_per_tile;  // j-th tile of this rank
     const uint32_t sb = bid - j * blocks_per_tile;
     const uint32_t tile = tile_start + j * tile_stride;
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-#if VHX_WAVE_TILE == 1  // experiment: 16x4 pixels per wave (waves stacked vertically in the 16x16 block)
-    const uint32_t lx = (sb % blocks_per_tile_x) * 16u + (lane & 15u);
-    const uint32_t ly = (sb / blocks_per_tile_x) * 16u + wave * 4u + (lane >> 4);
-#elif VHX_WAVE_TILE == 2  // experiment: 4x16 pixels per wave
-    const uint32_t lx = (sb % blocks_per_tile_x) * 16u + wave * 4u + (lane & 3u);
-    const uint32_t ly = (sb / blocks_per_tile_x) * 16u + (lane >> 2);
-#else  // 8x8 pixels per wave, four waves per 16x16 block
+    // 8x8 pixels per wave, four waves per 16x16 block
     const uint32_t lx = (sb % blocks_per_tile_x) * 16u + (wave & 1u) * 8u + (lane & 7u);
     const uint32_t ly = (sb / blocks_per_tile_x) * 16u + (wave >> 1) * 8u + (lane >> 3);
-#endif
     const uint32_t px = (tile % tiles_x) * T + lx, py = (tile / tiles_x) * T + ly;
     const bool valid = lx < T && ly < T && px < cam.width && py < cam.height;
     const uint64_t idx = layout == VHX_LAYOUT_FRAMEBUFFER ? (uint64_t)py * cam.width + px
@@ -669,7 +635,7 @@ template <bool COUNT, int BD, bool MIP = false>
 __global__ void __launch_bounds__(256) k_trace_rays(DevTree t, const float *__restrict__ rays, uint64_t n, OutD out,
                                                     PassQ q) {
     __shared__ uint64_t occ_tab[OCC_TAB_WORDS];
-    fill_occ_tab(occ_tab, t);
+    fill_occ_tab(occ_tab);
     __syncthreads();
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool done = true;
@@ -712,7 +678,7 @@ template <bool COUNT, int BD, bool MIP = false>
 __global__ void __launch_bounds__(256) VHX_QUEUE_ATTR k_trace_queue(DevTree t, const QueueArgs *qa, const uint32_t *__restrict__ in,
                                                      const uint32_t *in_n, uint32_t *grab, PassQ q) {
     __shared__ uint64_t occ_tab[OCC_TAB_WORDS];
-    fill_occ_tab(occ_tab, t);
+    fill_occ_tab(occ_tab);
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t n = *in_n;
@@ -782,80 +748,6 @@ __global__ void __launch_bounds__(256) VHX_QUEUE_ATTR k_trace_queue(DevTree t, c
             const uint64_t m = __ballot(push);
             if (push) q.tmp[(uint64_t)chunk * rpw + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = idx;
             if (lane == 0) q.counts[chunk] = (uint32_t)__popcll(m);
-        }
-    }
-}
-
-// Lane refill for the unbounded last pass of the lone-frame schedule. Persistent waves keep one
-// resumed ray per lane and step every lane one node iteration at a time; once `refill` or more lanes of a wave are idle
-// (their rays finished) the wave takes that many rays from the queue at once (one atomic per wave) and resumes them in
-// the idle lanes, so the pass's lanes stay busy instead of idling behind each chunk's longest ray (the wave simulator,
-// scripts/sim: 17.3 -> 26.2 active lanes per loop trip and 27 % fewer VALU instructions in the bench frame's tail pass
-// at a threshold of 32). Only which lane traces a ray and when change: every ray's traversal is the same uninterrupted
-// deterministic sequence (Trav), so results are bit-identical. Queue order (and its node sort) is the take order.
-template <int BD>
-__global__ void __launch_bounds__(256) VHX_QUEUE_ATTR_REFILL k_trace_refill(DevTree t, const QueueArgs *qa,
-                                                                            const uint32_t *__restrict__ in,
-                                                                            const uint32_t *in_n, uint32_t *grab,
-                                                                            PassQ q, uint32_t refill) {
-    __shared__ uint64_t occ_tab[OCC_TAB_WORDS];
-    fill_occ_tab(occ_tab, t);
-    __syncthreads();
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t n = *in_n;
-    Trav<false, BD, false> tr;
-    HitOut h;
-    F3d o = mk(0.0f, 0.0f, 0.0f);
-    uint32_t idx = 0;
-    bool active = false, drained = false;
-    for (;;) {
-        const uint64_t act = __ballot(active);
-        const uint32_t nidle = 64u - (uint32_t)__popcll(act);
-        if (!drained && (nidle >= refill || act == 0ull)) {
-            uint32_t base = 0;
-            if (lane == 0) base = atomicAdd(grab, nidle);
-            base = __builtin_amdgcn_readfirstlane(__shfl(base, 0));
-            if (base + nidle >= n) drained = true;  // wave-uniform: no later take can find a ray
-            if (!active) {
-                const uint32_t i = base + (uint32_t)__popcll(~act & ((1ull << lane) - 1ull));  // rank among idle lanes
-                if (i < n) {
-                    idx = in[i];
-                    const QueueArgs *a = qa;
-                    asm volatile("" : "+s"(a));  // loads through `a` stay here (not hoisted into live registers)
-                    F3d d;
-                    ray_of(a->cam, a->src, idx, o, d);
-                    h.bytes = 0;
-                    h.iters = 0;
-                    active = tr.begin(t, o, d, h, q.state, idx, true);  // a resumed ray always continues
-                }
-            }
-        }
-        if (__ballot(active) == 0ull) {
-            if (drained) break;  // wave-uniform: nothing traced, nothing left to take
-            continue;
-        }
-        // step the wave's rays until enough lanes are idle for a take (or, drained, until none traces): an inner loop
-        // of node iterations only, so that the resume code above stays out of the hot loop
-        const uint32_t keep = drained ? 1u : 65u - refill;  // leave once fewer than `keep` lanes still trace
-        // (a lane whose ray ends waits, its state in place, until the loop is left: the hit record and the stores are
-        // written after it, outside the node loop)
-        bool tracing = true;
-        for (;;) {
-            if (active && tracing) {
-                tr.step(t, occ_tab, h, VHX_MAX_ITERS);
-                tracing = tr.ex == 0u;
-            }
-            if ((uint32_t)__popcll(__ballot(active && tracing)) < keep) break;
-        }
-        if (active && !tracing) {
-            tr.end(t, h, nullptr, 0);
-            const QueueArgs *b = qa;
-            asm volatile("" : "+s"(b));
-            if (b->src.kind == 3u)
-                store_shadow(b->out, idx, h);
-            else
-                store(t, b->out, idx, o, h);
-            active = false;
         }
     }
 }
@@ -1185,7 +1077,6 @@ static void select_schedule(vhx_ctx *c) {
     if (!c->adaptive) {
         c->last_sched = -1;
         c->qsort = c->qsort_force >= 0 ? (uint32_t)c->qsort_force : c->sched_busy.qsort;  // a fixed schedule: the busy one's
-        c->refill = c->refill_force >= 0 ? (uint32_t)c->refill_force : c->sched_busy.refill;
         return;
     }
     bool busy = false;
@@ -1204,7 +1095,6 @@ static void select_schedule(vhx_ctx *c) {
     c->queue_waves = s.queue_waves_per_cu * c->cus;
     c->qorder = s.qorder;
     c->qsort = c->qsort_force >= 0 ? (uint32_t)c->qsort_force : s.qsort;
-    c->refill = c->refill_force >= 0 ? (uint32_t)c->refill_force : s.refill;
     c->last_sched = busy ? 1 : 0;
 }
 
@@ -1371,12 +1261,7 @@ static int launch_queue_passes(vhx_ctx *c, const DevTree &t, const CamD &cam, co
     }
     QueueArgs *qa = nullptr;
     if (first < npass && (rc = put_qargs(c, cam, src, o, qa))) return rc;
-#ifdef VHX_PROBE_PASSES  // diagnostic builds only: run the first VHX_PROBE_PASSES passes (the frame is incomplete)
-    const uint32_t np_run = std::min<uint32_t>(npass, VHX_PROBE_PASSES);
-#else
-    const uint32_t np_run = npass;
-#endif
-    for (uint32_t p = first; p < np_run && !rc; ++p) {
+    for (uint32_t p = first; p < npass && !rc; ++p) {
         const uint32_t *in = (const uint32_t *)c->queue[(p - 1) & 1u].ptr;  // p = 0: queue[1]
         const uint32_t *in_n = p > 0 ? ctl + (p - 1) : ctl + 7;
         const PassQ q = pass_q(c, p, npass);
@@ -1384,18 +1269,8 @@ static int launch_queue_passes(vhx_ctx *c, const DevTree &t, const CamD &cam, co
         const uint32_t qwaves = p == 0 ? c->queue_waves0
                                 : (p + 1 < npass && c->queue_waves_mid ? c->queue_waves_mid : c->queue_waves);
         const unsigned qgrid = (qwaves * 64u + c->qblock - 1) / c->qblock;
-        bool launched = false;
-        if constexpr (!COUNT && !MIP) {
-            // the unbounded last pass over resumed rays with lane refill (Sched::refill, the lone-frame schedule)
-            if (p + 1 == npass && p > 0 && c->refill && q.resume && q.state) {
-                k_trace_refill<BD><<<qgrid, c->qblock, 0, c->stream>>>(t, qa, in, in_n,
-                                                                       ctl + 16u + QCTL_PASS_WORDS * p, q, c->refill);
-                launched = true;
-            }
-        }
-        if (!launched)
-            k_trace_queue<COUNT, BD, MIP><<<qgrid, c->qblock, 0, c->stream>>>(t, qa, in, in_n,
-                                                                             ctl + 16u + QCTL_PASS_WORDS * p, q);
+        k_trace_queue<COUNT, BD, MIP><<<qgrid, c->qblock, 0, c->stream>>>(t, qa, in, in_n,
+                                                                         ctl + 16u + QCTL_PASS_WORDS * p, q);
         debug_passes(c, "queue pass");
         if (p + 1 < npass) {
             rc = compact_chunks(c, 0, in_n, q.rpw, q.rpw, (uint32_t *)c->queue[p & 1u].ptr, ctl + p,
@@ -1616,9 +1491,6 @@ static int apply_tuning(vhx_ctx *c, const std::string &key, const std::string &v
     } else if (key == "qsort") {  // segment length of the queue passes' node sort: 0 = off, else 256 .. VHX_QSORT_MAX
         if (!parse_u32(val, x) || (x && (x < 256 || x > VHX_QSORT_MAX || (x & (x - 1))))) return bad();
         c->qsort_force = (int)x;
-    } else if (key == "refill") {  // lane refill of the unbounded last pass: idle lanes that trigger a take, 0 = off
-        if (!parse_u32(val, x) || x > 64) return bad();
-        c->refill_force = (int)x;
     } else if (key == "qsortp") {  // bit mask of the queue passes whose input is sorted
         if (!parse_u32(val, x)) return bad();
         c->qsort_passes = x;
@@ -1842,7 +1714,6 @@ void vhx::copy_sched(vhx_ctx *c, const vhx_ctx *owner) {
     c->qxcd = owner->qxcd;
     c->qxcd_all = owner->qxcd_all;
     c->qsort_force = owner->qsort_force;
-    c->refill_force = owner->refill_force;
     c->qsort_passes = owner->qsort_passes;
     c->qsort_blocks = owner->qsort_blocks;
     std::memcpy(c->sparse, owner->sparse, sizeof(c->sparse));
