@@ -72,11 +72,15 @@ def parse():
                    help="skip the untimed check of the in-flight frames (frames_equal / golden_match)")
     p.add_argument("--no-pmc", action="store_true",
                    help="skip the rocprofv3 FETCH_SIZE child run (roofline.traffic from profiles/traffic.json)")
-    p.add_argument("--inflight", type=int, default=20,
-                   help="frames in flight per GPU: F contexts sharing the tree (vhx_create_shared), each on its own "
-                        "stream, frame i traced by context i %% F, so a frame's latency-bound long-ray tail overlaps the "
-                        "next frame's pass 0 (1 = one frame at a time); GPU_MAX_HW_QUEUES is raised to F + 4 so that every "
-                        "frame's stream has a hardware queue of its own")
+    p.add_argument("--inflight", type=int, default=None,
+                   help="contexts in flight per GPU: F contexts sharing the tree (vhx_create_shared), each on its own "
+                        "stream, frame (or batch) i traced by context i %% F, so a latency-bound long-ray tail overlaps the "
+                        "next frame's pass 0 (1 = one at a time). Default 20 frames in flight, with GPU_MAX_HW_QUEUES "
+                        "raised to F + 4 so that every frame's stream has a hardware queue of its own; with --batch, "
+                        "default 2 and the hardware queues left at the process default")
+    p.add_argument("--batch", type=int, default=0, metavar="K",
+                   help="frames per vhx_trace_primary_batch call (one pass ladder over K frames on one stream); 0 = one "
+                        "vhx_trace_primary per frame")
     p.add_argument("--orbit", type=float, default=0.0,
                    help="moving camera: frame k (warm-up included) views from angle 40 + k*ORBIT rad on the glass "
                         "camera's circle (0 = the reference bench's static camera); the roofline bytes are then the "
@@ -120,8 +124,8 @@ def frame_size(args, world):
         mode = "strong" if world > 1 else "single"
     if args.width and args.height:
         return args.width, args.height, ("weak" if mode == "weak" else "strong")
-    if mode == "single":
-        return HEADLINE[0], HEADLINE[1], "weak"
+    if mode == "single":  # one GPU, the fixed headline frame: no scaling is measured
+        return HEADLINE[0], HEADLINE[1], "none"
     if mode == "strong":
         return CONFIG4[0], CONFIG4[1], "strong"
     w, h = HEADLINE
@@ -168,13 +172,15 @@ def pmc_traffic(workload):
     return None if e is None else e
 
 
-FRAME_KERNELS = ("k_trace_primary<false", "k_trace_queue<false", "k_count_flags", "k_scan_counts", "k_emit_flags",
+FRAME_KERNELS = ("k_trace_primary<false", "k_trace_primary_batch<", "k_trace_queue<false", "k_count_flags", "k_scan_counts", "k_emit_flags",
                  "k_gather_chunks", "k_put_queue_args")
 
 
-def parse_pmc_dir(d):
-    """Per-frame figures from rocprofv3 counter_collection CSVs under `d` (see measure_traffic), or None."""
-    tot, per_kernel, frames = {}, {}, set()
+def parse_pmc_dir(d, blocks_per_frame=None):
+    """Per-frame figures from rocprofv3 counter_collection CSVs under `d` (see measure_traffic), or None. A pass-0
+    dispatch is one frame; a batch's pass-0 dispatch (k_trace_primary_batch) is Grid_Size / (256 x blocks_per_frame)
+    frames."""
+    tot, per_kernel, frames, batch_frames = {}, {}, set(), {}
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for row in csv.DictReader(open(f)):
             n = row["Kernel_Name"].replace("void ", "")
@@ -186,9 +192,11 @@ def parse_pmc_dir(d):
             k[c] = k.get(c, 0.0) + v
             if n.startswith("k_trace_primary<false"):
                 frames.add(row["Dispatch_Id"])
-    if not frames or "FETCH_SIZE" not in tot:
+            elif n.startswith("k_trace_primary_batch<") and blocks_per_frame:
+                batch_frames[row["Dispatch_Id"]] = int(row["Grid_Size"]) // (256 * blocks_per_frame)
+    if not (frames or batch_frames) or "FETCH_SIZE" not in tot:
         return None
-    nf = len(frames)
+    nf = len(frames) + sum(batch_frames.values())
     lanes = {k: round(v["SQ_THREAD_CYCLES_VALU"] / max(1.0, v["SQ_ACTIVE_INST_VALU"]), 2)
              for k, v in per_kernel.items() if "trace" in k and "SQ_ACTIVE_INST_VALU" in v}
     return {"bytes": tot["FETCH_SIZE"] * 1024.0 * 2.0 / nf, "frames": nf,
@@ -197,7 +205,7 @@ def parse_pmc_dir(d):
             "lanes": lanes}
 
 
-def measure_traffic(busy_only=False, tune=None):
+def measure_traffic(busy_only=False, tune=None, blocks_per_frame=None):
     """Memory-side read bytes per frame, measured now: this bench (same arguments, 5 timed + 1 warm-up frames, no
     roofline / CPU leg) under `rocprofv3 --pmc FETCH_SIZE --kernel-trace` as a child process, FETCH_SIZE summed over
     the frame kernels and divided by the pass-0 dispatches, x1024 B and x2 (gfx950: FETCH_SIZE derives from
@@ -231,27 +239,38 @@ def measure_traffic(busy_only=False, tune=None):
             return None
         if rc != 0:
             return None
-        return parse_pmc_dir(d)
+        return parse_pmc_dir(d, blocks_per_frame)
     except (OSError, ValueError, KeyError):
         return None
     finally:
         shutil.rmtree(d, ignore_errors=True)
 
 
-def cpu_baseline(flat, cam, W, H, threads_all):
+def cpu_baseline(flat, cam, W, H, threads_all, light=None):
     """The oracle (reference semantics, oracle/) on the host cores over the bench frame: all cores available to the
     process (OpenMP, dynamic over pixels), 1 warm-up + median of 5 full frames; and 1 core, 1 warm-up + median of 5
     frames of the same view at a quarter of the resolution per axis (a uniform 1/16 sample of the frame's rays, about
-    0.4 s each, so that the default bench still finishes in minutes)."""
+    0.4 s each, so that the default bench still finishes in minutes). With a light (config 5) each frame is the
+    primary frame plus the oracle's hard-shadow pass over its hits."""
     from tests._oracle import Oracle
     orc = Oracle()
+    fields = ("rgba", "depth", "value", "impact", "normal") if light is not None else ("rgba", "depth")
+
+    rays = {}
+
+    def frame(w, h, c, threads):
+        hits = orc.trace_primary(flat, c, 0, 0, w, h, threads=threads, fields=fields)
+        rays[(w, h)] = w * h
+        if light is not None:
+            orc.trace_shadows(flat, light, hits, threads=threads)
+            rays[(w, h)] += int((hits["value"] != 0xFFFFFFFF).sum())  # one shadow ray per hit
 
     def timed(w, h, c, threads):
-        orc.trace_primary(flat, c, 0, 0, w, h, threads=threads, fields=("rgba", "depth"))  # warm-up
+        frame(w, h, c, threads)  # warm-up
         ts = []
         for _ in range(5):
             t0 = time.perf_counter()
-            orc.trace_primary(flat, c, 0, 0, w, h, threads=threads, fields=("rgba", "depth"))
+            frame(w, h, c, threads)
             ts.append(time.perf_counter() - t0)
         return sorted(ts)[2]
 
@@ -260,7 +279,7 @@ def cpu_baseline(flat, cam, W, H, threads_all):
     w1, h1 = max(1, W // 4), max(1, H // 4)
     c1 = vhx.glass_camera(int(flat.desc.boxtree_size), w1, h1, target=(flat.desc.boxtree_size / 2.0,) * 3)
     t_one = timed(w1, h1, c1, 1)
-    return t_all, t_one, (w1, h1)
+    return t_all, t_one, (w1, h1), rays[(W, H)], rays[(w1, h1)]
 
 
 GOLDEN = os.path.join(ROOT, "tests", "golden", "frames.json")
@@ -357,7 +376,13 @@ def hw_queues(frames):
 
 def main():
     args = parse()
-    queues = hw_queues(max(1, args.inflight))
+    if args.inflight is None:
+        args.inflight = 2 if args.batch else 20
+    if args.batch:
+        # one stream per batch in flight: the box's default hardware queues (GPU_MAX_HW_QUEUES unset: 4) suffice
+        queues = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
+    else:
+        queues = hw_queues(max(1, args.inflight))
     import torch
     import torch.distributed as dist
 
@@ -517,7 +542,10 @@ def main():
     if budgets is not None:
         for r in rts:
             r.set_pass_budgets(tuple(int(b) for b in budgets.split(",") if b.strip()))
-    for _ in range(len(rts)):
+    K = args.batch if (mg is None and world == 1 and not args.shadows) else 0
+    if args.batch and not K:
+        raise SystemExit("--batch is a one-GPU primary-ray mode (no --shadows, N = 1)")
+    for _ in range(len(rts) * max(1, K)):  # batch mode: K output sets per context, outs[f * K + j]
         o = {"rgba": torch.zeros(n_out, dtype=torch.int32, device=dev),
              "depth": torch.zeros(n_out, dtype=torch.float32, device=dev)}
         if args.shadows:
@@ -569,6 +597,35 @@ def main():
         if pipe is not None:
             pipe.submit()
 
+    batch_i = [0]
+
+    def submit_batch(nf, timed):
+        """One vhx_trace_primary_batch of the next nf frames on context batch_i % F."""
+        f = batch_i[0] % len(rts)
+        batch_i[0] += 1
+        r, s_ = rts[f], streams[f]
+        cams_b = [cams[(frame[0] + j) % len(cams)] for j in range(nf)]
+        frame[0] += nf
+        for j in range(nf):
+            last_cam[f * K + j] = cams_b[j]
+        if timed and not NOEV:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s_)
+        r.trace_primary_batch(cams_b, outs[f * K:f * K + nf])
+        if timed and not NOEV:
+            e1.record(s_)
+            ev.append((e0, e1, nf))
+
+    def run(n, timed):
+        """n frames: one step each, or batches of K."""
+        if K:
+            while n > 0:
+                submit_batch(min(K, n), timed)
+                n -= min(K, n)
+        else:
+            for _ in range(n):
+                step(timed)
+
     def drain():
         if pipe is not None:
             pipe.drain()
@@ -576,10 +633,11 @@ def main():
             mg.sync()
         torch.cuda.synchronize(dev)
 
-    # setup (not a step): one untimed frame per context allocates its queues and state buffers, so that no
-    # allocation (hipMalloc synchronises the device) falls into the timed region when F exceeds the warm-up count
+    # setup (not a step): one untimed frame (batch mode: one batch of K frames) per context allocates its queues and
+    # state buffers, so that no allocation (hipMalloc synchronises the device) falls into the timed region when F
+    # exceeds the warm-up count
     for _ in range(len(rts) if mg is None else 1):
-        step(False)
+        run(max(1, K), False)
     drain()
     split = None
     if mg is not None:
@@ -594,15 +652,14 @@ def main():
         step(False)  # the buffers of the chosen split are allocated outside the timed region
         drain()
     frame[0] = 0
-    for _ in range(args.warmup):
-        step(False)
+    batch_i[0] = 0
+    run(args.warmup, False)
     drain()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(True)
+    run(args.steps, True)
     submit_s = time.perf_counter() - t0  # host time to submit the K steps (the GPU runs behind it)
     drain()  # the last frame's gather and untile are inside the timed region
     if world > 1:
@@ -626,8 +683,8 @@ def main():
 
     # per-launch duration: with frames in flight (HIP events on each launch's stream, over the timed region); the
     # isolated launch (one frame at a time, libvhx's own events) after it
-    if ev:
-        kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    if ev:  # per frame: a batch's device time over its frames
+        kernel_ms = float(np.mean([e[0].elapsed_time(e[1]) / (e[2] if len(e) > 2 else 1) for e in ev]))
     iso, iso_wall = [], []
     for _ in range(5):
         tw0 = time.perf_counter()
@@ -635,13 +692,17 @@ def main():
             mg.render(cam, fb_rgba, fb_depth)
             iso.append(mg.sync())
         else:
-            rt.trace_primary(cam, out=out, **trace_kw)
-            if args.shadows:
+            if args.shadows:  # the primary frame and its shadow rays, between events on the context's stream
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                rt.trace_primary(cam, out=out, **trace_kw)
                 rt.trace_shadows(light, out, shadowed=out["shadowed"])
+                e1.record(stream)
                 rt.sync()
-                iso = None
-                break
-            iso.append(rt.sync())
+                iso.append(e0.elapsed_time(e1))
+            else:
+                rt.trace_primary(cam, out=out, **trace_kw)
+                iso.append(rt.sync())
         iso_wall.append(time.perf_counter() - tw0)
     kernel_ms_isolated = float(np.median(iso)) if iso else None
     sched_iso = None if mg is not None else rt.pass_budgets()
@@ -662,7 +723,20 @@ def main():
             seen = {}
             torch.cuda.synchronize(dev)
             to0 = None
-            for k in range(wo + ko):
+            if K:  # batches of K distinct cameras, the warm-up frames first
+                cams_o, kk, bi = ocams, 0, 0
+                while kk < wo + ko:
+                    nf = min(K, (wo if kk < wo else wo + ko) - kk)
+                    if kk == wo:
+                        torch.cuda.synchronize(dev)
+                        to0 = time.perf_counter()
+                    f = bi % len(rts)
+                    bi += 1
+                    rts[f].trace_primary_batch(cams_o[kk:kk + nf], outs[f * K:f * K + nf])
+                    for j in range(nf):
+                        seen[f * K + j] = cams_o[kk + j]
+                    kk += nf
+            for k in range(0 if K else wo + ko):
                 if k == wo:
                     torch.cuda.synchronize(dev)
                     to0 = time.perf_counter()
@@ -749,13 +823,28 @@ def main():
 
     # ---- roofline: algorithmic bytes of this rank's launch (instrumented kernel, untimed) -------------------------
     roof = None
-    if not args.no_roofline and not args.shadows:
+    shadow_bytes = None
+    if not args.no_roofline:
         views = [cam] if len(cams) == 1 else [cams[args.warmup], cams[args.warmup + args.steps // 2], cams[-1]]
         tree_bytes = float(np.mean([rt.trace_primary(v, fields=(), count_bytes=True, **trace_kw)["bytes"]
                                     .astype(np.float64).sum() for v in views]))
         my_rays = W * H if world == 1 else M.rank_rays(W, H, T, rank, world)
         out_bytes = 8.0 * my_rays  # rgba8 + f32 depth per ray
         launch_bytes = tree_bytes + out_bytes
+        if args.shadows:
+            # config 5: the primary pass also writes the hit records the shadow rays start from (value, impact, normal:
+            # 28 B per ray); each shadow ray reads its record (28 B), walks the tree (its counted bytes), writes its flag
+            # (4 B) and darkens the pixel (rgba read + write, 8 B); the hit compaction reads every value (4 B per ray)
+            sv = []
+            for v in views:
+                o = {"rgba": out["rgba"], "depth": out["depth"], "value": out["value"], "impact": out["impact"],
+                     "normal": out["normal"]}
+                rt.trace_primary(v, out=o, **trace_kw)
+                sv.append(rt.trace_shadows(light, o, shadowed=out["shadowed"], count_bytes=True)["bytes"]
+                          .to(torch.float64).sum().item())
+            n_sh = int((out["value"] != -1).sum().item())
+            shadow_bytes = float(np.mean(sv))
+            launch_bytes += shadow_bytes + 28.0 * my_rays + 4.0 * my_rays + (28.0 + 4.0 + 8.0) * n_sh
         # chip-level: a launch's bytes per frame period (F frames in flight overlap: each launch's own duration
         # includes the time it shares the GPU with its neighbours)
         period_ms = ms_per_step if world == 1 else (kernel_ms_isolated or kernel_ms)
@@ -764,11 +853,13 @@ def main():
         measured = None
         if world == 1 and rank == 0 and not args.no_pmc and mg is None:
             # the timed frames run the frames-in-flight schedule whenever F > 1 and the schedule is adaptive
-            measured = measure_traffic(busy_only=F > 1 and budgets is None, tune=args.tune)
+            measured = measure_traffic(busy_only=F > 1 and budgets is None and not K, tune=args.tune,
+                                       blocks_per_frame=((W + 15) // 16) * ((H + 15) // 16))
         roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5),
                 "basis": ("algorithmic bytes of one frame's launch / the frame period (wall time per frame with "
-                          f"{F} frames in flight)") if world == 1 else
+                          + (f"batches of {K} frames on {F} contexts in flight)" if K else f"{F} frames in flight)"))
+                         if world == 1 else
                          "algorithmic bytes of rank 0's launch / its isolated launch duration",
                 "achieved_per_launch": round(launch_bytes / (kernel_ms * 1e-3) / 1e9, 2),
                 "achieved_isolated_launch": None if not kernel_ms_isolated else
@@ -788,6 +879,10 @@ def main():
                 "kernel_ms_isolated": None if kernel_ms_isolated is None else round(kernel_ms_isolated, 4),
                 "frames_in_flight": F,
                 "algorithmic_bytes_per_launch": launch_bytes, "tree_bytes_per_ray": round(tree_bytes / max(1, my_rays), 2)}
+        if args.shadows:
+            roof["shadow_tree_bytes_per_shadow_ray"] = round(shadow_bytes / max(1, n_sh), 2)
+            roof["kernel"] = ("primary frame (vhx_trace_primary) + its hard-shadow rays (vhx_trace_shadows: hit "
+                              "compaction, then the shadow queue passes), timed together on the trace stream")
         iss = None
         if measured and measured["valu"] > 0:
             iss = {"valu_wave_instructions_per_frame": measured["valu"], "useful_lane_frac": round(measured["useful"], 4),
@@ -814,16 +909,18 @@ def main():
 
     # ---- CPU baseline: the oracle (reference semantics) on the host cores, rank 0 at N=1 only ----------------------
     cpu = None
-    if world == 1 and rank == 0 and not args.no_cpu_baseline and not args.shadows:
+    if world == 1 and rank == 0 and not args.no_cpu_baseline:
         cores, affinity, quota = cpu_cores()
-        t_all, t_one, (w1, h1) = cpu_baseline(flat, cam, W, H, cores)
-        cpu = {"value": round(W * H / t_all / 1e6, 4), "unit": "Mrays/s", "cores": cores, "kind": "port",
-               "value_1core": round(w1 * h1 / t_one / 1e6, 4),
+        t_all, t_one, (w1, h1), r_all, r_one = cpu_baseline(flat, cam, W, H, cores, light if args.shadows else None)
+        cpu = {"value": round(r_all / t_all / 1e6, 4), "unit": "Mrays/s", "cores": cores, "kind": "port",
+               "value_1core": round(r_one / t_one / 1e6, 4),
                "nproc": os.cpu_count(), "affinity_cpus": affinity, "cgroup_cpu_quota": quota,
                "cpu_model": cpu_model(),
                "sample": f"all {cores} cores: 1 warm-up + median of 5 full {W}x{H} frames ({t_all:.2f} s per frame); "
                          f"1 core: 1 warm-up + median of 5 {w1}x{h1} frames of the same view ({t_one:.2f} s each); "
-                         f"same tree and camera, OpenMP dynamic over pixels"}
+                         f"same tree and camera, OpenMP dynamic over pixels"
+                         + (f"; each frame = primary rays + the oracle's shadow pass over its hits ({r_all} rays in the "
+                            f"full frame)" if args.shadows else "")}
 
     if rank == 0:
         metric = BASELINE["metric"]
@@ -843,7 +940,8 @@ def main():
             "metric": metric, "value": round(mrays, 3), "unit": "Mrays/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": "f32",
-            "frames_in_flight": F, "gpu_max_hw_queues": queues,
+            "frames_in_flight": F * max(1, K), "contexts_in_flight": F, "batch": K or None,
+            "gpu_max_hw_queues": queues,
             "host_submit_ms_per_step": round(submit_s * 1e3 / args.steps, 4),
             "pass_budgets": args.budgets if args.budgets is not None else ("one pass" if args.mip_lod is not None
                                                                            else "library default (adaptive)"),

@@ -232,6 +232,15 @@ int vhx_tree_device_bytes(const vhx_ctx *ctx, uint64_t *bytes);
  * (host outputs). */
 int vhx_trace_primary(vhx_ctx *ctx, const vhx_camera *cam, uint32_t tile_size, uint32_t tile_start,
                       uint32_t tile_stride, uint32_t layout, const vhx_hits *out, int on_device);
+/* A batch of n whole frames (framebuffer layout, device outputs) traced as ONE pass ladder on the context's stream: pass
+ * 0 over every pixel of every frame in one launch, one compaction over the union of their abandoned rays, and queue
+ * passes shared by all frames (the frames-in-flight schedule), so a renderer gets frames-in-flight throughput from one
+ * stream and one hardware queue (no GPU_MAX_HW_QUEUES setting; the per-frame dispatch of VhxRenderNode::run,
+ * src/raytracing/bevy/pipeline/mod.rs:96-155, batched). Frame k is cams[k] (every camera the same width x height)
+ * into outs[k] (device pointers, any subset of fields; byte counting and node MIPs are refused); results equal n
+ * vhx_trace_primary calls bit for bit. The depth-prepass mode does not apply (the batch traces the exact path).
+ * At most 2^31 rays per batch. Stream-ordered like vhx_trace_primary; vhx_sync reports the batch's device time. */
+int vhx_trace_primary_batch(vhx_ctx *ctx, const vhx_camera *cams, uint32_t n, const vhx_hits *outs);
 /* Depth-prepass fast mode (opt-in; NOT the reference's CPU semantics, so outside the parity bar; the WGSL path's
  * prepass, src/raytracing/bevy/viewport_render.wgsl:702-726). When enabled, a vhx_trace_primary of a whole frame in
  * the FRAMEBUFFER layout without byte counting first traces a half-resolution depth frame (texel (X, Y) through the

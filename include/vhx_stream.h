@@ -70,6 +70,10 @@ int vhx_stream_upload(vhx_stream *stream, vhx_stream_stats *stats);
 int vhx_stream_upload_frames(vhx_stream *stream, uint32_t frames, vhx_stream_stats *stats);
 int vhx_stream_resize(vhx_stream *stream);
 int vhx_stream_reload(vhx_stream *stream);
+/* Diagnostics: after a viewport move the view set (upload_queue.rs:60-148 rebuild) is updated incrementally where the
+ * walk root stays the same; this recomputes it in full at the last rebuild's viewport and compares (VHX_OK: equal,
+ * VHX_E_STATE: different), leaving the stream unchanged, and reports how many rebuilds ran in full / incrementally. */
+int vhx_stream_view_set_check(vhx_stream *stream, uint64_t *full_rebuilds, uint64_t *incremental_rebuilds);
 int vhx_stream_view(const vhx_stream *stream, vhx_tree_desc *out);
 /* the view's node MIP descriptors (host mirror, nodes_in_view entries; all VHX_EMPTY unless the tree's MIP maps are
  * enabled, in which case the stream also writes the MIP bricks and hands the descriptors to vhx_set_node_mips) */

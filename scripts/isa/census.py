@@ -3,6 +3,8 @@ count by class (VALU, SALU, VMEM, SMEM, LDS, branch, wait), its successors, and 
 traversal blocks can be matched to the source (trace.hpp) and weighted by block-execution counts.
 
 Usage: census.py FILE.s 'k_trace_queue<false, 4, false>' [--asm LABEL...]   (--asm prints those blocks' code)
+       census.py FILE.s KERNEL --lines [FILE_SUBSTR]   (a -gline-tables-only build: instructions per source line of
+                                                        FILE_SUBSTR, default trace.hpp, with the blocks they fall in)
 """
 import re
 import subprocess
@@ -68,7 +70,50 @@ def blocks_of(body):
     return blocks
 
 
+def lines_census(body, want):
+    files, cur, per = {}, None, {}
+    block = "entry"
+    for l in body:
+        t = l.strip()
+        m = re.match(r"^\.file\s+(\d+)\s+\"([^\"]*)\"\s+\"([^\"]*)\"", t)
+        if m:
+            files[m.group(1)] = m.group(3)
+            continue
+        m = re.match(r"^\.loc\s+(\d+)\s+(\d+)", t)
+        if m:
+            cur = (m.group(1), int(m.group(2)))
+            continue
+        m = re.match(r"^(\.LBB[0-9_]+):", l)
+        if m:
+            block = m.group(1)
+            continue
+        if not t or t.startswith((";", ".", "//")):
+            continue
+        k = klass(t.split()[0])
+        e = per.setdefault(cur, {"valu": 0, "salu": 0, "other": 0, "blocks": set()})
+        e["valu" if k == "valu" else ("salu" if k == "salu" else "other")] += 1
+        e["blocks"].add(block)
+    return files, per
+
+
 def main():
+    if "--lines" in sys.argv:
+        i = sys.argv.index("--lines")
+        want = sys.argv[i + 1] if len(sys.argv) > i + 1 else "trace.hpp"
+        text = open(sys.argv[1]).read().split("\n")
+        name, body = extract(sys.argv[1], sys.argv[2])
+        files, per = lines_census([l for l in text if l.strip().startswith(".file")] + body, want)
+        print(name)
+        rows = sorted(((files.get(f, f), ln, e) for (f, ln), e in ((k, v) for k, v in per.items() if k)),
+                      key=lambda r: (r[0], r[1]))
+        tot = {}
+        for fn, ln, e in rows:
+            tot[fn] = tot.get(fn, 0) + e["valu"]
+            if want in fn:
+                print(f"{fn}:{ln:<5d} valu {e['valu']:4d} salu {e['salu']:3d} other {e['other']:3d}  "
+                      + " ".join(sorted(e["blocks"]))[:90])
+        print("VALU per file:", tot)
+        return
     name, body = extract(sys.argv[1], sys.argv[2])
     show = sys.argv[sys.argv.index("--asm") + 1:] if "--asm" in sys.argv else []
     blocks = blocks_of(body)

@@ -11,7 +11,9 @@ reads (FETCH_SIZE x 1024 B x 2, the gfx950 correction of scripts/pmc_frame.py).
 seen) and come after the first SKIP frames of the run (--skip SKIP: the setup frames that allocate the contexts and the
 warm-up), so that the lone frames of the run (the setup's first frame, the isolated frames after the timed region) do
 not mix into the per-pass figures.
-usage: pmc_passes.py PROFILE_DIR [OUT_TXT] [--inflight-only] [--skip SKIP]"""
+--primary-passes P (config 5, bench.py --shadows): a frame's dispatches after its first P are the shadow trace's passes
+(vhx_trace_shadows on the same stream); they are labelled "shadow pass p - P".
+usage: pmc_passes.py PROFILE_DIR [OUT_TXT] [--inflight-only] [--skip SKIP] [--primary-passes P]"""
 import csv
 import glob
 import os
@@ -23,6 +25,9 @@ inflight_only = "--inflight-only" in sys.argv
 skip = int(sys.argv[sys.argv.index("--skip") + 1]) if "--skip" in sys.argv else 0
 if "--skip" in sys.argv:
     args.remove(str(skip))
+prim = int(sys.argv[sys.argv.index("--primary-passes") + 1]) if "--primary-passes" in sys.argv else None
+if prim is not None:
+    args.remove(str(prim))
 d = args[0]
 sums = defaultdict(lambda: defaultdict(float))  # (run, pass) -> counter -> total
 runs = {}  # run -> (counter names, frames)
@@ -70,7 +75,7 @@ for p in passes:
     wc, waves = per_frame(p, "SQ_WAVE_CYCLES"), per_frame(p, "SQ_WAVES")
     act, wi, wa = per_frame(p, "SQ_ACTIVE_INST_ANY"), per_frame(p, "SQ_WAIT_INST_ANY"), per_frame(p, "SQ_WAIT_ANY")
     fetch = per_frame(p, "FETCH_SIZE")
-    parts = [f"pass {p}:"]
+    parts = [f"pass {p}:" if prim is None or p < prim else f"shadow pass {p - prim}:"]
     if waves is not None:
         parts.append(f"waves {waves:.0f}")
     if valu is not None:

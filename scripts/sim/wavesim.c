@@ -9,6 +9,7 @@
  *   0  current: per iteration top, probe, brick walk loop (max brick steps), pop / push / walk setup, advance loop
  *   1  capped brick walks: at most `cap` brick trips per iteration; a lane whose walk is unfinished carries it into
  *      the next iteration (it skips the node blocks there)
+ *   5  merged walk: pop / push / walk setup first, then one loop over brick and node steps (block 15: switch)
  * Output: per pass and block, waves and lanes (same blocks as the VHX_PROF kernel build), so that design 0 can be
  * checked against the GPU counts of scripts/probes/probe_blocks.py.
  *
@@ -182,6 +183,61 @@ static void sim_wave(const cfg_t *c, int p, lane_t *L, int n, uint32_t budget, u
         if (nfresh) add(s, p, 0, nfresh);
         for (int a = 0; a < na; ++a) npr += fresh[a] && r[a]->probe;
         if (npr) add(s, p, 1, npr);
+        if (c->design == 5) {
+            /* merged walk: pop / push / walk setup before one walk loop in which a lane walks its brick and then (a
+               miss) its node-level walk: trips = max over lanes of brick steps + node steps, plus a transition block
+               (block 15) in every trip where some lane switches from its brick to its node walk */
+            uint32_t npop5 = 0, npush5 = 0, nws5 = 0, nres5 = 0, mt = 0, tr[64], tot[64];
+            for (int a = 0; a < na; ++a) {
+                npop5 += r[a]->pop;
+                npush5 += r[a]->push;
+                if (r[a]->pop || r[a]->na) ++nws5;
+                nres5 += r[a]->restart;
+                const uint32_t w = r[a]->pop ? 1u : r[a]->na;
+                tr[a] = w ? r[a]->nb : 0xFFFFFFFFu;  /* the trip at which the lane switches (none: no node walk) */
+                tot[a] = r[a]->nb + w;
+                if (tot[a] > mt) mt = tot[a];
+            }
+            if (npop5) add(s, p, 3, npop5);
+            if (npush5) add(s, p, 4, npush5);
+            if (nws5) add(s, p, 5, nws5);
+            for (uint32_t t = 0; t < mt; ++t) {
+                uint32_t k = 0, sw = 0;
+                for (int a = 0; a < na; ++a) {
+                    k += tot[a] > t;
+                    sw += tr[a] == t;
+                }
+                if (sw) add(s, p, 15, sw);
+                add(s, p, 2, k);
+            }
+            if (nres5) add(s, p, 7, nres5);
+            uint32_t still5 = 0;
+            for (int a = 0; a < na; ++a) {
+                lane_t *l = &L[act[a]];
+                l->iters += r[a]->nb + r[a]->na;
+                l->cur += 1;
+                const uint32_t nit = (uint32_t)(g_off[l->ray + 1] - g_off[l->ray]);
+                if (l->cur >= nit) {
+                    done[act[a]] = 1;
+                    continue;
+                }
+                l->iters += 1;
+                if (l->iters > budget) {
+                    done[act[a]] = 1;
+                    out[(*nout)++] = *l;
+                    continue;
+                }
+                ++still5;
+            }
+            if (sparse && still5 && still5 < sparse) {
+                for (int i = 0; i < n; ++i)
+                    if (!done[i]) {
+                        done[i] = 1;
+                        out[(*nout)++] = L[i];
+                    }
+            }
+            continue;
+        }
         for (uint32_t t = 0; t < mb; ++t) {
             uint32_t k = 0;
             for (int a = 0; a < na; ++a) k += nb_now[a] > t;

@@ -16,9 +16,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 sys.path.insert(0, ROOT)
 LIB = os.path.join(ROOT, "scripts", "sim", "_build", "libwavesim.so")
 BLOCKS = {13: "loop trip", 0: "iteration top", 1: "probe", 2: "brick trip", 8: "post", 3: "pop", 4: "push",
-          5: "walk setup", 6: "advance trip", 7: "restart", 9: "refill", 14: "refill check"}
+          5: "walk setup", 6: "advance trip", 7: "restart", 9: "refill", 14: "refill check", 15: "walk switch"}
 # VALU instructions per wave execution of each block (ISA of the bd-4 queue kernel, round 3)
-COSTS = {13: 15, 0: 25, 1: 55, 2: 28, 8: 15, 3: 30, 4: 40, 5: 20, 6: 28, 7: 55, 9: 300, 14: 4}
+COSTS = {13: 15, 0: 25, 1: 55, 2: 28, 8: 15, 3: 30, 4: 40, 5: 20, 6: 28, 7: 55, 9: 300, 14: 4, 15: 12}
 RAY_SETUP = 250  # ray generation + begin (divisions, square roots) per pass-0 wave
 
 

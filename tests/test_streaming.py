@@ -242,3 +242,44 @@ def test_batched_uploads_equal_single_uploads(batch):
             assert np.array_equal(va[k], vb[k]), f"batch {batch} step {step}: {k} differs"
     a.close()
     b.close()
+
+
+@pytest.mark.parametrize("size,bd,dist,step", [(256, 4, 64.0, 3.0), (128, 2, 20.0, 5.0), (128, 8, 60.0, 7.0),
+                                               (64, 1, 16.0, 2.5), (256, 4, 40.0, 31.0)])
+def test_incremental_view_set_equals_full_rebuild(size, bd, dist, step):
+    """After every viewport move (small steps along an orbit, and jumps across node boundaries) the view set the
+    incremental rebuild keeps equals the set a full rebuild at that viewport makes (vhx_stream_view_set_check), and
+    most moves are incremental."""
+    t = _tree(size, bd)
+    S = float(size)
+    s = vhx.StreamingView(t, None, (S / 2, S / 2, S / 2), dist)
+    s.set_rates(25, 50, 10)
+    s.upload()
+    rng = np.random.default_rng(size + bd)
+    for k in range(40):
+        a = 2.0 * np.pi * k * step / (4.0 * S)
+        c = (S / 2 + 0.3 * S * np.cos(a), S / 2 + (rng.uniform(-1, 1) if k % 3 == 0 else 0.0), S / 2 + 0.3 * S * np.sin(a))
+        if k % 13 == 12:
+            c = tuple(rng.uniform(-0.1 * S, 1.1 * S, 3))  # a jump (partly outside the tree)
+        s.set_viewport(c, dist)
+        if s.upload()[1]:
+            s.resize()  # the view grew (re_evaluate_view_size): re-create it, as a renderer does
+        same, full, inc = s.view_set_check()
+        assert same, f"move {k} to {c}: incremental view set differs from a full rebuild"
+    assert inc >= 10, (full, inc)
+
+
+def test_incremental_view_set_with_tree_edits():
+    """Tree edits between moves (queued changes force the next rebuild to be full); the set stays equal to a full
+    rebuild's."""
+    t = _tree(256, 4)
+    s = vhx.StreamingView(t, None, (128.0, 128.0, 128.0), 48.0)
+    s.upload()
+    for k in range(12):
+        s.set_viewport((128.0 + 5 * k, 128.0, 120.0 - 4 * k), 48.0)
+        if k % 4 == 1:
+            t.insert((120 + k, 40, 140), vhx.Albedo(10, 20, 30, 255))
+        if s.upload()[1]:
+            s.resize()
+        same, _, _ = s.view_set_check()
+        assert same, f"move {k}"

@@ -108,6 +108,7 @@ SIGNATURES = [
     ("vhx_read_derived", c_int, [c_void_p, c_int, c_u64, c_u64, c_void_p]),
     ("vhx_tree_device_bytes", c_int, [c_void_p, P(c_u64)]),
     ("vhx_trace_primary", c_int, [c_void_p, P(Camera), c_u32, c_u32, c_u32, c_u32, P(Hits), c_int]),
+    ("vhx_trace_primary_batch", c_int, [c_void_p, c_void_p, c_u32, c_void_p]),
     ("vhx_profile_counters", c_int, [c_void_p, P(c_u64), c_u32, c_int]),
     ("vhx_trace_rays", c_int, [c_void_p, c_void_p, c_u64, P(Hits), c_int]),
     ("vhx_trace_shadows", c_int, [c_void_p, P(c_f32), c_u64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
@@ -150,6 +151,7 @@ SIGNATURES = [
     ("vhx_stream_upload_frames", c_int, [c_void_p, c_u32, c_void_p]),
     ("vhx_stream_resize", c_int, [c_void_p]),
     ("vhx_stream_reload", c_int, [c_void_p]),
+    ("vhx_stream_view_set_check", c_int, [c_void_p, P(ctypes.c_uint64), P(ctypes.c_uint64)]),
     ("vhx_stream_view", c_int, [c_void_p, P(TreeDesc)]),
     ("vhx_stream_node_mips", c_int, [c_void_p, P(c_void_p), P(c_u32)]),
     ("vhx_boxtree_node_info", c_int, [c_void_p, c_f32, c_f32, c_f32, P(c_u64), P(c_u32), P(c_u64), P(c_u32)]),

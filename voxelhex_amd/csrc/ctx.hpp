@@ -103,6 +103,9 @@ struct vhx_ctx {
         bool used = false;
     } pinned[2];
     uint32_t pinned_next = 0;
+    // vhx_trace_primary_batch: the batch's cameras and outputs (pinned staging, and their device copy)
+    Pinned batch_pinned;
+    DevBuf batch_args;
     DevBuf upd;
     hipStream_t upd_stream = nullptr;  // the stream of the last scatter (reads upd)
     // depth-prepass mode (vhx_set_depth_prepass; opt-in, not the reference path)

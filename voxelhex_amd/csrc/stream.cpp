@@ -24,6 +24,7 @@
 // (streaming/mod.rs:35-286) at the start of the next upload frames, before the regular upload queue.
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <system_error>
 #include <thread>
 #include <array>
@@ -124,29 +125,57 @@ struct vhx_stream {
             if (!on) return;
             resident_key.resize(std::max<size_t>(key + 1, resident_key.size() * 2), 0u);
         }
+        if ((resident_key[key] != 0u) != on && nodes_to_see.count(key)) {
+            if (on)
+                ++nodes_to_see.n_resident;
+            else
+                --nodes_to_see.n_resident;
+        }
         resident_key[key] = on ? 1u : 0u;
     }
     bool is_resident(size_t key) const { return key < resident_key.size() && resident_key[key] != 0u; }
     std::unordered_map<size_t, std::pair<size_t, uint8_t>> node_index_vs_parent;
     // nodes_to_see (upload_queue.rs: a HashSet of node keys): a set over the pool's dense keys, stamped by generation so
-    // that the per-rebuild clear is O(1); membership and size are what the queue logic reads (no iteration order)
+    // that the per-rebuild clear is O(1); membership and size are what the queue logic reads (no iteration order).
+    // erase (the incremental rebuild) swaps the member with the last one: pos[k] is k's place in `members`
+    // `resident` (the stream's resident_key flags) lets the set count its members that are resident, so that the
+    // stats' "not resident" count needs no pass over the set
     struct KeySet {
         std::vector<uint32_t> stamp;
+        std::vector<uint32_t> pos;
         std::vector<size_t> members;
         uint32_t gen = 1;
+        const std::vector<uint8_t> *resident = nullptr;
+        size_t n_resident = 0;
+        bool res(size_t k) const { return resident && k < resident->size() && (*resident)[k] != 0u; }
         void clear() {
             members.clear();
+            n_resident = 0;
             if (++gen == 0) {  // wrapped: reset every stamp once
                 std::fill(stamp.begin(), stamp.end(), 0u);
                 gen = 1;
             }
         }
         void insert(size_t k) {
-            if (k >= stamp.size()) stamp.resize(std::max<size_t>(k + 1, stamp.size() * 2), 0u);
+            if (k >= stamp.size()) {
+                stamp.resize(std::max<size_t>(k + 1, stamp.size() * 2), 0u);
+                pos.resize(stamp.size(), 0u);
+            }
             if (stamp[k] != gen) {
                 stamp[k] = gen;
+                pos[k] = (uint32_t)members.size();
                 members.push_back(k);
+                n_resident += res(k) ? 1u : 0u;
             }
+        }
+        void erase(size_t k) {
+            if (k >= stamp.size() || stamp[k] != gen) return;
+            stamp[k] = 0u;  // never a generation
+            n_resident -= res(k) ? 1u : 0u;
+            const size_t last = members.back();
+            members[pos[k]] = last;
+            pos[last] = pos[k];
+            members.pop_back();
         }
         size_t count(size_t k) const { return k < stamp.size() && stamp[k] == gen ? 1u : 0u; }
         size_t size() const { return members.size(); }
@@ -174,7 +203,17 @@ struct vhx_stream {
     void apply_pending_rebuild() {
         if (!rebuild_pending) return;
         rebuild_pending = false;
+#ifdef VHX_STREAM_TIMING
+        const auto t0 = std::chrono::steady_clock::now();
+#endif
         rebuild(pending_origin, pending_distance);
+#ifdef VHX_STREAM_TIMING
+        fprintf(stderr, "[stream] rebuild %.3f ms, %zu nodes to see, shell %lu ins %lu era %lu (full %lu inc %lu)\n",
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(), nodes_to_see.size(),
+                (unsigned long)dbg_shell, (unsigned long)dbg_ins, (unsigned long)dbg_era, (unsigned long)rebuilds_full,
+                (unsigned long)rebuilds_incremental);
+        dbg_shell = dbg_ins = dbg_era = 0;
+#endif
         target_node_stack = node_stack_init();
     }
     // statistics of the last upload
@@ -310,8 +349,10 @@ struct vhx_stream {
         meta_by_key.clear();
         key_by_meta.clear();
         std::fill(resident_key.begin(), resident_key.end(), 0u);
+        nodes_to_see.n_resident = 0;
         node_index_vs_parent.clear();
         nodes_to_see.clear();
+        view_walk.valid = false;
         bricks_to_upload.clear();
         reload = true;
         rebuild_pending = false;  // the reload rebuilds at the current viewport
@@ -327,6 +368,14 @@ struct vhx_stream {
         Cube nb;
         uint32_t mip;
     };
+    // the relevant-sectant mask each exploring node of the view had in the walk that last explored it, with the box
+    // corner it was computed for (incremental rebuild): written by the walks (one element per node key, so the threads
+    // of a full walk write disjoint elements); sized to the node pool before a walk
+    struct VMask {
+        uint64_t m;
+        U3 lo;
+    };
+    mutable std::vector<VMask> vmask;
     template <class F>
     void view_children(const ViewItem &it, F3 vc, float dist, uint32_t min_mip, F &&visit) const {
         if (it.mip < min_mip) return;
@@ -334,10 +383,13 @@ struct vhx_stream {
         const F3 c = sub(vc, unit(include / 2.f));
         const U3 cbl{round_u32(c.x), round_u32(c.y), round_u32(c.z)};
         if (node(it.key).content != Content::Internal) return;
+        uint64_t m = 0;
         relevant_sectants(it.nb, cbl, as_u32(include), [&](U3, U3, uint8_t cs, const Cube &tb) {
+            m |= 1ull << cs;
             size_t ck;
             if (valid_child(it.key, cs, ck)) visit(ViewItem{ck, tb, it.mip - 1});
         });
+        if (it.key < vmask.size()) vmask[it.key] = VMask{m, cbl};
     }
     void view_subtree(const ViewItem &it, F3 vc, float dist, uint32_t min_mip, std::vector<size_t> &out) const {
         view_children(it, vc, dist, min_mip, [&](const ViewItem &ch) {
@@ -389,8 +441,165 @@ struct vhx_stream {
         for (const auto &l : lists)
             for (size_t k : l) nodes_to_see.insert(k);
     }
+    // Incremental rebuild: the view set of a rebuild is the root path to the walk root plus every
+    // node reached from the walk root through relevant sectants (view_children: a node at MIP level m >= min_mip takes
+    // its children that overlap the include box B_m, of edge dist * 4^(m - 1) around the clamped viewport centre). When
+    // the walk root, its path, the view distance and the deepest level are those of the last rebuild, the new set is
+    // the last one changed only where the boxes moved: starting at the walk root, a child relevant under both centres
+    // is descended into unless its whole cube lies inside the smallest box any node of its subtree explores with, under
+    // both centres (then every node below it was and stays in the view: every child of a node inside its box is
+    // relevant); a child relevant under only the new centre joins with its new subtree, one relevant under only the
+    // old centre leaves with its old subtree. The result is the set a full rebuild makes (tests/test_streaming.py
+    // compares them after every move); the walk costs the shell of nodes near the moving box faces.
+    struct ViewWalk {
+        bool valid = false;
+        std::vector<size_t> path;  // root .. walk root
+        Cube nb{};
+        uint32_t mip = 0, min_mip = 0;
+        F3 vc{}, center{};  // the clamped and the given centre of the last rebuild
+        float dist = 0.f;
+        int mip1_internal = -1;  // an Internal node at MIP level 1 exists (explores with B_1): -1 unknown
+    } view_walk;
+    uint64_t rebuilds_full = 0, rebuilds_incremental = 0;
+    uint64_t dbg_shell = 0, dbg_ins = 0, dbg_era = 0;
+    // whether any Internal node sits at MIP level 1 (children of the size of a brick); then subtrees explore down to
+    // B_1, otherwise down to B_2
+    bool mip1_internal() {
+        if (view_walk.mip1_internal >= 0) return view_walk.mip1_internal != 0;
+        bool found = false;
+        std::vector<std::pair<size_t, uint32_t>> st{{0, max_mip_level()}};
+        while (!st.empty() && !found) {
+            const auto [k, m] = st.back();
+            st.pop_back();
+            if (!key_valid(k) || node(k).content != Content::Internal || m == 0) continue;
+            if (m == 1) {
+                found = true;
+                break;
+            }
+            for (uint8_t c = 0; c < kChildren; ++c) {
+                size_t ck;
+                if (valid_child(k, c, ck)) st.push_back({ck, m - 1});
+            }
+        }
+        view_walk.mip1_internal = found ? 1 : 0;
+        return found;
+    }
+    static bool cube_in_box(const Cube &c, U3 lo, uint32_t size) {
+        const float s = (float)size;
+        return (float)lo.x <= c.min.x && (float)lo.y <= c.min.y && (float)lo.z <= c.min.z && c.min.x + c.size <= (float)lo.x + s &&
+               c.min.y + c.size <= (float)lo.y + s && c.min.z + c.size <= (float)lo.z + s;
+    }
+    // relevant_sectants of a node depends on the box corner `lo` (edge I) only through, per axis, the node cell holding the
+    // lower face (or "below the node" / "past it") and the number of node cells the upper face lo + I reaches into (see
+    // relevant_sectants, boxtree.hpp: the samples start at max(lo, node min) and step by a cell; a cell is taken while
+    // its lower edge lies below lo + I): boxes with equal keys give the same mask
+    static uint32_t mask_key(const Cube &nb, U3 lo, uint32_t I) {
+        const float cell = nb.size / 4.f, nx[3] = {nb.min.x, nb.min.y, nb.min.z};
+        const uint32_t l[3] = {lo.x, lo.y, lo.z};
+        uint32_t key = 0;
+        for (int a = 0; a < 3; ++a) {
+            const float lf = (float)l[a], end = lf + (float)I;
+            int klo = lf > nx[a] + nb.size ? 5 : (lf < nx[a] ? -1 : std::min(4, (int)std::floor((lf - nx[a]) / cell)));
+            int kend = (int)std::ceil((end - nx[a]) / cell);
+            kend = kend < 0 ? 0 : (kend > 4 ? 4 : kend);
+            key |= ((uint32_t)(klo + 1) | ((uint32_t)kend << 3)) << (6 * a);
+        }
+        return key;
+    }
+    static void include_box(F3 vc, float dist, uint32_t mip, U3 &lo, uint32_t &size) {  // view_children's box
+        const float include = dist * std::pow(4.f, (float)mip - 1.f);
+        const F3 c = sub(vc, unit(include / 2.f));
+        lo = U3{round_u32(c.x), round_u32(c.y), round_u32(c.z)};
+        size = as_u32(include);
+    }
+    uint64_t relevant_mask(const Cube &nb, U3 lo, uint32_t size) const {
+        uint64_t m = 0;
+        relevant_sectants(nb, lo, size, [&](U3, U3, uint8_t cs, const Cube &) { m |= 1ull << cs; });
+        return m;
+    }
+    // the node's mask under box corner lo: its cached one when the keys agree, else computed
+    uint64_t mask_at(const ViewItem &it, U3 lo, uint32_t size, uint32_t key) {
+        const VMask &c = vmask[it.key];
+        if (mask_key(it.nb, c.lo, size) == key) return c.m;
+        return relevant_mask(it.nb, lo, size);
+    }
+    void view_subtree_apply(const ViewItem &it, F3 vc, float dist, uint32_t min_mip, bool insert) {
+        std::vector<size_t> keys;
+        view_subtree(it, vc, dist, min_mip, keys);
+        for (size_t k : keys) insert ? nodes_to_see.insert(k) : nodes_to_see.erase(k);
+    }
+    static Cube child_cube(const Cube &nb, uint8_t cs) {  // relevant_sectants' tb (integer cubes: floor / ceil exact)
+        Cube tb = child_bounds_for(nb, cs);
+        return Cube{F3{std::floor(tb.min.x), std::floor(tb.min.y), std::floor(tb.min.z)}, std::ceil(tb.size)};
+    }
+    // the children of a node whose cubes lie inside the box [lo, lo + I] (all axes): per axis the node cells inside the
+    // box's interval, combined into a sectant mask (bit x + 4y + 16z)
+    static uint64_t inside_mask(const Cube &nb, U3 lo, uint32_t I) {
+        const float cell = nb.size / 4.f, mn[3] = {nb.min.x, nb.min.y, nb.min.z};
+        const uint32_t l[3] = {lo.x, lo.y, lo.z};
+        uint32_t ax[3];
+        for (int a = 0; a < 3; ++a) {
+            ax[a] = 0;
+            const float lf = (float)l[a], hf = lf + (float)I;
+            for (uint32_t c = 0; c < 4; ++c)
+                if (lf <= mn[a] + (float)c * cell && mn[a] + (float)(c + 1) * cell <= hf) ax[a] |= 1u << c;
+        }
+        uint64_t row = 0, m = 0;
+        for (uint32_t y = 0; y < 4; ++y)
+            if ((ax[1] >> y) & 1u) row |= (uint64_t)ax[0] << (4u * y);
+        for (uint32_t z = 0; z < 4; ++z)
+            if ((ax[2] >> z) & 1u) m |= row << (16u * z);
+        return m;
+    }
+    // include boxes of the two centres per MIP level (shell walk)
+    struct LevelBoxes {
+        U3 lo0[32], lo1[32];
+        uint32_t size[32];
+    };
+    void shell_walk(const ViewItem &it, const LevelBoxes &bx, F3 vc1, float dist, uint32_t min_mip, uint32_t jmin) {
+        if (it.mip < min_mip || it.mip >= 32 || node(it.key).content != Content::Internal) return;  // explores in neither
+        const U3 b0 = bx.lo0[it.mip], b1 = bx.lo1[it.mip];
+        const uint32_t sz = bx.size[it.mip];
+        const uint32_t k0 = mask_key(it.nb, b0, sz), k1 = mask_key(it.nb, b1, sz);
+        const uint64_t m0 = mask_at(it, b0, sz, k0), m1 = k1 == k0 ? m0 : relevant_mask(it.nb, b1, sz);
+        vmask[it.key] = VMask{m1, b1};
+        // children relevant under both centres need a look only if their subtrees explore (level >= jmin) and their
+        // cubes are not inside the smallest exploring box under both centres (then nothing below them changes)
+        uint64_t look = m0 ^ m1;
+        if (it.mip - 1 >= jmin)
+            look |= (m0 & m1) & ~(inside_mask(it.nb, bx.lo0[jmin], bx.size[jmin]) &
+                                  inside_mask(it.nb, bx.lo1[jmin], bx.size[jmin]));
+        for (; look; look &= look - 1) {
+            const uint8_t cs = (uint8_t)__builtin_ctzll(look);
+            size_t ck;
+            if (!valid_child(it.key, cs, ck)) continue;
+            const ViewItem ch{ck, child_cube(it.nb, cs), it.mip - 1};
+            const bool in0 = (m0 >> cs) & 1u, in1 = (m1 >> cs) & 1u;
+            if (in1 && !in0) {
+                nodes_to_see.insert(ck);
+                view_subtree_apply(ch, vc1, dist, min_mip, true);  // records the masks of its explored nodes
+            } else if (in0 && !in1) {
+                std::vector<size_t> keys;
+                view_subtree_cached(ch, min_mip, keys);  // the subtree as the view holds it
+                for (size_t k : keys) nodes_to_see.erase(k);
+                nodes_to_see.erase(ck);
+            } else {
+                shell_walk(ch, bx, vc1, dist, min_mip, jmin);
+            }
+        }
+    }
+    // the explored subtree below `it` as the last walks left it (cached masks: the old centre's, or equal to them)
+    void view_subtree_cached(const ViewItem &it, uint32_t min_mip, std::vector<size_t> &out) const {
+        if (it.mip < min_mip || node(it.key).content != Content::Internal) return;
+        for (uint64_t m = vmask[it.key].m; m; m &= m - 1) {
+            const uint8_t cs = (uint8_t)__builtin_ctzll(m);
+            size_t ck;
+            if (!valid_child(it.key, cs, ck)) continue;
+            out.push_back(ck);
+            view_subtree_cached(ViewItem{ck, child_cube(it.nb, cs), it.mip - 1}, min_mip, out);
+        }
+    }
     void rebuild(F3 center_, float dist) {  // upload_queue.rs:60-142
-        nodes_to_see.clear();
         walk_started = false;
         last_cycle_work = UINT64_MAX;
         const float S = (float)tree->boxtree_size;
@@ -411,7 +620,7 @@ struct vhx_stream {
         // Deviation: the whole access path root -> center joins the view set. The reference marks only the center
         // node and its parent's relevant children, which leaves the root's slot 0 evictable and makes a center two
         // or more levels down unreachable for next_valid_node (it only descends into nodes of the view set).
-        nodes_to_see.insert(0);
+        std::vector<size_t> path{0};
         for (;;) {
             const Content c = node(key).content;
             if (c != Content::Internal || (nb.size / 4.f) <= dist || !contains(nb, bl) || !contains(nb, tr)) break;
@@ -423,15 +632,63 @@ struct vhx_stream {
             parent_bounds = nb;
             parent_mip = mip;
             key = ck;
-            nodes_to_see.insert(ck);
+            path.push_back(ck);
             nb = child_bounds_for(nb, cs);
             mip -= 1;
         }
-        nodes_to_see.insert(key);
-        if (have_parent)
-            add_children_nodes_to_upload_queue(parent_key, parent_bounds, parent_mip, vc, dist, deepest);
-        else
-            add_children_nodes_to_upload_queue(key, nb, mip, vc, dist, deepest);
+        path.push_back(key);
+        const ViewItem wr = have_parent ? ViewItem{parent_key, parent_bounds, parent_mip} : ViewItem{key, nb, mip};
+        ViewWalk &vw = view_walk;
+        if (vmask.size() < tree->nodes.len()) {
+            vmask.resize(tree->nodes.len(), VMask{0, U3{0, 0, 0}});
+            vw.valid = false;  // nodes the cache does not know yet
+        }
+        if (vw.valid && vw.path == path && vw.dist == dist && vw.min_mip == deepest && vw.mip == wr.mip &&
+            vw.nb.min.x == wr.nb.min.x && vw.nb.min.y == wr.nb.min.y && vw.nb.min.z == wr.nb.min.z &&
+            vw.nb.size == wr.nb.size) {
+            // the same walk root: change the set where the include boxes moved
+            const uint32_t jmin = std::max(deepest, mip1_internal() ? 1u : 2u);
+            LevelBoxes bx;
+            for (uint32_t m = 1; m <= std::min(wr.mip, 31u); ++m) {
+                include_box(vw.vc, dist, m, bx.lo0[m], bx.size[m]);
+                include_box(vc, dist, m, bx.lo1[m], bx.size[m]);
+            }
+            shell_walk(wr, bx, vc, dist, deepest, jmin);
+            ++rebuilds_incremental;
+        } else {
+            nodes_to_see.clear();
+            for (size_t k : path) nodes_to_see.insert(k);
+            add_children_nodes_to_upload_queue(wr.key, wr.nb, wr.mip, vc, dist, deepest);
+            ++rebuilds_full;
+        }
+        vw.valid = true;
+        vw.path = std::move(path);
+        vw.nb = wr.nb;
+        vw.mip = wr.mip;
+        vw.min_mip = deepest;
+        vw.vc = vc;
+        vw.center = center_;
+        vw.dist = dist;
+    }
+    // diagnostics (vhx_stream_view_set_check): the view set a full rebuild at the last rebuild's viewport makes, against
+    // the one held (after incremental rebuilds); the stream's state is left as it was
+    bool view_set_matches_full() {
+        if (!view_walk.valid) return true;
+        KeySet held = nodes_to_see;
+        const ViewWalk vw = view_walk;
+        const bool ws = walk_started;
+        const uint64_t lcw = last_cycle_work, nf = rebuilds_full;
+        view_walk.valid = false;
+        rebuild(vw.center, vw.dist);
+        std::vector<size_t> a(held.begin(), held.end()), b(nodes_to_see.begin(), nodes_to_see.end());
+        std::sort(a.begin(), a.end());
+        std::sort(b.begin(), b.end());
+        nodes_to_see = std::move(held);
+        view_walk = vw;
+        walk_started = ws;
+        last_cycle_work = lcw;
+        rebuilds_full = nf;
+        return a == b;
     }
     std::vector<StackItem> node_stack_init() const {  // streaming/mod.rs:553-559
         return {StackItem{0, (uint8_t)kChildren, Cube{f3(0.f, 0.f, 0.f), (float)tree->boxtree_size}}};
@@ -812,6 +1069,10 @@ struct vhx_stream {
             const size_t parent_key = ch.node_stack.back().first;
             Cube node_bounds{f3(0.f, 0.f, 0.f), (float)tree->boxtree_size};
             for (const auto &e : ch.node_stack) nodes_to_see.insert(e.first);
+            // the set now holds more than a walk's: the next rebuild is a full one; the tree changed: so may the
+            // levels of its Internal nodes
+            view_walk.valid = false;
+            view_walk.mip1_internal = -1;
             for (const auto &e : ch.node_stack) {
                 size_t ck;
                 if (valid_child(e.first, e.second, ck)) {  // BoxTree::valid_child_for
@@ -995,12 +1256,19 @@ struct vhx_stream {
         // streaming::upload (streaming/mod.rs:446-457): a reloading view runs the upload queue; otherwise queued tree
         // changes go first, and the upload queue runs in a frame without any
         bool fits;
+#ifdef VHX_STREAM_TIMING
+        const auto t0 = std::chrono::steady_clock::now();
+#endif
         if (reload) {
             fits = process(updates);
         } else {
             fits = handle_tree_updates(updates, node_uploads_per_frame);
             if (fits && updates.empty()) fits = process(updates);
         }
+#ifdef VHX_STREAM_TIMING
+        fprintf(stderr, "[stream] process %.3f ms\n",
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+#endif
         int rc = VHX_OK;
         // palettes: deltas of the host tree's palettes (capacity kPaletteCapacity entries on the device)
         if (tree->color_palette.size() > kPaletteCapacity || tree->data_palette.size() > kPaletteCapacity)
@@ -1082,6 +1350,7 @@ int vhx_stream_create(const vhx_boxtree *tree, vhx_ctx *ctx, const float origin[
     s->tree = tree->tree;
     s->tree->track_changes += 1;  // the tree queues its changes for the stream (BoxTreeGPUHost::new's trigger)
     s->ctx = ctx;
+    s->nodes_to_see.resident = &s->resident_key;
     s->origin = f3(origin[0], origin[1], origin[2]);
     s->view_distance = view_distance;
     s->upload_range = Cube{sub(s->origin, unit(view_distance / 2.f)), view_distance};
@@ -1138,12 +1407,20 @@ int vhx_stream_upload_frames(vhx_stream *s, uint32_t frames, vhx_stream_stats *s
         stats->nodes_in_view = s->nodes_in_view;
         stats->bricks_in_view = s->bricks_in_view;
         stats->nodes_to_see = s->nodes_to_see.size();
-        uint64_t missing = 0;
-        for (size_t k : s->nodes_to_see) missing += s->is_resident(k) ? 0u : 1u;
+        const uint64_t missing = s->nodes_to_see.size() - s->nodes_to_see.n_resident;
         stats->pending = missing + s->bricks_to_upload.size() + s->tree->changes.size() +
                          (s->last_cycle_work == 0 ? 0u : 1u);
     }
     return rc;
+}
+
+int vhx_stream_view_set_check(vhx_stream *s, uint64_t *full_rebuilds, uint64_t *incremental_rebuilds) {
+    if (!s) return VHX_E_INVALID_ARG;
+    if (full_rebuilds) *full_rebuilds = s->rebuilds_full;
+    if (incremental_rebuilds) *incremental_rebuilds = s->rebuilds_incremental;
+    size_t res = 0;  // the set's resident count, kept incrementally, against a count over the set
+    for (size_t k : s->nodes_to_see) res += s->is_resident(k) ? 1u : 0u;
+    return s->view_set_matches_full() && res == s->nodes_to_see.n_resident ? VHX_OK : VHX_E_STATE;
 }
 
 int vhx_stream_resize(vhx_stream *s) {

@@ -357,6 +357,9 @@ __device__ __forceinline__ uint32_t flag_bits(const void *src, uint64_t i, uint6
 // a result.
 struct FlagOrder {
     uint32_t W, H, tx, ty, tsl, mdim, zin;
+    // a batch of frames (vhx_trace_primary_batch): positions [f * fpos, (f + 1) * fpos) are frame f's, in the order
+    // above, and its pixels are output indices [f * fpix, (f + 1) * fpix); fpos = 0: one frame
+    uint64_t fpos, fpix;
 };
 __device__ __forceinline__ uint32_t compact_bits(uint32_t v) {  // even bits of v -> low half
     v &= 0x55555555u;
@@ -392,14 +395,26 @@ __device__ __forceinline__ bool order_pixel(const FlagOrder &o, uint64_t k, uint
     py = (gy << o.tsl) + iy;
     return gx < o.tx && gy < o.ty && px < o.W && py < o.H;
 }
+// output index of position k; false if it names no pixel
+__device__ __forceinline__ bool order_index(const FlagOrder &o, uint64_t k, uint64_t &i) {
+    uint64_t base = 0;
+    if (o.fpos) {
+        const uint64_t f = k / o.fpos;
+        k -= f * o.fpos;
+        base = f * o.fpix;
+    }
+    uint32_t px, py;
+    if (!order_pixel(o, k, px, py)) return false;
+    i = base + (uint64_t)py * o.W + px;
+    return true;
+}
 // flags of positions k..k+3 (bit j: position k + j): a pass-0 flag byte, or with HITS a hit value != VHX_EMPTY
 template <bool HITS>
 __device__ __forceinline__ uint32_t order_bits(const void *src, const FlagOrder &o, uint64_t k) {
     uint32_t bits = 0;
     for (uint32_t j = 0; j < 4u; ++j) {
-        uint32_t px, py;
-        if (!order_pixel(o, k + j, px, py)) continue;
-        const uint64_t i = (uint64_t)py * o.W + px;
+        uint64_t i;
+        if (!order_index(o, k + j, i)) continue;
         // a pass-0 flag byte: 1 = abandoned
         if (HITS ? ((const uint32_t *)src)[i] != VHX_EMPTY : (((const uint8_t *)src)[i] & 1u) != 0) bits |= 1u << j;
     }
@@ -447,9 +462,9 @@ __global__ void __launch_bounds__(256) k_emit_flags(const void *__restrict__ src
     for (uint32_t w = 0; w < wave; ++w) o += s_wave[w];
     for (uint32_t k = 0; k < 4; ++k)
         if (bits & (1u << k)) {
-            uint32_t px = 0, py = 0;
-            if (ord.W) order_pixel(ord, i + k, px, py);
-            out[o++] = ord.W ? py * ord.W + px : (uint32_t)(i + k);
+            uint64_t ix = i + k;
+            if (ord.W) order_index(ord, i + k, ix);
+            out[o++] = (uint32_t)ix;
         }
 }
 
@@ -515,11 +530,16 @@ __global__ void __launch_bounds__(QSORT_THREADS) k_sort_segments(uint32_t *__res
 
 // Where a queued output index comes from: a primary-ray frame (framebuffer or tile layout) or an explicit ray batch.
 struct RaySrc {
-    uint32_t kind;  // 0 framebuffer, 1 tiles, 2 explicit rays, 3 shadow rays from hit records
+    uint32_t kind;  // 0 framebuffer, 1 tiles, 2 explicit rays, 3 shadow rays from hit records, 4 a batch of frames
     uint32_t T, tiles_x, tile_start, tile_stride;
     const float *rays;
     const float *impact, *normal;  // kind 3
     float lx, ly, lz;               // kind 3: light position
+    // kind 4 (vhx_trace_primary_batch): frame f = idx / npix of the batch has camera cams[f] and outputs outs[f]
+    // (framebuffer layout, index idx - f * npix); device arrays of the batch
+    const CamD *cams;
+    const OutD *outs;
+    uint32_t npix;
 };
 
 // Hard-shadow ray of hit record idx (BASELINE config 5; semantics in DESIGN.md §9): from impact + normal * 1e-3
@@ -538,6 +558,13 @@ __device__ __forceinline__ void ray_of(const CamD &cam, const RaySrc &src, uint3
     if (src.kind == 2u) {
         o = mk(src.rays[6ull * idx], src.rays[6ull * idx + 1], src.rays[6ull * idx + 2]);
         d = mk(src.rays[6ull * idx + 3], src.rays[6ull * idx + 4], src.rays[6ull * idx + 5]);
+        return;
+    }
+    if (src.kind == 4u) {  // a batch: the frame's camera, read where the ray is set up
+        const uint32_t f = idx / src.npix, local = idx - f * src.npix;
+        const CamD *cf = src.cams + f;
+        const uint32_t W = cf->width, py = local / W;
+        primary_ray(*cf, local - py * W, py, o, d);
         return;
     }
     uint32_t px, py;
@@ -629,6 +656,34 @@ __global__ void __launch_bounds__(256) k_trace_primary(DevTree t, CamD cam, OutD
     // frame (a lane past the frame edge has no entry of its own: its idx aliases the next row or runs past the end)
     if (q.flags && (layout == VHX_LAYOUT_FRAMEBUFFER ? valid : (lx < T && ly < T)))
         q.flags[idx] = done ? 0 : 1;
+}
+
+// Pass 0 of a batch of frames (vhx_trace_primary_batch): frame f's 16x16 pixel blocks are blocks [f * nblocks_frame,
+// (f + 1) * nblocks_frame) of one launch (XCD-dealt like k_trace_primary), with the frame's camera and outputs read from
+// the batch arrays (block-uniform: scalar loads). Framebuffer layout; output index f * npix + y * width + x.
+template <int BD>
+__global__ void __launch_bounds__(256) k_trace_primary_batch(DevTree t, const CamD *__restrict__ cams,
+                                                             const OutD *__restrict__ outs, uint32_t nblocks_frame,
+                                                             uint32_t blocks_x, uint32_t npix, PassQ q) {
+    __shared__ uint64_t occ_tab[OCC_TAB_WORDS];
+    fill_occ_tab(occ_tab);
+    __syncthreads();
+    const uint32_t bid = xcd_block(blockIdx.x, gridDim.x, q.xcd_group);
+    const uint32_t f = bid / nblocks_frame, sb = bid - f * nblocks_frame;
+    const CamD cam = cams[f];
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    const uint32_t px = (sb % blocks_x) * 16u + (wave & 1u) * 8u + (lane & 7u);
+    const uint32_t py = (sb / blocks_x) * 16u + (wave >> 1) * 8u + (lane >> 3);
+    if (px >= cam.width || py >= cam.height) return;
+    const uint32_t local = py * cam.width + px;
+    const uint64_t idx = (uint64_t)f * npix + local;
+    F3d o, d;
+    primary_ray(cam, px, py, o, d);
+    HitOut h;
+    h.bytes = 0;
+    const bool done = get_by_ray<false, BD>(t, occ_tab, o, d, h, q.budget, q.state, (uint32_t)idx, false, 0.0f, q.sparse);
+    if (done) store(t, outs[f], local, o, h);
+    if (q.flags) q.flags[idx] = done ? 0 : 1;
 }
 
 template <bool COUNT, int BD, bool MIP = false>
@@ -739,6 +794,9 @@ __global__ void __launch_bounds__(256) VHX_QUEUE_ATTR k_trace_queue(DevTree t, c
                 if (COUNT && q.state) b->out.bytes[idx] = h.bytes;
             } else if (b->src.kind == 3u) {
                 store_shadow(b->out, idx, h);
+            } else if (b->src.kind == 4u) {
+                const uint32_t f = idx / b->src.npix;
+                store(t, b->src.outs[f], idx - f * b->src.npix, o, h);
             } else {
                 store(t, b->out, idx, o, h);
             }
@@ -1073,14 +1131,16 @@ static int finish_out(vhx_ctx *c, HostOut &ho) {
 // Adaptive scheduling (ctx.hpp, Sched): the busy schedule while another context of the tree has a frame in flight on
 // another stream (its last trace's use event not yet reached), else the idle one. A host-side query per other context;
 // no waits.
-static void select_schedule(vhx_ctx *c) {
+static void select_schedule(vhx_ctx *c, bool batch = false) {
     if (!c->adaptive) {
         c->last_sched = -1;
         c->qsort = c->qsort_force >= 0 ? (uint32_t)c->qsort_force : c->sched_busy.qsort;  // a fixed schedule: the busy one's
         return;
     }
-    bool busy = false;
-    {
+    // a batch of frames is a throughput job by itself: the frames-in-flight schedule (its passes re-pack the surviving
+    // rays of every frame of the batch; the last pass's tail is shared by them all)
+    bool busy = batch;
+    if (!busy) {
         std::lock_guard<std::mutex> lock(c->tree->mu);
         for (vhx_ctx *u : c->tree->users)
             if (u != c && u->use_recorded && u->use_stream != c->stream && hipEventQuery(u->use_ev) == hipErrorNotReady) {
@@ -1098,8 +1158,9 @@ static void select_schedule(vhx_ctx *c) {
     c->last_sched = busy ? 1 : 0;
 }
 
-static int prepare_passes(vhx_ctx *c, uint64_t nout, uint64_t nblocks0, uint32_t &npass, bool shadow = false) {
-    select_schedule(c);
+static int prepare_passes(vhx_ctx *c, uint64_t nout, uint64_t nblocks0, uint32_t &npass, bool shadow = false,
+                          bool batch = false) {
+    select_schedule(c, batch);
     npass = nout < 0x7FFFFFFFull ? c->npass : 1u;
     if (npass < 2 && !shadow) return VHX_OK;
     uint64_t chunks = std::max(nblocks0, (nout + 1023) / 1024), list = nblocks0 * 256;
@@ -1196,18 +1257,23 @@ static int sort_segments(vhx_ctx *c, uint32_t p, uint32_t npass, uint32_t *queue
 
 // The FlagOrder of code `qorder` for a W x H framebuffer frame (W = 0 or qorder = 0: output-index order) and the
 // number of positions its compaction scans (npos: in / out)
-static FlagOrder flag_order(uint32_t qorder, uint32_t W, uint32_t H, uint64_t &npos) {
+static FlagOrder flag_order(uint32_t qorder, uint32_t W, uint32_t H, uint64_t &npos, uint32_t frames = 1) {
     FlagOrder ord{};
     if (!qorder || !W || !H) return ord;
     const uint32_t tsl = qorder & 15u, ts = 1u << tsl;
-    ord = FlagOrder{W, H, (W + ts - 1u) / ts, (H + ts - 1u) / ts, tsl, 0u, (qorder & 64u) ? 2u : (qorder & 32u) ? 1u : 0u};
+    ord = FlagOrder{W, H, (W + ts - 1u) / ts, (H + ts - 1u) / ts, tsl, 0u, (qorder & 64u) ? 2u : (qorder & 32u) ? 1u : 0u,
+                    0u, 0u};
     if (qorder & 16u)  // Morton order over the smallest 2^m x 2^m grid of tiles covering the frame
         while ((1u << ord.mdim) < std::max(ord.tx, ord.ty)) ++ord.mdim;
     const uint64_t np = (ord.mdim ? 1ull << (2u * ord.mdim) : (uint64_t)ord.tx * ord.ty) << (2u * tsl);
     // the chunk counts are sized for ceil(pixels / 256) chunks, the compaction needs ceil(npos / 1024): a tile far
     // larger than the frame keeps output-index order
     if (np > 4ull * W * H) return FlagOrder{};
-    npos = np;
+    npos = np * frames;
+    if (frames > 1) {
+        ord.fpos = np;
+        ord.fpix = (uint64_t)W * H;
+    }
     return ord;
 }
 
@@ -1238,14 +1304,15 @@ static int put_qargs(vhx_ctx *c, const CamD &cam, const RaySrc &src, const OutD 
 template <bool COUNT, int BD, bool MIP = false>
 static int launch_queue_passes(vhx_ctx *c, const DevTree &t, const CamD &cam, const RaySrc &src, const OutD &o,
                                uint32_t first, uint32_t npass, uint64_t nout, uint64_t nblocks0,
-                               bool flags_pass0 = false, uint32_t order_w = 0, uint32_t order_h = 0) {
+                               bool flags_pass0 = false, uint32_t order_w = 0, uint32_t order_h = 0,
+                               uint32_t frames = 1) {
     uint32_t *ctl = (uint32_t *)c->qctl.ptr;
     int rc = VHX_OK;
     if (first > 0 && npass > 1) {
         if (flags_pass0) {  // primary frames: per-ray flags compacted in output-index (frame) order
             // tile order (c->qorder, framebuffer layout only): positions over the frame's tiles
             uint64_t npos = nout;
-            const FlagOrder ord = flag_order(c->qorder, order_w, order_h, npos);
+            const FlagOrder ord = flag_order(c->qorder, order_w, order_h, npos, frames);
             const unsigned nb = (unsigned)((npos + 1023) / 1024);
             uint32_t *counts = (uint32_t *)c->counts.ptr, *offsets = (uint32_t *)c->offsets.ptr;
             const uint8_t *flags = (const uint8_t *)c->flags.ptr;
@@ -1266,8 +1333,12 @@ static int launch_queue_passes(vhx_ctx *c, const DevTree &t, const CamD &cam, co
         const uint32_t *in_n = p > 0 ? ctl + (p - 1) : ctl + 7;
         const PassQ q = pass_q(c, p, npass);
         // a first pass over fresh rays (the shadow path) is throughput-bound like a grid launch: more waves
-        const uint32_t qwaves = p == 0 ? c->queue_waves0
-                                : (p + 1 < npass && c->queue_waves_mid ? c->queue_waves_mid : c->queue_waves);
+        uint32_t qwaves = p == 0 ? c->queue_waves0
+                          : (p + 1 < npass && c->queue_waves_mid ? c->queue_waves_mid : c->queue_waves);
+        // a batch of frames: the waves the same frames would bring as frames in flight (one frame's queue waves each),
+        // up to the queue kernel's residency (5 waves per SIMD): its queue passes are memory-latency bound and need
+        // the waves in flight
+        if (frames > 1 && p > 0) qwaves = (uint32_t)std::min<uint64_t>((uint64_t)qwaves * frames, 20ull * c->cus);
         const unsigned qgrid = (qwaves * 64u + c->qblock - 1) / c->qblock;
         k_trace_queue<COUNT, BD, MIP><<<qgrid, c->qblock, 0, c->stream>>>(t, qa, in, in_n,
                                                                          ctl + 16u + QCTL_PASS_WORDS * p, q);
@@ -1368,11 +1439,11 @@ void vhx_destroy(vhx_ctx *c) {
     c->tree.reset();  // frees the device tree with its last context
     if (c->use_ev) (void)hipEventDestroy(c->use_ev);
     for (DevBuf *b : {&c->scratch, &c->rays, &c->queue[0], &c->queue[1], &c->qctl, &c->tmp, &c->counts, &c->offsets,
-                      &c->flags, &c->qargs, &c->state, &c->upd, &c->prepass_depth})
+                      &c->flags, &c->qargs, &c->state, &c->upd, &c->prepass_depth, &c->batch_args})
         if (b->ptr) (void)hipFree(b->ptr);
-    for (auto &P : c->pinned) {
-        if (P.ptr) (void)hipHostFree(P.ptr);
-        if (P.done) (void)hipEventDestroy(P.done);
+    for (auto *P : {&c->pinned[0], &c->pinned[1], &c->batch_pinned}) {
+        if (P->ptr) (void)hipHostFree(P->ptr);
+        if (P->done) (void)hipEventDestroy(P->done);
     }
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -2048,6 +2119,86 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
     c->timed = true;
     if ((rc = tscope.end())) return rc;  // a later write of the tree waits for this frame
     return finish_out(c, ho);
+}
+
+int vhx_trace_primary_batch(vhx_ctx *c, const vhx_camera *cams, uint32_t n, const vhx_hits *outs) {
+    if (!c || !cams || !outs || n == 0) return VHX_E_INVALID_ARG;
+    if (!c->tree->uploaded) return fail(c, VHX_E_STATE, "vhx_trace_primary_batch before vhx_upload_tree");
+    const uint32_t W = cams[0].width, H = cams[0].height;
+    for (uint32_t k = 0; k < n; ++k) {
+        if (cams[k].width != W || cams[k].height != H || W == 0 || H == 0 || cams[k].ray_model > VHX_RAY_GLASS)
+            return fail(c, VHX_E_INVALID_ARG, "vhx_trace_primary_batch: every frame needs one valid camera model and the "
+                                              "same non-empty width x height");
+        if (outs[k].bytes)
+            return fail(c, VHX_E_INVALID_ARG, "vhx_trace_primary_batch: byte counting is a vhx_trace_primary option");
+    }
+    const uint64_t npix = (uint64_t)W * H, nout = npix * n;
+    const uint32_t bx = (W + 15) / 16, by = (H + 15) / 16;
+    const uint64_t nbf = (uint64_t)bx * by, nblocks = nbf * n;
+    if (nout > 0x7FFFFFFFull || nblocks > 0x7FFFFFFFull)
+        return fail(c, VHX_E_INVALID_ARG, "vhx_trace_primary_batch: more than 2^31 rays in one batch");
+    VHX_HIP(c, hipSetDevice(c->device));
+    VHX_STREAM(c);
+    TraceScope tscope(c);
+    int rc = tscope.rc;
+    if (rc) return rc;
+    if ((rc = refresh_child_rec(c))) return rc;
+    const DevTree t = dev_tree(c);
+    if (t.mips) return fail(c, VHX_E_INVALID_ARG, "vhx_trace_primary_batch: not available with node MIPs");
+    // the batch's cameras and outputs: packed in pinned memory, one copy to the device ahead of the launches on the
+    // context's stream (the previous batch's copy out of the same slot has long completed: it was the first operation of
+    // that batch)
+    const uint64_t cam_bytes = ((uint64_t)n * sizeof(CamD) + 255) & ~255ull, args_bytes = cam_bytes + (uint64_t)n * sizeof(OutD);
+    vhx_ctx::Pinned &P = c->batch_pinned;
+    if (P.used) VHX_HIP(c, hipEventSynchronize(P.done));
+    if (P.bytes < args_bytes) {
+        if (P.ptr) VHX_HIP(c, hipHostFree(P.ptr));
+        P.ptr = nullptr;
+        P.bytes = 0;
+        VHX_HIP(c, hipHostMalloc(&P.ptr, args_bytes, hipHostMallocDefault));
+        P.bytes = args_bytes;
+    }
+    if (!P.done) VHX_HIP(c, hipEventCreateWithFlags(&P.done, hipEventDisableTiming));
+    // the device copy is read by this context's earlier batches: a stream change waits for them
+    if (c->use_recorded && c->use_stream != c->stream) VHX_HIP(c, hipStreamWaitEvent(c->stream, c->use_ev, 0));
+    if ((rc = ensure(c, c->batch_args, args_bytes))) return rc;
+    CamD *hc = (CamD *)P.ptr;
+    OutD *ho = (OutD *)((uint8_t *)P.ptr + cam_bytes);
+    for (uint32_t k = 0; k < n; ++k) {
+        hc[k] = cam_of(&cams[k]);
+        ho[k] = OutD{outs[k].value, outs[k].cell,   outs[k].voxel, outs[k].rgba,
+                     nullptr,       outs[k].impact, outs[k].normal, outs[k].depth};
+    }
+    uint32_t npass = 1;
+    if ((rc = prepare_passes(c, nout, nblocks, npass, false, n > 1))) return rc;
+    VHX_HIP(c, hipEventRecord(c->ev0, c->stream));
+    VHX_HIP(c, hipMemcpyAsync(c->batch_args.ptr, P.ptr, args_bytes, hipMemcpyHostToDevice, c->stream));
+    VHX_HIP(c, hipEventRecord(P.done, c->stream));
+    P.used = true;
+    const CamD *dcams = (const CamD *)c->batch_args.ptr;
+    const OutD *douts = (const OutD *)((const uint8_t *)c->batch_args.ptr + cam_bytes);
+    RaySrc src{};
+    src.kind = 4u;
+    src.cams = dcams;
+    src.outs = douts;
+    src.npix = (uint32_t)npix;
+    const CamD cd{};
+    int qrc = VHX_OK;
+    auto launch = [&](auto bd_tag) {
+        constexpr int BD = decltype(bd_tag)::value;
+        PassQ q0 = pass_q(c, 0, npass);
+        if (npass > 1) q0.flags = (uint8_t *)c->flags.ptr;
+        k_trace_primary_batch<BD><<<(unsigned)nblocks, 256, 0, c->stream>>>(t, dcams, douts, (uint32_t)nbf, bx,
+                                                                            (uint32_t)npix, q0);
+        qrc = launch_queue_passes<false, BD>(c, t, cd, src, OutD{}, 1, npass, nout, nblocks, true, W, H, n);
+    };
+    if (!dispatch_bd(c->tree->desc.brick_dim, launch)) return fail(c, VHX_E_INVALID_ARG, "unsupported brick_dim");
+    if (qrc) return qrc;
+    VHX_HIP(c, hipGetLastError());
+    c->last_fb_w = c->last_fb_h = 0;  // no single frame's order for a later shadow trace
+    VHX_HIP(c, hipEventRecord(c->ev1, c->stream));
+    c->timed = true;
+    return tscope.end();
 }
 
 int vhx_profile_counters(vhx_ctx *c, uint64_t *out, uint32_t n, int reset) {

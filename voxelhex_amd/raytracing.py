@@ -347,6 +347,25 @@ class Raytracer:
                                               ctypes.byref(hs), 0))
         return res
 
+    def trace_primary_batch(self, cams, outs):
+        """vhx_trace_primary_batch: whole frames cams[k] -> outs[k] (dicts of device tensors, framebuffer layout) as one
+        pass ladder on this context's stream; results equal one trace_primary per frame."""
+        if len(cams) != len(outs) or not cams:
+            raise ValueError("trace_primary_batch: one output dict per camera")
+        n = cams[0].width * cams[0].height
+        for out in outs:
+            if _on_device(out) != 1:
+                raise ValueError("trace_primary_batch writes device tensors")
+            for name, dt, k in HIT_FIELDS:
+                a = out.get(name)
+                if a is not None and a.numel() * a.element_size() < n * k * 4:
+                    raise ValueError(f"out[{name!r}] holds {a.numel() * a.element_size()} bytes, a frame needs {n * k * 4}")
+        cs = (N.Camera * len(cams))(*cams)
+        hs = (N.Hits * len(outs))(*[_hits_struct(o) for o in outs])
+        self._check(N.lib().vhx_trace_primary_batch(self._h, ctypes.cast(cs, ctypes.c_void_p), len(cams),
+                                                    ctypes.cast(hs, ctypes.c_void_p)))
+        return outs
+
     def trace_shadows(self, light, hits, shadowed=None, darken=True, count_bytes=False):
         """Hard shadow rays (vhx_trace_shadows) for the device-resident hit records `hits` of a previous trace
         (dict of torch tensors with value, impact, normal and optionally rgba). Returns a dict with the int32

@@ -80,6 +80,14 @@ class StreamingView:
     def reload(self):
         N.check(N.lib().vhx_stream_reload(self._h))
 
+    def view_set_check(self):
+        """vhx_stream_view_set_check: (equal to a full rebuild, full rebuilds, incremental rebuilds)."""
+        f, i = ctypes.c_uint64(), ctypes.c_uint64()
+        rc = N.lib().vhx_stream_view_set_check(self._h, ctypes.byref(f), ctypes.byref(i))
+        if rc not in (N.VHX_OK, N.VHX_E_STATE):
+            N.check(rc)
+        return rc == N.VHX_OK, f.value, i.value
+
     def upload_all(self, max_frames=100000):
         """Uploads frame by frame (resizing when the view is too small) until nothing is pending."""
         frames = resizes = 0
