@@ -38,12 +38,6 @@ def oracle():
 
 @pytest.fixture(scope="session")
 def gpu():
-    # torch's HIP runtime first, then libvhx's: the order of every full-suite run. (A run of only the loopback rank
-    # tests followed by this fixture has seen no HIP device in this process once those subprocesses had used the GPU
-    # first; in the full suite the process initialises the GPU long before them.)
-    import torch
-    if torch.cuda.is_available():
-        torch.cuda.init()
     from voxelhex_amd import Raytracer
     rt = Raytracer(0)
     yield rt
