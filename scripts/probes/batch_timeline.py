@@ -2,12 +2,19 @@
 k_trace_primary_batch dispatch and the dispatches on its queue up to the next one), every kernel with its start offset
 and duration, and the idle time between consecutive dispatches (the GPU runs nothing of the batch then: with one
 context in flight, nothing at all). Prints one batch in full and the mean per kernel over the batches after --skip.
-usage: batch_timeline.py ks_kernel_trace.csv [--skip N] [--show I]"""
+usage: batch_timeline.py ks_kernel_trace.csv|ks_results.db [--skip N] [--show I]   (.db: rocprofv3's default rocpd
+output, its `kernels` view)"""
 import csv
 import sys
 from collections import defaultdict
 
-rows = list(csv.DictReader(open(sys.argv[1])))
+if sys.argv[1].endswith(".db"):
+    import sqlite3
+    con = sqlite3.connect(sys.argv[1])
+    rows = [{"Kernel_Name": n, "Start_Timestamp": a, "End_Timestamp": b, "Queue_Id": str(q)}
+            for n, a, b, q in con.execute("select name, start, end, queue_id from kernels")]
+else:
+    rows = list(csv.DictReader(open(sys.argv[1])))
 skip = int(sys.argv[sys.argv.index("--skip") + 1]) if "--skip" in sys.argv else 2
 show = int(sys.argv[sys.argv.index("--show") + 1]) if "--show" in sys.argv else skip
 ks = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"].removeprefix("void ").split("(")[0],

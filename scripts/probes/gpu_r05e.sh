@@ -5,6 +5,8 @@
 cd "$GRAFT_REPO_ROOT" || exit 1
 O=gpurun_out/r05e; mkdir -p $O
 T="python -u -m pytest -x -v --timeout 300 --timeout-method thread"
+timeout -k 10 120 $T tests/test_abi_c.py tests/test_gpu_batch.py -m gpu -k "consumer or golden" > $O/gpu_first.log 2>&1 || { echo "first tests failed"; tail -30 $O/gpu_first.log; exit 1; }
+tail -1 $O/gpu_first.log
 timeout -k 10 600 $T tests -m gpu > $O/gpu_all.log 2>&1 || { echo "gpu suite failed"; tail -30 $O/gpu_all.log; exit 1; }
 tail -1 $O/gpu_all.log
 summ() {

@@ -13,7 +13,7 @@ from collections import defaultdict
 rows = list(csv.DictReader(open(sys.argv[1])))
 skip, steps = int(sys.argv[2]), int(sys.argv[3])
 frame_k = ("k_trace_primary<false", "k_trace_queue<false", "k_count_flags", "k_scan_counts", "k_emit_flags",
-           "k_gather_chunks", "k_put_queue_args")
+           "k_gather_chunks", "k_put_queue_args", "k_scan_sums")
 ks = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"].replace("void ", ""))
             for r in rows)
 p0 = [k for k in ks if k[2].startswith("k_trace_primary<false")]
@@ -45,7 +45,7 @@ span = end - t0
 classes = defaultdict(list)
 for s_, e_, n in sel:
     k = n.split("(")[0]
-    classes["trace (pass 0 + queue passes)" if "trace" in k else "compaction (count/scan/emit/gather/args)"].append((s_, e_))
+    classes["trace (pass 0 + queue passes)" if "trace" in k else "compaction (count/scan/emit/gather/args/sums)"].append((s_, e_))
     classes[k].append((s_, e_))
 classes["any frame kernel"] = [(s_, e_) for s_, e_, _ in sel]
 print("busy time (union of dispatch intervals) per frame:")

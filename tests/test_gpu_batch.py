@@ -71,7 +71,8 @@ def test_batch_vs_oracle(gpu, oracle):
 
 @pytest.mark.parametrize("tune", ["budgets=1,2,3,5,8,13", "budgets=4", "budgets=", "qorder=0", "qorder=8r",
                                   "qorder=m16", "qorder=32z", "rpw=0,16,8,4", "resume=0", "qsort=256",
-                                  "qwaves=64;qxcd=0", "sparse=60,60,60"])
+                                  "qwaves=64;qxcd=0", "sparse=60,60,60", "p0lists=0", "qorder=16z", "qorder=128z",
+                                  "scan_multi=1"])
 def test_batch_schedules_are_bit_identical(gpu, tune):
     flat = vhx.FlatTree.build_scene(N.VHX_SCENE_LATTICE_CUBE, 256, 4)
     rt = vhx.Raytracer(0, tune=tune)

@@ -89,6 +89,7 @@ struct vhx_ctx {
     DevBuf tmp;       // chunk-local lists of abandoned rays (a block's or a queue chunk's, in lane order)
     DevBuf counts;    // rays listed per chunk
     DevBuf offsets;   // exclusive scan of counts
+    DevBuf scan_part; // scans of more than scan_multi segments: the segments' sums, then their exclusive scan
     DevBuf flags;     // primary pass 0: abandoned flag per output index
     DevBuf qargs;     // QueueArgs of the queue passes: slot 0 primary rays / ray batches, slot 1 shadow rays
     std::vector<uint8_t> qargs_host[2];  // the QueueArgs last written to each slot (skips the upload when unchanged)
@@ -147,6 +148,8 @@ struct vhx_ctx {
     uint32_t npass = 5;
     uint32_t rpw[VHX_MAX_BUDGETS + 1] = {64u, 64u, 64u, 64u, 64u, 64u, 64u};  // rays per wave of each pass (tune "rpw=64,16" style override; 0 = adaptive)
     uint32_t tw = 1024;            // adaptive rays per wave: target waves per queue pass (tune "tw")
+    uint32_t scan_multi = 8;       // chunk scans of more segments (SCAN_SEG counts) run on one workgroup per segment
+    bool p0lists = true;           // pass 0 lists its abandoned rays in the queue order (ListOrder; tune "p0lists")
     bool resume = true;            // abandoned rays continue from saved state (tune "resume=0": re-traced from scratch)
     // passes before save_from keep no state: the rays they abandon are traced again from scratch by pass save_from,
     // which saves (tune "save_from"; 0 = every budgeted pass saves)

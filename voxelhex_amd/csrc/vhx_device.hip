@@ -236,6 +236,7 @@ struct PassQ {
     uint32_t xcd_group;  // pass 0: XCD-aware block runs (xcd_block), 0 = dispatch order
     uint32_t qxcd;       // queue passes: runs of this many chunks dealt over the 8 XCDs, one counter each (0 = off)
     uint32_t sparse;     // budgeted passes with saved state: abandon a wave's rays once fewer lanes trace (0 = off)
+    uint32_t *zero;      // pass 0 with block lists: the queue passes' work counters, zeroed by workgroup 0
 };
 
 // Rays per wave of a queue pass over n rays: fixed, or (rpw == 0) as many as spread the pass over about `tw` waves.
@@ -248,8 +249,9 @@ __device__ __forceinline__ uint32_t pass_rpw(uint32_t rpw, uint32_t tw, uint32_t
 }
 
 // Block-level ordered append (all 256 threads of the workgroup call it): the workgroup's rays with push set are
-// listed at tmp[blockIdx * 256 ...] in thread order, their number at counts[blockIdx].
-__device__ __forceinline__ void block_append(bool push, uint32_t idx, uint32_t *tmp, uint32_t *counts) {
+// listed at tmp[pos * 256 ...] in thread order, their number at counts[pos] (pos: the workgroup's chunk position).
+__device__ __forceinline__ void block_append(bool push, uint32_t idx, uint32_t *tmp, uint32_t *counts,
+                                             uint32_t pos) {
     __shared__ uint32_t s_cnt[4];
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
     const uint64_t m = __ballot(push);
@@ -257,8 +259,8 @@ __device__ __forceinline__ void block_append(bool push, uint32_t idx, uint32_t *
     __syncthreads();
     uint32_t before = 0;
     for (uint32_t w = 0; w < wave; ++w) before += s_cnt[w];
-    if (push) tmp[(uint64_t)blockIdx.x * 256u + before + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = idx;
-    if (threadIdx.x == 0) counts[blockIdx.x] = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+    if (push) tmp[(uint64_t)pos * 256u + before + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = idx;
+    if (threadIdx.x == 0) counts[pos] = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
 }
 
 // Exclusive scan of the chunk counts in one workgroup of SCAN_THREADS threads; nchunks = ceil(*n_in / per_chunk) when
@@ -274,20 +276,35 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, uint32_t lane) {
     }
     return v;
 }
+#define SCAN_SEG (SCAN_THREADS * 16u)  // counts per segment
+__device__ __forceinline__ uint32_t scan_nchunks(uint32_t nchunks_host, const uint32_t *n_in, uint32_t per_chunk,
+                                                 uint32_t tw) {
+    if (!n_in) return nchunks_host;
+    const uint32_t pc = pass_rpw(per_chunk, tw, *n_in);
+    return (*n_in + pc - 1) / pc;
+}
+// seg_base == null: one workgroup walks every segment and writes *total. seg_base != null (a large scan, launch_scan):
+// workgroup b scans segment b only, starting from seg_base[b] (the exclusive scan of the segments' sums).
 __global__ void __launch_bounds__(SCAN_THREADS) k_scan_counts(const uint32_t *__restrict__ counts,
                                                               uint32_t nchunks_host, const uint32_t *n_in,
                                                               uint32_t per_chunk, uint32_t tw,
-                                                              uint32_t *__restrict__ offsets, uint32_t *total) {
+                                                              uint32_t *__restrict__ offsets, uint32_t *total,
+                                                              const uint32_t *__restrict__ seg_base = nullptr) {
     constexpr uint32_t NW = SCAN_THREADS / 64u;
     __shared__ uint32_t s_wave[NW];
     __shared__ uint32_t s_carry;
-    const uint32_t pc = n_in ? pass_rpw(per_chunk, tw, *n_in) : per_chunk;
-    const uint32_t nchunks = n_in ? (*n_in + pc - 1) / pc : nchunks_host;
+    const uint32_t nchunks = scan_nchunks(nchunks_host, n_in, per_chunk, tw);
     const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
     constexpr uint32_t K = 16;  // rows of 64 per wave per segment; loads issued together
-    if (t == 0) s_carry = 0;
+    uint32_t seg0 = 0, seg_end = nchunks;
+    if (seg_base) {
+        seg0 = blockIdx.x * SCAN_SEG;
+        if (seg0 >= nchunks) return;  // the whole workgroup
+        seg_end = seg0 + 1u;
+    }
+    if (t == 0) s_carry = seg_base ? seg_base[blockIdx.x] : 0u;
     __syncthreads();
-    for (uint32_t seg = 0; seg < nchunks; seg += SCAN_THREADS * K) {
+    for (uint32_t seg = seg0; seg < seg_end; seg += SCAN_THREADS * K) {
         const uint32_t b = seg + wave * (64u * K) + lane;
         uint32_t v[K];
 #pragma unroll
@@ -315,7 +332,29 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_scan_counts(const uint32_t *__
         }
         __syncthreads();
     }
-    if (t == 0) *total = s_carry;
+    if (t == 0 && !seg_base) *total = s_carry;
+}
+// sums[b] = the sum of segment b's counts (0 past the end)
+__global__ void __launch_bounds__(SCAN_THREADS) k_scan_sums(const uint32_t *__restrict__ counts, uint32_t nchunks_host,
+                                                            const uint32_t *n_in, uint32_t per_chunk, uint32_t tw,
+                                                            uint32_t *__restrict__ sums) {
+    __shared__ uint32_t s_wave[SCAN_THREADS / 64u];
+    const uint32_t nchunks = scan_nchunks(nchunks_host, n_in, per_chunk, tw);
+    const uint32_t t = threadIdx.x, base = blockIdx.x * SCAN_SEG;
+    uint32_t v = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 16u; ++k) {
+        const uint32_t i = base + k * SCAN_THREADS + t;
+        v += base < nchunks && i < nchunks ? counts[i] : 0u;
+    }
+    for (uint32_t d = 32; d > 0; d >>= 1) v += __shfl_down(v, d);
+    if ((t & 63u) == 0) s_wave[t >> 6] = v;
+    __syncthreads();
+    if (t == 0) {
+        uint32_t sum = 0;
+        for (uint32_t w = 0; w < SCAN_THREADS / 64u; ++w) sum += s_wave[w];
+        sums[blockIdx.x] = sum;
+    }
 }
 
 // Flag compaction in output-index order, 1024 entries per workgroup, 4 per thread. The flag of entry i is flags[i]
@@ -617,23 +656,63 @@ __device__ __forceinline__ float prepass_start(const FastD &f, uint32_t px, uint
     return m - f.margin;
 }
 
+// Pass 0's abandoned rays listed per workgroup in the order of the pass-1 queue (ListOrder, lo.tx > 0; the
+// framebuffer layout): workgroup position b is block (bx, by) of a tile of 2^tbl x 2^tbl blocks, the tiles row-major
+// (tx per row), the blocks of a tile and the pixels of a block in Morton order -- the 16x16 block's four 8x8 waves are
+// its Morton quadrants, and lane l is pixel (even bits of l, odd bits of l) of its wave's 8x8 -- so the lists in
+// position order are the frame's abandoned rays in the FlagOrder of 2^(tbl+4)-pixel tiles with Morton inside (zin 1),
+// without a flag per pixel and the compaction kernels over every pixel. A wave holds the same 64 pixels either way.
+struct ListOrder {
+    uint32_t tx, tbl;
+};
+__device__ __forceinline__ void list_block(const ListOrder &lo, uint32_t b, uint32_t &bx, uint32_t &by) {
+    const uint32_t tb = b >> (2u * lo.tbl), m = b & ((1u << (2u * lo.tbl)) - 1u);
+    bx = ((tb % lo.tx) << lo.tbl) + compact_bits(m);
+    by = ((tb / lo.tx) << lo.tbl) + compact_bits(m >> 1);
+}
+// Wave-level ordered append (no barrier: a wave that finishes early leaves at once): the wave's rays with push set are
+// listed at tmp[pos * 64 ...] in lane order, their number at counts[pos].
+__device__ __forceinline__ void wave_append(bool push, uint32_t idx, uint32_t *tmp, uint32_t *counts, uint32_t pos) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t m = __ballot(push);
+    if (push) tmp[(uint64_t)pos * 64u + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = idx;
+    if (lane == 0) counts[pos] = (uint32_t)__popcll(m);
+}
+__device__ __forceinline__ void zero_ctl(uint32_t *zero) {
+    if (zero && blockIdx.x == 0)
+        for (uint32_t w = threadIdx.x; w < QCTL_WORDS - 16u; w += blockDim.x) zero[w] = 0u;
+}
+
 template <bool COUNT, int BD, bool FAST = false, bool MIP = false>
 __global__ void __launch_bounds__(256) k_trace_primary(DevTree t, CamD cam, OutD out, uint32_t T, uint32_t tiles_x,
                                                        uint32_t tile_start, uint32_t tile_stride, uint32_t layout,
                                                        uint32_t blocks_per_tile_x, uint32_t blocks_per_tile,
-                                                       PassQ q, FastD fast = FastD{}) {
+                                                       PassQ q, FastD fast = FastD{}, ListOrder lo = ListOrder{}) {
     __shared__ uint64_t occ_tab[OCC_TAB_WORDS];
     fill_occ_tab(occ_tab);
+    zero_ctl(q.zero);
     __syncthreads();
     const uint32_t bid = xcd_block(blockIdx.x, gridDim.x, q.xcd_group);
-    const uint32_t j = bid / blocks_per_tile;  // j-th tile of this rank
-    const uint32_t sb = bid - j * blocks_per_tile;
-    const uint32_t tile = tile_start + j * tile_stride;
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-    // 8x8 pixels per wave, four waves per 16x16 block
-    const uint32_t lx = (sb % blocks_per_tile_x) * 16u + (wave & 1u) * 8u + (lane & 7u);
-    const uint32_t ly = (sb / blocks_per_tile_x) * 16u + (wave >> 1) * 8u + (lane >> 3);
-    const uint32_t px = (tile % tiles_x) * T + lx, py = (tile / tiles_x) * T + ly;
+    uint32_t lx, ly, px, py;
+    if (lo.tx) {  // framebuffer layout (T = 16: a tile per block), workgroups in list order
+        uint32_t bx, by;
+        list_block(lo, bid, bx, by);
+        lx = (wave & 1u) * 8u + compact_bits(lane);
+        ly = (wave >> 1) * 8u + compact_bits(lane >> 1);
+        px = bx * 16u + lx;
+        py = by * 16u + ly;
+    } else {
+        const uint32_t j = bid / blocks_per_tile;  // j-th tile of this rank
+        const uint32_t sb = bid - j * blocks_per_tile;
+        const uint32_t tile = tile_start + j * tile_stride;
+        // 8x8 pixels per wave, four waves per 16x16 block
+        lx = (sb % blocks_per_tile_x) * 16u + (wave & 1u) * 8u + (lane & 7u);
+        ly = (sb / blocks_per_tile_x) * 16u + (wave >> 1) * 8u + (lane >> 3);
+        px = (tile % tiles_x) * T + lx;
+        py = (tile / tiles_x) * T + ly;
+    }
+    const uint32_t j = lo.tx ? 0u : bid / blocks_per_tile;
     const bool valid = lx < T && ly < T && px < cam.width && py < cam.height;
     const uint64_t idx = layout == VHX_LAYOUT_FRAMEBUFFER ? (uint64_t)py * cam.width + px
                                                           : (uint64_t)j * T * T + (uint64_t)ly * T + lx;
@@ -656,6 +735,7 @@ __global__ void __launch_bounds__(256) k_trace_primary(DevTree t, CamD cam, OutD
     // frame (a lane past the frame edge has no entry of its own: its idx aliases the next row or runs past the end)
     if (q.flags && (layout == VHX_LAYOUT_FRAMEBUFFER ? valid : (lx < T && ly < T)))
         q.flags[idx] = done ? 0 : 1;
+    if (lo.tx && q.tmp) wave_append(!done, (uint32_t)idx, q.tmp, q.counts, bid * 4u + wave);
 }
 
 // Pass 0 of a batch of frames (vhx_trace_primary_batch): frame f's 16x16 pixel blocks are blocks [f * nblocks_frame,
@@ -664,26 +744,40 @@ __global__ void __launch_bounds__(256) k_trace_primary(DevTree t, CamD cam, OutD
 template <int BD>
 __global__ void __launch_bounds__(256) k_trace_primary_batch(DevTree t, const CamD *__restrict__ cams,
                                                              const OutD *__restrict__ outs, uint32_t nblocks_frame,
-                                                             uint32_t blocks_x, uint32_t npix, PassQ q) {
+                                                             uint32_t blocks_x, uint32_t npix, PassQ q,
+                                                             ListOrder lo = ListOrder{}) {
     __shared__ uint64_t occ_tab[OCC_TAB_WORDS];
     fill_occ_tab(occ_tab);
+    zero_ctl(q.zero);
     __syncthreads();
     const uint32_t bid = xcd_block(blockIdx.x, gridDim.x, q.xcd_group);
     const uint32_t f = bid / nblocks_frame, sb = bid - f * nblocks_frame;
     const CamD cam = cams[f];
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-    const uint32_t px = (sb % blocks_x) * 16u + (wave & 1u) * 8u + (lane & 7u);
-    const uint32_t py = (sb / blocks_x) * 16u + (wave >> 1) * 8u + (lane >> 3);
-    if (px >= cam.width || py >= cam.height) return;
+    uint32_t px, py;
+    if (lo.tx) {  // this frame's blocks in list order (k_trace_primary)
+        uint32_t bx, by;
+        list_block(lo, sb, bx, by);
+        px = bx * 16u + (wave & 1u) * 8u + compact_bits(lane);
+        py = by * 16u + (wave >> 1) * 8u + compact_bits(lane >> 1);
+    } else {
+        px = (sb % blocks_x) * 16u + (wave & 1u) * 8u + (lane & 7u);
+        py = (sb / blocks_x) * 16u + (wave >> 1) * 8u + (lane >> 3);
+    }
+    const bool valid = px < cam.width && py < cam.height;
     const uint32_t local = py * cam.width + px;
     const uint64_t idx = (uint64_t)f * npix + local;
-    F3d o, d;
-    primary_ray(cam, px, py, o, d);
-    HitOut h;
-    h.bytes = 0;
-    const bool done = get_by_ray<false, BD>(t, occ_tab, o, d, h, q.budget, q.state, (uint32_t)idx, false, 0.0f, q.sparse);
-    if (done) store(t, outs[f], local, o, h);
-    if (q.flags) q.flags[idx] = done ? 0 : 1;
+    bool done = true;
+    if (valid) {
+        F3d o, d;
+        primary_ray(cam, px, py, o, d);
+        HitOut h;
+        h.bytes = 0;
+        done = get_by_ray<false, BD>(t, occ_tab, o, d, h, q.budget, q.state, (uint32_t)idx, false, 0.0f, q.sparse);
+        if (done) store(t, outs[f], local, o, h);
+        if (q.flags) q.flags[idx] = done ? 0 : 1;
+    }
+    if (lo.tx && q.tmp) wave_append(!done, (uint32_t)idx, q.tmp, q.counts, bid * 4u + wave);
 }
 
 template <bool COUNT, int BD, bool MIP = false>
@@ -705,7 +799,7 @@ __global__ void __launch_bounds__(256) k_trace_rays(DevTree t, const float *__re
         else if (COUNT && q.state)
             out.bytes[i] = h.bytes;
     }
-    if (q.tmp) block_append(!done, (uint32_t)i, q.tmp, q.counts);
+    if (q.tmp) block_append(!done, (uint32_t)i, q.tmp, q.counts, blockIdx.x);
 }
 
 
@@ -1177,6 +1271,7 @@ static int prepare_passes(vhx_ctx *c, uint64_t nout, uint64_t nblocks0, uint32_t
     if (!rc) rc = ensure(c, c->tmp, list * 4);
     if (!rc) rc = ensure(c, c->counts, chunks * 4);
     if (!rc) rc = ensure(c, c->offsets, chunks * 4);
+    if (!rc) rc = ensure(c, c->scan_part, ((chunks + SCAN_SEG - 1) / SCAN_SEG) * 8);
     if (!rc) rc = ensure(c, c->flags, ((nout + 3) & ~3ull));
     if (!rc && c->resume && npass > 1) rc = ensure(c, c->state, nout * 64);
     return rc;
@@ -1193,7 +1288,7 @@ static int reset_passes(vhx_ctx *c, uint32_t npass) {
 // Pass 0 traces fresh rays (the grid kernel of primary and explicit rays, or the shadow path's first queue pass);
 // every later pass resumes the rays its predecessor abandoned.
 static PassQ pass_q(const vhx_ctx *c, uint32_t p, uint32_t npass) {
-    PassQ q;
+    PassQ q{};  // every field a kernel reads is set below or zero (q.zero, q.flags: null unless a caller sets them)
     const bool last = p + 1 >= npass;
     q.budget = last ? VHX_MAX_ITERS : c->budgets[p];
     q.rpw = c->rpw[p];
@@ -1226,13 +1321,36 @@ static void debug_passes(vhx_ctx *c, const char *what) {
             v[7], v[8], v[9], v[10], v[11]);
 }
 
+// Exclusive scan of nchunks counts (nchunks_host, or derived on the device from *n_in) into offsets, their sum at
+// *total. At most max_chunks counts: up to c->scan_multi segments one workgroup walks them (a frame's scans); a larger
+// scan (a batch of frames: one workgroup took ~10 us per segment while the rest of the GPU waited) sums the segments,
+// scans the sums and scans every segment from its base, one workgroup per segment.
+static void launch_scan(vhx_ctx *c, const uint32_t *counts, uint32_t nchunks_host, const uint32_t *n_in,
+                        uint32_t per_chunk, uint32_t *offsets, uint32_t *total, uint64_t max_chunks) {
+    const uint64_t nseg = (max_chunks + SCAN_SEG - 1) / SCAN_SEG;
+    if (nseg <= c->scan_multi || c->scan_multi == 0 || !c->scan_part.ptr || c->scan_part.bytes < nseg * 8) {
+        k_scan_counts<<<1, SCAN_THREADS, 0, c->stream>>>(counts, nchunks_host, n_in, per_chunk, c->tw, offsets, total);
+        return;
+    }
+    uint32_t *sums = (uint32_t *)c->scan_part.ptr, *base = sums + nseg;
+    k_scan_sums<<<(unsigned)nseg, SCAN_THREADS, 0, c->stream>>>(counts, nchunks_host, n_in, per_chunk, c->tw, sums);
+    k_scan_counts<<<1, SCAN_THREADS, 0, c->stream>>>(sums, (uint32_t)nseg, nullptr, 1, c->tw, base, total);
+    k_scan_counts<<<(unsigned)nseg, SCAN_THREADS, 0, c->stream>>>(counts, nchunks_host, n_in, per_chunk, c->tw,
+                                                                   offsets, nullptr, base);
+}
+
 // Chunk lists -> queue `out` with its length at *total: pass-0 style (nchunks_host workgroup chunks of stride 256) or
 // queue-pass style (chunks of per_chunk rays, their number derived from the device-side input length n_in).
 static int compact_chunks(vhx_ctx *c, uint32_t nchunks_host, const uint32_t *n_in, uint32_t per_chunk,
                           uint32_t stride, uint32_t *out, uint32_t *total, uint64_t max_chunks) {
     const uint32_t *counts = (const uint32_t *)c->counts.ptr;
     uint32_t *offsets = (uint32_t *)c->offsets.ptr;
-    k_scan_counts<<<1, SCAN_THREADS, 0, c->stream>>>(counts, nchunks_host, n_in, per_chunk, c->tw, offsets, total);
+    // adaptive rays per chunk (pass_rpw, per_chunk 0; max_chunks is then the ray count): ceil(n / ceil(n / tw)) <= tw
+    // chunks, or ceil(n / 64) once a chunk holds 64 rays
+    const uint64_t scan_max = n_in && per_chunk == 0u
+                                  ? std::min<uint64_t>(max_chunks, std::max<uint64_t>(c->tw, (max_chunks + 63) / 64))
+                                  : max_chunks;
+    launch_scan(c, counts, nchunks_host, n_in, per_chunk, offsets, total, scan_max);
     const uint64_t want = (max_chunks + 3) / 4;
     const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(want, c->queue_blocks));
     k_gather_chunks<<<grid, 256, 0, c->stream>>>((const uint32_t *)c->tmp.ptr, stride, counts, offsets,
@@ -1277,6 +1395,28 @@ static FlagOrder flag_order(uint32_t qorder, uint32_t W, uint32_t H, uint64_t &n
     return ord;
 }
 
+// The ListOrder of code `qorder` for a W x H framebuffer frame, when pass 0 can list its rays in that order itself:
+// tiles row-major (no Morton over the tiles), Morton inside, at least 16 pixels per side (the default, 38); nblocks =
+// the workgroups of pass 0 over whole tiles. Else false (pass 0 writes flags, flag_order compacts them).
+static bool list_order(uint32_t qorder, uint32_t W, uint32_t H, ListOrder &lo, uint64_t &nblocks) {
+    const uint32_t tsl = qorder & 15u;
+    if (!qorder || !W || !H || (qorder & (16u | 64u)) || !(qorder & 32u) || tsl < 4u) return false;
+    const uint32_t ts = 1u << tsl, ty = (H + ts - 1u) / ts;
+    lo = ListOrder{(W + ts - 1u) / ts, tsl - 4u};
+    nblocks = ((uint64_t)lo.tx * ty) << (2u * lo.tbl);
+    // flag_order keeps output-index order for tiles far larger than the frame
+    return nblocks * 256u <= 4ull * W * H;
+}
+
+// Pass 0's workgroups over whole tiles of the list order: the buffers of its per-workgroup lists
+static int ensure_lists(vhx_ctx *c, uint64_t nblocks) {
+    int rc = ensure(c, c->tmp, nblocks * 256 * 4);
+    if (!rc) rc = ensure(c, c->counts, nblocks * 4 * 4);
+    if (!rc) rc = ensure(c, c->offsets, nblocks * 4 * 4);
+    if (!rc) rc = ensure(c, c->scan_part, ((nblocks * 4 + SCAN_SEG - 1) / SCAN_SEG) * 8);
+    return rc;
+}
+
 // The QueueArgs slot of a frame (camera, ray source, outputs) on c's stream. They rarely change between frames: the
 // device copy is rewritten only when they do.
 static int put_qargs(vhx_ctx *c, const CamD &cam, const RaySrc &src, const OutD &o, QueueArgs *&qa) {
@@ -1300,16 +1440,19 @@ static int put_qargs(vhx_ctx *c, const CamD &cam, const RaySrc &src, const OutD 
 
 // Queue passes first..npass-1: pass p re-traces the queue of pass p-1 (pass 0's queue, for first == 0, is the list
 // in queue[1] with its length in qctl[7]); what exceeds its budget is listed per chunk and compacted into the next
-// pass's queue. For first == 1, pass 0 (a grid kernel of nblocks0 workgroups) has just run and is compacted first.
+// pass's queue. For first == 1, pass 0 (a grid kernel of nblocks0 workgroups) has just run and is compacted first:
+// its per-workgroup lists (P0_LISTS, in workgroup order; P0_ORDERED, already in the queue order, ListOrder), or its
+// per-ray flags in the queue order (P0_FLAGS).
+enum { P0_LISTS = 0, P0_FLAGS = 1, P0_ORDERED = 2 };
 template <bool COUNT, int BD, bool MIP = false>
 static int launch_queue_passes(vhx_ctx *c, const DevTree &t, const CamD &cam, const RaySrc &src, const OutD &o,
                                uint32_t first, uint32_t npass, uint64_t nout, uint64_t nblocks0,
-                               bool flags_pass0 = false, uint32_t order_w = 0, uint32_t order_h = 0,
+                               int pass0 = P0_LISTS, uint32_t order_w = 0, uint32_t order_h = 0,
                                uint32_t frames = 1) {
     uint32_t *ctl = (uint32_t *)c->qctl.ptr;
     int rc = VHX_OK;
     if (first > 0 && npass > 1) {
-        if (flags_pass0) {  // primary frames: per-ray flags compacted in output-index (frame) order
+        if (pass0 == P0_FLAGS) {  // primary frames: per-ray flags compacted in output-index (frame) order
             // tile order (c->qorder, framebuffer layout only): positions over the frame's tiles
             uint64_t npos = nout;
             const FlagOrder ord = flag_order(c->qorder, order_w, order_h, npos, frames);
@@ -1317,11 +1460,15 @@ static int launch_queue_passes(vhx_ctx *c, const DevTree &t, const CamD &cam, co
             uint32_t *counts = (uint32_t *)c->counts.ptr, *offsets = (uint32_t *)c->offsets.ptr;
             const uint8_t *flags = (const uint8_t *)c->flags.ptr;
             k_count_flags<false><<<nb, 256, 0, c->stream>>>(flags, npos, counts, ctl + 16, nullptr, ord);
-            k_scan_counts<<<1, SCAN_THREADS, 0, c->stream>>>(counts, nb, nullptr, 1, c->tw, offsets, ctl);
+            launch_scan(c, counts, nb, nullptr, 1, offsets, ctl, nb);
             k_emit_flags<false><<<nb, 256, 0, c->stream>>>(flags, npos, offsets, (uint32_t *)c->queue[0].ptr, ord);
             VHX_HIP(c, hipGetLastError());
             debug_passes(c, "compacted flags");
             if ((rc = sort_segments(c, 1, npass, (uint32_t *)c->queue[0].ptr, ctl, nout))) return rc;
+        } else if (pass0 == P0_ORDERED) {  // per-wave lists (wave_append): 4 chunks of 64 per workgroup
+            rc = compact_chunks(c, (uint32_t)(nblocks0 * 4), nullptr, 64, 64, (uint32_t *)c->queue[0].ptr, ctl,
+                                nblocks0 * 4);
+            if (!rc) rc = sort_segments(c, 1, npass, (uint32_t *)c->queue[0].ptr, ctl, nout);
         } else {
             rc = compact_chunks(c, (uint32_t)nblocks0, nullptr, 256, 256, (uint32_t *)c->queue[0].ptr, ctl, nblocks0);
         }
@@ -1528,6 +1675,12 @@ static int apply_tuning(vhx_ctx *c, const std::string &key, const std::string &v
     } else if (key == "qwavesm") {
         if (!parse_u32(val, x)) return bad();
         c->queue_waves_mid = x;
+    } else if (key == "p0lists") {  // pass 0 of primary frames: 1 = lists in the queue order (ListOrder), 0 = flags
+        if (!parse_u32(val, x) || x > 1) return bad();
+        c->p0lists = x != 0;
+    } else if (key == "scan_multi") {  // 0 = every scan on one workgroup
+        if (!parse_u32(val, x)) return bad();
+        c->scan_multi = x;
     } else if (key == "qwaves0") {
         if (!parse_u32(val, x) || x == 0) return bad();
         c->queue_waves0 = x;
@@ -1769,6 +1922,8 @@ void vhx::copy_sched(vhx_ctx *c, const vhx_ctx *owner) {
     std::memcpy(c->rpw, owner->rpw, sizeof(c->rpw));
     c->npass = owner->npass;
     c->tw = owner->tw;
+    c->scan_multi = owner->scan_multi;
+    c->p0lists = owner->p0lists;
     c->resume = owner->resume;
     c->save_from = owner->save_from;
     c->qorder = owner->qorder;
@@ -2038,6 +2193,17 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
     uint32_t npass = 1;
     rc = prepare_passes(c, nout, nblocks, npass);
     if (rc) return rc;
+    // pass 0's list buffers for either schedule's queue order: a context's first frames often run alone (the idle
+    // schedule), and growing the buffers at its first frame among others would hipFree -- a device-wide
+    // synchronisation that drains every frame in flight (measured: 0.61 against 0.54 ms per bench frame)
+    if (c->p0lists && layout == VHX_LAYOUT_FRAMEBUFFER && T == 16 && tile_start == 0 && tile_stride == 1) {
+        const uint32_t orders[2] = {c->sched_busy.qorder, c->qorder};
+        for (uint32_t o : orders) {
+            ListOrder l2{};
+            uint64_t nb2 = 0;
+            if (list_order(o, cam->width, cam->height, l2, nb2) && (rc = ensure_lists(c, nb2))) return rc;
+        }
+    }
     RaySrc src{};
     src.kind = layout == VHX_LAYOUT_FRAMEBUFFER ? 0u : 1u;
     src.T = T;
@@ -2085,26 +2251,39 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
     // order against 2.071-2.074 with the tiles re-ordered Morton inside, profiles/r03/qorder/mgpu1_*.log)
     const uint32_t ow = layout == VHX_LAYOUT_FRAMEBUFFER ? cam->width : 0u;
     const uint32_t oh = cam->height;
+    // a whole framebuffer frame in the default queue order: pass 0 lists its rays in that order itself (ListOrder)
+    ListOrder lo{};
+    uint64_t nb0 = nblocks;
+    const bool listed = c->p0lists && npass > 1 && layout == VHX_LAYOUT_FRAMEBUFFER && T == 16 && tile_start == 0 &&
+                        tile_stride == 1 && list_order(c->qorder, cam->width, cam->height, lo, nb0);
+    if (!listed) lo = ListOrder{}, nb0 = nblocks;
+    if (listed && (rc = ensure_lists(c, nb0))) return rc;
+    if ((listed ? nb0 * 4 : nb0) > 0x7FFFFFFFull) return fail(c, VHX_E_INVALID_ARG, "frame too large");
+    const int p0 = listed ? P0_ORDERED : P0_FLAGS;
     auto launch = [&](auto bd_tag) {
         constexpr int BD = decltype(bd_tag)::value;
         PassQ q0 = pass_q(c, 0, npass);
-        if (npass > 1) q0.flags = (uint8_t *)c->flags.ptr;
+        if (listed)
+            q0.zero = (uint32_t *)c->qctl.ptr + 16;
+        else if (npass > 1)
+            q0.flags = (uint8_t *)c->flags.ptr;
+        const unsigned g0 = (unsigned)nb0;
         if (t.mips) {  // MIP stand-ins (no byte counting, no depth prepass: refused above)
-            k_trace_primary<false, BD, false, true><<<(unsigned)nblocks, 256, 0, c->stream>>>(
-                t, cd, ho.dev, T, tiles_x, tile_start, tile_stride, layout, bpx, bpt, q0);
-            qrc = launch_queue_passes<false, BD, true>(c, t, cd, src, ho.dev, 1, npass, nout, nblocks, true, ow, oh);
+            k_trace_primary<false, BD, false, true><<<g0, 256, 0, c->stream>>>(
+                t, cd, ho.dev, T, tiles_x, tile_start, tile_stride, layout, bpx, bpt, q0, FastD{}, lo);
+            qrc = launch_queue_passes<false, BD, true>(c, t, cd, src, ho.dev, 1, npass, nout, nb0, p0, ow, oh);
         } else if (count) {
-            k_trace_primary<true, BD><<<(unsigned)nblocks, 256, 0, c->stream>>>(
-                t, cd, ho.dev, T, tiles_x, tile_start, tile_stride, layout, bpx, bpt, q0);
-            qrc = launch_queue_passes<true, BD>(c, t, cd, src, ho.dev, 1, npass, nout, nblocks, true, ow, oh);
+            k_trace_primary<true, BD><<<g0, 256, 0, c->stream>>>(
+                t, cd, ho.dev, T, tiles_x, tile_start, tile_stride, layout, bpx, bpt, q0, FastD{}, lo);
+            qrc = launch_queue_passes<true, BD>(c, t, cd, src, ho.dev, 1, npass, nout, nb0, p0, ow, oh);
         } else {
             if (fast)
-                k_trace_primary<false, BD, true><<<(unsigned)nblocks, 256, 0, c->stream>>>(
-                    t, cd, ho.dev, T, tiles_x, tile_start, tile_stride, layout, bpx, bpt, q0, fd);
+                k_trace_primary<false, BD, true><<<g0, 256, 0, c->stream>>>(
+                    t, cd, ho.dev, T, tiles_x, tile_start, tile_stride, layout, bpx, bpt, q0, fd, lo);
             else
-                k_trace_primary<false, BD><<<(unsigned)nblocks, 256, 0, c->stream>>>(
-                    t, cd, ho.dev, T, tiles_x, tile_start, tile_stride, layout, bpx, bpt, q0);
-            qrc = launch_queue_passes<false, BD>(c, t, cd, src, ho.dev, 1, npass, nout, nblocks, true, ow, oh);
+                k_trace_primary<false, BD><<<g0, 256, 0, c->stream>>>(
+                    t, cd, ho.dev, T, tiles_x, tile_start, tile_stride, layout, bpx, bpt, q0, FastD{}, lo);
+            qrc = launch_queue_passes<false, BD>(c, t, cd, src, ho.dev, 1, npass, nout, nb0, p0, ow, oh);
         }
     };
     const bool bd_ok = dispatch_bd(c->tree->desc.brick_dim, launch);
@@ -2184,13 +2363,23 @@ int vhx_trace_primary_batch(vhx_ctx *c, const vhx_camera *cams, uint32_t n, cons
     src.npix = (uint32_t)npix;
     const CamD cd{};
     int qrc = VHX_OK;
+    // the frames' blocks over whole tiles of the list order (k_trace_primary), or flags in the flag order
+    ListOrder lo{};
+    uint64_t nbf0 = nbf;
+    const bool listed = c->p0lists && npass > 1 && list_order(c->qorder, W, H, lo, nbf0) && nbf0 * n * 4 <= 0x7FFFFFFFull;
+    if (!listed) lo = ListOrder{}, nbf0 = nbf;
+    if (listed && (rc = ensure_lists(c, nbf0 * n))) return rc;
     auto launch = [&](auto bd_tag) {
         constexpr int BD = decltype(bd_tag)::value;
         PassQ q0 = pass_q(c, 0, npass);
-        if (npass > 1) q0.flags = (uint8_t *)c->flags.ptr;
-        k_trace_primary_batch<BD><<<(unsigned)nblocks, 256, 0, c->stream>>>(t, dcams, douts, (uint32_t)nbf, bx,
-                                                                            (uint32_t)npix, q0);
-        qrc = launch_queue_passes<false, BD>(c, t, cd, src, OutD{}, 1, npass, nout, nblocks, true, W, H, n);
+        if (listed)
+            q0.zero = (uint32_t *)c->qctl.ptr + 16;
+        else if (npass > 1)
+            q0.flags = (uint8_t *)c->flags.ptr;
+        k_trace_primary_batch<BD><<<(unsigned)(nbf0 * n), 256, 0, c->stream>>>(t, dcams, douts, (uint32_t)nbf0, bx,
+                                                                               (uint32_t)npix, q0, lo);
+        qrc = launch_queue_passes<false, BD>(c, t, cd, src, OutD{}, 1, npass, nout, nbf0 * n,
+                                             listed ? P0_ORDERED : P0_FLAGS, W, H, n);
     };
     if (!dispatch_bd(c->tree->desc.brick_dim, launch)) return fail(c, VHX_E_INVALID_ARG, "unsupported brick_dim");
     if (qrc) return qrc;
@@ -2391,7 +2580,7 @@ int vhx_trace_shadows(vhx_ctx *c, const float light[3], uint64_t n, const uint32
         uint32_t *counts = (uint32_t *)c->counts.ptr, *offsets = (uint32_t *)c->offsets.ptr;
         k_count_flags<true><<<nb, 256, 0, c->stream>>>(value, npos, counts, (uint32_t *)c->qctl.ptr + 16, shadowed,
                                                        ord, n);
-        k_scan_counts<<<1, SCAN_THREADS, 0, c->stream>>>(counts, nb, nullptr, 1, c->tw, offsets, (uint32_t *)c->qctl.ptr + 7);
+        launch_scan(c, counts, nb, nullptr, 1, offsets, (uint32_t *)c->qctl.ptr + 7, nb);
         k_emit_flags<true><<<nb, 256, 0, c->stream>>>(value, npos, offsets, (uint32_t *)c->queue[1].ptr, ord);
         VHX_HIP(c, hipGetLastError());
     }
