@@ -75,12 +75,13 @@ def parse():
     p.add_argument("--inflight", type=int, default=None,
                    help="contexts in flight per GPU: F contexts sharing the tree (vhx_create_shared), each on its own "
                         "stream, frame (or batch) i traced by context i %% F, so a latency-bound long-ray tail overlaps the "
-                        "next frame's pass 0 (1 = one at a time). Default 20 frames in flight, with GPU_MAX_HW_QUEUES "
-                        "raised to F + 4 so that every frame's stream has a hardware queue of its own; with --batch, "
-                        "default 2 and the hardware queues left at the process default")
-    p.add_argument("--batch", type=int, default=0, metavar="K",
+                        "next frame's pass 0 (1 = one at a time). Default with batches 3 (the hardware queues left at "
+                        "the process default), without 20 frames in flight with GPU_MAX_HW_QUEUES raised to F + 4 so "
+                        "that every frame's stream has a hardware queue of its own")
+    p.add_argument("--batch", type=int, default=None, metavar="K",
                    help="frames per vhx_trace_primary_batch call (one pass ladder over K frames on one stream); 0 = one "
-                        "vhx_trace_primary per frame")
+                        "vhx_trace_primary per frame. Default 7 for one-GPU primary frames (DESIGN.md §16.1: 7 frames "
+                        "x 3 contexts was the fastest split of the driver's 20-frame window), else 0")
     p.add_argument("--orbit", type=float, default=0.0,
                    help="moving camera: frame k (warm-up included) views from angle 40 + k*ORBIT rad on the glass "
                         "camera's circle (0 = the reference bench's static camera); the roofline bytes are then the "
@@ -193,7 +194,8 @@ def parse_pmc_dir(d, blocks_per_frame=None):
             if n.startswith("k_trace_primary<false"):
                 frames.add(row["Dispatch_Id"])
             elif n.startswith("k_trace_primary_batch<") and blocks_per_frame:
-                batch_frames[row["Dispatch_Id"]] = int(row["Grid_Size"]) // (256 * blocks_per_frame)
+                # the list order pads a frame to whole 64x64 tiles (< 1 % more workgroups): nearest whole frame count
+                batch_frames[row["Dispatch_Id"]] = round(int(row["Grid_Size"]) / (256 * blocks_per_frame))
     if not (frames or batch_frames) or "FETCH_SIZE" not in tot:
         return None
     nf = len(frames) + sum(batch_frames.values())
@@ -376,6 +378,11 @@ def hw_queues(frames):
 
 def main():
     args = parse()
+    if args.batch is None:  # batches wherever vhx_trace_primary_batch applies: one GPU, primary rays, the exact path
+        single = int(os.environ.get("WORLD_SIZE", "1")) == 1 and os.environ.get("VHX_BENCH_MGPU1") != "1"
+        args.batch = 7 if (single and not args.shadows and args.depth_prepass is None and args.mip_lod is None) else 0
+        if args.batch and args.inflight is None:
+            args.inflight = 3
     if args.inflight is None:
         args.inflight = 2 if args.batch else 20
     if args.batch:

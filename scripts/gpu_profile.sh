@@ -3,8 +3,7 @@
 # kernel trace + stats of `bench.py --steps 20 --warmup 5`, then FETCH_SIZE (memory-side read bytes) and two passes of
 # SQ counters (issue, lanes) over the same command, each pass a run of its own (rocprofv3 does not split counters over
 # passes; MI355X_MICROARCH.md). The PMC runs skip the frame check and the lone / orbit extras, and pmc_passes.py keeps
-# only frames-in-flight frames after the setup and warm-up frames (SKIP, default 25 = 20 setup frames, one per context
-# of the default F = 20, + 5 warm-up). PPASSES=5 with --shadows labels a frame's dispatches after the first 5 as the shadow
+# only frames-in-flight frames after the setup and warm-up frames (SKIP frames / GSKIP pass-0 groups, defaults below). PPASSES=5 with --shadows labels a frame's dispatches after the first 5 as the shadow
 # trace's passes. usage: [SKIP=n] [PPASSES=p] gpu_profile.sh TAG [bench args...]
 cd "$GRAFT_REPO_ROOT" || exit 1
 TAG=$1; shift
@@ -22,6 +21,12 @@ for P in "$P0" "$P1" "$P2"; do
   echo "pmc pass $j rc=$rc"; [ $rc -ne 0 ] && { tail -5 "$D/pmc$j.log"; exit $rc; }
   j=$((j+1))
 done
-cd "$R" && python3 scripts/pmc_passes.py "$D" "$D/passes.txt" --inflight-only --skip "${SKIP:-25}" ${PPASSES:+--primary-passes $PPASSES} && \
-  python3 scripts/trace_frames.py "$(find "$D" -name "ks_kernel_trace.csv" | head -1)" "${SKIP:-25}" 20 > "$D/trace_frames.txt" 2>&1
+# bench.py's default at N = 1 (round 5): batches of 7 frames on 3 contexts -- 3 setup batches + a warm-up batch of 5,
+# 26 frames in 4 pass-0 groups; frames one at a time (--batch 0, --shadows): 20 setup + 5 warm-up frames
+case " $* " in
+  *" --shadows "*|*" --batch 0 "*) DSKIP=25; DGSKIP=25 ;;
+  *) DSKIP=26; DGSKIP=4 ;;
+esac
+cd "$R" && python3 scripts/pmc_passes.py "$D" "$D/passes.txt" --inflight-only --skip "${GSKIP:-$DGSKIP}" ${PPASSES:+--primary-passes $PPASSES} && \
+  python3 scripts/trace_frames.py "$(find "$D" -name "ks_kernel_trace.csv" | head -1)" "${SKIP:-$DSKIP}" 20 > "$D/trace_frames.txt" 2>&1
 tail -5 "$D/trace_frames.txt"

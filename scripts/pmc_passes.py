@@ -13,7 +13,10 @@ warm-up), so that the lone frames of the run (the setup's first frame, the isola
 not mix into the per-pass figures.
 --primary-passes P (config 5, bench.py --shadows): a frame's dispatches after its first P are the shadow trace's passes
 (vhx_trace_shadows on the same stream); they are labelled "shadow pass p - P".
-usage: pmc_passes.py PROFILE_DIR [OUT_TXT] [--inflight-only] [--skip SKIP] [--primary-passes P]"""
+Batches (bench.py --batch, vhx_trace_primary_batch): a k_trace_primary_batch dispatch opens a group of K frames (K =
+its grid / (256 x --frame-blocks, default 32400 = 3840x2160 in 16x16 blocks), rounded: the list order pads a frame to
+whole tiles); its passes' sums are divided by the frames of the kept groups, and SKIP counts groups.
+usage: pmc_passes.py PROFILE_DIR [OUT_TXT] [--inflight-only] [--skip SKIP] [--primary-passes P] [--frame-blocks B]"""
 import csv
 import glob
 import os
@@ -28,6 +31,9 @@ if "--skip" in sys.argv:
 prim = int(sys.argv[sys.argv.index("--primary-passes") + 1]) if "--primary-passes" in sys.argv else None
 if prim is not None:
     args.remove(str(prim))
+fblocks = int(sys.argv[sys.argv.index("--frame-blocks") + 1]) if "--frame-blocks" in sys.argv else 32400
+if "--frame-blocks" in sys.argv:
+    args.remove(str(fblocks))
 d = args[0]
 sums = defaultdict(lambda: defaultdict(float))  # (run, pass) -> counter -> total
 runs = {}  # run -> (counter names, frames)
@@ -36,24 +42,27 @@ for path in sorted(glob.glob(os.path.join(d, "pmc*_counter_collection.csv"))):
     disp, names = {}, set()
     for r in csv.DictReader(open(path)):  # one row per (dispatch, counter)
         e = disp.setdefault(int(r["Dispatch_Id"]),
-                            {"name": r["Kernel_Name"].replace("void ", ""), "queue": r["Queue_Id"], "c": defaultdict(float)})
+                            {"name": r["Kernel_Name"].replace("void ", ""), "queue": r["Queue_Id"], "c": defaultdict(float),
+                             "grid": int(r["Grid_Size"])})
         e["c"][r["Counter_Name"]] += float(r["Counter_Value"])
         names.add(r["Counter_Name"])
-    frames, open_frame = [], {}  # per frame (in dispatch order of its pass 0): its dispatches by pass; queue -> frame
+    # per frame (or batch: a group of K frames, in dispatch order of its pass 0): its dispatches by pass; queue -> group
+    frames, weight, open_frame = [], [], {}
     for k in sorted(disp):
         e = disp[k]
-        if e["name"].startswith("k_trace_primary<false"):
+        if e["name"].startswith(("k_trace_primary<false", "k_trace_primary_batch<")):
             open_frame[e["queue"]] = len(frames)
             frames.append([e])
+            weight.append(max(1, round(e["grid"] / (256 * fblocks))) if "batch" in e["name"] else 1)
         elif e["name"].startswith("k_trace_queue<false") and e["queue"] in open_frame:
             frames[open_frame[e["queue"]]].append(e)
     most = max((len(f) for f in frames), default=0)
-    keep = [f for i, f in enumerate(frames) if i >= skip and (not inflight_only or len(f) == most)]
-    for f in keep:
-        for p, e in enumerate(f):
+    keep = [i for i, f in enumerate(frames) if i >= skip and (not inflight_only or len(f) == most)]
+    for i in keep:
+        for p, e in enumerate(frames[i]):
             for c, v in e["c"].items():
                 sums[(run, p)][c] += v
-    runs[run] = (names, len(keep))
+    runs[run] = (names, sum(weight[i] for i in keep))
 
 passes = sorted({p for (_, p) in sums})
 
