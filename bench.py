@@ -70,6 +70,9 @@ def parse():
     p.add_argument("--no-roofline", action="store_true")
     p.add_argument("--no-frame-check", action="store_true",
                    help="skip the untimed check of the in-flight frames (frames_equal / golden_match)")
+    p.add_argument("--no-isolated", action="store_true",
+                   help="skip the isolated (one frame at a time) launches after the timed region: the PMC child's "
+                        "counters then cover the timed frames' schedule only")
     p.add_argument("--no-pmc", action="store_true",
                    help="skip the rocprofv3 FETCH_SIZE child run (roofline.traffic from profiles/traffic.json)")
     p.add_argument("--inflight", type=int, default=None,
@@ -226,7 +229,7 @@ def measure_traffic(busy_only=False, tune=None, blocks_per_frame=None):
     cmd = ([rp, "--pmc"] + counters + ["--kernel-trace", "-f", "csv", "-d", d, "-o", "pmc", "--", sys.executable,
                                        os.path.abspath(__file__)] + sys.argv[1:] +
            ["--steps", "5", "--warmup", "1", "--no-cpu-baseline", "--no-roofline", "--no-pmc",
-            "--no-frame-check", "--no-extra"] +
+            "--no-frame-check", "--no-extra", "--no-isolated"] +
            (["--tune", (tune + ";" if tune else "") + "adaptive=0"] if busy_only else []))
     env = dict(os.environ, TMPDIR="/tmp")
     env.pop("VHX_BENCH_MGPU1", None)  # the child times the single-GPU path only
@@ -693,7 +696,7 @@ def main():
     if ev:  # per frame: a batch's device time over its frames
         kernel_ms = float(np.mean([e[0].elapsed_time(e[1]) / (e[2] if len(e) > 2 else 1) for e in ev]))
     iso, iso_wall = [], []
-    for _ in range(5):
+    for _ in range(0 if args.no_isolated else 5):
         tw0 = time.perf_counter()
         if mg is not None:
             mg.render(cam, fb_rgba, fb_depth)
