@@ -310,3 +310,57 @@ def test_writes_and_traces_from_two_threads(oracle):
         sh.close()
     finally:
         owner.close()
+
+
+@pytest.mark.gpu
+def test_write_is_not_starved_by_continuous_traces():
+    """ADVICE r04 (writer priority): two host threads submit frames back to back on two shared contexts, so the tree
+    is almost never free of traces in flight; a third thread's ranged writes must still get in while they run
+    (write_begin raises writers_waiting, and trace_begin waits while it is non-zero), not only after they stop."""
+    import threading
+    import time
+
+    import torch
+    size, W, H = 128, 320, 200
+    base = vhx.FlatTree.build_scene(N.VHX_SCENE_LATTICE_CUBE, size, 4)
+    pal = _pal_edit(base)
+    cam = vhx.glass_camera(size, W, H, target=(size / 2,) * 3)
+    owner = vhx.Raytracer(0)
+    try:
+        owner.upload(base)
+        tracers = [owner.shared(), owner.shared()]
+        dev = torch.device("cuda", 0)
+        outs = [_frame_out(W * H, dev) for _ in tracers]
+        torch.cuda.synchronize()
+        stop, errors, frames, write_done = threading.Event(), [], [0, 0], []
+
+        def trace(i):
+            try:
+                while not stop.is_set() and frames[i] < 200000:
+                    tracers[i].trace_primary(cam, out=outs[i])
+                    frames[i] += 1
+            except Exception as e:  # noqa: BLE001
+                errors.append(e)
+
+        ths = [threading.Thread(target=trace, args=(i,)) for i in range(2)]
+        for th in ths:
+            th.start()
+        tw = time.perf_counter()
+        while min(frames) < 20 and not errors and time.perf_counter() - tw < 60:  # both tracers running
+            time.sleep(0.001)
+        t0 = time.perf_counter()
+        for k in range(6):
+            owner.update_ranges([(N.VHX_BUF_COLOR_PALETTE, 0, pal if k % 2 == 0 else base.color_palette)])
+        write_done.append(time.perf_counter() - t0)
+        running = [th.is_alive() for th in ths]
+        stop.set()
+        for th in ths:
+            th.join(timeout=120)
+        assert not errors, errors
+        assert all(running), "the tracers stopped before the writes completed: the writes were starved"
+        assert write_done[0] < 30.0, write_done
+        torch.cuda.synchronize()
+        for t in tracers:
+            t.close()
+    finally:
+        owner.close()
