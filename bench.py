@@ -83,8 +83,9 @@ def parse():
                         "that every frame's stream has a hardware queue of its own")
     p.add_argument("--batch", type=int, default=None, metavar="K",
                    help="frames per vhx_trace_primary_batch call (one pass ladder over K frames on one stream); 0 = one "
-                        "vhx_trace_primary per frame. Default 7 for one-GPU primary frames (DESIGN.md §16.1: 7 frames "
-                        "x 3 contexts was the fastest split of the driver's 20-frame window), else 0")
+                        "vhx_trace_primary per frame. Default 7 (on 3 contexts) for one-GPU primary frames without --inflight "
+                        "(DESIGN.md §16.1: 7 frames x 3 contexts was the fastest split of the driver's 20-frame window), "
+                        "else 0")
     p.add_argument("--orbit", type=float, default=0.0,
                    help="moving camera: frame k (warm-up included) views from angle 40 + k*ORBIT rad on the glass "
                         "camera's circle (0 = the reference bench's static camera); the roofline bytes are then the "
@@ -381,10 +382,13 @@ def hw_queues(frames):
 
 def main():
     args = parse()
-    if args.batch is None:  # batches wherever vhx_trace_primary_batch applies: one GPU, primary rays, the exact path
+    if args.batch is None:
+        # batches wherever vhx_trace_primary_batch applies: one GPU, primary rays, the exact path, and no explicit
+        # --inflight (which asks for that many per-frame contexts)
         single = int(os.environ.get("WORLD_SIZE", "1")) == 1 and os.environ.get("VHX_BENCH_MGPU1") != "1"
-        args.batch = 7 if (single and not args.shadows and args.depth_prepass is None and args.mip_lod is None) else 0
-        if args.batch and args.inflight is None:
+        args.batch = 7 if (single and args.inflight is None and not args.shadows and args.depth_prepass is None
+                           and args.mip_lod is None) else 0
+        if args.batch:
             args.inflight = 3
     if args.inflight is None:
         args.inflight = 2 if args.batch else 20
