@@ -321,7 +321,7 @@ def test_write_is_not_starved_by_continuous_traces():
     import time
 
     import torch
-    size, W, H = 128, 320, 200
+    size, W, H = 256, 320, 200
     base = vhx.FlatTree.build_scene(N.VHX_SCENE_LATTICE_CUBE, size, 4)
     pal = _pal_edit(base)
     cam = vhx.glass_camera(size, W, H, target=(size / 2,) * 3)

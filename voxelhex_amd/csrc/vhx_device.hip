@@ -215,6 +215,37 @@ __device__ __forceinline__ void primary_ray(const CamD &c, uint32_t px, uint32_t
     }
 }
 
+// A glass-camera ray that misses the root cube by a clear margin (the sky around the tree: two thirds of the bench
+// frame's pass-0 waves hold no ray that enters it) ends as the miss record whatever its exact direction, so the exact
+// setup -- normalising the direction (3 divisions, a square root) and the root slab test (6 divisions; cpu.rs:302-313,
+// spatial/raytracing/mod.rs:33-62) -- is skipped. The test runs on the unnormalised direction v = gp - o with
+// approximate reciprocals: t'_k = (bound - o_k) * rcp(v_k) and the exact t_k = (bound - o_k) / (v_k / |v|) agree up to
+// the common factor |v| within a few roundings (6 ulp, 4e-7 relative), so tmax' < -m or tmin' - tmax' > m with
+// m = 1e-5 * max(|tmin'|, |tmax'|) implies the exact test's miss (tmax < 0 or tmin > tmax). A zero, tiny or non-finite
+// component, or anything closer, takes the exact path.
+__device__ __forceinline__ bool glass_clear_miss(const CamD &c, uint32_t px, uint32_t py, float tsize) {
+    if (c.model != VHX_RAY_GLASS) return false;
+    const uint32_t x = px, y = c.height - 1u - py;
+    const F3d o = mk(c.ox, c.oy, c.oz);
+    const F3d gp = vadd(vadd(mk(c.blx, c.bly, c.blz), vmul(vmul(mk(c.rx, c.ry, c.rz), (float)x), c.pw)),
+                        vmul(vmul(mk(c.ux, c.uy, c.uz), (float)y), c.ph));
+    const F3d v = vsub(gp, o);
+    const float vk[3] = {v.x, v.y, v.z}, ok[3] = {o.x, o.y, o.z};
+    float tmin = -__builtin_huge_valf(), tmax = __builtin_huge_valf();
+    bool safe = true;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        safe = safe && __builtin_fabsf(vk[k]) > 1e-20f;  // false for NaN too
+        const float r = __builtin_amdgcn_rcpf(vk[k]);
+        const float t1 = (0.0f - ok[k]) * r, t2 = (tsize - ok[k]) * r;
+        tmin = __builtin_fmaxf(tmin, __builtin_fminf(t1, t2));
+        tmax = __builtin_fminf(tmax, __builtin_fmaxf(t1, t2));
+    }
+    if (!safe || !__builtin_isfinite(tmin) || !__builtin_isfinite(tmax)) return false;
+    const float m = 1e-5f * __builtin_fmaxf(__builtin_fabsf(tmin), __builtin_fabsf(tmax));
+    return tmax < -m || tmin - tmax > m;
+}
+
 // ------------------------------------------------------------------------------------------- multi-pass scheduling
 // Per-ray work is heavy-tailed (bench frame: mean 14 steps, p99 311, max 2160), and a wave64 runs as long as its
 // longest lane. Pass 0 traces every ray with a small step budget; the rays that exhaust it are listed per chunk (a
@@ -719,12 +750,18 @@ __global__ void __launch_bounds__(256) k_trace_primary(DevTree t, CamD cam, OutD
     bool done = true;
     if (valid) {
         F3d o, d;
-        primary_ray(cam, px, py, o, d);
         HitOut h;
         h.bytes = 0;
-        const float start = FAST ? prepass_start(fast, px, py) : 0.0f;
-        done = get_by_ray<COUNT, BD, FAST, MIP>(t, occ_tab, o, d, h, q.budget, q.state, (uint32_t)idx, false, start,
-                                                q.sparse);
+        if (glass_clear_miss(cam, px, py, (float)t.size)) {  // the miss record, as get_by_ray's root test gives it
+            o = mk(cam.ox, cam.oy, cam.oz);
+            h.hit = false;
+            h.iters = 0;
+        } else {
+            primary_ray(cam, px, py, o, d);
+            const float start = FAST ? prepass_start(fast, px, py) : 0.0f;
+            done = get_by_ray<COUNT, BD, FAST, MIP>(t, occ_tab, o, d, h, q.budget, q.state, (uint32_t)idx, false,
+                                                    start, q.sparse);
+        }
         if (done)
             store(t, out, idx, o, h);
         else if (COUNT && q.state)
@@ -770,10 +807,17 @@ __global__ void __launch_bounds__(256) k_trace_primary_batch(DevTree t, const Ca
     bool done = true;
     if (valid) {
         F3d o, d;
-        primary_ray(cam, px, py, o, d);
         HitOut h;
         h.bytes = 0;
-        done = get_by_ray<false, BD>(t, occ_tab, o, d, h, q.budget, q.state, (uint32_t)idx, false, 0.0f, q.sparse);
+        if (glass_clear_miss(cam, px, py, (float)t.size)) {  // k_trace_primary
+            o = mk(cam.ox, cam.oy, cam.oz);
+            h.hit = false;
+            h.iters = 0;
+        } else {
+            primary_ray(cam, px, py, o, d);
+            done = get_by_ray<false, BD>(t, occ_tab, o, d, h, q.budget, q.state, (uint32_t)idx, false, 0.0f,
+                                         q.sparse);
+        }
         if (done) store(t, outs[f], local, o, h);
         if (q.flags) q.flags[idx] = done ? 0 : 1;
     }
