@@ -383,8 +383,10 @@ def hw_queues(frames):
 def main():
     args = parse()
     if args.batch is None:
-        # batches wherever vhx_trace_primary_batch applies: one GPU, primary rays, the exact path, and no explicit
-        # --inflight (which asks for that many per-frame contexts)
+        # batches wherever they are the faster line: one GPU, primary rays on the exact path, and no explicit
+        # --inflight (which asks for that many per-frame contexts). Config 5 (--shadows) keeps twenty per-frame
+        # contexts: its batches (vhx_trace_shadows_batch, --batch K) measured 1.31 against 1.17-1.23 ms per frame
+        # 
         single = int(os.environ.get("WORLD_SIZE", "1")) == 1 and os.environ.get("VHX_BENCH_MGPU1") != "1"
         args.batch = 7 if (single and args.inflight is None and not args.shadows and args.depth_prepass is None
                            and args.mip_lod is None) else 0
@@ -556,9 +558,9 @@ def main():
     if budgets is not None:
         for r in rts:
             r.set_pass_budgets(tuple(int(b) for b in budgets.split(",") if b.strip()))
-    K = args.batch if (mg is None and world == 1 and not args.shadows) else 0
+    K = args.batch if (mg is None and world == 1) else 0
     if args.batch and not K:
-        raise SystemExit("--batch is a one-GPU primary-ray mode (no --shadows, N = 1)")
+        raise SystemExit("--batch is a one-GPU mode (N = 1)")
     for _ in range(len(rts) * max(1, K)):  # batch mode: K output sets per context, outs[f * K + j]
         o = {"rgba": torch.zeros(n_out, dtype=torch.int32, device=dev),
              "depth": torch.zeros(n_out, dtype=torch.float32, device=dev)}
@@ -626,6 +628,9 @@ def main():
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(s_)
         r.trace_primary_batch(cams_b, outs[f * K:f * K + nf])
+        if args.shadows:  # config 5: the batch's shadow rays, one more pass ladder on the same stream
+            ob = outs[f * K:f * K + nf]
+            r.trace_shadows_batch(light, ob, shadowed_list=[o["shadowed"] for o in ob])
         if timed and not NOEV:
             e1.record(s_)
             ev.append((e0, e1, nf))

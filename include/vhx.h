@@ -279,6 +279,21 @@ int vhx_trace_rays(vhx_ctx *ctx, const float *rays, uint64_t n, const vhx_hits *
  * (shadowed, rgba, bytes) must not overlap the hit records (value, impact, normal) or each other: VHX_E_INVALID_ARG. */
 int vhx_trace_shadows(vhx_ctx *ctx, const float light[3], uint64_t n, const uint32_t *value, const float *impact,
                       const float *normal, uint32_t *shadowed, uint32_t *rgba, uint32_t *bytes);
+/* One frame of a shadow batch (vhx_trace_shadows_batch): a primary frame's hit records (value, impact, normal: n, 3n,
+ * 3n entries) and its outputs (shadowed: n; rgba: n, optional, darkened in place), all device memory. */
+typedef struct vhx_shadow_frame {
+    const uint32_t *value;
+    const float *impact;
+    const float *normal;
+    uint32_t *shadowed;
+    uint32_t *rgba;
+} vhx_shadow_frame;
+/* Hard shadows of n_frames frames (n records each) as ONE pass ladder on the context's stream: the hit records of
+ * every frame compacted together, shared queue passes (vhx_trace_primary_batch's shape for BASELINE config 5, e.g.
+ * right after it on the same context). Results equal n_frames vhx_trace_shadows calls bit for bit; no byte counting
+ * and no node MIPs; at most 2^31 records per batch; outputs must not overlap any frame's hit records or each other. */
+int vhx_trace_shadows_batch(vhx_ctx *ctx, const float light[3], uint32_t n_frames, uint64_t n,
+                            const vhx_shadow_frame *frames);
 
 /* Scatters tile-major RGBA buffers gathered from `ranks` ranks (rank r traced tiles r, r+ranks, ...; each rank's
  * buffer holds tiles_per_rank*T*T pixels, concatenated by rank) into a width x height framebuffer.       */

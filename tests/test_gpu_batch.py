@@ -193,3 +193,51 @@ def test_batch_argument_errors(gpu):
         gpu.trace_primary_batch([a], [{"rgba": np.zeros(32 * 32, np.uint32)}])  # host outputs
     # a valid call after the refusals still works
     _check_batch(gpu, [a, a], "after errors", fields=("rgba",))
+
+
+def _shadow_records(gpu, cams):
+    import torch
+    n = cams[0].width * cams[0].height
+    outs = [_outs(n, ("value", "impact", "normal", "rgba")) for _ in cams]
+    torch.cuda.synchronize()
+    gpu.trace_primary_batch(cams, outs)
+    gpu.sync()
+    return outs
+
+
+@pytest.mark.parametrize("W,H,nf", [(200, 136, 4), (97, 33, 3), (64, 64, 1), (1, 1, 5)])
+def test_shadow_batch_equals_single_shadow_traces(gpu, W, H, nf):
+    """vhx_trace_shadows_batch over nf frames' hit records equals one vhx_trace_shadows per frame: the shadowed flags
+    and the darkened RGBA, bit for bit (the single shadow trace is pinned to the oracle's shadow pass elsewhere)."""
+    import torch
+    size = 256
+    gpu.upload(vhx.FlatTree.build_scene(N.VHX_SCENE_LATTICE_CUBE, size, 4))
+    cams = _orbit(size, W, H, nf, step=0.15)
+    light = (float(size),) * 3
+    recs = _shadow_records(gpu, cams)
+    singles = []
+    for r in recs:
+        h = {k: v.clone() for k, v in r.items()}
+        torch.cuda.synchronize()
+        res = gpu.trace_shadows(light, h)
+        gpu.sync()
+        singles.append((res["shadowed"].cpu().numpy(), h["rgba"].cpu().numpy()))
+    torch.cuda.synchronize()
+    sh = gpu.trace_shadows_batch(light, recs)
+    gpu.sync()
+    for k in range(nf):
+        assert np.array_equal(sh[k].cpu().numpy(), singles[k][0]), f"frame {k}: shadowed differs"
+        assert np.array_equal(recs[k]["rgba"].cpu().numpy(), singles[k][1]), f"frame {k}: rgba differs"
+    if W * H > 1000:
+        assert sum(int(s.sum().item()) for s in sh) > 0, "no shadowed pixel: the case tests nothing"
+
+
+def test_shadow_batch_argument_errors(gpu):
+    import torch
+    gpu.upload(vhx.FlatTree.build_scene(N.VHX_SCENE_LATTICE_CUBE, 64, 4))
+    recs = _shadow_records(gpu, _orbit(64, 32, 32, 2))
+    with pytest.raises(ValueError):
+        gpu.trace_shadows_batch((64.0,) * 3, [recs[0], {k: v[:100] for k, v in recs[1].items()}])
+    # an output aliasing another frame's hit records is refused
+    with pytest.raises(N.VhxError):
+        gpu.trace_shadows_batch((64.0,) * 3, recs, shadowed_list=[recs[1]["value"], torch.empty_like(recs[0]["value"])])

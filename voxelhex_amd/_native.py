@@ -83,6 +83,11 @@ class Hits(ctypes.Structure):
     ]
 
 
+class ShadowFrame(ctypes.Structure):  # vhx_shadow_frame
+    _fields_ = [("value", c_void_p), ("impact", c_void_p), ("normal", c_void_p), ("shadowed", c_void_p),
+                ("rgba", c_void_p)]
+
+
 # (name, restype, argtypes) — one line per symbol declared in include/*.h
 SIGNATURES = [
     ("vhx_abi_version", c_u32, []),
@@ -113,6 +118,7 @@ SIGNATURES = [
     ("vhx_trace_rays", c_int, [c_void_p, c_void_p, c_u64, P(Hits), c_int]),
     ("vhx_trace_shadows", c_int, [c_void_p, P(c_f32), c_u64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                   c_void_p]),
+    ("vhx_trace_shadows_batch", c_int, [c_void_p, P(c_f32), c_u32, c_u64, c_void_p]),
     ("vhx_untile_rgba", c_int, [c_void_p, c_void_p, c_u32, c_u32, c_u32, c_u32, c_u32, c_void_p, c_int]),
     ("vhx_untile_frame", c_int, [c_void_p, c_void_p, c_u32, c_u32, c_u32, c_u32, c_u32, c_u32, c_void_p, c_void_p]),
     ("vhx_mgpu_unique_id", c_int, [c_void_p]),

@@ -107,6 +107,9 @@ struct vhx_ctx {
     // vhx_trace_primary_batch: the batch's cameras and outputs (pinned staging, and their device copy)
     Pinned batch_pinned;
     DevBuf batch_args;
+    // vhx_trace_shadows_batch: the frames' ShD records and hit-value pointers (pinned staging, device copy)
+    Pinned shadow_pinned;
+    DevBuf shadow_args;
     DevBuf upd;
     hipStream_t upd_stream = nullptr;  // the stream of the last scatter (reads upd)
     // depth-prepass mode (vhx_set_depth_prepass; opt-in, not the reference path)

@@ -430,7 +430,14 @@ struct FlagOrder {
     // a batch of frames (vhx_trace_primary_batch): positions [f * fpos, (f + 1) * fpos) are frame f's, in the order
     // above, and its pixels are output indices [f * fpix, (f + 1) * fpix); fpos = 0: one frame
     uint64_t fpos, fpix;
+    // a shadow batch (vhx_trace_shadows_batch): frame f's hit values are the array at fvals[f] (entry i of the batch
+    // is fvals[i / fpix][i % fpix]), not one array
+    const uint64_t *fvals;
 };
+__device__ __forceinline__ bool frame_hit(const FlagOrder &o, uint64_t i) {
+    const uint64_t f = i / o.fpix;
+    return ((const uint32_t *)o.fvals[f])[i - f * o.fpix] != VHX_EMPTY;
+}
 __device__ __forceinline__ uint32_t compact_bits(uint32_t v) {  // even bits of v -> low half
     v &= 0x55555555u;
     v = (v | (v >> 1)) & 0x33333333u;
@@ -486,8 +493,17 @@ __device__ __forceinline__ uint32_t order_bits(const void *src, const FlagOrder 
         uint64_t i;
         if (!order_index(o, k + j, i)) continue;
         // a pass-0 flag byte: 1 = abandoned
-        if (HITS ? ((const uint32_t *)src)[i] != VHX_EMPTY : (((const uint8_t *)src)[i] & 1u) != 0) bits |= 1u << j;
+        const bool hit = HITS && o.fvals ? frame_hit(o, i) : ((const uint32_t *)src)[i] != VHX_EMPTY;
+        if (HITS ? hit : (((const uint8_t *)src)[i] & 1u) != 0) bits |= 1u << j;
     }
+    return bits;
+}
+
+// hit flags of entries i..i+3 of a shadow batch in output-index order (FlagOrder::fvals)
+__device__ __forceinline__ uint32_t frame_bits(const FlagOrder &o, uint64_t i, uint64_t n) {
+    uint32_t bits = 0;
+    for (uint64_t k = i; k < n && k < i + 4; ++k)
+        if (frame_hit(o, k)) bits |= 1u << (k - i);
     return bits;
 }
 
@@ -505,7 +521,8 @@ __global__ void __launch_bounds__(256) k_count_flags(const void *__restrict__ sr
     const uint64_t i = ((uint64_t)blockIdx.x * 256u + threadIdx.x) * 4u;
     if (clear)
         for (uint64_t k = i; k < nclear && k < i + 4u; ++k) clear[k] = 0u;
-    uint32_t c = __popc(ord.W ? (i < n ? order_bits<HITS>(src, ord, i) : 0u) : flag_bits<HITS>(src, i, n));
+    uint32_t c = __popc(ord.W ? (i < n ? order_bits<HITS>(src, ord, i) : 0u)
+                              : (HITS && ord.fvals ? frame_bits(ord, i, n) : flag_bits<HITS>(src, i, n)));
     for (uint32_t d = 32; d > 0; d >>= 1) c += __shfl_down(c, d);
     if ((threadIdx.x & 63u) == 0) s_cnt[threadIdx.x >> 6] = c;
     __syncthreads();
@@ -519,7 +536,8 @@ __global__ void __launch_bounds__(256) k_emit_flags(const void *__restrict__ src
     __shared__ uint32_t s_wave[4];
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     const uint64_t i = ((uint64_t)blockIdx.x * 256u + threadIdx.x) * 4u;
-    const uint32_t bits = ord.W ? (i < n ? order_bits<HITS>(src, ord, i) : 0u) : flag_bits<HITS>(src, i, n);
+    const uint32_t bits = ord.W ? (i < n ? order_bits<HITS>(src, ord, i) : 0u)
+                                : (HITS && ord.fvals ? frame_bits(ord, i, n) : flag_bits<HITS>(src, i, n));
     const uint32_t c = __popc(bits);
     uint32_t inc = c;
     for (uint32_t d = 1; d < 64; d <<= 1) {
@@ -598,9 +616,17 @@ __global__ void __launch_bounds__(QSORT_THREADS) k_sort_segments(uint32_t *__res
     }
 }
 
+// One frame of a shadow batch on the device (vhx_shadow_frame)
+struct ShD {
+    const uint32_t *value;
+    const float *impact, *normal;
+    uint32_t *shadowed, *rgba;
+};
+
 // Where a queued output index comes from: a primary-ray frame (framebuffer or tile layout) or an explicit ray batch.
 struct RaySrc {
-    uint32_t kind;  // 0 framebuffer, 1 tiles, 2 explicit rays, 3 shadow rays from hit records, 4 a batch of frames
+    uint32_t kind;  // 0 framebuffer, 1 tiles, 2 explicit rays, 3 shadow rays from hit records, 4 a batch of frames,
+                    // 5 a batch of shadow frames
     uint32_t T, tiles_x, tile_start, tile_stride;
     const float *rays;
     const float *impact, *normal;  // kind 3
@@ -610,18 +636,27 @@ struct RaySrc {
     const CamD *cams;
     const OutD *outs;
     uint32_t npix;
+    const ShD *shs;  // kind 5: frame f = idx / npix is shs[f], entry idx - f * npix
 };
 
 // Hard-shadow ray of hit record idx (BASELINE config 5; semantics in DESIGN.md §9): from impact + normal * 1e-3
 // toward the light, direction normalised like V3c::normalized (src/spatial/math/vector.rs).
 __device__ __forceinline__ void shadow_ray(const RaySrc &src, uint32_t idx, F3d &o, F3d &d) {
-    const float *ip = src.impact + 3ull * idx, *np = src.normal + 3ull * idx;
+    const float *ip, *np;
+    if (src.kind == 5u) {  // a shadow batch: frame f's records
+        const uint32_t f = idx / src.npix, local = idx - f * src.npix;
+        ip = src.shs[f].impact + 3ull * local;
+        np = src.shs[f].normal + 3ull * local;
+    } else {
+        ip = src.impact + 3ull * idx;
+        np = src.normal + 3ull * idx;
+    }
     o = mk(ip[0] + np[0] * 1e-3f, ip[1] + np[1] * 1e-3f, ip[2] + np[2] * 1e-3f);
     d = vnorm(mk(src.lx - o.x, src.ly - o.y, src.lz - o.z));
 }
 
 __device__ __forceinline__ void ray_of(const CamD &cam, const RaySrc &src, uint32_t idx, F3d &o, F3d &d) {
-    if (src.kind == 3u) {
+    if (src.kind == 3u || src.kind == 5u) {
         shadow_ray(src, idx, o, d);
         return;
     }
@@ -932,6 +967,12 @@ __global__ void __launch_bounds__(256) VHX_QUEUE_ATTR k_trace_queue(DevTree t, c
                 if (COUNT && q.state) b->out.bytes[idx] = h.bytes;
             } else if (b->src.kind == 3u) {
                 store_shadow(b->out, idx, h);
+            } else if (b->src.kind == 5u) {
+                const uint32_t f = idx / b->src.npix;
+                OutD so{};
+                so.value = b->src.shs[f].shadowed;
+                so.rgba = b->src.shs[f].rgba;
+                store_shadow(so, idx - f * b->src.npix, h);
             } else if (b->src.kind == 4u) {
                 const uint32_t f = idx / b->src.npix;
                 store(t, b->src.outs[f], idx - f * b->src.npix, o, h);
@@ -1464,7 +1505,7 @@ static int ensure_lists(vhx_ctx *c, uint64_t nblocks) {
 // The QueueArgs slot of a frame (camera, ray source, outputs) on c's stream. They rarely change between frames: the
 // device copy is rewritten only when they do.
 static int put_qargs(vhx_ctx *c, const CamD &cam, const RaySrc &src, const OutD &o, QueueArgs *&qa) {
-    const uint32_t slot = src.kind == 3u ? 1u : 0u;  // a shadow frame alternates with its primary frame
+    const uint32_t slot = src.kind == 3u || src.kind == 5u ? 1u : 0u;  // a shadow frame alternates with its primary
     qa = (QueueArgs *)c->qargs.ptr + slot;
     QueueArgs a;
     std::memset(&a, 0, sizeof(a));  // padding included, for the comparison
@@ -1630,9 +1671,10 @@ void vhx_destroy(vhx_ctx *c) {
     c->tree.reset();  // frees the device tree with its last context
     if (c->use_ev) (void)hipEventDestroy(c->use_ev);
     for (DevBuf *b : {&c->scratch, &c->rays, &c->queue[0], &c->queue[1], &c->qctl, &c->tmp, &c->counts, &c->offsets,
-                      &c->flags, &c->qargs, &c->state, &c->upd, &c->prepass_depth, &c->batch_args})
+                      &c->flags, &c->qargs, &c->state, &c->upd, &c->prepass_depth, &c->batch_args, &c->scan_part,
+                      &c->shadow_args})
         if (b->ptr) (void)hipFree(b->ptr);
-    for (auto *P : {&c->pinned[0], &c->pinned[1], &c->batch_pinned}) {
+    for (auto *P : {&c->pinned[0], &c->pinned[1], &c->batch_pinned, &c->shadow_pinned}) {
         if (P->ptr) (void)hipHostFree(P->ptr);
         if (P->done) (void)hipEventDestroy(P->done);
     }
@@ -2428,7 +2470,9 @@ int vhx_trace_primary_batch(vhx_ctx *c, const vhx_camera *cams, uint32_t n, cons
     if (!dispatch_bd(c->tree->desc.brick_dim, launch)) return fail(c, VHX_E_INVALID_ARG, "unsupported brick_dim");
     if (qrc) return qrc;
     VHX_HIP(c, hipGetLastError());
-    c->last_fb_w = c->last_fb_h = 0;  // no single frame's order for a later shadow trace
+    // a shadow trace (or shadow batch) of these frames' hit records lists them in the same tile order
+    c->last_fb_w = W;
+    c->last_fb_h = H;
     VHX_HIP(c, hipEventRecord(c->ev1, c->stream));
     c->timed = true;
     return tscope.end();
@@ -2637,6 +2681,119 @@ int vhx_trace_shadows(vhx_ctx *c, const float light[3], uint64_t n, const uint32
             qrc = launch_queue_passes<true, BD>(c, t, cd, src, so, 0, npass, n, nb64);
         else
             qrc = launch_queue_passes<false, BD>(c, t, cd, src, so, 0, npass, n, nb64);
+    };
+    if (!dispatch_bd(c->tree->desc.brick_dim, launch)) return fail(c, VHX_E_INVALID_ARG, "unsupported brick_dim");
+    if (qrc) return qrc;
+    VHX_HIP(c, hipGetLastError());
+    VHX_HIP(c, hipEventRecord(c->ev1, c->stream));
+    c->timed = true;
+    return tscope.end();
+}
+
+int vhx_trace_shadows_batch(vhx_ctx *c, const float light[3], uint32_t nf, uint64_t n, const vhx_shadow_frame *frames) {
+    if (!c || !light || nf == 0 || !frames) return VHX_E_INVALID_ARG;
+    if (!c->tree->uploaded) return fail(c, VHX_E_STATE, "vhx_trace_shadows_batch before vhx_upload_tree");
+    if (n == 0) return VHX_OK;
+    const uint64_t ntot = n * nf;
+    if (ntot >= 0x7FFFFFFFull) return fail(c, VHX_E_INVALID_ARG, "vhx_trace_shadows_batch: more than 2^31 records");
+    // every frame's outputs are written while every frame's hit records are read: no overlaps anywhere in the batch
+    {
+        struct R {
+            const void *p;
+            uint64_t bytes;
+        };
+        std::vector<R> outs, ins;
+        for (uint32_t k = 0; k < nf; ++k) {
+            const vhx_shadow_frame &f = frames[k];
+            if (!f.value || !f.impact || !f.normal || !f.shadowed)
+                return fail(c, VHX_E_INVALID_ARG, "vhx_trace_shadows_batch: a frame lacks value, impact, normal or shadowed");
+            outs.push_back({f.shadowed, n * 4});
+            if (f.rgba) outs.push_back({f.rgba, n * 4});
+            ins.push_back({f.value, n * 4});
+            ins.push_back({f.impact, n * 12});
+            ins.push_back({f.normal, n * 12});
+        }
+        auto overlap = [](const R &a, const R &b) {
+            return (const char *)a.p < (const char *)b.p + b.bytes && (const char *)b.p < (const char *)a.p + a.bytes;
+        };
+        for (size_t i = 0; i < outs.size(); ++i) {
+            for (const R &in : ins)
+                if (overlap(outs[i], in))
+                    return fail(c, VHX_E_INVALID_ARG, "vhx_trace_shadows_batch: an output overlaps the hit records");
+            for (size_t j = i + 1; j < outs.size(); ++j)
+                if (overlap(outs[i], outs[j]))
+                    return fail(c, VHX_E_INVALID_ARG, "vhx_trace_shadows_batch: outputs overlap each other");
+        }
+    }
+    VHX_HIP(c, hipSetDevice(c->device));
+    VHX_STREAM(c);
+    TraceScope tscope(c);
+    int rc = tscope.rc;
+    if (rc) return rc;
+    if ((rc = refresh_child_rec(c))) return rc;
+    const DevTree t = dev_tree(c);
+    if (t.mips) return fail(c, VHX_E_INVALID_ARG, "vhx_trace_shadows_batch: not available with node MIPs");
+    uint32_t npass = 1;
+    const uint64_t nb64 = (ntot + 255) / 256;
+    if ((rc = prepare_passes(c, ntot, nb64, npass, true, nf > 1))) return rc;
+    // the frames' ShD records, then their value pointers (FlagOrder::fvals), staged like vhx_trace_primary_batch's
+    const uint64_t sh_bytes = ((uint64_t)nf * sizeof(ShD) + 255) & ~255ull, args_bytes = sh_bytes + (uint64_t)nf * 8;
+    vhx_ctx::Pinned &P = c->shadow_pinned;
+    if (P.used) VHX_HIP(c, hipEventSynchronize(P.done));
+    if (P.bytes < args_bytes) {
+        if (P.ptr) VHX_HIP(c, hipHostFree(P.ptr));
+        P.ptr = nullptr;
+        P.bytes = 0;
+        VHX_HIP(c, hipHostMalloc(&P.ptr, args_bytes, hipHostMallocDefault));
+        P.bytes = args_bytes;
+    }
+    if (!P.done) VHX_HIP(c, hipEventCreateWithFlags(&P.done, hipEventDisableTiming));
+    if (c->use_recorded && c->use_stream != c->stream) VHX_HIP(c, hipStreamWaitEvent(c->stream, c->use_ev, 0));
+    if ((rc = ensure(c, c->shadow_args, args_bytes))) return rc;
+    ShD *hs = (ShD *)P.ptr;
+    uint64_t *hv = (uint64_t *)((uint8_t *)P.ptr + sh_bytes);
+    for (uint32_t k = 0; k < nf; ++k) {
+        hs[k] = ShD{frames[k].value, frames[k].impact, frames[k].normal, frames[k].shadowed, frames[k].rgba};
+        hv[k] = (uint64_t)(uintptr_t)frames[k].value;
+    }
+    VHX_HIP(c, hipEventRecord(c->ev0, c->stream));
+    VHX_HIP(c, hipMemcpyAsync(c->shadow_args.ptr, P.ptr, args_bytes, hipMemcpyHostToDevice, c->stream));
+    VHX_HIP(c, hipEventRecord(P.done, c->stream));
+    P.used = true;
+    // shadowed = 0 where no shadow ray is cast (vhx_trace_shadows clears inside its count kernel)
+    for (uint32_t k = 0; k < nf; ++k) VHX_HIP(c, hipMemsetAsync(frames[k].shadowed, 0, n * 4, c->stream));
+    RaySrc src{};
+    src.kind = 5u;
+    src.lx = light[0];
+    src.ly = light[1];
+    src.lz = light[2];
+    src.npix = (uint32_t)n;
+    src.shs = (const ShD *)c->shadow_args.ptr;
+    {
+        // every frame's hit records in the tile order of the frames they came from (c->last_fb_*), frame by frame
+        uint64_t npos = ntot;
+        const bool fb = c->last_fb_w && (uint64_t)c->last_fb_w * c->last_fb_h == n;
+        FlagOrder ord = flag_order(fb ? c->qorder : 0u, c->last_fb_w, c->last_fb_h, npos, nf);
+        if (!ord.W) npos = ntot;
+        ord.fpix = n;
+        ord.fvals = (const uint64_t *)((const uint8_t *)c->shadow_args.ptr + sh_bytes);
+        const unsigned nb = (unsigned)((npos + 1023) / 1024);
+        uint32_t *counts = (uint32_t *)c->counts.ptr, *offsets = (uint32_t *)c->offsets.ptr;
+        if ((uint64_t)nb * 4 > c->counts.bytes || (uint64_t)nb * 4 > c->offsets.bytes) {
+            if ((rc = ensure_lists(c, nb))) return rc;
+            counts = (uint32_t *)c->counts.ptr;
+            offsets = (uint32_t *)c->offsets.ptr;
+        }
+        k_count_flags<true><<<nb, 256, 0, c->stream>>>(nullptr, npos, counts, (uint32_t *)c->qctl.ptr + 16, nullptr, ord);
+        launch_scan(c, counts, nb, nullptr, 1, offsets, (uint32_t *)c->qctl.ptr + 7, nb);
+        k_emit_flags<true><<<nb, 256, 0, c->stream>>>(nullptr, npos, offsets, (uint32_t *)c->queue[1].ptr, ord);
+        VHX_HIP(c, hipGetLastError());
+    }
+    int qrc = VHX_OK;
+    const CamD cd{};
+    auto launch = [&](auto bd_tag) {
+        constexpr int BD = decltype(bd_tag)::value;
+        qrc = launch_queue_passes<false, BD>(c, t, cd, src, OutD{}, 0, npass, ntot, nb64, P0_LISTS, 0, 0, nf);
     };
     if (!dispatch_bd(c->tree->desc.brick_dim, launch)) return fail(c, VHX_E_INVALID_ARG, "unsupported brick_dim");
     if (qrc) return qrc;

@@ -366,6 +366,30 @@ class Raytracer:
                                                     ctypes.cast(hs, ctypes.c_void_p)))
         return outs
 
+    def trace_shadows_batch(self, light, hits_list, shadowed_list=None, darken=True):
+        """vhx_trace_shadows_batch: the hard shadows of several frames' device-resident hit records (dicts like
+        trace_shadows' `hits`, the same record count each) as one pass ladder; returns the int32 `shadowed` tensors.
+        Equal to one trace_shadows per frame."""
+        import torch
+        if not hits_list:
+            raise ValueError("trace_shadows_batch: no frames")
+        n = hits_list[0]["value"].numel()
+        if any(h["value"].numel() != n for h in hits_list):
+            raise ValueError("trace_shadows_batch: every frame needs the same record count")
+        for h in hits_list:
+            if _on_device(h) != 1:
+                raise ValueError("trace_shadows_batch reads device tensors")
+        if shadowed_list is None:
+            shadowed_list = [torch.empty(n, dtype=torch.int32, device=h["value"].device) for h in hits_list]
+        fr = (N.ShadowFrame * len(hits_list))()
+        for k, h in enumerate(hits_list):
+            rgba = h.get("rgba") if darken else None
+            fr[k] = N.ShadowFrame(_ptr(h["value"]), _ptr(h["impact"]), _ptr(h["normal"]), _ptr(shadowed_list[k]),
+                                  None if rgba is None else _ptr(rgba))
+        lt = (ctypes.c_float * 3)(*[float(v) for v in light])
+        self._check(N.lib().vhx_trace_shadows_batch(self._h, lt, len(hits_list), n, ctypes.cast(fr, ctypes.c_void_p)))
+        return shadowed_list
+
     def trace_shadows(self, light, hits, shadowed=None, darken=True, count_bytes=False):
         """Hard shadow rays (vhx_trace_shadows) for the device-resident hit records `hits` of a previous trace
         (dict of torch tensors with value, impact, normal and optionally rgba). Returns a dict with the int32
