@@ -84,6 +84,7 @@ for p in passes:
     wc, waves = per_frame(p, "SQ_WAVE_CYCLES"), per_frame(p, "SQ_WAVES")
     act, wi, wa = per_frame(p, "SQ_ACTIVE_INST_ANY"), per_frame(p, "SQ_WAIT_INST_ANY"), per_frame(p, "SQ_WAIT_ANY")
     fetch = per_frame(p, "FETCH_SIZE")
+    hit, miss = per_frame(p, "TCC_HIT_sum"), per_frame(p, "TCC_MISS_sum")
     parts = [f"pass {p}:" if prim is None or p < prim else f"shadow pass {p - prim}:"]
     if waves is not None:
         parts.append(f"waves {waves:.0f}")
@@ -97,6 +98,8 @@ for p in passes:
         parts.append(f"issuing {act / wc:.0%}, dependency waits {wi / wc:.0%}, memory waits {wa / wc:.0%} of wave cycles")
     if fetch is not None:
         parts.append(f"reads {fetch * 2048 / 1e6:.1f} MB")
+    if hit is not None and miss is not None and hit + miss > 0:
+        parts.append(f"L2 hit rate {hit / (hit + miss):.1%} of {(hit + miss) / 1e6:.1f} M requests")
     lines.append("  " + "  ".join(parts))
 txt = "\n".join(lines)
 print(txt)
