@@ -48,7 +48,13 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.
 
 def parse():
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=None,
+                   help="GPUs (ranks) of the run, default 1. Under torchrun (WORLD_SIZE set) it must equal WORLD_SIZE; "
+                        "without it and N > 1 this process starts the N rank processes itself (launch_ranks) and "
+                        "relays rank 0's line")
+    p.add_argument("--print-launch", action="store_true",
+                   help="N > 1 without WORLD_SIZE: print the rank processes that would be started (command and "
+                        "environment) as one JSON line and exit, starting nothing")
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--size", type=int, default=1024)
@@ -364,6 +370,139 @@ def check_frames(args, rt, rts, outs, last_cam, light, W, H, dev):
     return res
 
 
+def visible_gpus():
+    """GPUs a rank process would see, counted in a child process (torch.cuda.device_count reads the device list
+    without initialising HIP; the child keeps even that out of the launcher). -1 if the count failed."""
+    try:
+        r = subprocess.run([sys.executable, "-c", "import torch; print(torch.cuda.device_count())"],
+                           capture_output=True, text=True, timeout=600)
+        return int(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else -1
+    except (OSError, ValueError, IndexError, subprocess.TimeoutExpired):
+        return -1
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_plan(n, argv, port):
+    """The N rank processes of `bench.py --gpus N`: this script with the same arguments, one process per GPU, with the
+    environment torchrun would give them (RANK, LOCAL_RANK, WORLD_SIZE, LOCAL_WORLD_SIZE, MASTER_ADDR/PORT on
+    127.0.0.1)."""
+    cmd = [sys.executable, os.path.abspath(__file__)] + list(argv)
+    plan = []
+    for r in range(n):
+        env = {"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(n), "LOCAL_WORLD_SIZE": str(n),
+               "GROUP_RANK": "0", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port),
+               "HSA_ENABLE_IPC_MODE_LEGACY": "0", "VHX_BENCH_LAUNCHED": "1"}
+        plan.append({"rank": r, "cmd": cmd, "env": env})
+    return plan
+
+
+def launch_ranks(args):
+    """`python bench.py --gpus N` (N > 1) with no WORLD_SIZE in the environment: this process is only the launcher.
+    It imports neither torch nor libvhx and touches no GPU: it counts the visible GPUs in a child process, fails with
+    a message (exit 2) if there are fewer than N, starts N rank processes of this script (rank_plan) in sessions of
+    their own, and exits with 0 once all N exit 0 -- rank 0 prints the JSON line straight to the shared stdout --
+    or, as soon as one rank fails, stops the others and exits with that rank's status. One-GPU runs never come here,
+    so `--gpus N` can never print a one-GPU line."""
+    n = args.gpus
+    argv = [a for a in sys.argv[1:] if a != "--print-launch"]
+    port = free_port()
+    plan = rank_plan(n, argv, port)
+    if args.print_launch:
+        print(json.dumps({"launcher": "bench.py", "world": n, "master": f"127.0.0.1:{port}", "ranks": plan,
+                          "torch_imported": "torch" in sys.modules,
+                          "vhx_imported": any(m.startswith("voxelhex_amd") for m in sys.modules)}), flush=True)
+        return 0
+    if os.environ.get("VHX_BENCH_SKIP_DEVICE_CHECK") != "1":
+        have = visible_gpus()
+        if have < n:
+            print(f"bench.py --gpus {n}: {n} GPUs requested, "
+                  + (f"{have} visible" if have >= 0 else "the device count failed")
+                  + " -- refusing to run (no line is printed for fewer GPUs than requested)", file=sys.stderr,
+                  flush=True)
+            return 2
+    procs = []
+    for p in plan:
+        procs.append(subprocess.Popen(p["cmd"], env=dict(os.environ, **p["env"]), start_new_session=True))
+
+    def stop_all(sig=signal.SIGTERM):
+        for q in procs:
+            if q.poll() is None:
+                try:
+                    os.killpg(q.pid, sig)
+                except OSError:
+                    pass
+
+    def on_signal(signum, _frame):
+        stop_all(signal.SIGTERM)
+        raise SystemExit(128 + signum)
+
+    signal.signal(signal.SIGTERM, on_signal)
+    signal.signal(signal.SIGINT, on_signal)
+    rc = 0
+    live = set(range(n))
+    while live:
+        for r in sorted(live):
+            s = procs[r].poll()
+            if s is None:
+                continue
+            live.discard(r)
+            if s != 0 and rc == 0:
+                rc = s if s > 0 else 128 - s
+                print(f"bench.py --gpus {n}: rank {r} exited with status {s}; stopping the other ranks",
+                      file=sys.stderr, flush=True)
+                stop_all(signal.SIGTERM)
+                deadline = time.time() + 15
+                while time.time() < deadline and any(q.poll() is None for q in procs):
+                    time.sleep(0.1)
+                stop_all(signal.SIGKILL)
+        time.sleep(0.05)
+    for q in procs:
+        q.wait()
+    return rc
+
+
+def scaling_n1(args):
+    """The scaling curve's N = 1 point: the N > 1 default workload -- BASELINE config 4, the
+    7680x4320 frame (--scaling strong) -- run by the N > 1 ranks' own code (vhx_mgpu on a one-rank RCCL communicator,
+    VHX_BENCH_MGPU1, frames in flight, the tiles untiled into rank 0's framebuffer) as a child process of this bench
+    (its own hardware queues, like every rank of an N > 1 run), 20 timed frames after 5 warm-up frames. Returns the
+    sub-object for the line; value(N) / (N x this value) is then like-for-like strong scaling."""
+    cmd = [sys.executable, os.path.abspath(__file__), "--scaling", "strong", "--steps", "20", "--warmup", "5",
+           "--size", str(args.size), "--brick-dim", str(args.brick_dim), "--scene", str(args.scene),
+           "--tile", str(args.tile), "--planes", str(args.planes), "--no-cpu-baseline", "--no-roofline", "--no-pmc",
+           "--no-extra", "--no-isolated"]
+    env = dict(os.environ, VHX_BENCH_MGPU1="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()),
+               RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    env.pop("GPU_MAX_HW_QUEUES", None)  # the child raises it for its frames in flight, as an N > 1 rank does
+    t0 = time.time()
+    try:
+        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240, start_new_session=True)
+    except subprocess.TimeoutExpired:
+        return {"error": "timed out after 240 s"}
+    line = None
+    for ln in r.stdout.splitlines():
+        if ln.startswith("{"):
+            try:
+                line = json.loads(ln)
+            except ValueError:
+                pass
+    if r.returncode != 0 or line is None:
+        return {"error": f"exit {r.returncode}", "stderr_tail": r.stderr[-400:]}
+    return {"value": line["value"], "unit": line["unit"], "ms_per_step": line["ms_per_step"], "steps": line["steps"],
+            "warmup": line["warmup"], "workload": line["config"]["workload"], "parallelism": line["config"]["parallelism"],
+            "frames_in_flight": line.get("frames_in_flight"), "frame_equal": (line.get("multi_gpu_check") or {}).get(
+                "frame_equal"), "mgpu_fallback": line.get("mgpu_fallback"), "child_wall_s": round(time.time() - t0, 1),
+            "basis": "N = 1 point of the multi-GPU curve: the workload every N > 1 run of this bench times (BASELINE "
+                     "config 4, strong scaling) through the same rank code (vhx_mgpu, one-rank RCCL communicator, tile "
+                     "layout + untile), run as a child process of this bench; scaling at N = value(N) / (N x this)"}
+
+
 def hw_queues(frames):
     """Hardware queues for F frames in flight: HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues per process (4
     by default) round-robin, and the default stream holds one, so with the default four frames in flight two frames
@@ -382,6 +521,20 @@ def hw_queues(frames):
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus is not None and args.gpus > 1:
+            sys.exit(launch_ranks(args))
+        if args.gpus is not None and args.gpus < 1:
+            raise SystemExit(f"bench.py --gpus {args.gpus}: at least one GPU")
+    elif args.gpus is not None and args.gpus != int(os.environ["WORLD_SIZE"]):
+        raise SystemExit(f"bench.py --gpus {args.gpus} under a launcher with WORLD_SIZE={os.environ['WORLD_SIZE']}: "
+                         "the two must agree")
+    echo = os.environ.get("VHX_BENCH_RANK_ECHO")
+    if echo is not None and os.environ.get("VHX_BENCH_LAUNCHED") == "1":
+        # launcher self-test (tests/test_bench_launch.py): the rank reports its environment and exits before torch
+        keys = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")
+        print(json.dumps({"rank_echo": {k: os.environ.get(k) for k in keys}, "argv": sys.argv[1:]}), flush=True)
+        sys.exit(3 if echo == "fail" + os.environ.get("RANK", "") else 0)
     if args.batch is None:
         # batches wherever they are the faster line: one GPU, primary rays on the exact path, and no explicit
         # --inflight (which asks for that many per-frame contexts). Config 5 (--shadows) keeps twenty per-frame
@@ -419,6 +572,9 @@ def main():
     use_vhx_mgpu = (world > 1 or force1) and args.mgpu == "vhx" and not rehearsal
     if rehearsal:
         local = 0
+    elif world > 1 and torch.cuda.device_count() < world:
+        raise SystemExit(f"bench.py rank {rank}: WORLD_SIZE={world} needs {world} visible GPUs, "
+                         f"{torch.cuda.device_count()} visible")
     if force1:
         for k, v in (("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", "29533"), ("RANK", "0"), ("WORLD_SIZE", "1")):
             os.environ.setdefault(k, v)
@@ -941,6 +1097,11 @@ def main():
                          + (f"; each frame = primary rays + the oracle's shadow pass over its hits ({r_all} rays in the "
                             f"full frame)" if args.shadows else "")}
 
+    scal = None
+    if (world == 1 and mg is None and not args.no_extra and not args.shadows and not args.vox and not args.orbit
+            and args.mip_lod is None and args.depth_prepass is None and args.scaling == "auto" and not args.width):
+        scal = scaling_n1(args)
+
     if rank == 0:
         metric = BASELINE["metric"]
         if args.shadows:
@@ -993,6 +1154,11 @@ def main():
             line["lone"] = lone
         if orbit is not None:
             line["orbit"] = orbit
+        if scal is not None:
+            line["scaling_n1"] = scal
+        if world > 1 and cfg4:
+            line["scaling_basis"] = ("strong scaling of BASELINE config 4 (7680x4320); its N = 1 point is the "
+                                     "`scaling_n1` object of the N = 1 line (same workload, same rank code)")
         if args.tune:
             line["tune"] = args.tune
         if mgpu is not None:

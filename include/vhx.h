@@ -239,7 +239,11 @@ int vhx_trace_primary(vhx_ctx *ctx, const vhx_camera *cam, uint32_t tile_size, u
  * src/raytracing/bevy/pipeline/mod.rs:96-155, batched). Frame k is cams[k] (every camera the same width x height)
  * into outs[k] (device pointers, any subset of fields; byte counting and node MIPs are refused); results equal n
  * vhx_trace_primary calls bit for bit. The depth-prepass mode does not apply (the batch traces the exact path).
- * At most 2^31 rays per batch. Stream-ordered like vhx_trace_primary; vhx_sync reports the batch's device time. */
+ * At most 2^31 rays per batch; output arrays of different frames (or fields) must not overlap: VHX_E_INVALID_ARG.
+ * Stream-ordered like vhx_trace_primary; vhx_sync reports the batch's device time. The cameras and output pointers
+ * are staged through a ring of 4 pinned slots per context, so up to 4 batches can be queued back to back on one
+ * context before the call waits on the host (batches on one context still run one after another on its stream; for
+ * batches that overlap on the GPU, round-robin over shared contexts). */
 int vhx_trace_primary_batch(vhx_ctx *ctx, const vhx_camera *cams, uint32_t n, const vhx_hits *outs);
 /* Depth-prepass fast mode (opt-in; NOT the reference's CPU semantics, so outside the parity bar; the WGSL path's
  * prepass, src/raytracing/bevy/viewport_render.wgsl:702-726). When enabled, a vhx_trace_primary of a whole frame in

@@ -9,6 +9,8 @@
  *   TREE_FILE: "VHXT", u32 version 1, u32 sizeof(vhx_camera), the 8 u32 counts of vhx_tree_desc, the vhx_camera bytes,
  *              then the 7 arrays in VHX_BUF_* order (sizes from the counts)
  *   OUT_DIR:   frame0.bin  value|cell|voxel|impact|normal|depth|rgba of the uploaded tree
+ *              batch.bin   value|depth|rgba of the 5 frames of two back-to-back vhx_trace_primary_batch calls, then
+ *                          the shadowed flags of the 2 frames of one vhx_trace_shadows_batch (light (S, S, S))
  *              frame1.bin  value|depth|rgba after clearing the first `clear` voxels (the count is printed)
  *              mgpu.bin    rgba|depth of the one-rank vhx_mgpu render of the uploaded tree
  * exit 0 = every call behaved as expected; 3 = no HIP device (vhx_create returned VHX_E_NO_DEVICE); 1 = failure. */
@@ -128,6 +130,63 @@ int main(int argc, char **argv) {
     uint64_t hits = 0;
     for (uint64_t i = 0; i < n; ++i) hits += value[i] != VHX_EMPTY;
     printf("frame0 %ux%u hits %llu trace_ms %.3f\n", cam.width, cam.height, (unsigned long long)hits, ms);
+
+    /* ---- batches (vhx_trace_primary_batch), device outputs: two batches back to back on ONE context (3 + 2 frames
+     * of the same camera; the staging ring lets the second call queue behind the first without a host wait), an
+     * aliasing batch that must be refused, then the hard shadows of two frames as one vhx_trace_shadows_batch ---- */
+    {
+        enum { NB = 5 };
+        void *dv[NB], *dd[NB], *dr[NB], *di[2], *dn[2], *ds[2];
+        for (int k = 0; k < NB; ++k)
+            if (hipMalloc(&dv[k], 4 * n) != hipSuccess || hipMalloc(&dd[k], 4 * n) != hipSuccess ||
+                hipMalloc(&dr[k], 4 * n) != hipSuccess)
+                return 1;
+        for (int k = 0; k < 2; ++k)
+            if (hipMalloc(&di[k], 12 * n) != hipSuccess || hipMalloc(&dn[k], 12 * n) != hipSuccess ||
+                hipMalloc(&ds[k], 4 * n) != hipSuccess)
+                return 1;
+        vhx_camera bc[NB];
+        vhx_hits bh[NB];
+        for (int k = 0; k < NB; ++k) {
+            bc[k] = cam;
+            vhx_hits z = {(uint32_t *)dv[k], NULL, NULL, k < 2 ? (float *)di[k] : NULL, k < 2 ? (float *)dn[k] : NULL,
+                          (float *)dd[k], (uint32_t *)dr[k], NULL};
+            bh[k] = z;
+        }
+        CHECK(vhx_trace_primary_batch(ctx, bc, 3, bh));
+        CHECK(vhx_trace_primary_batch(ctx, bc + 3, 2, bh + 3));
+        vhx_hits alias[2] = {bh[0], bh[0]};
+        alias[1].value = (uint32_t *)dv[1];
+        alias[1].depth = (float *)dd[1];
+        rc = vhx_trace_primary_batch(ctx, bc, 2, alias); /* both frames would write one rgba array */
+        printf("batch_overlap %d \"%s\"\n", rc, vhx_last_error(ctx));
+        if (rc != VHX_E_INVALID_ARG) return 1;
+        const float light[3] = {(float)t.boxtree_size, (float)t.boxtree_size, (float)t.boxtree_size};
+        vhx_shadow_frame sf[2];
+        for (int k = 0; k < 2; ++k) {
+            vhx_shadow_frame z = {(const uint32_t *)dv[k], (const float *)di[k], (const float *)dn[k], (uint32_t *)ds[k],
+                                  NULL};
+            sf[k] = z;
+        }
+        CHECK(vhx_trace_shadows_batch(ctx, light, 2, n, sf));
+        CHECK(vhx_sync(ctx, &ms));
+        uint32_t *host = malloc(4 * n * (3 * NB + 2));
+        if (!host) return 1;
+        for (int k = 0; k < NB; ++k)
+            if (hipMemcpy(host + (3 * k) * n, dv[k], 4 * n, hipMemcpyDeviceToHost) != hipSuccess ||
+                hipMemcpy(host + (3 * k + 1) * n, dd[k], 4 * n, hipMemcpyDeviceToHost) != hipSuccess ||
+                hipMemcpy(host + (3 * k + 2) * n, dr[k], 4 * n, hipMemcpyDeviceToHost) != hipSuccess)
+                return 1;
+        for (int k = 0; k < 2; ++k)
+            if (hipMemcpy(host + (3 * NB + k) * n, ds[k], 4 * n, hipMemcpyDeviceToHost) != hipSuccess) return 1;
+        const void *parts[1] = {host};
+        const size_t bytes[1] = {4 * n * (3 * NB + 2)};
+        if (write_parts(argv[2], "batch.bin", parts, bytes, 1)) return 1;
+        printf("batch frames %d shadow_frames 2\n", NB);
+        free(host);
+        for (int k = 0; k < NB; ++k) (void)hipFree(dv[k]), (void)hipFree(dd[k]), (void)hipFree(dr[k]);
+        for (int k = 0; k < 2; ++k) (void)hipFree(di[k]), (void)hipFree(dn[k]), (void)hipFree(ds[k]);
+    }
 
     /* ---- a second context on the same tree (a frame in flight) traces the same frame ---- */
     vhx_ctx *sh = NULL;

@@ -1,8 +1,10 @@
 """A compiled C consumer of the C ABI (tests/abi_c/consumer.c, gcc -std=c99 against include/*.h, linked to the in-tree
 libvhx.so): the call shape of the reference-side Rust `extern "C"` block. The CPU test builds and
 links it and runs its no-device path; the GPU test feeds it the BASELINE config-2 tree and camera through a file and
-checks what it wrote: the first frame against the committed golden digests (tests/golden/frames.json), the frame after
-its ranged write against the oracle, and the one-rank vhx_mgpu frame against the golden RGBA / depth."""
+checks what it wrote: the first frame against the committed golden digests (tests/golden/frames.json), five frames of
+two back-to-back vhx_trace_primary_batch calls on one context against the same digests and a two-frame
+vhx_trace_shadows_batch against the oracle's shadow pass, the frame after its ranged write against the oracle, and the
+one-rank vhx_mgpu frame against the golden RGBA / depth."""
 import hashlib
 import json
 import os
@@ -74,6 +76,17 @@ def test_c_consumer_frames(tmp_path, oracle):
         part = raw[off:off + n * widths[k]]
         off += n * widths[k]
         assert hashlib.sha256(part.tobytes()).hexdigest() == meta["sha256"][k], f"frame0 {k} differs from golden"
+    # the batches: five frames of two back-to-back vhx_trace_primary_batch calls on one context, then the shadow batch
+    assert "batch_overlap -1" in out and "batch frames 5 shadow_frames 2" in out, out
+    bt = np.fromfile(str(tmp_path / "batch.bin"), np.uint32).reshape(17, n)
+    for k in range(5):
+        for i, f in enumerate(("value", "depth", "rgba")):
+            assert hashlib.sha256(bt[3 * k + i].tobytes()).hexdigest() == meta["sha256"][f], f"batch frame {k} {f}"
+    hits = oracle.trace_primary(flat, cam, 0, 0, W, H, fields=("value", "impact", "normal", "rgba"))
+    sh = oracle.trace_shadows(flat, (float(size),) * 3, hits)["shadowed"]
+    assert sh.sum() > 0
+    for k in range(2):
+        assert np.array_equal(bt[15 + k], sh), f"shadow batch frame {k}"
     # frame 1: the C program cleared the first brick_count // 3 bricks' voxels through vhx_update_range
     clear = int(out.split("cleared_voxels ")[1].split()[0])
     flat.voxels[:clear] = N.VHX_EMPTY

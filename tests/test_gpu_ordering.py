@@ -364,3 +364,65 @@ def test_write_is_not_starved_by_continuous_traces():
             t.close()
     finally:
         owner.close()
+
+
+@pytest.mark.gpu
+def test_depth_prepass_frames_with_concurrent_writes():
+    """a depth-prepass frame traces its half-resolution frame from inside its own trace scope. With
+    writer priority, a write queued between the outer and the inner trace_begin used to wait for the outer trace while
+    the inner one waited for the writer: both threads blocked for good. The inner frame now joins the outer scope;
+    prepass frames on two shared contexts and ranged writes from a third thread must all complete."""
+    import threading
+    import time
+
+    import torch
+    size, W, H = 256, 320, 200
+    base = vhx.FlatTree.build_scene(N.VHX_SCENE_LATTICE_CUBE, size, 4)
+    pal = _pal_edit(base)
+    cam = vhx.glass_camera(size, W, H, target=(size / 2,) * 3)
+    owner = vhx.Raytracer(0)
+    try:
+        owner.upload(base)
+        tracers = [owner.shared(), owner.shared()]
+        for t in tracers:
+            t.set_depth_prepass(True, 0.5)
+        dev = torch.device("cuda", 0)
+        outs = [_frame_out(W * H, dev) for _ in tracers]
+        torch.cuda.synchronize()
+        stop, errors, frames = threading.Event(), [], [0, 0]
+
+        def trace(i):
+            try:
+                while not stop.is_set() and frames[i] < 100000:
+                    tracers[i].trace_primary(cam, out=outs[i])
+                    frames[i] += 1
+            except Exception as e:  # noqa: BLE001
+                errors.append(e)
+
+        ths = [threading.Thread(target=trace, args=(i,), daemon=True) for i in range(2)]
+        for th in ths:
+            th.start()
+        tw = time.perf_counter()
+        while min(frames) < 10 and not errors and time.perf_counter() - tw < 60:
+            time.sleep(0.001)
+        done = []
+
+        def writer():
+            for k in range(40):
+                owner.update_ranges([(N.VHX_BUF_COLOR_PALETTE, 0, pal if k % 2 == 0 else base.color_palette)])
+            done.append(True)
+
+        wt = threading.Thread(target=writer, daemon=True)
+        wt.start()
+        wt.join(timeout=60)
+        stop.set()
+        for th in ths:
+            th.join(timeout=60)
+        assert not errors, errors
+        assert done, "the writes did not complete: deadlock between a prepass frame and a writer"
+        assert not any(th.is_alive() for th in ths), "a prepass tracer never returned: deadlock"
+        torch.cuda.synchronize()
+        for t in tracers:
+            t.close()
+    finally:
+        owner.close()

@@ -283,3 +283,31 @@ def test_incremental_view_set_with_tree_edits():
             s.resize()
         same, _, _ = s.view_set_check()
         assert same, f"move {k}"
+
+
+def test_incremental_view_set_with_edits_inside_the_view():
+    """a move and an edit in the same upload. The move's rebuild runs before the upload applies
+    the queued edit, so an incremental walk would start from masks of the tree before it. Edits inside the current
+    include box that subdivide a node (one voxel of another colour in a filled region) or collapse one (a whole
+    aligned cube overwritten, then simplified) must leave the set equal to a full rebuild's, and the upload
+    converges (nothing pending)."""
+    t = _tree(256, 4)
+    s = vhx.StreamingView(t, None, (128.0, 128.0, 128.0), 48.0)
+    s.upload()
+    for k in range(16):
+        c = (128.0 + 3 * k, 128.0 - 2 * k, 120.0 + 2 * k)
+        s.set_viewport(c, 48.0)
+        p = tuple(int(v) + 4 for v in c)
+        if k % 3 == 0:
+            t.insert(p, vhx.Albedo(200, 10 + k, 30, 255))  # subdivides the leaf around p
+        elif k % 3 == 1:
+            q = tuple((v // 16) * 16 for v in p)
+            t.insert_at_lod(q, 16, vhx.Albedo(40, 50, 60 + k, 255))  # one aligned 16^3 cube, uniform content
+            t.simplify(True)
+        if s.upload()[1]:
+            s.resize()
+        same, _, _ = s.view_set_check()
+        assert same, f"move {k}"
+    stats, _, _ = s.upload_all()
+    assert stats["pending"] == 0
+    assert s.view_set_check()[0]

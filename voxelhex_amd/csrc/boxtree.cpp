@@ -891,12 +891,14 @@ int BoxTree::insert_at_lod_internal(bool overwrite, U3 pos_u32, uint32_t insert_
         node_stack.pop_back();
         bounds_stack.pop_back();
     }
+    ++edit_seq;
     if (track_changes > 0) changes.push_back(Change{node_stack_clone, modified_bottom});  // insert.rs:401-404
     return 0;
 }
 
 bool BoxTree::simplify(size_t key, bool recursive) {  // src/boxtree/update/mod.rs:617-867
     if (!nodes.key_is_valid(key)) return false;
+    ++edit_seq;
     Node &node = nodes.get(key);
     switch (node.content) {
         case Content::Nothing: return true;

@@ -155,6 +155,9 @@ class BoxTree {
     };
     mutable std::deque<Change> changes;
     mutable int track_changes = 0;
+    // bumped by every structural edit (update_at_lod, simplify), tracked or not: a stream's cached view walk is valid
+    // only for the edit_seq it was made on (vhx_stream rebuild)
+    uint64_t edit_seq = 0;
     ObjectPool nodes;
     std::vector<uint32_t> color_palette;
     std::vector<uint32_t> data_palette;

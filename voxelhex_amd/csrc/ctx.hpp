@@ -104,11 +104,16 @@ struct vhx_ctx {
         bool used = false;
     } pinned[2];
     uint32_t pinned_next = 0;
-    // vhx_trace_primary_batch: the batch's cameras and outputs (pinned staging, and their device copy)
-    Pinned batch_pinned;
+    // vhx_trace_primary_batch: the batch's cameras and outputs (a ring of pinned staging slots, and their device
+    // copy). A slot is rewritten only once the copy that read it has run; with VHX_STAGE_SLOTS slots a caller can queue
+    // that many batches on one context before the host waits (the device copy itself is stream-ordered)
+    static constexpr uint32_t VHX_STAGE_SLOTS = 4;
+    Pinned batch_pinned[VHX_STAGE_SLOTS];
+    uint32_t batch_next = 0;
     DevBuf batch_args;
-    // vhx_trace_shadows_batch: the frames' ShD records and hit-value pointers (pinned staging, device copy)
-    Pinned shadow_pinned;
+    // vhx_trace_shadows_batch: the frames' ShD records and hit-value pointers (pinned staging ring, device copy)
+    Pinned shadow_pinned[VHX_STAGE_SLOTS];
+    uint32_t shadow_next = 0;
     DevBuf shadow_args;
     DevBuf upd;
     hipStream_t upd_stream = nullptr;  // the stream of the last scatter (reads upd)
@@ -235,11 +240,15 @@ int trace_begin(vhx_ctx *c);
 int trace_end(vhx_ctx *c);
 // trace_begin .. trace_end (write_begin .. write_end) as a scope: the end runs on every exit once the begin succeeded,
 // so an error return after the first launch still records the trace's use (or the write) for the ordering
+// nested = true: a trace issued from inside an open scope of the same context and thread (the depth prepass's inner
+// frame) joins the enclosing scope instead of opening a second one -- a second trace_begin would wait for a writer
+// queued behind the enclosing trace, which in turn waits for that trace to end (a deadlock)
 struct TraceScope {
     vhx_ctx *c;
     int rc;
     bool open;
-    explicit TraceScope(vhx_ctx *ctx) : c(ctx), rc(trace_begin(ctx)), open(true) {}
+    explicit TraceScope(vhx_ctx *ctx, bool nested = false)
+        : c(ctx), rc(nested ? VHX_OK : trace_begin(ctx)), open(!nested) {}
     int end() {
         if (!open) return VHX_OK;
         open = false;

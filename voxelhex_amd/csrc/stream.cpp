@@ -459,6 +459,7 @@ struct vhx_stream {
         F3 vc{}, center{};  // the clamped and the given centre of the last rebuild
         float dist = 0.f;
         int mip1_internal = -1;  // an Internal node at MIP level 1 exists (explores with B_1): -1 unknown
+        uint64_t edit_seq = 0;   // the tree's edit_seq the walk (and mip1_internal) was made on
     } view_walk;
     uint64_t rebuilds_full = 0, rebuilds_incremental = 0;
     uint64_t dbg_shell = 0, dbg_ins = 0, dbg_era = 0;
@@ -600,6 +601,13 @@ struct vhx_stream {
         }
     }
     void rebuild(F3 center_, float dist) {  // upload_queue.rs:60-142
+        // a walk made on an older tree is no base for an incremental rebuild: collect_frame runs a pending move's
+        // rebuild before handle_tree_updates applies the same upload's queued edits, and the cached masks and levels
+        // describe the tree before them
+        if (view_walk.edit_seq != tree->edit_seq) {
+            view_walk.valid = false;
+            view_walk.mip1_internal = -1;
+        }
         walk_started = false;
         last_cycle_work = UINT64_MAX;
         const float S = (float)tree->boxtree_size;
@@ -662,6 +670,7 @@ struct vhx_stream {
             ++rebuilds_full;
         }
         vw.valid = true;
+        vw.edit_seq = tree->edit_seq;
         vw.path = std::move(path);
         vw.nb = wr.nb;
         vw.mip = wr.mip;

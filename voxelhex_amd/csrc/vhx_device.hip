@@ -1674,7 +1674,10 @@ void vhx_destroy(vhx_ctx *c) {
                       &c->flags, &c->qargs, &c->state, &c->upd, &c->prepass_depth, &c->batch_args, &c->scan_part,
                       &c->shadow_args})
         if (b->ptr) (void)hipFree(b->ptr);
-    for (auto *P : {&c->pinned[0], &c->pinned[1], &c->batch_pinned, &c->shadow_pinned}) {
+    std::vector<vhx_ctx::Pinned *> pins = {&c->pinned[0], &c->pinned[1]};
+    for (auto &P : c->batch_pinned) pins.push_back(&P);
+    for (auto &P : c->shadow_pinned) pins.push_back(&P);
+    for (auto *P : pins) {
         if (P->ptr) (void)hipHostFree(P->ptr);
         if (P->done) (void)hipEventDestroy(P->done);
     }
@@ -2264,7 +2267,9 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
                                                            : (uint64_t)my_tiles * T * T;
     VHX_HIP(c, hipSetDevice(c->device));
     VHX_STREAM(c);
-    TraceScope tscope(c);  // after the tree's last write (an update through the owner, on its stream)
+    // after the tree's last write (an update through the owner, on its stream); the prepass's inner frame runs inside
+    // the outer frame's scope
+    TraceScope tscope(c, c->in_prepass);
     int rc = tscope.rc;
     if (rc) return rc;
     HostOut ho;
@@ -2386,6 +2391,24 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
     return finish_out(c, ho);
 }
 
+// The next slot of a context's pinned staging ring, sized for `bytes`: the host waits only if that slot's previous copy
+// (VHX_STAGE_SLOTS batches ago on this context) has not run yet
+static int stage_slot(vhx_ctx *c, vhx_ctx::Pinned *ring, uint32_t &next, uint64_t bytes, vhx_ctx::Pinned *&out) {
+    vhx_ctx::Pinned &P = ring[next];
+    next = (next + 1) % vhx_ctx::VHX_STAGE_SLOTS;
+    if (P.used) VHX_HIP(c, hipEventSynchronize(P.done));
+    if (P.bytes < bytes) {
+        if (P.ptr) VHX_HIP(c, hipHostFree(P.ptr));
+        P.ptr = nullptr;
+        P.bytes = 0;
+        VHX_HIP(c, hipHostMalloc(&P.ptr, bytes, hipHostMallocDefault));
+        P.bytes = bytes;
+    }
+    if (!P.done) VHX_HIP(c, hipEventCreateWithFlags(&P.done, hipEventDisableTiming));
+    out = &P;
+    return VHX_OK;
+}
+
 int vhx_trace_primary_batch(vhx_ctx *c, const vhx_camera *cams, uint32_t n, const vhx_hits *outs) {
     if (!c || !cams || !outs || n == 0) return VHX_E_INVALID_ARG;
     if (!c->tree->uploaded) return fail(c, VHX_E_STATE, "vhx_trace_primary_batch before vhx_upload_tree");
@@ -2398,6 +2421,26 @@ int vhx_trace_primary_batch(vhx_ctx *c, const vhx_camera *cams, uint32_t n, cons
             return fail(c, VHX_E_INVALID_ARG, "vhx_trace_primary_batch: byte counting is a vhx_trace_primary option");
     }
     const uint64_t npix = (uint64_t)W * H, nout = npix * n;
+    // the frames are traced concurrently: two frames writing one output range would leave a result that depends on the
+    // schedule instead of equalling n vhx_trace_primary calls
+    {
+        struct R {
+            const char *p;
+            uint64_t bytes;
+        };
+        std::vector<R> rs;
+        for (uint32_t k = 0; k < n; ++k) {
+            const vhx_hits &o = outs[k];
+            const void *f[7] = {o.value, o.cell, o.rgba, o.depth, o.voxel, o.impact, o.normal};
+            const uint64_t w[7] = {1, 1, 1, 1, 3, 3, 3};
+            for (int j = 0; j < 7; ++j)
+                if (f[j]) rs.push_back({(const char *)f[j], npix * 4 * w[j]});
+        }
+        std::sort(rs.begin(), rs.end(), [](const R &a, const R &b) { return a.p < b.p; });
+        for (size_t i = 1; i < rs.size(); ++i)
+            if (rs[i].p < rs[i - 1].p + rs[i - 1].bytes)
+                return fail(c, VHX_E_INVALID_ARG, "vhx_trace_primary_batch: output arrays overlap each other");
+    }
     const uint32_t bx = (W + 15) / 16, by = (H + 15) / 16;
     const uint64_t nbf = (uint64_t)bx * by, nblocks = nbf * n;
     if (nout > 0x7FFFFFFFull || nblocks > 0x7FFFFFFFull)
@@ -2410,20 +2453,13 @@ int vhx_trace_primary_batch(vhx_ctx *c, const vhx_camera *cams, uint32_t n, cons
     if ((rc = refresh_child_rec(c))) return rc;
     const DevTree t = dev_tree(c);
     if (t.mips) return fail(c, VHX_E_INVALID_ARG, "vhx_trace_primary_batch: not available with node MIPs");
-    // the batch's cameras and outputs: packed in pinned memory, one copy to the device ahead of the launches on the
-    // context's stream (the previous batch's copy out of the same slot has long completed: it was the first operation of
-    // that batch)
+    // the batch's cameras and outputs: packed into the next slot of the context's pinned staging ring, one copy to the
+    // device ahead of the launches on the context's stream (stage_slot: back-to-back batches on one context do not
+    // wait on the host until the ring wraps onto a copy that has not run)
     const uint64_t cam_bytes = ((uint64_t)n * sizeof(CamD) + 255) & ~255ull, args_bytes = cam_bytes + (uint64_t)n * sizeof(OutD);
-    vhx_ctx::Pinned &P = c->batch_pinned;
-    if (P.used) VHX_HIP(c, hipEventSynchronize(P.done));
-    if (P.bytes < args_bytes) {
-        if (P.ptr) VHX_HIP(c, hipHostFree(P.ptr));
-        P.ptr = nullptr;
-        P.bytes = 0;
-        VHX_HIP(c, hipHostMalloc(&P.ptr, args_bytes, hipHostMallocDefault));
-        P.bytes = args_bytes;
-    }
-    if (!P.done) VHX_HIP(c, hipEventCreateWithFlags(&P.done, hipEventDisableTiming));
+    vhx_ctx::Pinned *PP = nullptr;
+    if ((rc = stage_slot(c, c->batch_pinned, c->batch_next, args_bytes, PP))) return rc;
+    vhx_ctx::Pinned &P = *PP;
     // the device copy is read by this context's earlier batches: a stream change waits for them
     if (c->use_recorded && c->use_stream != c->stream) VHX_HIP(c, hipStreamWaitEvent(c->stream, c->use_ev, 0));
     if ((rc = ensure(c, c->batch_args, args_bytes))) return rc;
@@ -2694,8 +2730,9 @@ int vhx_trace_shadows_batch(vhx_ctx *c, const float light[3], uint32_t nf, uint6
     if (!c || !light || nf == 0 || !frames) return VHX_E_INVALID_ARG;
     if (!c->tree->uploaded) return fail(c, VHX_E_STATE, "vhx_trace_shadows_batch before vhx_upload_tree");
     if (n == 0) return VHX_OK;
+    // tested before the product is formed (a huge n would wrap n * nf)
+    if (n >= 0x7FFFFFFFull / nf) return fail(c, VHX_E_INVALID_ARG, "vhx_trace_shadows_batch: more than 2^31 records");
     const uint64_t ntot = n * nf;
-    if (ntot >= 0x7FFFFFFFull) return fail(c, VHX_E_INVALID_ARG, "vhx_trace_shadows_batch: more than 2^31 records");
     // every frame's outputs are written while every frame's hit records are read: no overlaps anywhere in the batch
     {
         struct R {
@@ -2738,16 +2775,9 @@ int vhx_trace_shadows_batch(vhx_ctx *c, const float light[3], uint32_t nf, uint6
     if ((rc = prepare_passes(c, ntot, nb64, npass, true, nf > 1))) return rc;
     // the frames' ShD records, then their value pointers (FlagOrder::fvals), staged like vhx_trace_primary_batch's
     const uint64_t sh_bytes = ((uint64_t)nf * sizeof(ShD) + 255) & ~255ull, args_bytes = sh_bytes + (uint64_t)nf * 8;
-    vhx_ctx::Pinned &P = c->shadow_pinned;
-    if (P.used) VHX_HIP(c, hipEventSynchronize(P.done));
-    if (P.bytes < args_bytes) {
-        if (P.ptr) VHX_HIP(c, hipHostFree(P.ptr));
-        P.ptr = nullptr;
-        P.bytes = 0;
-        VHX_HIP(c, hipHostMalloc(&P.ptr, args_bytes, hipHostMallocDefault));
-        P.bytes = args_bytes;
-    }
-    if (!P.done) VHX_HIP(c, hipEventCreateWithFlags(&P.done, hipEventDisableTiming));
+    vhx_ctx::Pinned *PP = nullptr;
+    if ((rc = stage_slot(c, c->shadow_pinned, c->shadow_next, args_bytes, PP))) return rc;
+    vhx_ctx::Pinned &P = *PP;
     if (c->use_recorded && c->use_stream != c->stream) VHX_HIP(c, hipStreamWaitEvent(c->stream, c->use_ev, 0));
     if ((rc = ensure(c, c->shadow_args, args_bytes))) return rc;
     ShD *hs = (ShD *)P.ptr;

@@ -381,6 +381,21 @@ class Raytracer:
                 raise ValueError("trace_shadows_batch reads device tensors")
         if shadowed_list is None:
             shadowed_list = [torch.empty(n, dtype=torch.int32, device=h["value"].device) for h in hits_list]
+        if len(shadowed_list) != len(hits_list):
+            raise ValueError("trace_shadows_batch: one shadowed tensor per frame")
+
+        def need(a, words, what):
+            # the library trusts n for every array of every frame: a short tensor would be read or written past its end
+            if a is None or not hasattr(a, "numel") or not a.is_cuda or a.numel() * a.element_size() < 4 * words:
+                raise ValueError(f"trace_shadows_batch: {what} must be a device tensor of at least {4 * words} bytes")
+
+        for k, h in enumerate(hits_list):
+            need(h["value"], n, f"frame {k} value")
+            need(h["impact"], 3 * n, f"frame {k} impact")
+            need(h["normal"], 3 * n, f"frame {k} normal")
+            need(shadowed_list[k], n, f"frame {k} shadowed")
+            if darken and h.get("rgba") is not None:
+                need(h["rgba"], n, f"frame {k} rgba")
         fr = (N.ShadowFrame * len(hits_list))()
         for k, h in enumerate(hits_list):
             rgba = h.get("rgba") if darken else None
