@@ -521,6 +521,8 @@ def hw_queues(frames):
 
 def main():
     args = parse()
+    if args.tune in ("", "-"):
+        args.tune = None  # "-": the library defaults (scripts that loop over specs)
     if "WORLD_SIZE" not in os.environ:
         if args.gpus is not None and args.gpus > 1:
             sys.exit(launch_ranks(args))

@@ -175,7 +175,8 @@ int vhx_set_adaptive_schedule(vhx_ctx *ctx, int on);
 int vhx_get_pass_budgets(const vhx_ctx *ctx, uint32_t *budgets, uint32_t *n, int *schedule);
 /* Scheduling knobs (no reference counterpart; results never depend on them -- experiments and probes): `spec` is
  * "key=value[;key=value...]" with keys budgets (list, fixes the schedule), adaptive (0/1), rpw (list: rays per wave of
- * queue passes 1.., 0 = adaptive), tw, xcdg, resume (0/1), save_from, qblock (64/128/256), qwaves (fixes the schedule),
+ * queue passes 1.., 0 = adaptive), tw, xcdg, resume (0/1), qstate (0/1: states in queue order), save_from, qblock
+ *  (64/128/256), tlists (0/1: tile sets list pass 0), qwaves (fixes the schedule),
  * qwavesm, qwaves0, qxcd, qxcd_all (0/1), sparse (list, fixes the schedule), qorder ("[m]N[z|r]" or 0), qsort (0 or
  * 256..2048: segment node sort of the queue passes), qsortp (pass mask), qsortb (workgroups). The
  * library reads no environment variable for any of them. Unknown keys or malformed values:
@@ -271,6 +272,13 @@ int vhx_set_node_mips(vhx_ctx *ctx, const uint32_t *node_mips, uint32_t count);
  * and the lanes active in them, as out[2 * (pass * 16 + block)] and out[2 * (pass * 16 + block) + 1], accumulated
  * over every trace since the last reset. */
 int vhx_profile_counters(vhx_ctx *ctx, uint64_t *out, uint32_t n, int reset);
+/* Diagnostics of a VHX_CHAIN build (libvhx_chain.so, scripts/chain_profile.py; a regular build returns VHX_E_STATE):
+ * the primary rays of the n pixels (index y * width + x of `cam`'s frame, host array) each traced alone in a wave of
+ * its own, its dependent chain stamped per node iteration; out (host, n x 64 words): [0] cycles of the traversal,
+ * [1] node-load waits, [2] leaf probes, [3] POP / PUSH bookkeeping, [4] ADVANCE walks, [5] loop overhead, [6] node
+ * iterations, [7] probes, [8] ADVANCE walks, [9] steps, [10] hit value, [16..63] node-load wait histogram in 64-cycle
+ * buckets (the last one open). Shader cycles (s_memtime). */
+int vhx_chain_profile(vhx_ctx *ctx, const vhx_camera *cam, const uint32_t *pixels, uint32_t n, uint64_t *out);
 /* Traces n explicit rays; rays = 6 f32 per ray (origin xyz, direction xyz), host or device per on_device. */
 int vhx_trace_rays(vhx_ctx *ctx, const float *rays, uint64_t n, const vhx_hits *out, int on_device);
 /* Hard shadows (BASELINE config 5; the reference has no shadow rays — semantics defined in DESIGN.md §9): for

@@ -117,8 +117,8 @@ int64_t wavesim_build(const vhx_tree_desc *t, const vhx_camera *cam, uint32_t W,
 }
 
 /* blocks (as the VHX_PROF build): 0 iteration, 1 leaf target (probe), 2 brick trip, 3 pop, 4 push, 5 walk setup,
- * 6 advance trip, 7 restart, 13 iteration-end bookkeeping, 14 carried walk (design 1) */
-#define NB 16
+ * 6 advance trip, 7 restart, 13 iteration-end bookkeeping, 14 carried walk (design 1), 16 regroup exchange (6, 7) */
+#define NB 17
 #define NP 8 /* passes */
 typedef struct {
     uint64_t waves[NP][NB], lanes[NP][NB];
@@ -299,6 +299,105 @@ static void sim_wave(const cfg_t *c, int p, lane_t *L, int n, uint32_t budget, u
                     done[i] = 1;
                     out[(*nout)++] = L[i];
                 }
+        }
+    }
+}
+
+/* designs 6 / 7 (workgroup regroup): the 4 waves of a workgroup (pass 0: the 4 waves of a 16x16
+ * block; queue passes: 4 consecutive chunks) run each node iteration in lockstep (a barrier per iteration). The node
+ * blocks run per wave as in design 0; the brick walks (design 6), or the brick and the ADVANCE walks (design 7), of
+ * every lane of the 4 waves that needs one are compacted through LDS into ceil(k / 64) full waves (in wave-major lane
+ * order, as a prefix-sum compaction gives them), walked there, and the results handed back: block 16 is that exchange,
+ * charged once per source wave with a walker and once per packed wave (write + read of the walk state and result). */
+static void walk_blocks(const cfg_t *c, int p, int blk, const uint32_t *len, int nk, int packed, stats_t *s) {
+    (void)c;
+    for (int i = 0; i < nk; i += 64) {
+        const int e = nk - i < 64 ? nk - i : 64;
+        uint32_t mx = 0;
+        for (int j = i; j < i + e; ++j)
+            if (len[j] > mx) mx = len[j];
+        for (uint32_t t = 0; t < mx; ++t) {
+            uint32_t k = 0;
+            for (int j = i; j < i + e; ++j) k += len[j] > t;
+            add(s, p, blk, k);
+        }
+        if (packed) add(s, p, 16, (uint32_t)e);
+    }
+}
+static void sim_group(const cfg_t *c, int p, lane_t *const *Lw, const int *nw, int G, uint32_t budget, uint32_t sparse,
+                      stats_t *s, lane_t *out, uint64_t *nout) {
+    int done[4][64];
+    memset(done, 0, sizeof(done));
+    for (;;) {
+        int any = 0;
+        uint32_t blen[256], alen[256];
+        int nbk = 0, nak = 0;
+        const it_t *rr[4][64];
+        int actv[4][64], nav[4];
+        for (int w = 0; w < G; ++w) {
+            nav[w] = 0;
+            for (int i = 0; i < nw[w]; ++i)
+                if (!done[w][i]) actv[w][nav[w]++] = i;
+            if (!nav[w]) continue;
+            any = 1;
+            const int na = nav[w];
+            add(s, p, 13, na);
+            add(s, p, 0, na);
+            uint32_t npr = 0, wb = 0;
+            for (int a = 0; a < na; ++a) {
+                const lane_t *l = &Lw[w][actv[w][a]];
+                rr[w][a] = &g_its[g_off[l->ray] + l->cur];
+                npr += rr[w][a]->probe;
+                if (rr[w][a]->nb) {
+                    blen[nbk++] = rr[w][a]->nb;
+                    ++wb;
+                }
+            }
+            if (npr) add(s, p, 1, npr);
+            if (wb && c->design >= 6) add(s, p, 16, wb);  /* the source wave's exchange */
+            if (c->design < 6) walk_blocks(c, p, 2, blen + nbk - wb, (int)wb, 0, s);
+        }
+        if (!any) break;
+        if (c->design >= 6) walk_blocks(c, p, 2, blen, nbk, 1, s);
+        for (int w = 0; w < G; ++w) {
+            const int na = nav[w];
+            if (!na) continue;
+            uint32_t npop = 0, npush = 0, nws = 0, nres = 0, wa = 0;
+            for (int a = 0; a < na; ++a) {
+                const it_t *r = rr[w][a];
+                npop += r->pop, npush += r->push, nres += r->restart;
+                const uint32_t k = r->pop ? 1u : r->na;
+                if (r->pop || r->na) ++nws;
+                if (k) {
+                    alen[nak++] = k;
+                    ++wa;
+                }
+            }
+            if (npop) add(s, p, 3, npop);
+            if (npush) add(s, p, 4, npush);
+            if (nws) add(s, p, 5, nws);
+            if (wa && c->design >= 7) add(s, p, 16, wa);
+            if (c->design < 7) walk_blocks(c, p, 6, alen + nak - wa, (int)wa, 0, s);
+            if (nres) add(s, p, 7, nres);
+        }
+        if (c->design >= 7) walk_blocks(c, p, 6, alen, nak, 1, s);
+        for (int w = 0; w < G; ++w) {
+            uint32_t still = 0;
+            for (int a = 0; a < nav[w]; ++a) {
+                const int i = actv[w][a];
+                lane_t *l = &Lw[w][i];
+                const it_t *r = rr[w][a];
+                l->iters += r->nb + r->na;
+                l->cur += 1;
+                const uint32_t nit = (uint32_t)(g_off[l->ray + 1] - g_off[l->ray]);
+                if (l->cur >= nit) { done[w][i] = 1; continue; }
+                l->iters += 1;
+                if (l->iters > budget) { done[w][i] = 1; out[(*nout)++] = *l; continue; }
+                ++still;
+            }
+            if (sparse && still && still < sparse)
+                for (int i = 0; i < nw[w]; ++i)
+                    if (!done[w][i]) { done[w][i] = 1; out[(*nout)++] = Lw[w][i]; }
         }
     }
 }
@@ -587,6 +686,25 @@ int wavesim_run(const cfg_t *c, stats_t *s) {
                     ++np;
                 }
         sim_refill_pass(c, 0, q2, np, b0, c->nwaves, c->cap, s, q, &nq);
+    } else if (c->design >= 6) {
+        for (uint32_t b = 0; b < bx * by; ++b) {
+            lane_t L4[4][64];
+            lane_t *Lw[4] = {L4[0], L4[1], L4[2], L4[3]};
+            int nw[4] = {0, 0, 0, 0};
+            for (uint32_t w = 0; w < 4; ++w) {
+                for (uint32_t k = 0; k < 64; ++k) {
+                    const uint32_t x = (b % bx) * 16 + (w & 1) * 8 + (k & 7), y = (b / bx) * 16 + (w >> 1) * 8 + (k >> 3);
+                    if (x >= W || y >= H) continue;
+                    const uint32_t ray = y * W + x;
+                    s->rays_in[0] += 1;
+                    if (g_off[ray + 1] == g_off[ray]) continue;
+                    lane_t *l = &L4[w][nw[w]++];
+                    l->ray = ray, l->cur = 0, l->iters = 1, l->carry = 0;
+                }
+                s->waves_pass[0] += 1;
+            }
+            sim_group(c, 0, Lw, nw, 4, b0, c->npass > 1 ? c->sparse0 : 0, s, q, &nq);
+        }
     } else
     for (uint32_t b = 0; b < bx * by; ++b)
         for (uint32_t w = 0; w < 4; ++w) {
@@ -621,7 +739,7 @@ int wavesim_run(const cfg_t *c, stats_t *s) {
         const int slot = (int)p;
         const uint32_t rpw = c->rpw[p] ? c->rpw[p] : 64u;
         uint64_t nq2 = 0;
-        if (c->design >= 3) {
+        if (c->design >= 3 && c->design < 6) {
             sim_refill_pass(c, slot, q, nq, budget, c->nwaves, c->cap, s, q2, &nq2);
             lane_t *t = q;
             q = q2;
@@ -630,6 +748,25 @@ int wavesim_run(const cfg_t *c, stats_t *s) {
             continue;
         }
         s->rays_in[slot] += nq;
+        if (c->design >= 6) {
+            for (uint64_t i = 0; i < nq; i += 4 * (uint64_t)rpw) {
+                lane_t *Lw[4];
+                int nw[4] = {0, 0, 0, 0}, G = 0;
+                for (int w = 0; w < 4 && i + (uint64_t)w * rpw < nq; ++w) {
+                    const uint64_t o = i + (uint64_t)w * rpw;
+                    Lw[w] = q + o;
+                    nw[w] = (int)(nq - o < rpw ? nq - o : rpw);
+                    s->waves_pass[slot] += 1;
+                    G = w + 1;
+                }
+                sim_group(c, slot, Lw, nw, G, budget, 0, s, q2, &nq2);
+            }
+            lane_t *t = q;
+            q = q2;
+            q2 = t;
+            nq = nq2;
+            continue;
+        }
         for (uint64_t i = 0; i < nq; i += rpw) {
             const int nl = (int)(nq - i < rpw ? nq - i : rpw);
             s->waves_pass[slot] += 1;

@@ -16,17 +16,20 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 sys.path.insert(0, ROOT)
 LIB = os.path.join(ROOT, "scripts", "sim", "_build", "libwavesim.so")
 BLOCKS = {13: "loop trip", 0: "iteration top", 1: "probe", 2: "brick trip", 8: "post", 3: "pop", 4: "push",
-          5: "walk setup", 6: "advance trip", 7: "restart", 9: "refill", 14: "refill check", 15: "walk switch"}
+          5: "walk setup", 6: "advance trip", 7: "restart", 9: "refill", 14: "refill check", 15: "walk switch",
+          16: "regroup exchange"}
 # VALU instructions per wave execution of each block (ISA of the bd-4 queue kernel, round 3)
-COSTS = {13: 15, 0: 25, 1: 55, 2: 28, 8: 15, 3: 30, 4: 40, 5: 20, 6: 28, 7: 55, 9: 300, 14: 4, 15: 12}
+COSTS = {13: 15, 0: 25, 1: 55, 2: 28, 8: 15, 3: 30, 4: 40, 5: 20, 6: 28, 7: 55, 9: 300, 14: 4, 15: 12,
+         16: int(os.environ.get("REGROUP_COST", "30"))}  # 16: LDS write + read of a walk's state and result, per wave
 RAY_SETUP = 250  # ray generation + begin (divisions, square roots) per pass-0 wave
 
 
 NP = 8
+NB = 17  # blocks (wavesim.c)
 
 
 class Stats(ctypes.Structure):
-    _fields_ = [("waves", (ctypes.c_uint64 * 16) * NP), ("lanes", (ctypes.c_uint64 * 16) * NP),
+    _fields_ = [("waves", (ctypes.c_uint64 * NB) * NP), ("lanes", (ctypes.c_uint64 * NB) * NP),
                 ("rays_in", ctypes.c_uint64 * NP), ("waves_pass", ctypes.c_uint64 * NP),
                 ("max_wave", ctypes.c_double * NP)]
 
@@ -34,7 +37,7 @@ class Stats(ctypes.Structure):
 class Cfg(ctypes.Structure):
     _fields_ = [("budgets", ctypes.c_uint32 * NP), ("npass", ctypes.c_uint32), ("sparse0", ctypes.c_uint32),
                 ("design", ctypes.c_uint32), ("cap", ctypes.c_uint32), ("rpw", ctypes.c_uint32 * NP),
-                ("cost", ctypes.c_uint32 * 16), ("order", ctypes.c_uint32), ("nwaves", ctypes.c_uint32), ("seg", ctypes.c_uint32)]
+                ("cost", ctypes.c_uint32 * NB), ("order", ctypes.c_uint32), ("nwaves", ctypes.c_uint32), ("seg", ctypes.c_uint32)]
 
 
 def build():

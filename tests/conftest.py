@@ -7,9 +7,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
-# Frames in flight (tests/test_gpu_inflight.py, the bench's configuration): every context stream needs a hardware queue
-# of its own, and HIP reads GPU_MAX_HW_QUEUES once, when it initialises -- so it is raised here, before any test
-# imports torch or loads libvhx (the same rule as bench.py's hw_queues: F + 4 for the bench's F = 16)
+# Per-frame contexts in flight (tests/test_gpu_inflight.py and the ordering tests: up to 16 shared contexts, each on its
+# own stream -- the shape of bench.py --batch 0, which the N > 1 ranks and --shadows run) need a hardware queue per
+# stream, and HIP reads GPU_MAX_HW_QUEUES once, when it initialises -- so it is raised here, before any test imports
+# torch or loads libvhx (bench.py's hw_queues rule, F + 4). The N = 1 default bench (batches of 7 on 3 contexts) needs
+# no raise; the batch tests pass either way.
 try:
     if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 20:
         os.environ["GPU_MAX_HW_QUEUES"] = "20"

@@ -17,6 +17,8 @@ LIB = os.path.join(LIBDIR, "libvhx.so")
 # diagnostic variant builds (never loaded by the package unless VHX_LIB names them): the negative control of the tree-write
 # ordering (tests/test_gpu_tuning.py), with libvhx's waits compiled out
 UNORDERED_LIB = os.path.join(LIBDIR, "libvhx_unordered.so")
+# ... and the chain-stamp build of scripts/chain_profile.py (VHX_CHAIN: vhx_chain_profile)
+CHAIN_LIB = os.path.join(LIBDIR, "libvhx_chain.so")
 ARCH = os.environ.get("VHX_OFFLOAD_ARCH", "gfx950")
 
 HOST_SRCS = ["boxtree.cpp", "flatten.cpp", "vox.cpp", "stream.cpp"]
@@ -86,6 +88,8 @@ def build_variants(verbose=False, force=False):
     """The diagnostic variant libraries the GPU tests load in child processes (built here, in-tree, so they travel)."""
     build(verbose=verbose, force=force, lib=UNORDERED_LIB, build_dir=os.path.join(ROOT, "build", "vhx_unordered"),
           defines=("VHX_UNORDERED_WRITES=1",))
+    build(verbose=verbose, force=force, lib=CHAIN_LIB, build_dir=os.path.join(ROOT, "build", "vhx_chain"),
+          defines=("VHX_CHAIN=1",))
 
 
 if __name__ == "__main__":

@@ -94,7 +94,8 @@ struct vhx_ctx {
     DevBuf qargs;     // QueueArgs of the queue passes: slot 0 primary rays / ray batches, slot 1 shadow rays
     std::vector<uint8_t> qargs_host[2];  // the QueueArgs last written to each slot (skips the upload when unchanged)
     void *qargs_host_ptr[2] = {nullptr, nullptr};  // qargs.ptr they were written to
-    DevBuf state;     // saved traversal state per output index (64 B) of rays abandoned at a budget
+    DevBuf state;     // saved traversal state (64 B) of rays abandoned at a budget: per output index, or per list slot
+    DevBuf stateq;    // queue-state mode: the states moved into the next pass's queue order by the compaction
     // ranged writes (vhx_update_ranges): two pinned host staging slots, alternating, each reusable once the
     // host-to-device copy that read it has completed (event), and the device staging buffer the scatter kernel reads
     struct Pinned {
@@ -159,6 +160,14 @@ struct vhx_ctx {
     uint32_t scan_multi = 8;       // chunk scans of more segments (SCAN_SEG counts) run on one workgroup per segment
     bool p0lists = true;           // pass 0 lists its abandoned rays in the queue order (ListOrder; tune "p0lists")
     bool resume = true;            // abandoned rays continue from saved state (tune "resume=0": re-traced from scratch)
+    // queue-state mode (tune "qstate=0" turns it off): where a pass lists its abandoned rays per wave or chunk (the
+    // listed pass 0 of the frames-in-flight and batch schedules, every queue pass), it saves their states at their list
+    // slots, the compaction moves them into the next queue's order, and the next pass reads a ray's state at its queue
+    // position -- coalesced, and in the same load round as the ray's output index instead of after it
+    bool qstate = true;
+    // a tile set (VHX_LAYOUT_TILES) under the frames-in-flight schedule: pass 0 lists its rays (ListOrder::tl; tune
+    // "tlists=0" falls back to flags compacted in output-index order)
+    bool tile_lists = true;
     // passes before save_from keep no state: the rays they abandon are traced again from scratch by pass save_from,
     // which saves (tune "save_from"; 0 = every budgeted pass saves)
     uint32_t save_from = 0;

@@ -75,11 +75,40 @@ struct DevTree {
     uint32_t occ_words;  // max(1, bd^3/64)
 };
 
+// VHX_CHAIN (diagnostic builds only, libvhx_chain.so, scripts/chain_profile.py): the dependent chain of one ray traced
+// alone in its wave, broken down per node iteration by s_memtime stamps (MI355X_MICROARCH.md: tick = shader cycle) --
+// the wait for the iteration's node loads (header + child record, issued together), the leaf probe (brick walk), the
+// POP / PUSH bookkeeping, the ADVANCE walk (or POP's step), and the loop overhead between iterations -- with a
+// histogram of the node-load waits in 64-cycle buckets (the cache level that served them). vhx_chain_profile.
+#ifndef VHX_CHAIN
+#define VHX_CHAIN 0
+#endif
+#define VHX_CHAIN_HIST 48u
+struct ChainAcc {
+    unsigned long long load, probe, move, adv, other, last;
+    uint32_t nload, nprobe, nadv, npad;
+    uint32_t hist[VHX_CHAIN_HIST];
+};
+#if VHX_CHAIN
+// one stamp, the wait for its own result inside the statement (the guide's recipe); the scheduling barriers keep the
+// traversal's instructions on their side of it
+__device__ __forceinline__ unsigned long long chain_stamp() {
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#endif
+
 struct HitOut {
     uint32_t value, cell, vx, vy, vz, bytes;
     uint32_t iters;  // loop steps of the whole traversal at its end (0 for a ray that misses the root cube)
     float ix, iy, iz, nx, ny, nz;
     bool hit;
+#if VHX_CHAIN
+    ChainAcc chain;
+#endif
 };
 
 struct F3d {
@@ -479,6 +508,8 @@ struct Trav {
     template <bool START = false>
     __device__ __forceinline__ bool begin(const DevTree &t, F3d o, F3d d, HitOut &h, const uint4 *sbase, uint32_t sidx,
                                           bool resume, float start = 0.0f) {
+        // sbase + 4 * sidx: the resumed ray's saved state (by output index, or by queue position in the queue-state
+        // mode, where the compaction moved every abandoned ray's state into the next pass's queue order)
         h.hit = false;
         ray_setup(r, o, d);
         {
@@ -545,6 +576,10 @@ struct Trav {
         uint4 lh;
         uint32_t slot;
         uint64_t cocc = 0;
+#if VHX_CHAIN
+        const unsigned long long tA = chain_stamp();
+        if (h.chain.last) h.chain.other += tA - h.chain.last;
+#endif
         if (Brick<BD>::WORDS == 1) {
             lh = t.hdr[node];
             const uint4 cr = t.child_rec[(uint64_t)node * 64u + (target & 63u)];
@@ -558,6 +593,13 @@ struct Trav {
         // here instead of next to its use after the probe, where its latency was exposed)
         uint64_t omask = occ_tab[(target & 63u) * 8u + dir_idx];
         asm volatile("" : "+v"(omask));
+#if VHX_CHAIN
+        asm volatile("" ::"v"(lh.x), "v"(lh.y), "v"(lh.z), "v"(slot), "v"((uint32_t)cocc));  // the loads have landed
+        const unsigned long long tB = chain_stamp();
+        h.chain.load += tB - tA;
+        h.chain.nload += 1;
+        h.chain.hist[min((uint32_t)((tB - tA) >> 6), VHX_CHAIN_HIST - 1u)] += 1;
+#endif
         const uint64_t occ = ((uint64_t)lh.y << 32) | (uint64_t)lh.x;
         const uint32_t ntype = lh.z;
         if (COUNT) h.bytes += 12;
@@ -574,7 +616,15 @@ struct Trav {
             CubeD bb = uniform ? cur : tb;
             if (!uniform && tbok == 0u) bb = child_bounds(cur, target);
             ex = probe_brick<COUNT, BD>(t, r, p, hdesc, cocc, bb, h, iters, hflat, pp) ? 1u : 0u;
+#if VHX_CHAIN
+            h.chain.nprobe += 1;
+#endif
         }
+#if VHX_CHAIN
+        const unsigned long long tP = chain_stamp();
+        h.chain.probe += tP - tB;
+        unsigned long long tQ = tP;
+#endif
         // MIP stand-in (viewport_render.wgsl:438-454, probe_MIP 328-364): the target sectant is occupied but its child
         // entry is absent (a view that does not hold it). The node's MIP brick is traced over the node's cube from a
         // copy of the ray point; a hit ends the ray, a miss ADVANCEs past the sectant instead of pushing into the
@@ -647,8 +697,15 @@ struct Trav {
                 tbok = 1u;
                 ex = slot >= t.node_count ? 2u : 0u;  // the reference would panic on an invalid key: a miss here
             }
+#if VHX_CHAIN
+            tQ = chain_stamp();
+            h.chain.move += tQ - tP;
+#endif
             if (!push) {
                 VHX_PROF_BLOCK(pp, 5);
+#if VHX_CHAIN
+                h.chain.nadv += 1;
+#endif
                 // ADVANCE (cpu.rs:416-437), or POP's single step: at most 9 steps across the node, the pass budget
                 // is checked after it. Same form as the brick walk (exit planes, direction-normalised sectant
                 // coordinates); the exit-plane difference equals the reference's dda_step_to_next_sibling for a point
@@ -720,10 +777,22 @@ struct Trav {
             // not be resumed for one more iteration (its probe could hit; tests/test_gpu_parity.py, degenerate rays)
             if (ex == 0u && ++iters > budget) ex = budget >= VHX_MAX_ITERS || iters > VHX_MAX_ITERS ? 2u : 3u;
         }
+#if VHX_CHAIN
+        const unsigned long long tR = chain_stamp();
+        h.chain.adv += tR - tQ;
+        h.chain.last = tR;
+#endif
     }
 
-    __device__ __forceinline__ bool end(const DevTree &t, HitOut &h, uint4 *sbase, uint32_t sidx) {
+    __device__ __forceinline__ bool end(const DevTree &t, HitOut &h, uint4 *sbase, uint32_t sidx, bool slots = false) {
         h.iters = iters;
+        // slots (queue-state mode): sidx is the first slot of this wave's chunk list, and the wave's abandoned rays take
+        // consecutive slots in lane order -- the positions its chunk list gives them (wave_append, the queue pass's
+        // chunk append), so the compaction can move the states along with the list
+        if (slots) {
+            const uint64_t m = __ballot(ex == 3u);
+            sidx += (uint32_t)__popcll(m & ((1ull << (threadIdx.x & 63u)) - 1ull));
+        }
         // an abandoned ray's state is the loop state at its exit (saved here, outside the hot loop)
         if (ex == 3u && sbase) save_state(sbase + 4ull * sidx, p, iters, cur, tb, target, count, node, s1, s2, s3);
         if (ex == 1u) {  // the loop left on the hit: node, cur, target and p are those of the probe
@@ -741,14 +810,17 @@ struct Trav {
 // sparse (a budgeted pass with saved state): once fewer than `sparse` lanes of the wave still trace, they are abandoned
 // like rays over the budget (their state saved, the next pass resumes them packed into full waves) instead of keeping
 // the wave's issue slots for a few lanes. 0 = off. The result is the same either way (the traversal is deterministic).
+// rbase (queue-state mode): a resumed ray's state is read at rbase + 4 * ridx and an abandoned ray's is saved at
+// sbase + 4 * (sidx + its rank among the wave's abandoned rays) (Trav::end); without it both use sbase + 4 * sidx.
 template <bool COUNT, int BD, bool START = false, bool MIP = false>
 __device__ __forceinline__ bool get_by_ray(const DevTree &t, const uint64_t *occ_tab, F3d o, F3d d, HitOut &h,
                                            uint32_t budget, uint4 *sbase = nullptr, uint32_t sidx = 0,
-                                           bool resume = false, float start = 0.0f, uint32_t sparse = 0) {
+                                           bool resume = false, float start = 0.0f, uint32_t sparse = 0,
+                                           const uint4 *rbase = nullptr, uint32_t ridx = 0, bool slots = false) {
     Trav<COUNT, BD, MIP> tr;
     VHX_PROF_BLOCK(pass_of_budget(budget), 10);
     h.iters = 0;
-    if (!tr.template begin<START>(t, o, d, h, sbase, sidx, resume, start)) return true;
+    if (!tr.template begin<START>(t, o, d, h, rbase ? rbase : sbase, rbase ? ridx : sidx, resume, start)) return true;
     VHX_PROF_BLOCK(pass_of_budget(budget), 11);
     for (;;) {
         VHX_PROF_BLOCK(pass_of_budget(budget), 0);
@@ -760,7 +832,7 @@ __device__ __forceinline__ bool get_by_ray(const DevTree &t, const uint64_t *occ
         }
     }
     VHX_PROF_BLOCK(pass_of_budget(budget), 12);
-    return tr.end(t, h, sbase, sidx);
+    return tr.end(t, h, sbase, sidx, slots);
 }
 
 }  // namespace vhx

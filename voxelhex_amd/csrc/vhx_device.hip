@@ -263,7 +263,10 @@ struct PassQ {
     uint32_t *tmp;     // chunk-local lists of abandoned rays (null on the final pass)
     uint32_t *counts;  // per chunk
     uint8_t *flags;    // primary pass 0: abandoned flag per output index (every entry written, no clearing needed)
-    uint4 *state;      // per output index, 4 x uint4: saved traversal state of an abandoned ray (null: re-trace)
+    uint4 *state;      // per output index, 4 x uint4: saved traversal state of an abandoned ray (null: re-trace); in the
+                       // queue-state mode per slot of this pass's chunk lists instead
+    const uint4 *sin;  // queue-state mode: the input rays' states in queue order (k_gather_chunks moved them there)
+    uint32_t qmode;    // 1: queue-state mode (states saved by list slot, resumed by queue position), 0: by output index
     uint32_t xcd_group;  // pass 0: XCD-aware block runs (xcd_block), 0 = dispatch order
     uint32_t qxcd;       // queue passes: runs of this many chunks dealt over the 8 XCDs, one counter each (0 = off)
     uint32_t sparse;     // budgeted passes with saved state: abandon a wave's rays once fewer lanes trace (0 = off)
@@ -556,12 +559,16 @@ __global__ void __launch_bounds__(256) k_emit_flags(const void *__restrict__ src
         }
 }
 
-// One wave per chunk: copies the chunk's list to the queue at its offset.
+// One wave per chunk: copies the chunk's list to the queue at its offset; in the queue-state mode (st_q) the listed
+// rays' saved states too, from their list slots to their queue positions (64 B each, coalesced both ways), so that the
+// next pass reads a ray's state at its queue position, in the same load round as its output index.
 __global__ void __launch_bounds__(256) k_gather_chunks(const uint32_t *__restrict__ tmp, uint32_t stride,
                                                        const uint32_t *__restrict__ counts,
                                                        const uint32_t *__restrict__ offsets, uint32_t nchunks_host,
                                                        const uint32_t *n_in, uint32_t per_chunk, uint32_t tw,
-                                                       uint32_t *__restrict__ out) {
+                                                       uint32_t *__restrict__ out,
+                                                       const uint4 *__restrict__ st_slot = nullptr,
+                                                       uint4 *__restrict__ st_q = nullptr) {
     const uint32_t pc = n_in ? pass_rpw(per_chunk, tw, *n_in) : per_chunk;
     const uint32_t nchunks = n_in ? (*n_in + pc - 1) / pc : nchunks_host;
     if (n_in) stride = pc;  // a queue pass lists its chunk c at tmp[c * rays per wave]
@@ -570,6 +577,16 @@ __global__ void __launch_bounds__(256) k_gather_chunks(const uint32_t *__restric
     for (uint32_t c = blockIdx.x * 4u + (threadIdx.x >> 6); c < nchunks; c += waves) {
         const uint32_t n = counts[c], o = offsets[c];
         for (uint32_t k = lane; k < n; k += 64u) out[o + k] = tmp[(uint64_t)c * stride + k];
+        if (st_q)
+            for (uint32_t k = lane; k < n; k += 64u) {
+                const uint4 *src = st_slot + 4ull * ((uint64_t)c * stride + k);
+                uint4 *dst = st_q + 4ull * ((uint64_t)o + k);
+                const uint4 a = src[0], b = src[1], e = src[2], f = src[3];
+                dst[0] = a;
+                dst[1] = b;
+                dst[2] = e;
+                dst[3] = f;
+            }
     }
 }
 
@@ -730,6 +747,10 @@ __device__ __forceinline__ float prepass_start(const FastD &f, uint32_t px, uint
 // without a flag per pixel and the compaction kernels over every pixel. A wave holds the same 64 pixels either way.
 struct ListOrder {
     uint32_t tx, tbl;
+    // tl = 1: the tile layout (a rank's tile set, vhx_mgpu) lists its abandoned rays too, in its own block order --
+    // tile by tile, 16x16 blocks row-major inside a tile, a block's four 8x8 waves, each wave's 64 pixels row-major:
+    // the queue order of its flags (output-index order) up to the order of the waves inside a 16x16 block
+    uint32_t tl;
 };
 __device__ __forceinline__ void list_block(const ListOrder &lo, uint32_t b, uint32_t &bx, uint32_t &by) {
     const uint32_t tb = b >> (2u * lo.tbl), m = b & ((1u << (2u * lo.tbl)) - 1u);
@@ -794,8 +815,10 @@ __global__ void __launch_bounds__(256) k_trace_primary(DevTree t, CamD cam, OutD
         } else {
             primary_ray(cam, px, py, o, d);
             const float start = FAST ? prepass_start(fast, px, py) : 0.0f;
-            done = get_by_ray<COUNT, BD, FAST, MIP>(t, occ_tab, o, d, h, q.budget, q.state, (uint32_t)idx, false,
-                                                    start, q.sparse);
+            // queue-state mode (listed pass 0 only): this wave's abandoned rays take the slots of its list
+            done = get_by_ray<COUNT, BD, FAST, MIP>(t, occ_tab, o, d, h, q.budget, q.state,
+                                                    q.qmode ? (bid * 4u + wave) * 64u : (uint32_t)idx, false, start,
+                                                    q.sparse, nullptr, 0, q.qmode != 0);
         }
         if (done)
             store(t, out, idx, o, h);
@@ -807,7 +830,7 @@ __global__ void __launch_bounds__(256) k_trace_primary(DevTree t, CamD cam, OutD
     // frame (a lane past the frame edge has no entry of its own: its idx aliases the next row or runs past the end)
     if (q.flags && (layout == VHX_LAYOUT_FRAMEBUFFER ? valid : (lx < T && ly < T)))
         q.flags[idx] = done ? 0 : 1;
-    if (lo.tx && q.tmp) wave_append(!done, (uint32_t)idx, q.tmp, q.counts, bid * 4u + wave);
+    if ((lo.tx || lo.tl) && q.tmp) wave_append(!done, (uint32_t)idx, q.tmp, q.counts, bid * 4u + wave);
 }
 
 // Pass 0 of a batch of frames (vhx_trace_primary_batch): frame f's 16x16 pixel blocks are blocks [f * nblocks_frame,
@@ -850,8 +873,9 @@ __global__ void __launch_bounds__(256) k_trace_primary_batch(DevTree t, const Ca
             h.iters = 0;
         } else {
             primary_ray(cam, px, py, o, d);
-            done = get_by_ray<false, BD>(t, occ_tab, o, d, h, q.budget, q.state, (uint32_t)idx, false, 0.0f,
-                                         q.sparse);
+            done = get_by_ray<false, BD>(t, occ_tab, o, d, h, q.budget, q.state,
+                                         q.qmode ? (bid * 4u + wave) * 64u : (uint32_t)idx, false, 0.0f, q.sparse,
+                                         nullptr, 0, q.qmode != 0);
         }
         if (done) store(t, outs[f], local, o, h);
         if (q.flags) q.flags[idx] = done ? 0 : 1;
@@ -881,6 +905,37 @@ __global__ void __launch_bounds__(256) k_trace_rays(DevTree t, const float *__re
     if (q.tmp) block_append(!done, (uint32_t)i, q.tmp, q.counts, blockIdx.x);
 }
 
+
+#if VHX_CHAIN
+// One ray per wave (lane 0; a workgroup of one wave per ray), traced whole with the chain stamps (trace.hpp,
+// VHX_CHAIN): per ray VHX_CHAIN_WORDS words -- [0] cycles of the traversal, [1] node-load waits, [2] probes, [3] POP /
+// PUSH bookkeeping, [4] ADVANCE walks, [5] loop overhead, [6] node iterations, [7] probes, [8] ADVANCE walks,
+// [9] steps, [10] hit value, [16..16+VHX_CHAIN_HIST) node-load wait histogram (64-cycle buckets)
+#define VHX_CHAIN_WORDS 64u
+template <int BD>
+__global__ void __launch_bounds__(64) k_chain(DevTree t, CamD cam, const uint32_t *__restrict__ pix, uint32_t n,
+                                              unsigned long long *__restrict__ out) {
+    __shared__ uint64_t occ_tab[OCC_TAB_WORDS];
+    fill_occ_tab(occ_tab);
+    __syncthreads();
+    if (threadIdx.x != 0 || blockIdx.x >= n) return;
+    const uint32_t idx = pix[blockIdx.x], py = idx / cam.width, px = idx - py * cam.width;
+    F3d o, d;
+    primary_ray(cam, px, py, o, d);
+    HitOut h;
+    h.bytes = 0;
+    h.chain = ChainAcc{};
+    const unsigned long long t0 = chain_stamp();
+    get_by_ray<false, BD>(t, occ_tab, o, d, h, VHX_MAX_ITERS);
+    const unsigned long long t1 = chain_stamp();
+    unsigned long long *w = out + (uint64_t)blockIdx.x * VHX_CHAIN_WORDS;
+    const unsigned long long v[11] = {t1 - t0,        h.chain.load,   h.chain.probe, h.chain.move,
+                                      h.chain.adv,    h.chain.other,  h.chain.nload, h.chain.nprobe,
+                                      h.chain.nadv,   h.iters,        h.hit ? h.value : VHX_EMPTY};
+    for (uint32_t k = 0; k < 11u; ++k) w[k] = v[k];
+    for (uint32_t k = 0; k < VHX_CHAIN_HIST; ++k) w[16 + k] = h.chain.hist[k];
+}
+#endif
 
 // Queue pass: each wave takes 64 consecutive queue entries at a time from a shared counter until the queue written
 // by the previous pass is drained (its length is read on the device; the host never synchronises between passes).
@@ -958,8 +1013,11 @@ __global__ void __launch_bounds__(256) VHX_QUEUE_ATTR k_trace_queue(DevTree t, c
             ray_of(a->cam, a->src, idx, o, d);
             HitOut h;
             h.bytes = COUNT && q.resume ? a->out.bytes[idx] : 0u;
-            const bool fin = get_by_ray<COUNT, BD, false, MIP>(t, occ_tab, o, d, h, q.budget, q.state, idx,
-                                                               q.resume != 0, 0.0f, q.sparse);
+            // queue-state mode: resumed from queue position i, abandoned into this chunk's list slots (base = chunk *
+            // rays per wave, the chunk's list position)
+            const bool fin = get_by_ray<COUNT, BD, false, MIP>(
+                t, occ_tab, o, d, h, q.budget, q.state, q.qmode ? base : idx, q.resume != 0, 0.0f, q.sparse,
+                q.qmode ? q.sin : nullptr, i, q.qmode && q.tmp);
             const QueueArgs *b = qa;
             asm volatile("" : "+s"(b));
             if (!fin) {
@@ -1358,7 +1416,8 @@ static int prepare_passes(vhx_ctx *c, uint64_t nout, uint64_t nblocks0, uint32_t
     if (!rc) rc = ensure(c, c->offsets, chunks * 4);
     if (!rc) rc = ensure(c, c->scan_part, ((chunks + SCAN_SEG - 1) / SCAN_SEG) * 8);
     if (!rc) rc = ensure(c, c->flags, ((nout + 3) & ~3ull));
-    if (!rc && c->resume && npass > 1) rc = ensure(c, c->state, nout * 64);
+    if (!rc && c->resume && npass > 1) rc = ensure(c, c->state, std::max<uint64_t>(nout, c->qstate ? list : 0ull) * 64);
+    if (!rc && c->resume && c->qstate && npass > 1) rc = ensure(c, c->stateq, nout * 64);
     return rc;
 }
 
@@ -1372,7 +1431,7 @@ static int reset_passes(vhx_ctx *c, uint32_t npass) {
 
 // Pass 0 traces fresh rays (the grid kernel of primary and explicit rays, or the shadow path's first queue pass);
 // every later pass resumes the rays its predecessor abandoned.
-static PassQ pass_q(const vhx_ctx *c, uint32_t p, uint32_t npass) {
+static PassQ pass_q(const vhx_ctx *c, uint32_t p, uint32_t npass, bool qm = false) {
     PassQ q{};  // every field a kernel reads is set below or zero (q.zero, q.flags: null unless a caller sets them)
     const bool last = p + 1 >= npass;
     q.budget = last ? VHX_MAX_ITERS : c->budgets[p];
@@ -1390,7 +1449,20 @@ static PassQ pass_q(const vhx_ctx *c, uint32_t p, uint32_t npass) {
     q.state = c->resume && npass > 1 && p >= c->save_from ? (uint4 *)c->state.ptr : nullptr;
     q.resume = c->resume && p > c->save_from ? 1u : 0u;
     q.sparse = last || !q.state ? 0u : c->sparse[p];
+    q.qmode = qm && q.state ? 1u : 0u;
+    q.sin = q.qmode ? (const uint4 *)c->stateq.ptr : nullptr;
     return q;
+}
+
+// Whether a trace runs in the queue-state mode (PassQ::qmode): its pass 0 lists its abandoned rays per wave or chunk
+// (listed: the ordered primary pass 0; first_queue: pass 0 is itself a queue pass, the shadow path), every pass saves
+// (save_from 0, resume on), and no queue is node-sorted (the sort reorders a queue by the states at output indices)
+static bool queue_state_mode(const vhx_ctx *c, bool listed, bool first_queue, uint32_t npass) {
+    if (!c->qstate || !c->resume || c->save_from != 0 || npass < 2 || !(listed || first_queue)) return false;
+    if (!c->stateq.ptr) return false;
+    for (uint32_t p = 1; p < npass && p < 32u; ++p)
+        if (c->qsort && ((c->qsort_passes >> p) & 1u)) return false;
+    return true;
 }
 
 // VHX_DEBUG_PASSES=1 (a diagnostic build only): synchronise after every pass step and print the queue counters
@@ -1427,7 +1499,7 @@ static void launch_scan(vhx_ctx *c, const uint32_t *counts, uint32_t nchunks_hos
 // Chunk lists -> queue `out` with its length at *total: pass-0 style (nchunks_host workgroup chunks of stride 256) or
 // queue-pass style (chunks of per_chunk rays, their number derived from the device-side input length n_in).
 static int compact_chunks(vhx_ctx *c, uint32_t nchunks_host, const uint32_t *n_in, uint32_t per_chunk,
-                          uint32_t stride, uint32_t *out, uint32_t *total, uint64_t max_chunks) {
+                          uint32_t stride, uint32_t *out, uint32_t *total, uint64_t max_chunks, bool move_state = false) {
     const uint32_t *counts = (const uint32_t *)c->counts.ptr;
     uint32_t *offsets = (uint32_t *)c->offsets.ptr;
     // adaptive rays per chunk (pass_rpw, per_chunk 0; max_chunks is then the ray count): ceil(n / ceil(n / tw)) <= tw
@@ -1439,7 +1511,9 @@ static int compact_chunks(vhx_ctx *c, uint32_t nchunks_host, const uint32_t *n_i
     const uint64_t want = (max_chunks + 3) / 4;
     const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(want, c->queue_blocks));
     k_gather_chunks<<<grid, 256, 0, c->stream>>>((const uint32_t *)c->tmp.ptr, stride, counts, offsets,
-                                                 nchunks_host, n_in, per_chunk, c->tw, out);
+                                                 nchunks_host, n_in, per_chunk, c->tw, out,
+                                                 move_state ? (const uint4 *)c->state.ptr : nullptr,
+                                                 move_state ? (uint4 *)c->stateq.ptr : nullptr);
     VHX_HIP(c, hipGetLastError());
     debug_passes(c, "compacted");
     return VHX_OK;
@@ -1496,6 +1570,8 @@ static bool list_order(uint32_t qorder, uint32_t W, uint32_t H, ListOrder &lo, u
 // Pass 0's workgroups over whole tiles of the list order: the buffers of its per-workgroup lists
 static int ensure_lists(vhx_ctx *c, uint64_t nblocks) {
     int rc = ensure(c, c->tmp, nblocks * 256 * 4);
+    // the queue-state mode saves pass 0's abandoned rays at their list slots (every slot of whole tiles)
+    if (!rc && c->resume && c->qstate) rc = ensure(c, c->state, nblocks * 256 * 64);
     if (!rc) rc = ensure(c, c->counts, nblocks * 4 * 4);
     if (!rc) rc = ensure(c, c->offsets, nblocks * 4 * 4);
     if (!rc) rc = ensure(c, c->scan_part, ((nblocks * 4 + SCAN_SEG - 1) / SCAN_SEG) * 8);
@@ -1533,7 +1609,7 @@ template <bool COUNT, int BD, bool MIP = false>
 static int launch_queue_passes(vhx_ctx *c, const DevTree &t, const CamD &cam, const RaySrc &src, const OutD &o,
                                uint32_t first, uint32_t npass, uint64_t nout, uint64_t nblocks0,
                                int pass0 = P0_LISTS, uint32_t order_w = 0, uint32_t order_h = 0,
-                               uint32_t frames = 1) {
+                               uint32_t frames = 1, bool qm = false) {
     uint32_t *ctl = (uint32_t *)c->qctl.ptr;
     int rc = VHX_OK;
     if (first > 0 && npass > 1) {
@@ -1552,7 +1628,7 @@ static int launch_queue_passes(vhx_ctx *c, const DevTree &t, const CamD &cam, co
             if ((rc = sort_segments(c, 1, npass, (uint32_t *)c->queue[0].ptr, ctl, nout))) return rc;
         } else if (pass0 == P0_ORDERED) {  // per-wave lists (wave_append): 4 chunks of 64 per workgroup
             rc = compact_chunks(c, (uint32_t)(nblocks0 * 4), nullptr, 64, 64, (uint32_t *)c->queue[0].ptr, ctl,
-                                nblocks0 * 4);
+                                nblocks0 * 4, qm);
             if (!rc) rc = sort_segments(c, 1, npass, (uint32_t *)c->queue[0].ptr, ctl, nout);
         } else {
             rc = compact_chunks(c, (uint32_t)nblocks0, nullptr, 256, 256, (uint32_t *)c->queue[0].ptr, ctl, nblocks0);
@@ -1563,7 +1639,7 @@ static int launch_queue_passes(vhx_ctx *c, const DevTree &t, const CamD &cam, co
     for (uint32_t p = first; p < npass && !rc; ++p) {
         const uint32_t *in = (const uint32_t *)c->queue[(p - 1) & 1u].ptr;  // p = 0: queue[1]
         const uint32_t *in_n = p > 0 ? ctl + (p - 1) : ctl + 7;
-        const PassQ q = pass_q(c, p, npass);
+        const PassQ q = pass_q(c, p, npass, qm);
         // a first pass over fresh rays (the shadow path) is throughput-bound like a grid launch: more waves
         uint32_t qwaves = p == 0 ? c->queue_waves0
                           : (p + 1 < npass && c->queue_waves_mid ? c->queue_waves_mid : c->queue_waves);
@@ -1577,7 +1653,7 @@ static int launch_queue_passes(vhx_ctx *c, const DevTree &t, const CamD &cam, co
         debug_passes(c, "queue pass");
         if (p + 1 < npass) {
             rc = compact_chunks(c, 0, in_n, q.rpw, q.rpw, (uint32_t *)c->queue[p & 1u].ptr, ctl + p,
-                                q.rpw ? (nout + q.rpw - 1) / q.rpw : nout);
+                                q.rpw ? (nout + q.rpw - 1) / q.rpw : nout, qm);
             if (!rc) rc = sort_segments(c, p + 1, npass, (uint32_t *)c->queue[p & 1u].ptr, ctl + p, nout);
         }
     }
@@ -1671,7 +1747,7 @@ void vhx_destroy(vhx_ctx *c) {
     c->tree.reset();  // frees the device tree with its last context
     if (c->use_ev) (void)hipEventDestroy(c->use_ev);
     for (DevBuf *b : {&c->scratch, &c->rays, &c->queue[0], &c->queue[1], &c->qctl, &c->tmp, &c->counts, &c->offsets,
-                      &c->flags, &c->qargs, &c->state, &c->upd, &c->prepass_depth, &c->batch_args, &c->scan_part,
+                      &c->flags, &c->qargs, &c->state, &c->stateq, &c->upd, &c->prepass_depth, &c->batch_args, &c->scan_part,
                       &c->shadow_args})
         if (b->ptr) (void)hipFree(b->ptr);
     std::vector<vhx_ctx::Pinned *> pins = {&c->pinned[0], &c->pinned[1]};
@@ -1751,6 +1827,12 @@ static int apply_tuning(vhx_ctx *c, const std::string &key, const std::string &v
     } else if (key == "resume") {
         if (!parse_u32(val, x) || x > 1) return bad();
         c->resume = x != 0;
+    } else if (key == "tlists") {
+        if (!parse_u32(val, x) || x > 1) return bad();
+        c->tile_lists = x != 0;
+    } else if (key == "qstate") {
+        if (!parse_u32(val, x) || x > 1) return bad();
+        c->qstate = x != 0;
     } else if (key == "save_from") {
         if (!parse_u32(val, x)) return bad();
         c->save_from = x;
@@ -2014,6 +2096,8 @@ void vhx::copy_sched(vhx_ctx *c, const vhx_ctx *owner) {
     c->scan_multi = owner->scan_multi;
     c->p0lists = owner->p0lists;
     c->resume = owner->resume;
+    c->qstate = owner->qstate;
+    c->tile_lists = owner->tile_lists;
     c->save_from = owner->save_from;
     c->qorder = owner->qorder;
     c->adaptive = owner->adaptive;
@@ -2345,15 +2429,22 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
     // a whole framebuffer frame in the default queue order: pass 0 lists its rays in that order itself (ListOrder)
     ListOrder lo{};
     uint64_t nb0 = nblocks;
-    const bool listed = c->p0lists && npass > 1 && layout == VHX_LAYOUT_FRAMEBUFFER && T == 16 && tile_start == 0 &&
-                        tile_stride == 1 && list_order(c->qorder, cam->width, cam->height, lo, nb0);
+    bool listed = c->p0lists && npass > 1 && layout == VHX_LAYOUT_FRAMEBUFFER && T == 16 && tile_start == 0 &&
+                  tile_stride == 1 && list_order(c->qorder, cam->width, cam->height, lo, nb0);
     if (!listed) lo = ListOrder{}, nb0 = nblocks;
+    // a tile set (the rank's share of a multi-GPU frame) under the frames-in-flight schedule lists its rays in its own
+    // block order: no flag per entry, no compaction over every entry, and the queue-state mode (ListOrder::tl)
+    if (!listed && c->p0lists && c->tile_lists && npass > 1 && layout == VHX_LAYOUT_TILES && c->qorder != 0) {
+        listed = true;
+        lo.tl = 1;
+    }
     if (listed && (rc = ensure_lists(c, nb0))) return rc;
     if ((listed ? nb0 * 4 : nb0) > 0x7FFFFFFFull) return fail(c, VHX_E_INVALID_ARG, "frame too large");
     const int p0 = listed ? P0_ORDERED : P0_FLAGS;
+    const bool qm = queue_state_mode(c, listed, false, npass);
     auto launch = [&](auto bd_tag) {
         constexpr int BD = decltype(bd_tag)::value;
-        PassQ q0 = pass_q(c, 0, npass);
+        PassQ q0 = pass_q(c, 0, npass, qm);
         if (listed)
             q0.zero = (uint32_t *)c->qctl.ptr + 16;
         else if (npass > 1)
@@ -2362,11 +2453,11 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
         if (t.mips) {  // MIP stand-ins (no byte counting, no depth prepass: refused above)
             k_trace_primary<false, BD, false, true><<<g0, 256, 0, c->stream>>>(
                 t, cd, ho.dev, T, tiles_x, tile_start, tile_stride, layout, bpx, bpt, q0, FastD{}, lo);
-            qrc = launch_queue_passes<false, BD, true>(c, t, cd, src, ho.dev, 1, npass, nout, nb0, p0, ow, oh);
+            qrc = launch_queue_passes<false, BD, true>(c, t, cd, src, ho.dev, 1, npass, nout, nb0, p0, ow, oh, 1, qm);
         } else if (count) {
             k_trace_primary<true, BD><<<g0, 256, 0, c->stream>>>(
                 t, cd, ho.dev, T, tiles_x, tile_start, tile_stride, layout, bpx, bpt, q0, FastD{}, lo);
-            qrc = launch_queue_passes<true, BD>(c, t, cd, src, ho.dev, 1, npass, nout, nb0, p0, ow, oh);
+            qrc = launch_queue_passes<true, BD>(c, t, cd, src, ho.dev, 1, npass, nout, nb0, p0, ow, oh, 1, qm);
         } else {
             if (fast)
                 k_trace_primary<false, BD, true><<<g0, 256, 0, c->stream>>>(
@@ -2374,7 +2465,7 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
             else
                 k_trace_primary<false, BD><<<g0, 256, 0, c->stream>>>(
                     t, cd, ho.dev, T, tiles_x, tile_start, tile_stride, layout, bpx, bpt, q0, FastD{}, lo);
-            qrc = launch_queue_passes<false, BD>(c, t, cd, src, ho.dev, 1, npass, nout, nb0, p0, ow, oh);
+            qrc = launch_queue_passes<false, BD>(c, t, cd, src, ho.dev, 1, npass, nout, nb0, p0, ow, oh, 1, qm);
         }
     };
     const bool bd_ok = dispatch_bd(c->tree->desc.brick_dim, launch);
@@ -2491,9 +2582,10 @@ int vhx_trace_primary_batch(vhx_ctx *c, const vhx_camera *cams, uint32_t n, cons
     const bool listed = c->p0lists && npass > 1 && list_order(c->qorder, W, H, lo, nbf0) && nbf0 * n * 4 <= 0x7FFFFFFFull;
     if (!listed) lo = ListOrder{}, nbf0 = nbf;
     if (listed && (rc = ensure_lists(c, nbf0 * n))) return rc;
+    const bool qm = queue_state_mode(c, listed, false, npass);
     auto launch = [&](auto bd_tag) {
         constexpr int BD = decltype(bd_tag)::value;
-        PassQ q0 = pass_q(c, 0, npass);
+        PassQ q0 = pass_q(c, 0, npass, qm);
         if (listed)
             q0.zero = (uint32_t *)c->qctl.ptr + 16;
         else if (npass > 1)
@@ -2501,7 +2593,7 @@ int vhx_trace_primary_batch(vhx_ctx *c, const vhx_camera *cams, uint32_t n, cons
         k_trace_primary_batch<BD><<<(unsigned)(nbf0 * n), 256, 0, c->stream>>>(t, dcams, douts, (uint32_t)nbf0, bx,
                                                                                (uint32_t)npix, q0, lo);
         qrc = launch_queue_passes<false, BD>(c, t, cd, src, OutD{}, 1, npass, nout, nbf0 * n,
-                                             listed ? P0_ORDERED : P0_FLAGS, W, H, n);
+                                             listed ? P0_ORDERED : P0_FLAGS, W, H, n, qm);
     };
     if (!dispatch_bd(c->tree->desc.brick_dim, launch)) return fail(c, VHX_E_INVALID_ARG, "unsupported brick_dim");
     if (qrc) return qrc;
@@ -2512,6 +2604,41 @@ int vhx_trace_primary_batch(vhx_ctx *c, const vhx_camera *cams, uint32_t n, cons
     VHX_HIP(c, hipEventRecord(c->ev1, c->stream));
     c->timed = true;
     return tscope.end();
+}
+
+int vhx_chain_profile(vhx_ctx *c, const vhx_camera *cam, const uint32_t *pixels, uint32_t n, uint64_t *out) {
+    if (!c || !cam || (n && (!pixels || !out))) return VHX_E_INVALID_ARG;
+#if VHX_CHAIN
+    if (!c->tree->uploaded) return fail(c, VHX_E_STATE, "vhx_chain_profile before vhx_upload_tree");
+    if (n == 0) return VHX_OK;
+    for (uint32_t k = 0; k < n; ++k)
+        if (pixels[k] >= (uint64_t)cam->width * cam->height) return fail(c, VHX_E_INVALID_ARG, "vhx_chain_profile: pixel outside the frame");
+    VHX_HIP(c, hipSetDevice(c->device));
+    VHX_STREAM(c);
+    TraceScope tscope(c);
+    int rc = tscope.rc;
+    if (rc) return rc;
+    if ((rc = refresh_child_rec(c))) return rc;
+    const DevTree t = dev_tree(c);
+    if (t.mips) return fail(c, VHX_E_INVALID_ARG, "vhx_chain_profile: not with node MIPs");
+    const uint64_t pbytes = ((uint64_t)n * 4 + 255) & ~255ull, obytes = (uint64_t)n * VHX_CHAIN_WORDS * 8;
+    if ((rc = ensure(c, c->scratch, pbytes + obytes))) return rc;
+    uint32_t *dpix = (uint32_t *)c->scratch.ptr;
+    unsigned long long *dout = (unsigned long long *)((uint8_t *)c->scratch.ptr + pbytes);
+    VHX_HIP(c, hipMemcpyAsync(dpix, pixels, (uint64_t)n * 4, hipMemcpyHostToDevice, c->stream));
+    const CamD cd = cam_of(cam);
+    auto launch = [&](auto bd_tag) {
+        constexpr int BD = decltype(bd_tag)::value;
+        k_chain<BD><<<n, 64, 0, c->stream>>>(t, cd, dpix, n, dout);
+    };
+    if (!dispatch_bd(c->tree->desc.brick_dim, launch)) return fail(c, VHX_E_INVALID_ARG, "unsupported brick_dim");
+    VHX_HIP(c, hipGetLastError());
+    VHX_HIP(c, hipMemcpyAsync(out, dout, obytes, hipMemcpyDeviceToHost, c->stream));
+    VHX_HIP(c, hipStreamSynchronize(c->stream));
+    return tscope.end();
+#else
+    return fail(c, VHX_E_STATE, "vhx_chain_profile: libvhx was built without VHX_CHAIN");
+#endif
 }
 
 int vhx_profile_counters(vhx_ctx *c, uint64_t *out, uint32_t n, int reset) {
@@ -2712,11 +2839,14 @@ int vhx_trace_shadows(vhx_ctx *c, const float light[3], uint64_t n, const uint32
     auto launch = [&](auto bd_tag) {
         constexpr int BD = decltype(bd_tag)::value;
         if (t.mips)
-            qrc = launch_queue_passes<false, BD, true>(c, t, cd, src, so, 0, npass, n, nb64);
+            qrc = launch_queue_passes<false, BD, true>(c, t, cd, src, so, 0, npass, n, nb64, P0_LISTS, 0, 0, 1,
+                                                     queue_state_mode(c, false, true, npass));
         else if (bytes)
-            qrc = launch_queue_passes<true, BD>(c, t, cd, src, so, 0, npass, n, nb64);
+            qrc = launch_queue_passes<true, BD>(c, t, cd, src, so, 0, npass, n, nb64, P0_LISTS, 0, 0, 1,
+                                                     queue_state_mode(c, false, true, npass));
         else
-            qrc = launch_queue_passes<false, BD>(c, t, cd, src, so, 0, npass, n, nb64);
+            qrc = launch_queue_passes<false, BD>(c, t, cd, src, so, 0, npass, n, nb64, P0_LISTS, 0, 0, 1,
+                                                     queue_state_mode(c, false, true, npass));
     };
     if (!dispatch_bd(c->tree->desc.brick_dim, launch)) return fail(c, VHX_E_INVALID_ARG, "unsupported brick_dim");
     if (qrc) return qrc;
@@ -2823,7 +2953,8 @@ int vhx_trace_shadows_batch(vhx_ctx *c, const float light[3], uint32_t nf, uint6
     const CamD cd{};
     auto launch = [&](auto bd_tag) {
         constexpr int BD = decltype(bd_tag)::value;
-        qrc = launch_queue_passes<false, BD>(c, t, cd, src, OutD{}, 0, npass, ntot, nb64, P0_LISTS, 0, 0, nf);
+        qrc = launch_queue_passes<false, BD>(c, t, cd, src, OutD{}, 0, npass, ntot, nb64, P0_LISTS, 0, 0, nf,
+                                             queue_state_mode(c, false, true, npass));
     };
     if (!dispatch_bd(c->tree->desc.brick_dim, launch)) return fail(c, VHX_E_INVALID_ARG, "unsupported brick_dim");
     if (qrc) return qrc;
