@@ -90,7 +90,7 @@ def parse():
     p.add_argument("--batch", type=int, default=None, metavar="K",
                    help="frames per vhx_trace_primary_batch call (one pass ladder over K frames on one stream); 0 = one "
                         "vhx_trace_primary per frame. Default 7 (on 3 contexts) for one-GPU primary frames without --inflight "
-                        "(DESIGN.md §16.1: 7 frames x 3 contexts was the fastest split of the driver's 20-frame window), "
+                        "(docs/DESIGN_LOG.md §16.1: 7 frames x 3 contexts was the fastest split of the driver's 20-frame window), "
                         "else 0")
     p.add_argument("--orbit", type=float, default=0.0,
                    help="moving camera: frame k (warm-up included) views from angle 40 + k*ORBIT rad on the glass "
@@ -541,18 +541,25 @@ def main():
         # batches wherever they are the faster line: one GPU, primary rays on the exact path, and no explicit
         # --inflight (which asks for that many per-frame contexts). Config 5 (--shadows) keeps twenty per-frame
         # contexts: its batches (vhx_trace_shadows_batch, --batch K) measured 1.31 against 1.17-1.23 ms per frame
-        # 
-        single = int(os.environ.get("WORLD_SIZE", "1")) == 1 and os.environ.get("VHX_BENCH_MGPU1") != "1"
-        args.batch = 7 if (single and args.inflight is None and not args.shadows and args.depth_prepass is None
-                           and args.mip_lod is None) else 0
+        # (docs/DESIGN_LOG.md §16.3)
+        # The multi-GPU ranks (vhx_mgpu) batch too: each rank's tile sets of K frames as one vhx_trace_tiles_batch
+        # (vhx_mgpu_render_batch) -- a rank's share of a config-4 frame is half a headline frame, and traced one frame
+        # at a time it ran at 55 % of the whole frame's rate (scripts/probes/probe_tiles.py)
+        world_env = int(os.environ.get("WORLD_SIZE", "1"))
+        single = world_env == 1 and os.environ.get("VHX_BENCH_MGPU1") != "1"
+        mgpu_path = (world_env > 1 or os.environ.get("VHX_BENCH_MGPU1") == "1") and args.mgpu == "vhx" and \
+            os.environ.get("VHX_BENCH_REHEARSAL") != "1"
+        args.batch = 7 if ((single or mgpu_path) and args.inflight is None and not args.shadows and
+                           args.depth_prepass is None and args.mip_lod is None) else 0
         if args.batch:
             args.inflight = 3
     if args.inflight is None:
         args.inflight = 2 if args.batch else 20
-    if args.batch:
+    if args.batch and int(os.environ.get("WORLD_SIZE", "1")) == 1 and os.environ.get("VHX_BENCH_MGPU1") != "1":
         # one stream per batch in flight: the box's default hardware queues (GPU_MAX_HW_QUEUES unset: 4) suffice
         queues = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
     else:
+        # per-frame contexts, or a multi-GPU rank's batch contexts plus its communication stream: a queue each
         queues = hw_queues(max(1, args.inflight))
     import torch
     import torch.distributed as dist
@@ -716,10 +723,16 @@ def main():
     if budgets is not None:
         for r in rts:
             r.set_pass_budgets(tuple(int(b) for b in budgets.split(",") if b.strip()))
-    K = args.batch if (mg is None and world == 1) else 0
+    K = args.batch if ((mg is None and world == 1) or mg is not None) else 0
     if args.batch and not K:
-        raise SystemExit("--batch is a one-GPU mode (N = 1)")
-    for _ in range(len(rts) * max(1, K)):  # batch mode: K output sets per context, outs[f * K + j]
+        raise SystemExit("--batch needs one GPU or the vhx_mgpu path (not --mgpu torch)")
+    fbs_rgba = fbs_depth = None
+    if mg is not None and rank == 0:
+        # a batch's frames land in K framebuffers (frame 0 of every batch in fb_rgba / fb_depth)
+        fbs_rgba = [fb_rgba] + [torch.zeros(W * H, dtype=torch.int32, device=dev) for _ in range(max(1, K) - 1)]
+        if fb_depth is not None:
+            fbs_depth = [fb_depth] + [torch.zeros(W * H, dtype=torch.float32, device=dev) for _ in range(max(1, K) - 1)]
+    for _ in range(len(rts) * max(1, K) if mg is None else 1):  # batch mode: K output sets per context, outs[f * K + j]
         o = {"rgba": torch.zeros(n_out, dtype=torch.int32, device=dev),
              "depth": torch.zeros(n_out, dtype=torch.float32, device=dev)}
         if args.shadows:
@@ -774,12 +787,17 @@ def main():
     batch_i = [0]
 
     def submit_batch(nf, timed):
-        """One vhx_trace_primary_batch of the next nf frames on context batch_i % F."""
+        """One vhx_trace_primary_batch of the next nf frames on context batch_i % F (vhx_mgpu: one
+        vhx_mgpu_render_batch, its contexts taken in turn by the library)."""
         f = batch_i[0] % len(rts)
         batch_i[0] += 1
         r, s_ = rts[f], streams[f]
         cams_b = [cams[(frame[0] + j) % len(cams)] for j in range(nf)]
         frame[0] += nf
+        if mg is not None:
+            mg.render_batch(cams_b, None if fbs_rgba is None else fbs_rgba[:nf],
+                            None if fbs_depth is None else fbs_depth[:nf])
+            return
         for j in range(nf):
             last_cam[f * K + j] = cams_b[j]
         if timed and not NOEV:
@@ -813,7 +831,7 @@ def main():
     # setup (not a step): one untimed frame (batch mode: one batch of K frames) per context allocates its queues and
     # state buffers, so that no allocation (hipMalloc synchronises the device) falls into the timed region when F
     # exceeds the warm-up count
-    for _ in range(len(rts) if mg is None else 1):
+    for _ in range(len(rts) if mg is None else (F if K else 1)):
         run(max(1, K), False)
     drain()
     split = None
@@ -826,7 +844,9 @@ def main():
             R, a, g = mg.balance(cam, frames=4)
             split = {"root_slots": R, "rank0_trace_ms_one_slot": round(a, 4), "transfer_ms_one_slot": round(g, 4),
                      "source": "vhx_mgpu_balance"}
-        step(False)  # the buffers of the chosen split are allocated outside the timed region
+        # the buffers of the chosen split are allocated outside the timed region (every batch context's)
+        for _ in range(F if K else 1):
+            run(max(1, K), False)
         drain()
     frame[0] = 0
     batch_i[0] = 0
@@ -984,8 +1004,17 @@ def main():
             if fb_depth is not None:
                 eq = eq and bool(np.array_equal(fb_depth.cpu().numpy().view(np.uint32), whole["depth"].view(np.uint32)))
                 fields.append("depth")
-            mgpu = {"frame_equal": eq, "fields": fields, "pixels": int(W * H),
-                    "basis": "the gathered, untiled frame of the timed configuration vs rank 0 tracing it alone"}
+            nfb = 1
+            if fbs_rgba is not None and not args.orbit:  # the other framebuffers of the timed batches
+                for k in range(1, len(fbs_rgba)):
+                    eq = eq and bool(np.array_equal(fbs_rgba[k].cpu().numpy().view(np.uint32), whole["rgba"]))
+                    if fbs_depth is not None:
+                        eq = eq and bool(np.array_equal(fbs_depth[k].cpu().numpy().view(np.uint32),
+                                                        whole["depth"].view(np.uint32)))
+                nfb = len(fbs_rgba)
+            mgpu = {"frame_equal": eq, "fields": fields, "pixels": int(W * H), "framebuffers": nfb,
+                    "basis": "the gathered, untiled frames of the timed configuration (every framebuffer of a batch) "
+                             "vs rank 0 tracing the frame alone"}
         if mg is not None and args.planes == 1:
             # the two-plane transfer too (collective on every rank): RGBA8 + depth gathered and untiled
             mg.set_planes(2)

@@ -178,8 +178,8 @@ int vhx_get_pass_budgets(const vhx_ctx *ctx, uint32_t *budgets, uint32_t *n, int
  * queue passes 1.., 0 = adaptive), tw, xcdg, resume (0/1), qstate (0/1: states in queue order), save_from, qblock
  *  (64/128/256), tlists (0/1: tile sets list pass 0), qwaves (fixes the schedule),
  * qwavesm, qwaves0, qxcd, qxcd_all (0/1), sparse (list, fixes the schedule), qorder ("[m]N[z|r]" or 0), qsort (0 or
- * 256..2048: segment node sort of the queue passes), qsortp (pass mask), qsortb (workgroups). The
- * library reads no environment variable for any of them. Unknown keys or malformed values:
+ * 256..2048: segment node sort of the queue passes, docs/DESIGN_LOG.md §15.3), qsortp (pass mask), qsortb (workgroups). The
+ * library reads no environment variable for any of them (docs/DESIGN_LOG.md §15). Unknown keys or malformed values:
  * VHX_E_INVALID_ARG and nothing is changed. */
 int vhx_set_tuning(vhx_ctx *ctx, const char *spec);
 
@@ -246,13 +246,20 @@ int vhx_trace_primary(vhx_ctx *ctx, const vhx_camera *cam, uint32_t tile_size, u
  * context before the call waits on the host (batches on one context still run one after another on its stream; for
  * batches that overlap on the GPU, round-robin over shared contexts). */
 int vhx_trace_primary_batch(vhx_ctx *ctx, const vhx_camera *cams, uint32_t n, const vhx_hits *outs);
+/* The same for tile sets (the rank's share of a multi-GPU frame, vhx_mgpu_render_batch): frame k is the TILES-layout
+ * trace of cams[k] over tiles tile_starts[k], tile_starts[k] + tile_stride, ... (tile_size T), into outs[k] exactly as
+ * vhx_trace_primary(ctx, &cams[k], T, tile_starts[k], tile_stride, VHX_LAYOUT_TILES, &outs[k], 1) writes it (entries
+ * past the frame edge are not written); one pass ladder for all n frames. Frames may hold different tile counts
+ * (a start past the last tile: no entries). Results equal n vhx_trace_primary calls bit for bit. */
+int vhx_trace_tiles_batch(vhx_ctx *ctx, const vhx_camera *cams, uint32_t n, uint32_t tile_size,
+                          const uint32_t *tile_starts, uint32_t tile_stride, const vhx_hits *outs);
 /* Depth-prepass fast mode (opt-in; NOT the reference's CPU semantics, so outside the parity bar; the WGSL path's
  * prepass, src/raytracing/bevy/viewport_render.wgsl:702-726). When enabled, a vhx_trace_primary of a whole frame in
  * the FRAMEBUFFER layout without byte counting first traces a half-resolution depth frame (texel (X, Y) through the
  * centre of full pixels 2X..2X+1, 2Y..2Y+1), then starts every full-resolution ray at the minimum of depth texels
  * (x/2, y/2), (x/2+1, y/2), (x/2, y/2+1), (x/2+1, y/2+1) minus `margin` (distance units; 0 = the WGSL's choice), and
  * reports a miss where all four texels missed. Thin or grazing geometry that none of the four texel rays hits first can
- * be skipped: the pixels that differ from the exact path are measured in tests/test_gpu_fast.py and DESIGN.md §10.
+ * be skipped: the pixels that differ from the exact path are measured in tests/test_gpu_fast.py and docs/DESIGN_LOG.md §10.
  * Other traces (tiles, ray batches, shadows, byte counting) stay exact. Default off. */
 int vhx_set_depth_prepass(vhx_ctx *ctx, int enable, float margin);
 /* MIP stand-ins for absent children (the WGSL path's probe_MIP, src/raytracing/bevy/viewport_render.wgsl:328-364,
@@ -281,7 +288,7 @@ int vhx_profile_counters(vhx_ctx *ctx, uint64_t *out, uint32_t n, int reset);
 int vhx_chain_profile(vhx_ctx *ctx, const vhx_camera *cam, const uint32_t *pixels, uint32_t n, uint64_t *out);
 /* Traces n explicit rays; rays = 6 f32 per ray (origin xyz, direction xyz), host or device per on_device. */
 int vhx_trace_rays(vhx_ctx *ctx, const float *rays, uint64_t n, const vhx_hits *out, int on_device);
-/* Hard shadows (BASELINE config 5; the reference has no shadow rays — semantics defined in DESIGN.md §9): for
+/* Hard shadows (BASELINE config 5; the reference has no shadow rays — semantics defined in docs/DESIGN_LOG.md §9): for
  * every ray i < n of a previous trace with a hit (value[i] != VHX_EMPTY), one shadow ray from
  * impact[i] + normal[i] * 1e-3 toward `light` (e.g. the reference's ambient_light_position = (size, size, size),
  * src/raytracing/bevy/view.rs:81-85) is traced with get_by_ray semantics; shadowed[i] = 1 if it hits a voxel, else 0
@@ -348,6 +355,14 @@ int vhx_mgpu_set_overlap(vhx_mgpu *m, int overlap);
  * NULL) are device framebuffers receiving the whole frame; other ranks pass NULL. Outputs are complete after
  * vhx_mgpu_sync. */
 int vhx_mgpu_render(vhx_mgpu *m, const vhx_camera *cam, uint32_t *fb_rgba, float *fb_depth);
+/* Collective: renders n frames (1..VHX_MGPU_MAX_INFLIGHT, every camera the same width x height) as one batch: each rank
+ * traces its tile slots of all n frames with ONE vhx_trace_tiles_batch (the per-frame pass ladder's fixed costs paid
+ * once per batch), then the n frames' transfers to rank 0 run as one RCCL group and rank 0 untiles frame k into
+ * fb_rgba[k] / fb_depth[k] (arrays of n device pointers on rank 0; fb_depth may be NULL; other ranks pass NULL).
+ * Successive batches are traced by the vhx_mgpu_set_frames_in_flight contexts in turn. Results equal n
+ * vhx_mgpu_render calls bit for bit; complete after vhx_mgpu_sync. */
+int vhx_mgpu_render_batch(vhx_mgpu *m, const vhx_camera *cams, uint32_t n, uint32_t *const *fb_rgba,
+                          float *const *fb_depth);
 /* Waits for every frame submitted on this rank (trace, gather and untile); optionally returns the device time of the
  * last frame's trace on this rank in milliseconds. */
 int vhx_mgpu_sync(vhx_mgpu *m, float *last_trace_ms);

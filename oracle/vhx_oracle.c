@@ -32,7 +32,7 @@
  * MIP stand-ins (vhx_oracle_set_node_mips; not the reference CPU path, which never reads MIPs): with node MIPs set,
  * a node iteration whose target sectant is occupied but whose child entry is absent traces the node's MIP brick over
  * the node's cube first -- the WGSL path's probe_MIP (src/raytracing/bevy/viewport_render.wgsl:328-364, 438-454) --
- * and ADVANCEs past the sectant on a miss instead of pushing into the missing child.
+ * and ADVANCEs past the sectant on a miss instead of pushing into the missing child (docs/DESIGN_LOG.md §10b).
  *
  * Deviation (documented in DESIGN.md): the reference loops have no iteration bound; this restatement stops a ray
  * after VHX_ORACLE_MAX_ITERS inner iterations and reports a miss (the GPU kernel uses the same bound).
@@ -580,7 +580,7 @@ int vhx_oracle_trace_primary(const vhx_tree_desc *t, const vhx_camera *cam, uint
     return VHX_OK;
 }
 
-/* Hard shadows (BASELINE config 5; no reference counterpart — DESIGN.md §9 defines them): for every hit record i
+/* Hard shadows (BASELINE config 5; no reference counterpart — docs/DESIGN_LOG.md §9 defines them): for every hit record i
  * (value[i] != 0xFFFFFFFF) one shadow ray from impact + normal * 1e-3 (multiply, then add) toward `light`, direction
  * normalised like V3c::normalized; shadowed[i] = hit ? 1 : 0; rgba (optional) gets rgb >> 1 where shadowed; bytes
  * (optional) the shadow ray's algorithmic bytes. */

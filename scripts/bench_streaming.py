@@ -1,4 +1,4 @@
-"""Streaming-frame timing: a device view of the 256^3 scene-S tree (brick_dim 4) around a viewport
+"""Streaming-frame timing (docs/DESIGN_LOG.md §9c, §14.2): a device view of the 256^3 scene-S tree (brick_dim 4) around a viewport
 that moves every frame, at the reference's default rates (node_uploads_per_frame 25, brick_uploads_per_frame 50,
 view.rs:109-111), each frame a 1920x1080 trace of the view -- the reference's render loop (upload::<T> then dispatch,
 streaming/mod.rs:420-635, pipeline/mod.rs:96-155).
@@ -12,7 +12,7 @@ the frames submitted before it and every frame after the writes submitted before
 (wall time / frames) next to the same loop at F = 1 without per-frame synchronisation.
 --batches K1,K2,... (with --inflight F): the uploads of K frames written once every K frames
 (vhx_stream_upload_frames), so that K frames in flight share one tree version; each K runs the same frames of the orbit,
-rounds interleaved.
+rounds interleaved (docs/DESIGN_LOG.md §15.4).
 --size / --width / --height: the tree (scene S, brick_dim 4; 1024 builds the host tree from the bulk image,
 BoxTree.from_scene) and the frame.
 usage: bench_streaming.py [frames] [--inflight F] [--batches 1,4,8] [--size 1024 --width 3840 --height 2160]"""

@@ -1,4 +1,4 @@
-"""The lone frame's dependent chain, per node iteration (VERDICT r05, next 5; DESIGN.md §6.3).
+"""The lone frame's dependent chain, per node iteration (VERDICT r05, next 5; DESIGN.md §3).
 
 Traces rays of the bench frame (3840x2160, scene S 1024^3 bd 4, glass camera) one per wave through the VHX_CHAIN build
 (libvhx_chain.so, vhx_chain_profile: s_memtime stamps around every block of a node iteration) and writes the cycle

@@ -1,5 +1,5 @@
 """Lone-frame latency (one frame at a time, synchronised; libvhx's events, like bench.py's `lone`) of the bench frame
-for each vhx_set_tuning spec on the command line, interleaved over REPS rounds so that box drift hits
+for each vhx_set_tuning spec on the command line (docs/DESIGN_LOG.md §15), interleaved over REPS rounds so that box drift hits
 every spec alike; also a lone orbiting frame (every frame a different view).
 usage: probe_lone.py "" "budgets=64,1024" ..."""
 import os

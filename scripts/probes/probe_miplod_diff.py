@@ -1,5 +1,5 @@
 """Fraction of the 3840x2160 headline frame (scene S 1024^3, brick_dim 4, glass camera) whose hit value differs between
-the exact path and the MIP stand-in views of vhx_scene_build_lod at depths 1 and 2."""
+the exact path and the MIP stand-in views of vhx_scene_build_lod at depths 1 and 2 (docs/DESIGN_LOG.md §10b)."""
 import numpy as np
 import voxelhex_amd as vhx
 from voxelhex_amd import _native as N

@@ -1,4 +1,4 @@
-"""The wave-simulator experiments of DESIGN.md §14.6 (diagnostics): the current design's block counts (compare with
+"""The wave-simulator experiments of docs/DESIGN_LOG.md §14.6 (diagnostics): the current design's block counts (compare with
 profiles/r03/blocks_default.log), capped brick walks, vote-aligned phases, budget schedules and the critical path of
 tail splits. Output: profiles/r03/sim_r03.txt.    python scripts/sim/experiments.py > profiles/r03/sim_r03.txt"""
 import contextlib

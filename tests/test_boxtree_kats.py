@@ -1,6 +1,6 @@
 """Tree-builder known-answer tests transcribed from the reference (src/boxtree/update/tests.rs): insert / get /
 update / insert_at_lod / auto-simplify behaviour of the C++ BoxTree restatement that builds every KAT tree and the
-streaming mirror. Tests that need `clear` are not transcribed (clear is not restated).
+streaming mirror. Tests that need `clear` are not transcribed (clear is not restated, docs/DESIGN_LOG.md §10).
 
 Each test cites the reference lines it follows; values, positions and expected counts are the reference's.
 """

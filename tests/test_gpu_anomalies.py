@@ -1,4 +1,4 @@
-"""Regression tests for the two GPU anomalies of round 1.
+"""Regression tests for the two GPU anomalies of round 1 (docs/DESIGN_LOG.md §13).
 
 1. Stale staging data: vhx_trace_rays once staged host rays in a stream-ordered hipMallocAsync buffer, and the kernel
    intermittently read data of an earlier call. scripts/anomalies/mallocasync_stale.hip reproduces it on the ROCm 7.2

@@ -241,3 +241,53 @@ def test_shadow_batch_argument_errors(gpu):
     # an output aliasing another frame's hit records is refused
     with pytest.raises(N.VhxError):
         gpu.trace_shadows_batch((64.0,) * 3, recs, shadowed_list=[recs[1]["value"], torch.empty_like(recs[0]["value"])])
+
+
+@pytest.mark.parametrize("W,H,T,stride,starts", [(200, 136, 64, 3, (0, 1, 2)), (200, 136, 16, 5, (0, 4, 4, 9)),
+                                                 (97, 33, 32, 2, (0, 1, 5)), (256, 256, 64, 1, (0, 0)),
+                                                 (130, 70, 20, 2, (1, 0, 3))])
+@pytest.mark.parametrize("tune", [None, "tlists=0", "budgets=4", "qstate=1", "resume=0"])
+def test_tiles_batch_equals_single_tile_traces(W, H, T, stride, starts, tune):
+    """vhx_trace_tiles_batch (a rank's tile sets of several frames, the multi-GPU split's batch): every frame equals
+    the single TILES-layout trace of its camera and tile set bit for bit, padding entries included (both untouched),
+    for sets of different sizes (a start past the last tile: no entries), tile sizes that are no multiple of 16, and the
+    listed, flag-compacted and other pass schedules."""
+    import torch
+    rt = vhx.Raytracer(0, tune=tune)
+    try:
+        rt.upload(vhx.FlatTree.build_scene(N.VHX_SCENE_LATTICE_CUBE, 64, 4))
+        cams = _orbit(64, W, H, len(starts), step=0.3)
+        ntiles = ((W + T - 1) // T) * ((H + T - 1) // T)
+        sizes = [max(0, (ntiles - s + stride - 1) // stride) * T * T for s in starts]
+        fields = ("value", "impact", "depth", "rgba")
+        got = [_outs(max(1, n), fields) for n in sizes]
+        ref = [_outs(max(1, n), fields) for n in sizes]
+        torch.cuda.synchronize()
+        rt.trace_tiles_batch(cams, T, starts, stride, got)
+        for k, cam in enumerate(cams):
+            if sizes[k]:
+                rt.trace_primary(cam, tile_size=T, tile_start=starts[k], tile_stride=stride,
+                                 layout=N.VHX_LAYOUT_TILES, out=ref[k])
+        rt.sync()
+        for k in range(len(cams)):
+            a, b = _host(got[k]), _host(ref[k])
+            for f in fields:
+                assert np.array_equal(a[f], b[f]), f"frame {k} (start {starts[k]}) field {f}"
+        assert sum((_host(g)["value"] != N.VHX_EMPTY).sum() for g in got) > 0
+    finally:
+        rt.close()
+
+
+def test_tiles_batch_argument_errors(gpu):
+    import torch
+    gpu.upload(vhx.FlatTree.build_scene(N.VHX_SCENE_LATTICE_CUBE, 32, 4))
+    cams = _orbit(32, 64, 64, 2)
+    o = [_outs(64 * 64, ("rgba",)) for _ in cams]
+    with pytest.raises(ValueError):
+        gpu.trace_tiles_batch(cams, 16, (0,), 1, o)  # one start per camera
+    shared = {"rgba": o[0]["rgba"]}
+    torch.cuda.synchronize()
+    with pytest.raises(N.VhxError):
+        gpu.trace_tiles_batch(cams, 16, (0, 0), 1, [shared, shared])  # both frames would write one array
+    with pytest.raises(N.VhxError):
+        gpu.trace_tiles_batch(cams, 16, (0, 1), 0, o)  # stride 0

@@ -1,6 +1,6 @@
 """Depth-prepass fast mode (vhx_set_depth_prepass; SURVEY.md 8f #4, the WGSL path's prepass,
 src/raytracing/bevy/viewport_render.wgsl:702-726): opt-in and outside the parity bar. These tests check that it never
-touches the exact path and measure how far it strays from it (the pixels whose hit differs)."""
+touches the exact path and measure how far it strays from it (the pixels whose hit differs; docs/DESIGN_LOG.md §10)."""
 import numpy as np
 import pytest
 

@@ -1,4 +1,4 @@
-"""Pass 0's per-wave lists in the queue order: a single frame on the frames-in-flight schedule
+"""Pass 0's per-wave lists in the queue order (docs/DESIGN_LOG.md §16.6): a single frame on the frames-in-flight schedule
 (adaptive=0: the busy ladder, qorder 38, so pass 0 lists its abandoned rays itself) equals the same frame on the lone
 schedule (output order, per-pixel flags) and the oracle, at frame sizes that leave partial 64x64 tiles, partial 16x16
 blocks and partial 8x8 waves; and the flag path (p0lists=0) equals both."""

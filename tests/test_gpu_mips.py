@@ -112,7 +112,7 @@ def test_mip_lod_without_mips_is_the_reference_path(oracle, rt, mip_tree):
 
 
 def test_mip_lod_trade_off(rt, mip_tree):
-    """Measured trade-off of the LOD views (printed): pixels whose hit value differs from the full
+    """Measured trade-off of the LOD views (printed; docs/DESIGN_LOG.md §10b): pixels whose hit value differs from the full
     tree's and frame time, for each cut depth."""
     import time
     tree, full = mip_tree

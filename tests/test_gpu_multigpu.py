@@ -85,6 +85,35 @@ def test_mgpu_one_rank_rccl_frame_vs_oracle(config4, overlap, inflight, root_slo
         rt.close()
 
 
+@pytest.mark.parametrize("batch,inflight,root_slots,planes", [(3, 1, 1, 2), (4, 2, 1, 1), (2, 2, 3, 2), (5, 3, 2, 1)])
+def test_mgpu_render_batch_one_rank_vs_oracle(config4, batch, inflight, root_slots, planes):
+    """vhx_mgpu_render_batch: K frames' tile slots traced as one vhx_trace_tiles_batch, transferred as one RCCL group
+    and untiled per frame; every frame of two back-to-back batches (successive contexts) equals the oracle's frame."""
+    import torch
+    flat, cam, ref = config4
+    rt = vhx.Raytracer(0)
+    try:
+        m = M.MgpuRenderer(rt, M.mgpu_unique_id(), 1, 0, tile_size=T4)
+        m.set_frames_in_flight(inflight)
+        m.broadcast_tree(flat)
+        m.set_root_slots(root_slots)
+        m.set_planes(planes)
+        fr = [torch.zeros(W4 * H4, dtype=torch.int32, device="cuda") for _ in range(2 * batch)]
+        fd = [torch.zeros(W4 * H4, dtype=torch.float32, device="cuda") for _ in range(2 * batch)] if planes == 2 else None
+        for b in range(2):
+            m.render_batch([cam] * batch, fr[b * batch:(b + 1) * batch],
+                           None if fd is None else fd[b * batch:(b + 1) * batch])
+        m.sync()
+        for k in range(2 * batch):
+            got = fr[k].cpu().numpy().view(np.uint32)
+            assert np.array_equal(got, ref["rgba"]), f"batch frame {k}: rgba"
+            if fd is not None:
+                assert np.array_equal(fd[k].cpu().numpy().view(np.uint32), ref["depth"].view(np.uint32)), k
+        m.close()
+    finally:
+        rt.close()
+
+
 def test_mgpu_balance_one_rank(config4):
     """vhx_mgpu_balance at N = 1: there is no transfer, every share models the same period, so R stays 1; the frames
     rendered after it match the oracle."""

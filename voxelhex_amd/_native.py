@@ -114,6 +114,7 @@ SIGNATURES = [
     ("vhx_tree_device_bytes", c_int, [c_void_p, P(c_u64)]),
     ("vhx_trace_primary", c_int, [c_void_p, P(Camera), c_u32, c_u32, c_u32, c_u32, P(Hits), c_int]),
     ("vhx_trace_primary_batch", c_int, [c_void_p, c_void_p, c_u32, c_void_p]),
+    ("vhx_trace_tiles_batch", c_int, [c_void_p, c_void_p, c_u32, c_u32, c_void_p, c_u32, c_void_p]),
     ("vhx_profile_counters", c_int, [c_void_p, P(c_u64), c_u32, c_int]),
     ("vhx_chain_profile", c_int, [c_void_p, c_void_p, P(c_u32), c_u32, P(c_u64)]),
     ("vhx_trace_rays", c_int, [c_void_p, c_void_p, c_u64, P(Hits), c_int]),
@@ -129,6 +130,7 @@ SIGNATURES = [
     ("vhx_mgpu_set_overlap", c_int, [c_void_p, c_int]),
     ("vhx_mgpu_set_frames_in_flight", c_int, [c_void_p, c_u32]),
     ("vhx_mgpu_render", c_int, [c_void_p, P(Camera), c_void_p, c_void_p]),
+    ("vhx_mgpu_render_batch", c_int, [c_void_p, c_void_p, c_u32, c_void_p, c_void_p]),
     ("vhx_mgpu_sync", c_int, [c_void_p, P(c_f32)]),
     ("vhx_mgpu_info", c_int, [c_void_p, c_u32, c_u32, P(c_int), P(c_int), P(c_u64)]),
     ("vhx_mgpu_set_root_slots", c_int, [c_void_p, c_u32]),

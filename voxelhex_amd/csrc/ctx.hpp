@@ -57,7 +57,7 @@ struct TreeStore {
 #define VHX_QORDER_BUSY 38u
 #define VHX_QORDER_IDLE 0u
 // Queue passes of the frames-in-flight schedule: every segment of VHX_QSORT_BUSY consecutive queue entries sorted by the
-// node each ray's saved state stands at (k_sort_segments in vhx_device.hip), so that a wave's rays start
+// node each ray's saved state stands at (k_sort_segments in vhx_device.hip; docs/DESIGN_LOG.md §15.3), so that a wave's rays start
 // at the same node; 0 = off. Off by default: 2-7 % fewer VALU instructions per frame, but no faster (0.527-0.564 against
 // 0.526-0.536 ms per bench frame over five sort variants, profiles/r04/qsort/); tune "qsort=N" turns it on
 #ifndef VHX_QSORT_BUSY
@@ -160,11 +160,13 @@ struct vhx_ctx {
     uint32_t scan_multi = 8;       // chunk scans of more segments (SCAN_SEG counts) run on one workgroup per segment
     bool p0lists = true;           // pass 0 lists its abandoned rays in the queue order (ListOrder; tune "p0lists")
     bool resume = true;            // abandoned rays continue from saved state (tune "resume=0": re-traced from scratch)
-    // queue-state mode (tune "qstate=0" turns it off): where a pass lists its abandoned rays per wave or chunk (the
+    // queue-state mode (tune "qstate=1"; off by default): where a pass lists its abandoned rays per wave or chunk (the
     // listed pass 0 of the frames-in-flight and batch schedules, every queue pass), it saves their states at their list
     // slots, the compaction moves them into the next queue's order, and the next pass reads a ray's state at its queue
-    // position -- coalesced, and in the same load round as the ray's output index instead of after it
-    bool qstate = true;
+    // position -- coalesced, and in the same load round as the ray's output index instead of after it. Measured slower:
+    // the bench frame 0.520-0.522 against 0.504 ms per frame (profiles/r06/qstate/): the compaction's chunk copies
+    // gain a dependent 64 B state load per ray on the path between two passes
+    bool qstate = false;
     // a tile set (VHX_LAYOUT_TILES) under the frames-in-flight schedule: pass 0 lists its rays (ListOrder::tl; tune
     // "tlists=0" falls back to flags compacted in output-index order)
     bool tile_lists = true;
@@ -225,6 +227,7 @@ static inline int fail(vhx_ctx *ctx, int code, const char *msg) {
     if (ctx) ctx->err = msg;
     return code;
 }
+static inline int fail(vhx_ctx *ctx, int code, const std::string &msg) { return fail(ctx, code, msg.c_str()); }
 
 namespace vhx {
 // device buffer of at least `bytes` (contents not kept when it grows)

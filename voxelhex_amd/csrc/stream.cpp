@@ -14,7 +14,7 @@
 //
 // Behavioural deviations: rebuild puts the whole root -> center access path into the view set (see rebuild); after
 // queued tree changes the view set is recomputed (see handle_tree_updates).
-// Differences in the layout the device kernel reads: node type is one u32 per node (not 2 bits
+// Differences in the layout the device kernel reads (docs/DESIGN_LOG.md §9c): node type is one u32 per node (not 2 bits
 // packed 16 per word), occupancy one u64, a Solid brick descriptor is 0x80000000 | index into a deduplicated solid
 // value table (the reference inlines the value, losing data-palette bits), MIP data is tracked for slot accounting
 // but never uploaded (the raytracer does not read MIPs). The reference computes the view set on a worker thread; here

@@ -590,7 +590,7 @@ __global__ void __launch_bounds__(256) k_gather_chunks(const uint32_t *__restric
     }
 }
 
-// Segment node sort of a queue pass's input: every segment of `seg` consecutive entries (a power of two
+// Segment node sort of a queue pass's input (docs/DESIGN_LOG.md §15.3): every segment of `seg` consecutive entries (a power of two
 // <= VHX_QSORT_MAX) is reordered by the node each ray's saved state stands at (the NodeStack top, state word 12), ties
 // in queue order, so that a wave's 64 rays start their first node iteration together and at the same node loads, while
 // the segments keep the queue's 2-D order. Bitonic sort of {node, position} keys in LDS; the queue length is read on the
@@ -654,9 +654,12 @@ struct RaySrc {
     const OutD *outs;
     uint32_t npix;
     const ShD *shs;  // kind 5: frame f = idx / npix is shs[f], entry idx - f * npix
+    // kind 4 with T > 0 (vhx_trace_tiles_batch): frame f is the tile set starts[f], starts[f] + tile_stride, ... of
+    // T x T tiles (tiles_x per row) in the tile layout; npix = the per-frame index stride (the largest set's entries)
+    const uint32_t *starts;
 };
 
-// Hard-shadow ray of hit record idx (BASELINE config 5; semantics in DESIGN.md §9): from impact + normal * 1e-3
+// Hard-shadow ray of hit record idx (BASELINE config 5; semantics in docs/DESIGN_LOG.md §9): from impact + normal * 1e-3
 // toward the light, direction normalised like V3c::normalized (src/spatial/math/vector.rs).
 __device__ __forceinline__ void shadow_ray(const RaySrc &src, uint32_t idx, F3d &o, F3d &d) {
     const float *ip, *np;
@@ -685,6 +688,12 @@ __device__ __forceinline__ void ray_of(const CamD &cam, const RaySrc &src, uint3
     if (src.kind == 4u) {  // a batch: the frame's camera, read where the ray is set up
         const uint32_t f = idx / src.npix, local = idx - f * src.npix;
         const CamD *cf = src.cams + f;
+        if (src.T) {  // a batch of tile sets: entry local of frame f's set in the tile layout
+            const uint32_t tt = src.T * src.T, j = local / tt, l = local - j * tt;
+            const uint32_t tile = src.starts[f] + j * src.tile_stride;
+            primary_ray(*cf, (tile % src.tiles_x) * src.T + l % src.T, (tile / src.tiles_x) * src.T + l / src.T, o, d);
+            return;
+        }
         const uint32_t W = cf->width, py = local / W;
         primary_ray(*cf, local - py * W, py, o, d);
         return;
@@ -836,11 +845,18 @@ __global__ void __launch_bounds__(256) k_trace_primary(DevTree t, CamD cam, OutD
 // Pass 0 of a batch of frames (vhx_trace_primary_batch): frame f's 16x16 pixel blocks are blocks [f * nblocks_frame,
 // (f + 1) * nblocks_frame) of one launch (XCD-dealt like k_trace_primary), with the frame's camera and outputs read from
 // the batch arrays (block-uniform: scalar loads). Framebuffer layout; output index f * npix + y * width + x.
+// A batch of tile sets (vhx_trace_tiles_batch; tb.T > 0): frame f's blocks cover the T x T tiles starts[f] +
+// j * stride, j < the largest set's tile count, 16x16 blocks row-major inside a tile (k_trace_primary's tile layout);
+// output index f * npix + j * T * T + y * T + x inside the tile.
+struct TileB {
+    uint32_t T, tiles_x, ntiles, stride, bpx, bpt;
+    const uint32_t *starts;
+};
 template <int BD>
 __global__ void __launch_bounds__(256) k_trace_primary_batch(DevTree t, const CamD *__restrict__ cams,
                                                              const OutD *__restrict__ outs, uint32_t nblocks_frame,
                                                              uint32_t blocks_x, uint32_t npix, PassQ q,
-                                                             ListOrder lo = ListOrder{}) {
+                                                             ListOrder lo = ListOrder{}, TileB tb = TileB{}) {
     __shared__ uint64_t occ_tab[OCC_TAB_WORDS];
     fill_occ_tab(occ_tab);
     zero_ctl(q.zero);
@@ -849,18 +865,31 @@ __global__ void __launch_bounds__(256) k_trace_primary_batch(DevTree t, const Ca
     const uint32_t f = bid / nblocks_frame, sb = bid - f * nblocks_frame;
     const CamD cam = cams[f];
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-    uint32_t px, py;
-    if (lo.tx) {  // this frame's blocks in list order (k_trace_primary)
-        uint32_t bx, by;
-        list_block(lo, sb, bx, by);
-        px = bx * 16u + (wave & 1u) * 8u + compact_bits(lane);
-        py = by * 16u + (wave >> 1) * 8u + compact_bits(lane >> 1);
+    uint32_t px, py, local;
+    bool valid, entry;  // entry: the position has an output entry (its flag is written)
+    if (tb.T) {
+        const uint32_t j = sb / tb.bpt, sbb = sb - j * tb.bpt;
+        const uint32_t lx = (sbb % tb.bpx) * 16u + (wave & 1u) * 8u + (lane & 7u);
+        const uint32_t ly = (sbb / tb.bpx) * 16u + (wave >> 1) * 8u + (lane >> 3);
+        const uint32_t tile = tb.starts[f] + j * tb.stride;
+        px = (tile % tb.tiles_x) * tb.T + lx;
+        py = (tile / tb.tiles_x) * tb.T + ly;
+        entry = lx < tb.T && ly < tb.T;
+        valid = entry && tile < tb.ntiles && px < cam.width && py < cam.height;
+        local = (j * tb.T + ly) * tb.T + lx;
     } else {
-        px = (sb % blocks_x) * 16u + (wave & 1u) * 8u + (lane & 7u);
-        py = (sb / blocks_x) * 16u + (wave >> 1) * 8u + (lane >> 3);
+        if (lo.tx) {  // this frame's blocks in list order (k_trace_primary)
+            uint32_t bx, by;
+            list_block(lo, sb, bx, by);
+            px = bx * 16u + (wave & 1u) * 8u + compact_bits(lane);
+            py = by * 16u + (wave >> 1) * 8u + compact_bits(lane >> 1);
+        } else {
+            px = (sb % blocks_x) * 16u + (wave & 1u) * 8u + (lane & 7u);
+            py = (sb / blocks_x) * 16u + (wave >> 1) * 8u + (lane >> 3);
+        }
+        valid = entry = px < cam.width && py < cam.height;
+        local = py * cam.width + px;
     }
-    const bool valid = px < cam.width && py < cam.height;
-    const uint32_t local = py * cam.width + px;
     const uint64_t idx = (uint64_t)f * npix + local;
     bool done = true;
     if (valid) {
@@ -878,9 +907,10 @@ __global__ void __launch_bounds__(256) k_trace_primary_batch(DevTree t, const Ca
                                          nullptr, 0, q.qmode != 0);
         }
         if (done) store(t, outs[f], local, o, h);
-        if (q.flags) q.flags[idx] = done ? 0 : 1;
     }
-    if (lo.tx && q.tmp) wave_append(!done, (uint32_t)idx, q.tmp, q.counts, bid * 4u + wave);
+    // every entry gets its flag (a tile set's entries past the frame edge or past a smaller set's tiles: 0)
+    if (q.flags && entry) q.flags[idx] = done ? 0 : 1;
+    if ((lo.tx || lo.tl) && q.tmp) wave_append(!done, (uint32_t)idx, q.tmp, q.counts, bid * 4u + wave);
 }
 
 template <bool COUNT, int BD, bool MIP = false>
@@ -2500,20 +2530,34 @@ static int stage_slot(vhx_ctx *c, vhx_ctx::Pinned *ring, uint32_t &next, uint64_
     return VHX_OK;
 }
 
-int vhx_trace_primary_batch(vhx_ctx *c, const vhx_camera *cams, uint32_t n, const vhx_hits *outs) {
-    if (!c || !cams || !outs || n == 0) return VHX_E_INVALID_ARG;
-    if (!c->tree->uploaded) return fail(c, VHX_E_STATE, "vhx_trace_primary_batch before vhx_upload_tree");
+// A batch of whole frames (T == 0: vhx_trace_primary_batch) or of tile sets (T > 0: vhx_trace_tiles_batch; frame k is
+// the tiles starts[k], starts[k] + stride, ... of its camera's T x T tile grid, in the tile layout) as one pass ladder.
+static int trace_batch(vhx_ctx *c, const vhx_camera *cams, uint32_t n, const vhx_hits *outs, uint32_t T,
+                       const uint32_t *starts, uint32_t stride, const char *fn) {
+    if (!c || !cams || !outs || n == 0 || (T && (!starts || stride == 0 || T > 4096))) return VHX_E_INVALID_ARG;
+    if (!c->tree->uploaded) return fail(c, VHX_E_STATE, std::string(fn) + " before vhx_upload_tree");
     const uint32_t W = cams[0].width, H = cams[0].height;
     for (uint32_t k = 0; k < n; ++k) {
         if (cams[k].width != W || cams[k].height != H || W == 0 || H == 0 || cams[k].ray_model > VHX_RAY_GLASS)
-            return fail(c, VHX_E_INVALID_ARG, "vhx_trace_primary_batch: every frame needs one valid camera model and the "
+            return fail(c, VHX_E_INVALID_ARG, std::string(fn) + ": every frame needs one valid camera model and the "
                                               "same non-empty width x height");
         if (outs[k].bytes)
-            return fail(c, VHX_E_INVALID_ARG, "vhx_trace_primary_batch: byte counting is a vhx_trace_primary option");
+            return fail(c, VHX_E_INVALID_ARG, std::string(fn) + ": byte counting is a vhx_trace_primary option");
     }
-    const uint64_t npix = (uint64_t)W * H, nout = npix * n;
+    // per frame: its output entries (a tile set: its tiles' entries), the index stride between frames (npix) and the
+    // pass-0 workgroups (nbf)
+    const uint32_t tiles_x = T ? (W + T - 1) / T : 0u, ntiles = T ? tiles_x * ((H + T - 1) / T) : 0u;
+    const uint32_t bpx = T ? (T + 15) / 16 : 0u, bpt = bpx * bpx;
+    auto set_tiles = [&](uint32_t k) -> uint64_t {
+        return starts[k] >= ntiles ? 0ull : (uint64_t)(ntiles - starts[k] + stride - 1) / stride;
+    };
+    uint64_t max_tiles = 0;
+    if (T)
+        for (uint32_t k = 0; k < n; ++k) max_tiles = std::max(max_tiles, set_tiles(k));
+    if (T && max_tiles == 0) return VHX_OK;  // no frame holds a tile
+    const uint64_t npix = T ? max_tiles * T * T : (uint64_t)W * H, nout = npix * n;
     // the frames are traced concurrently: two frames writing one output range would leave a result that depends on the
-    // schedule instead of equalling n vhx_trace_primary calls
+    // schedule instead of equalling n single-frame calls
     {
         struct R {
             const char *p;
@@ -2522,20 +2566,21 @@ int vhx_trace_primary_batch(vhx_ctx *c, const vhx_camera *cams, uint32_t n, cons
         std::vector<R> rs;
         for (uint32_t k = 0; k < n; ++k) {
             const vhx_hits &o = outs[k];
+            const uint64_t ent = T ? set_tiles(k) * T * T : npix;
             const void *f[7] = {o.value, o.cell, o.rgba, o.depth, o.voxel, o.impact, o.normal};
             const uint64_t w[7] = {1, 1, 1, 1, 3, 3, 3};
             for (int j = 0; j < 7; ++j)
-                if (f[j]) rs.push_back({(const char *)f[j], npix * 4 * w[j]});
+                if (f[j] && ent) rs.push_back({(const char *)f[j], ent * 4 * w[j]});
         }
         std::sort(rs.begin(), rs.end(), [](const R &a, const R &b) { return a.p < b.p; });
         for (size_t i = 1; i < rs.size(); ++i)
             if (rs[i].p < rs[i - 1].p + rs[i - 1].bytes)
-                return fail(c, VHX_E_INVALID_ARG, "vhx_trace_primary_batch: output arrays overlap each other");
+                return fail(c, VHX_E_INVALID_ARG, std::string(fn) + ": output arrays overlap each other");
     }
     const uint32_t bx = (W + 15) / 16, by = (H + 15) / 16;
-    const uint64_t nbf = (uint64_t)bx * by, nblocks = nbf * n;
+    const uint64_t nbf = T ? max_tiles * bpt : (uint64_t)bx * by, nblocks = nbf * n;
     if (nout > 0x7FFFFFFFull || nblocks > 0x7FFFFFFFull)
-        return fail(c, VHX_E_INVALID_ARG, "vhx_trace_primary_batch: more than 2^31 rays in one batch");
+        return fail(c, VHX_E_INVALID_ARG, std::string(fn) + ": more than 2^31 rays in one batch");
     VHX_HIP(c, hipSetDevice(c->device));
     VHX_STREAM(c);
     TraceScope tscope(c);
@@ -2543,11 +2588,13 @@ int vhx_trace_primary_batch(vhx_ctx *c, const vhx_camera *cams, uint32_t n, cons
     if (rc) return rc;
     if ((rc = refresh_child_rec(c))) return rc;
     const DevTree t = dev_tree(c);
-    if (t.mips) return fail(c, VHX_E_INVALID_ARG, "vhx_trace_primary_batch: not available with node MIPs");
-    // the batch's cameras and outputs: packed into the next slot of the context's pinned staging ring, one copy to the
-    // device ahead of the launches on the context's stream (stage_slot: back-to-back batches on one context do not
-    // wait on the host until the ring wraps onto a copy that has not run)
-    const uint64_t cam_bytes = ((uint64_t)n * sizeof(CamD) + 255) & ~255ull, args_bytes = cam_bytes + (uint64_t)n * sizeof(OutD);
+    if (t.mips) return fail(c, VHX_E_INVALID_ARG, std::string(fn) + ": not available with node MIPs");
+    // the batch's cameras, outputs (and tile-set starts): packed into the next slot of the context's pinned staging ring,
+    // one copy to the device ahead of the launches on the context's stream (stage_slot: back-to-back batches on one
+    // context do not wait on the host until the ring wraps onto a copy that has not run)
+    const uint64_t cam_bytes = ((uint64_t)n * sizeof(CamD) + 255) & ~255ull;
+    const uint64_t out_bytes = ((uint64_t)n * sizeof(OutD) + 255) & ~255ull;
+    const uint64_t args_bytes = cam_bytes + out_bytes + (T ? (uint64_t)n * 4 : 0ull);
     vhx_ctx::Pinned *PP = nullptr;
     if ((rc = stage_slot(c, c->batch_pinned, c->batch_next, args_bytes, PP))) return rc;
     vhx_ctx::Pinned &P = *PP;
@@ -2561,6 +2608,7 @@ int vhx_trace_primary_batch(vhx_ctx *c, const vhx_camera *cams, uint32_t n, cons
         ho[k] = OutD{outs[k].value, outs[k].cell,   outs[k].voxel, outs[k].rgba,
                      nullptr,       outs[k].impact, outs[k].normal, outs[k].depth};
     }
+    if (T) std::memcpy((uint8_t *)P.ptr + cam_bytes + out_bytes, starts, (size_t)n * 4);
     uint32_t npass = 1;
     if ((rc = prepare_passes(c, nout, nblocks, npass, false, n > 1))) return rc;
     VHX_HIP(c, hipEventRecord(c->ev0, c->stream));
@@ -2569,18 +2617,29 @@ int vhx_trace_primary_batch(vhx_ctx *c, const vhx_camera *cams, uint32_t n, cons
     P.used = true;
     const CamD *dcams = (const CamD *)c->batch_args.ptr;
     const OutD *douts = (const OutD *)((const uint8_t *)c->batch_args.ptr + cam_bytes);
+    const uint32_t *dstarts = T ? (const uint32_t *)((const uint8_t *)c->batch_args.ptr + cam_bytes + out_bytes) : nullptr;
     RaySrc src{};
     src.kind = 4u;
     src.cams = dcams;
     src.outs = douts;
     src.npix = (uint32_t)npix;
+    src.T = T;
+    src.tiles_x = tiles_x;
+    src.tile_stride = stride;
+    src.starts = dstarts;
+    const TileB tb{T, tiles_x, ntiles, stride, bpx, bpt, dstarts};
     const CamD cd{};
     int qrc = VHX_OK;
-    // the frames' blocks over whole tiles of the list order (k_trace_primary), or flags in the flag order
+    // the frames' blocks over whole tiles of the list order (k_trace_primary), or flags in the flag order; a batch of
+    // tile sets lists its rays in its own block order (ListOrder::tl) or compacts flags in output-index order
     ListOrder lo{};
     uint64_t nbf0 = nbf;
-    const bool listed = c->p0lists && npass > 1 && list_order(c->qorder, W, H, lo, nbf0) && nbf0 * n * 4 <= 0x7FFFFFFFull;
+    bool listed = !T && c->p0lists && npass > 1 && list_order(c->qorder, W, H, lo, nbf0) && nbf0 * n * 4 <= 0x7FFFFFFFull;
     if (!listed) lo = ListOrder{}, nbf0 = nbf;
+    if (T && c->p0lists && c->tile_lists && npass > 1 && nbf * n * 4 <= 0x7FFFFFFFull) {
+        listed = true;
+        lo.tl = 1;
+    }
     if (listed && (rc = ensure_lists(c, nbf0 * n))) return rc;
     const bool qm = queue_state_mode(c, listed, false, npass);
     auto launch = [&](auto bd_tag) {
@@ -2591,19 +2650,29 @@ int vhx_trace_primary_batch(vhx_ctx *c, const vhx_camera *cams, uint32_t n, cons
         else if (npass > 1)
             q0.flags = (uint8_t *)c->flags.ptr;
         k_trace_primary_batch<BD><<<(unsigned)(nbf0 * n), 256, 0, c->stream>>>(t, dcams, douts, (uint32_t)nbf0, bx,
-                                                                               (uint32_t)npix, q0, lo);
+                                                                               (uint32_t)npix, q0, lo, tb);
         qrc = launch_queue_passes<false, BD>(c, t, cd, src, OutD{}, 1, npass, nout, nbf0 * n,
-                                             listed ? P0_ORDERED : P0_FLAGS, W, H, n, qm);
+                                             listed ? P0_ORDERED : P0_FLAGS, T ? 0u : W, H, n, qm);
     };
     if (!dispatch_bd(c->tree->desc.brick_dim, launch)) return fail(c, VHX_E_INVALID_ARG, "unsupported brick_dim");
     if (qrc) return qrc;
     VHX_HIP(c, hipGetLastError());
     // a shadow trace (or shadow batch) of these frames' hit records lists them in the same tile order
-    c->last_fb_w = W;
-    c->last_fb_h = H;
+    c->last_fb_w = T ? 0u : W;
+    c->last_fb_h = T ? 0u : H;
     VHX_HIP(c, hipEventRecord(c->ev1, c->stream));
     c->timed = true;
     return tscope.end();
+}
+
+int vhx_trace_primary_batch(vhx_ctx *c, const vhx_camera *cams, uint32_t n, const vhx_hits *outs) {
+    return trace_batch(c, cams, n, outs, 0, nullptr, 1, "vhx_trace_primary_batch");
+}
+
+int vhx_trace_tiles_batch(vhx_ctx *c, const vhx_camera *cams, uint32_t n, uint32_t tile_size, const uint32_t *tile_starts,
+                          uint32_t tile_stride, const vhx_hits *outs) {
+    if (tile_size == 0) return c ? fail(c, VHX_E_INVALID_ARG, "vhx_trace_tiles_batch: tile_size 0") : VHX_E_INVALID_ARG;
+    return trace_batch(c, cams, n, outs, tile_size, tile_starts, tile_stride, "vhx_trace_tiles_batch");
 }
 
 int vhx_chain_profile(vhx_ctx *c, const vhx_camera *cam, const uint32_t *pixels, uint32_t n, uint64_t *out) {

@@ -111,7 +111,8 @@ struct vhx_mgpu {
     DevBuf send[VHX_MGPU_MAX_INFLIGHT], gathered[VHX_MGPU_MAX_INFLIGHT];
     vhx_ctx *last = nullptr;  // the context of the last frame submitted
     DevBuf hdr;  // tree counts during the broadcast
-    uint64_t k = 0;  // frames submitted
+    uint64_t k = 0;   // frames submitted
+    uint64_t kb = 0;  // batches submitted (vhx_mgpu_render_batch: batch b is traced by context b % F)
 };
 
 #define VHX_NCCL(m, call)                                                                                          \
@@ -284,6 +285,7 @@ int vhx_mgpu_set_frames_in_flight(vhx_mgpu *m, uint32_t frames) {
     m->F = frames;
     m->S = frames < 2 ? 2u : frames;
     m->k = 0;
+    m->kb = 0;
     for (bool &u : m->used) u = false;
     return VHX_OK;
 }
@@ -430,6 +432,102 @@ int vhx_mgpu_render(vhx_mgpu *m, const vhx_camera *cam, uint32_t *fb_rgba, float
     m->used[slot] = true;
     ++m->k;
     if (!m->overlap) VHX_HIP(c, hipStreamWaitEvent(tc->stream, m->free_[slot], 0));
+    return VHX_OK;
+}
+
+// K frames as one batch (vhx_mgpu_render_batch): every frame's slot parts traced by ONE vhx_trace_tiles_batch (K x the
+// rank's slots entries) on the batch's context, then the K frames' transfers in one RCCL group on the communication
+// stream and rank 0's K untiles. Frame k of the batch uses ring slot (frames submitted + k) % VHX_MGPU_MAX_INFLIGHT;
+// a slot is rewritten only after the transfer that read it (events, as vhx_mgpu_render).
+int vhx_mgpu_render_batch(vhx_mgpu *m, const vhx_camera *cams, uint32_t K, uint32_t *const *fb_rgba,
+                          float *const *fb_depth) {
+    if (!m || !cams || K == 0 || K > VHX_MGPU_MAX_INFLIGHT) return VHX_E_INVALID_ARG;
+    vhx_ctx *c = m->ctx;
+    const uint32_t W = cams[0].width, H = cams[0].height;
+    for (uint32_t k = 0; k < K; ++k)
+        if (cams[k].width != W || cams[k].height != H || W == 0 || H == 0)
+            return fail(c, VHX_E_INVALID_ARG, "vhx_mgpu_render_batch: every frame needs the same non-empty width x height");
+    if (m->rank == 0) {
+        if (!fb_rgba) return fail(c, VHX_E_INVALID_ARG, "vhx_mgpu_render_batch: rank 0 needs framebuffers");
+        for (uint32_t k = 0; k < K; ++k)
+            if (!fb_rgba[k] || (m->planes == 1 && fb_depth && fb_depth[k]))
+                return fail(c, VHX_E_INVALID_ARG, "vhx_mgpu_render_batch: rank 0 needs an RGBA framebuffer per frame (and "
+                                                  "no depth with one plane)");
+    }
+    if (!c->tree->uploaded) return fail(c, VHX_E_STATE, "vhx_mgpu_render_batch before the tree is uploaded");
+    const Rccl &r = rccl();
+    VHX_HIP(c, hipSetDevice(c->device));
+    uint32_t ntiles, per, first, count;
+    tiles_of(m, W, H, ntiles, per);
+    rank_slots(m, m->rank, first, count);
+    const uint32_t V = slots_of(m);
+    const uint64_t n_out = (uint64_t)per * m->T * m->T;
+    const uint32_t P = m->planes;
+    const uint32_t NS = VHX_MGPU_MAX_INFLIGHT;
+    vhx_ctx *tc = m->kb % m->F == 0 ? c : m->extra[m->kb % m->F - 1];  // the context tracing this batch
+    if (tc != c) copy_sched(tc, c);
+    VHX_STREAM(tc);
+    std::vector<uint32_t> slots(K);
+    std::vector<vhx_camera> bc;
+    std::vector<uint32_t> bstart;
+    std::vector<vhx_hits> bh;
+    for (uint32_t k = 0; k < K; ++k) {
+        const uint32_t slot = (uint32_t)((m->k + k) % NS);
+        slots[k] = slot;
+        if (m->used[slot]) VHX_HIP(c, hipStreamWaitEvent(tc->stream, m->free_[slot], 0));
+        DevBuf &buf = m->rank == 0 ? m->gathered[slot] : m->send[slot];
+        const uint64_t need = n_out * 4 * P * (m->rank == 0 ? (uint64_t)V : 1u);
+        if (buf.bytes < need) {
+            int rc = vhx_mgpu_sync(m, nullptr);  // (re)allocation: no frame may still use the old buffers
+            if (rc) return rc;
+            if ((rc = ensure(c, buf, need))) return rc;
+        }
+        uint32_t *parts = (uint32_t *)buf.ptr;
+        for (uint32_t s = first; s < first + count && s < ntiles; ++s) {
+            vhx_hits h{};
+            h.rgba = parts + P * n_out * (s - first);
+            h.depth = P == 2 ? (float *)(h.rgba + n_out) : nullptr;
+            bc.push_back(cams[k]);
+            bstart.push_back(s);
+            bh.push_back(h);
+        }
+    }
+    if (!bc.empty()) {
+        const int rc = vhx_trace_tiles_batch(tc, bc.data(), (uint32_t)bc.size(), m->T, bstart.data(), V, bh.data());
+        if (rc) return tc == c ? rc : fail(c, rc, tc->err.c_str());
+    }
+    m->last = tc;
+    VHX_HIP(c, hipEventRecord(m->ready[slots[0]], tc->stream));
+    VHX_HIP(c, hipStreamWaitEvent(m->cstream, m->ready[slots[0]], 0));
+    if (m->nranks > 1) {
+        VHX_NCCL(m, r.GroupStart());
+        for (uint32_t k = 0; k < K; ++k) {
+            uint32_t *parts = (uint32_t *)(m->rank == 0 ? m->gathered[slots[k]] : m->send[slots[k]]).ptr;
+            if (m->rank == 0) {
+                for (int q = 1; q < m->nranks; ++q) {
+                    uint32_t qf, qc;
+                    rank_slots(m, q, qf, qc);
+                    VHX_NCCL_GROUP(m, r.Recv(parts + P * n_out * qf, P * n_out, ncclUint32, q, m->comm, m->cstream));
+                }
+            } else {
+                VHX_NCCL_GROUP(m, r.Send(parts, P * n_out, ncclUint32, 0, m->comm, m->cstream));
+            }
+        }
+        VHX_NCCL(m, r.GroupEnd());
+    }
+    for (uint32_t k = 0; k < K; ++k) {
+        if (m->rank == 0) {
+            const uint32_t *parts = (const uint32_t *)m->gathered[slots[k]].ptr;
+            const int rc = launch_untile(c, m->cstream, parts, P, V, per, m->T, W, H, fb_rgba[k],
+                                         fb_depth ? fb_depth[k] : nullptr);
+            if (rc) return rc;
+        }
+        VHX_HIP(c, hipEventRecord(m->free_[slots[k]], m->cstream));
+        m->used[slots[k]] = true;
+    }
+    m->k += K;
+    ++m->kb;
+    if (!m->overlap) VHX_HIP(c, hipStreamWaitEvent(tc->stream, m->free_[slots[K - 1]], 0));
     return VHX_OK;
 }
 

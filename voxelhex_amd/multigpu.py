@@ -182,6 +182,16 @@ class MgpuRenderer:
         p = lambda t: ctypes.c_void_p(None if t is None else t.data_ptr())
         self._check(N.lib().vhx_mgpu_render(self._h, ctypes.byref(cam), p(fb_rgba), p(fb_depth)))
 
+    def render_batch(self, cams, fb_rgba=None, fb_depth=None):
+        """Collective (vhx_mgpu_render_batch): the frames of `cams` as one batch; rank 0 passes lists of device
+        framebuffers (one per camera; fb_depth may be None), the other ranks None."""
+        n = len(cams)
+        cs = (N.Camera * n)(*cams)
+        arr = lambda ts: None if ts is None else ctypes.cast((ctypes.c_void_p * n)(*[t.data_ptr() for t in ts]),
+                                                             ctypes.c_void_p)
+        self._check(N.lib().vhx_mgpu_render_batch(self._h, ctypes.cast(cs, ctypes.c_void_p), n, arr(fb_rgba),
+                                                  arr(fb_depth)))
+
     def sync(self):
         ms = ctypes.c_float()
         self._check(N.lib().vhx_mgpu_sync(self._h, ctypes.byref(ms)))

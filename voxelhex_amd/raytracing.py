@@ -366,6 +366,29 @@ class Raytracer:
                                                     ctypes.cast(hs, ctypes.c_void_p)))
         return outs
 
+    def trace_tiles_batch(self, cams, tile_size, tile_starts, tile_stride, outs):
+        """vhx_trace_tiles_batch: frame k = the tile set tile_starts[k], +tile_stride, ... of cams[k] (tile layout) into
+        outs[k] (dicts of device tensors) as one pass ladder; equal to one trace_primary(layout=TILES) per frame."""
+        if len(cams) != len(outs) or len(cams) != len(tile_starts) or not cams:
+            raise ValueError("trace_tiles_batch: one output dict and one tile start per camera")
+        T = tile_size
+        ntiles = ((cams[0].width + T - 1) // T) * ((cams[0].height + T - 1) // T)
+        for st, out in zip(tile_starts, outs):
+            if _on_device(out) != 1:
+                raise ValueError("trace_tiles_batch writes device tensors")
+            n = max(0, (ntiles - st + tile_stride - 1) // tile_stride) * T * T
+            for name, dt, k in HIT_FIELDS:
+                a = out.get(name)
+                if a is not None and a.numel() * a.element_size() < n * k * 4:
+                    raise ValueError(f"out[{name!r}] holds {a.numel() * a.element_size()} bytes, the set needs {n * k * 4}")
+        cs = (N.Camera * len(cams))(*cams)
+        st = (ctypes.c_uint32 * len(cams))(*[int(v) for v in tile_starts])
+        hs = (N.Hits * len(outs))(*[_hits_struct(o) for o in outs])
+        self._check(N.lib().vhx_trace_tiles_batch(self._h, ctypes.cast(cs, ctypes.c_void_p), len(cams), T,
+                                                  ctypes.cast(st, ctypes.c_void_p), tile_stride,
+                                                  ctypes.cast(hs, ctypes.c_void_p)))
+        return outs
+
     def trace_shadows_batch(self, light, hits_list, shadowed_list=None, darken=True):
         """vhx_trace_shadows_batch: the hard shadows of several frames' device-resident hit records (dicts like
         trace_shadows' `hits`, the same record count each) as one pass ladder; returns the int32 `shadowed` tensors.
