@@ -11,7 +11,8 @@
  *   FRAMES     frames rendered, alternating camera A and B (A first), every one submitted without waiting
  *   MODE       "plain" | "balance" | "rgba" (plain with one plane: vhx_mgpu_set_planes(m, 1) on every rank, rank 0
  *              passes fb_depth = NULL, so its depth framebuffers keep their 0xAB fill; first a set_planes call with
- *              different counts on rank 0 and the others, which every rank must refuse)
+ *              different counts on rank 0 and the others, which every rank must refuse) | "batch" / "batchrgba" (plain /
+ *              rgba with the frames submitted as vhx_mgpu_render_batch calls of 3 frames)
  *   OUT_FILE   rank 0's framebuffers after the last frame of each camera: rgbaA | depthA | rgbaB | depthB
  * prints one line per rank (rays, measured trace / transfer ms, bytes into rank 0 per frame) and "root_slots R", then
  * "ok"; exit 1 on failure. */
@@ -30,7 +31,7 @@
 static vhx_tree_desc g_tree;
 static vhx_camera g_cam[2];
 static uint8_t g_id[VHX_MGPU_ID_BYTES];
-static int g_n, g_R, g_F, g_overlap, g_frames, g_balance, g_rgba;
+static int g_n, g_R, g_F, g_overlap, g_frames, g_balance, g_rgba, g_batch;
 static const char *g_out;
 
 typedef struct {
@@ -90,8 +91,25 @@ static void *rank_main(void *arg) {
                 goto done;
             }
     /* every frame submitted back to back: frames in flight on F contexts, gathers overlapping the next traces */
-    for (int k = 0; k < g_frames; ++k)
-        RCHECK(vhx_mgpu_render(m, &g_cam[k & 1], (uint32_t *)fb[k & 1], g_rgba ? NULL : (float *)fbd[k & 1]));
+    if (g_batch) {
+        /* batches of g_batch frames (the last one shorter); frame k still alternates the cameras and framebuffers */
+        for (int k0 = 0; k0 < g_frames; k0 += g_batch) {
+            vhx_camera bc[8];
+            uint32_t *bf[8];
+            float *bd[8];
+            const int nb = g_frames - k0 < g_batch ? g_frames - k0 : g_batch;
+            for (int j = 0; j < nb; ++j) {
+                bc[j] = g_cam[(k0 + j) & 1];
+                bf[j] = (uint32_t *)fb[(k0 + j) & 1];
+                bd[j] = (float *)fbd[(k0 + j) & 1];
+            }
+            RCHECK(vhx_mgpu_render_batch(m, bc, (uint32_t)nb, s->rank == 0 ? bf : NULL,
+                                         s->rank == 0 && !g_rgba ? bd : NULL));
+        }
+    } else {
+        for (int k = 0; k < g_frames; ++k)
+            RCHECK(vhx_mgpu_render(m, &g_cam[k & 1], (uint32_t *)fb[k & 1], g_rgba ? NULL : (float *)fbd[k & 1]));
+    }
     RCHECK(vhx_mgpu_sync(m, NULL));
     RCHECK(vhx_mgpu_info(m, g_cam[0].width, g_cam[0].height, NULL, NULL, &s->rays));
     RCHECK(vhx_mgpu_frame_bytes(m, g_cam[0].width, g_cam[0].height, &s->root_bytes));
@@ -147,7 +165,8 @@ int main(int argc, char **argv) {
     g_overlap = atoi(argv[7]);
     g_frames = atoi(argv[8]);
     g_balance = strcmp(argv[9], "balance") == 0;
-    g_rgba = strcmp(argv[9], "rgba") == 0;
+    g_rgba = strcmp(argv[9], "rgba") == 0 || strcmp(argv[9], "batchrgba") == 0;
+    g_batch = strncmp(argv[9], "batch", 5) == 0 ? 3 : 0;
     if (g_n < 1 || g_n > MAX_RANKS || g_frames < 2) return 1;
     FILE *f = fopen(argv[1], "rb");
     char magic[4];

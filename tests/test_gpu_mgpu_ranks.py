@@ -73,6 +73,10 @@ def scene(tmp_path_factory, oracle):
     (3, 1, 1, 1, 4, "balance"),
     (2, 1, 1, 1, 4, "rgba"),
     (8, 3, 2, 1, 5, "rgba"),
+    (2, 1, 1, 1, 5, "batch"),
+    (4, 2, 2, 1, 7, "batch"),
+    (8, 1, 3, 0, 6, "batchrgba"),
+    (3, 3, 2, 1, 4, "batchrgba"),
 ])
 def test_ranks_frames_equal_golden_and_oracle(scene, nranks, root_slots, inflight, overlap, frames, mode):
     _build()
@@ -97,9 +101,9 @@ def test_ranks_frames_equal_golden_and_oracle(scene, nranks, root_slots, infligh
     # one plane of 32-bit words per tile entry in RGBA-only mode, two otherwise
     root_bytes = {int(line.split("root_bytes ")[1].split()[0]) for line in r.stdout.splitlines() if "root_bytes" in line}
     plan = tile_plan(nranks, R, 64, W, H, 0)
-    planes = 1 if mode == "rgba" else 2
+    planes = 1 if mode in ("rgba", "batchrgba") else 2
     assert root_bytes == {(nranks - 1) * plan["tiles_per_slot"] * 64 * 64 * 4 * planes}, root_bytes
-    if mode == "rgba":  # no depth plane crossed: rank 0's depth framebuffers keep their fill
+    if mode in ("rgba", "batchrgba"):  # no depth plane crossed: rank 0's depth framebuffers keep their fill
         assert (fb[1] == 0xABABABAB).all() and (fb[3] == 0xABABABAB).all()
         return
     assert hashlib.sha256(fb[1].tobytes()).hexdigest() == sha["depth"], "camera A depth differs from golden"
