@@ -844,6 +844,27 @@ def main():
             R, a, g = mg.balance(cam, frames=4)
             split = {"root_slots": R, "rank0_trace_ms_one_slot": round(a, 4), "transfer_ms_one_slot": round(g, 4),
                      "source": "vhx_mgpu_balance"}
+            if K and world > 1:
+                # vhx_mgpu_balance models the split from single frames, whose per-slot trace is about twice a batched
+                # one's: with batches, time the candidate shares directly instead (untimed region, every
+                # rank the same R; 3 batches per candidate, the first one a warm-up) and keep the fastest
+                cand = {}
+                for r_try in range(1, N.VHX_MGPU_MAX_ROOT_SLOTS + 1):
+                    mg.set_root_slots(r_try)
+                    run(K, False)
+                    drain()
+                    dist.barrier()
+                    tc0 = time.perf_counter()
+                    run(2 * K, False)
+                    drain()
+                    dist.barrier()
+                    tt = torch.tensor([time.perf_counter() - tc0], dtype=torch.float64)
+                    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+                    cand[r_try] = round(float(tt.item()) * 1e3 / (2 * K), 4)
+                R = min(cand, key=lambda r_: (cand[r_] * (1.0 if r_ == 1 else 1.02), r_))  # R > 1 must win by 2 %
+                mg.set_root_slots(R)
+                split.update(root_slots=R, source="batched search (ms per frame by R; vhx_mgpu_balance's pick "
+                                                  f"was {split['root_slots']})", candidates_ms_per_frame=cand)
         # the buffers of the chosen split are allocated outside the timed region (every batch context's)
         for _ in range(F if K else 1):
             run(max(1, K), False)

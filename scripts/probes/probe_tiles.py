@@ -78,3 +78,31 @@ ms = (time.perf_counter() - t0) * 1e3 / 40
 print(f"{'vhx_mgpu one rank, RGBA plane, untile':52s} {ms:.4f} ms per frame  equal {bool(np.array_equal(fbr.cpu().numpy(), fbs))}",
       flush=True)
 mg.close()
+
+
+def run_batches(label, n_out, T_, start, stride, K, C, frames=42):
+    """batches of K tile sets (vhx_trace_tiles_batch) on C contexts round-robin"""
+    o = [outs(n_out) for _ in range(K)]  # K output sets per context slot (reused round-robin)
+    ctxs = rts[:C]
+    torch.cuda.synchronize()
+
+    def go(nb):
+        for b in range(nb):
+            r = ctxs[b % C]
+            oo = [o[j][b % C] for j in range(K)]
+            r.trace_tiles_batch([cam] * K, T_, [start] * K, stride, oo)
+
+    go(2 * C)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    nb = frames // K
+    go(nb)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) * 1e3 / (nb * K)
+    print(f"{label:52s} {ms:.4f} ms per frame  batches of {K} on {C} contexts", flush=True)
+
+
+if len(rts) >= 3:
+    for K, C in ((7, 3), (4, 2), (14, 2)):
+        run_batches(f"batched tile set, every tile", ntile, T, 0, 1, K, C)
+        run_batches(f"batched tile set of rank 0 of {NR}", nr, T, 0, NR, K, C)

@@ -280,8 +280,8 @@ def test_tiles_batch_equals_single_tile_traces(W, H, T, stride, starts, tune):
 
 def test_tiles_batch_argument_errors(gpu):
     import torch
-    gpu.upload(vhx.FlatTree.build_scene(N.VHX_SCENE_LATTICE_CUBE, 32, 4))
-    cams = _orbit(32, 64, 64, 2)
+    gpu.upload(vhx.FlatTree.build_scene(N.VHX_SCENE_LATTICE_CUBE, 64, 4))
+    cams = _orbit(64, 64, 64, 2)
     o = [_outs(64 * 64, ("rgba",)) for _ in cams]
     with pytest.raises(ValueError):
         gpu.trace_tiles_batch(cams, 16, (0,), 1, o)  # one start per camera
@@ -289,5 +289,13 @@ def test_tiles_batch_argument_errors(gpu):
     torch.cuda.synchronize()
     with pytest.raises(N.VhxError):
         gpu.trace_tiles_batch(cams, 16, (0, 0), 1, [shared, shared])  # both frames would write one array
-    with pytest.raises(N.VhxError):
+    with pytest.raises(ValueError):
         gpu.trace_tiles_batch(cams, 16, (0, 1), 0, o)  # stride 0
+    import ctypes
+    cs = (N.Camera * 2)(*cams)
+    st = (ctypes.c_uint32 * 2)(0, 1)
+    # the library refuses the same through the C ABI (stride 0, tile size 0)
+    assert N.lib().vhx_trace_tiles_batch(gpu._h, ctypes.cast(cs, ctypes.c_void_p), 2, 16, ctypes.cast(st, ctypes.c_void_p),
+                                         0, None) == N.VHX_E_INVALID_ARG
+    assert N.lib().vhx_trace_tiles_batch(gpu._h, ctypes.cast(cs, ctypes.c_void_p), 2, 0, ctypes.cast(st, ctypes.c_void_p),
+                                         1, None) == N.VHX_E_INVALID_ARG

@@ -372,6 +372,8 @@ class Raytracer:
         if len(cams) != len(outs) or len(cams) != len(tile_starts) or not cams:
             raise ValueError("trace_tiles_batch: one output dict and one tile start per camera")
         T = tile_size
+        if T < 1 or tile_stride < 1:
+            raise ValueError("trace_tiles_batch: tile_size and tile_stride must be >= 1")
         ntiles = ((cams[0].width + T - 1) // T) * ((cams[0].height + T - 1) // T)
         for st, out in zip(tile_starts, outs):
             if _on_device(out) != 1:
