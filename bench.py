@@ -72,6 +72,10 @@ def parse():
     p.add_argument("--tile", type=int, default=64)
     p.add_argument("--shadows", action="store_true",
                    help="config 5: each step = primary frame + one hard-shadow ray per hit toward (S,S,S)")
+    p.add_argument("--shadow-mode", choices=("fused", "separate"), default="fused",
+                   help="--shadows: 'fused' = the shadow rays run in the primary trace (vhx_set_shadow_light: a lane "
+                        "goes on with its hit's shadow ray), 'separate' = vhx_trace_primary then vhx_trace_shadows "
+                        "(_batch) on the same stream (DESIGN.md §8.1)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-roofline", action="store_true")
     p.add_argument("--no-frame-check", action="store_true",
@@ -549,7 +553,8 @@ def main():
         single = world_env == 1 and os.environ.get("VHX_BENCH_MGPU1") != "1"
         mgpu_path = (world_env > 1 or os.environ.get("VHX_BENCH_MGPU1") == "1") and args.mgpu == "vhx" and \
             os.environ.get("VHX_BENCH_REHEARSAL") != "1"
-        args.batch = 7 if ((single or mgpu_path) and args.inflight is None and not args.shadows and
+        args.batch = 7 if ((single or mgpu_path) and args.inflight is None and
+                           (not args.shadows or args.shadow_mode == "fused") and
                            args.depth_prepass is None and args.mip_lod is None) else 0
         if args.batch:
             args.inflight = 3
@@ -723,6 +728,10 @@ def main():
     if budgets is not None:
         for r in rts:
             r.set_pass_budgets(tuple(int(b) for b in budgets.split(",") if b.strip()))
+    fused = args.shadows and args.shadow_mode == "fused"
+    if fused:  # config 5 in the primary trace: every timed trace casts its hits' shadow rays
+        for r in rts:
+            r.set_shadow_light(light)
     K = args.batch if ((mg is None and world == 1) or mg is not None) else 0
     if args.batch and not K:
         raise SystemExit("--batch needs one GPU or the vhx_mgpu path (not --mgpu torch)")
@@ -776,7 +785,7 @@ def main():
             if pipe is not None:
                 o["rgba"] = pipe.out_buffer()
             r.trace_primary(cam_k, out=o, **trace_kw)
-            if args.shadows:
+            if args.shadows and not fused:
                 r.trace_shadows(light, o, shadowed=o["shadowed"])
         if timed and mg is None and not NOEV:
             e1.record(s_)  # the launch on its own stream (the gather runs on the communication stream)
@@ -804,7 +813,7 @@ def main():
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(s_)
         r.trace_primary_batch(cams_b, outs[f * K:f * K + nf])
-        if args.shadows:  # config 5: the batch's shadow rays, one more pass ladder on the same stream
+        if args.shadows and not fused:  # config 5: the batch's shadow rays, one more pass ladder on the same stream
             ob = outs[f * K:f * K + nf]
             r.trace_shadows_batch(light, ob, shadowed_list=[o["shadowed"] for o in ob])
         if timed and not NOEV:
@@ -895,6 +904,10 @@ def main():
     # the schedule the timed frames ran (adaptive by default: the frames-in-flight one once other contexts' frames are
     # in flight; vhx_get_pass_budgets), read before the untimed frames below
     sched_timed = None if mg is not None else rts[-1].pass_budgets()
+    if fused:
+        # the owner context traces the untimed reference frames, the isolated launches and the byte counts the separate
+        # way (vhx_trace_primary + vhx_trace_shadows): the frame check then compares fused with separate shadows
+        rt.set_shadow_light(None)
     frames_check = None
     if mg is None and world == 1 and not args.no_frame_check:
         frames_check = check_frames(args, rt, rts, outs, last_cam, light, W, H, dev)
@@ -1108,7 +1121,9 @@ def main():
                 "algorithmic_bytes_per_launch": launch_bytes, "tree_bytes_per_ray": round(tree_bytes / max(1, my_rays), 2)}
         if args.shadows:
             roof["shadow_tree_bytes_per_shadow_ray"] = round(shadow_bytes / max(1, n_sh), 2)
-            roof["kernel"] = ("primary frame (vhx_trace_primary) + its hard-shadow rays (vhx_trace_shadows: hit "
+            roof["kernel"] = ("primary frame with its hard-shadow rays fused into the same passes (vhx_set_shadow_light: "
+                              "a lane goes on with its hit's shadow ray; leftovers ride the queue passes)" if fused else
+                              "primary frame (vhx_trace_primary) + its hard-shadow rays (vhx_trace_shadows: hit "
                               "compaction, then the shadow queue passes), timed together on the trace stream")
         iss = None
         if measured and measured["valu"] > 0:
@@ -1194,6 +1209,7 @@ def main():
                                    + (f", {T}x{T} tiles round-robin over {world} ranks" if world > 1 else ""),
                        "workload_key": workload,
                        "shadow_rays_per_frame": n_shadow if args.shadows else None,
+                       "shadow_mode": args.shadow_mode if args.shadows else None,
                        "camera_orbit_rad_per_frame": args.orbit, "tree_size": args.size, "brick_dim": args.brick_dim, "width": W, "height": H,
                        "scene": args.scene, "tile": T if world > 1 else None, "parallelism": par,
                        **{k: v for k, v in tree_info.items() if k != "size"}, "build_s": round(build_s, 2), "upload_s": round(upload_s, 2)},

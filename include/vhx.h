@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define VHX_ABI_VERSION 5u
+#define VHX_ABI_VERSION 6u
 
 /* ---- error codes ------------------------------------------------------------------------------------------ */
 #define VHX_OK 0
@@ -118,7 +118,9 @@ typedef struct vhx_camera {
  *   depth  : |impact - origin| (V3c::length);                   miss: +inf
  *   rgba   : r | g<<8 | b<<16 | a<<24 shaded as examples/gpu_render.rs:236-249 (miss 128,128,128,255;
  *            a hit without albedo - where the example would unwrap() None - is 0,0,0,255)
- *   bytes  : algorithmic bytes touched by this ray (instrumentation; definition in DESIGN.md)            */
+ *   bytes  : algorithmic bytes touched by this ray (instrumentation; definition in DESIGN.md)
+ *   shadowed : with a shadow light set (vhx_set_shadow_light): 1 where the hit's hard-shadow ray hits a voxel (rgba
+ *            then darkened, rgb >> 1), 0 elsewhere (misses included)                                          */
 typedef struct vhx_hits {
     uint32_t *value;
     uint32_t *cell;
@@ -128,6 +130,7 @@ typedef struct vhx_hits {
     float *depth;
     uint32_t *rgba;
     uint32_t *bytes;
+    uint32_t *shadowed; /* ABI 6 */
 } vhx_hits;
 
 typedef struct vhx_ctx vhx_ctx;
@@ -262,6 +265,15 @@ int vhx_trace_tiles_batch(vhx_ctx *ctx, const vhx_camera *cams, uint32_t n, uint
  * be skipped: the pixels that differ from the exact path are measured in tests/test_gpu_fast.py and docs/DESIGN_LOG.md §10.
  * Other traces (tiles, ray batches, shadows, byte counting) stay exact. Default off. */
 int vhx_set_depth_prepass(vhx_ctx *ctx, int enable, float margin);
+/* Fused hard shadows (BASELINE config 5; shadow semantics of vhx_trace_shadows): with a light set, vhx_trace_primary,
+ * vhx_trace_primary_batch and vhx_trace_tiles_batch also trace every hit's hard-shadow ray and write `shadowed` (and
+ * darken `rgba`) of their outputs, which then need value, impact, normal and shadowed. Under the frames-in-flight /
+ * batch schedule (pass 0 lists its rays) the shadow ray continues in the lane and pass that finished its primary ray,
+ * while the nodes of its descent are still in that CU's caches; otherwise (a lone frame's schedule) the frame's shadow
+ * rays are traced after its primary rays, as vhx_trace_shadows does. Results equal vhx_trace_primary followed by
+ * vhx_trace_shadows bit for bit. light = NULL turns it off (the default). No byte counting, depth prepass or node
+ * MIPs with a light set. */
+int vhx_set_shadow_light(vhx_ctx *ctx, const float *light);
 /* MIP stand-ins for absent children (the WGSL path's probe_MIP, src/raytracing/bevy/viewport_render.wgsl:328-364,
  * 438-454, enabled by tree_properties bit 16, streaming/mod.rs:288-290): node_mips[i] is node i's MIP brick descriptor
  * (same encoding as a leaf's child entry, VHX_EMPTY = none; the bricks live in voxels / solid_values like any other,

@@ -1,6 +1,7 @@
 #!/bin/bash
 # A/B of vhx_set_tuning specs on one box: the GPU tests first (FIRST = -k expression, skipped when empty), then for each
-# spec in SPECS (";"-separated specs, "|"-separated; "-" = defaults) the bench with BENCH_ARGS, twice in alternation.
+# spec in SPECS (";"-separated specs, "|"-separated; "-" = defaults; "+<args>" = extra bench arguments instead of a tuning
+# spec, e.g. "+--shadow-mode separate") the bench with BENCH_ARGS, twice in alternation.
 # Every GPU step under its own time limit; stops at the first failure. usage: TAG=x SPECS="-|qstate=0" gpu_ab.sh
 cd "$GRAFT_REPO_ROOT" || exit 1
 D=gpurun_out/${TAG:-ab}; mkdir -p "$D"
@@ -13,7 +14,7 @@ IFS='|' read -ra S <<< "${SPECS:--}"
 for rep in 1 2; do
   for k in "${!S[@]}"; do
     spec=${S[$k]}
-    if [ "$spec" = "-" ]; then a=""; else a="--tune $spec"; fi
+    if [ "$spec" = "-" ]; then a=""; elif [ "${spec:0:1}" = "+" ]; then a="${spec:1}"; else a="--tune $spec"; fi
     timeout -k 10 300 python3 bench.py --steps ${STEPS:-100} --warmup 10 --no-cpu-baseline --no-extra --no-pmc $BENCH_ARGS $a > $D/b${k}_$rep.log 2>&1 || { echo "bench $spec failed"; tail -5 $D/b${k}_$rep.log; exit 1; }
     python3 - "$D/b${k}_$rep.log" "$spec" <<'PY'
 import json, sys

@@ -118,7 +118,7 @@ int main(int argc, char **argv) {
     uint32_t *value = malloc(4 * n), *cell = malloc(4 * n), *voxel = malloc(12 * n), *rgba = malloc(4 * n);
     float *impact = malloc(12 * n), *normal = malloc(12 * n), *depth = malloc(4 * n);
     if (!value || !cell || !voxel || !rgba || !impact || !normal || !depth) return 1;
-    vhx_hits h = {value, cell, voxel, impact, normal, depth, rgba, NULL};
+    vhx_hits h = {value, cell, voxel, impact, normal, depth, rgba, NULL, NULL};
     CHECK(vhx_trace_primary(ctx, &cam, 0, 0, 1, VHX_LAYOUT_FRAMEBUFFER, &h, 0));
     float ms = 0.0f;
     CHECK(vhx_sync(ctx, &ms));
@@ -150,7 +150,7 @@ int main(int argc, char **argv) {
         for (int k = 0; k < NB; ++k) {
             bc[k] = cam;
             vhx_hits z = {(uint32_t *)dv[k], NULL, NULL, k < 2 ? (float *)di[k] : NULL, k < 2 ? (float *)dn[k] : NULL,
-                          (float *)dd[k], (uint32_t *)dr[k], NULL};
+                          (float *)dd[k], (uint32_t *)dr[k], NULL, NULL};
             bh[k] = z;
         }
         CHECK(vhx_trace_primary_batch(ctx, bc, 3, bh));
@@ -194,7 +194,7 @@ int main(int argc, char **argv) {
     uint32_t *value2 = malloc(4 * n), *rgba2 = malloc(4 * n);
     float *depth2 = malloc(4 * n);
     if (!value2 || !rgba2 || !depth2) return 1;
-    vhx_hits h2 = {value2, NULL, NULL, NULL, NULL, depth2, rgba2, NULL};
+    vhx_hits h2 = {value2, NULL, NULL, NULL, NULL, depth2, rgba2, NULL, NULL};
     CHECK(vhx_trace_primary(sh, &cam, 0, 0, 1, VHX_LAYOUT_FRAMEBUFFER, &h2, 0));
     const int shared_equal = !memcmp(value, value2, 4 * n) && !memcmp(rgba, rgba2, 4 * n) && !memcmp(depth, depth2, 4 * n);
     printf("shared_equal %d\n", shared_equal);

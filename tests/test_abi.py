@@ -39,10 +39,10 @@ def test_integration_binds_every_declared_function():
 
 
 def test_abi_version_and_struct_sizes():
-    assert N.lib().vhx_abi_version() == 5
+    assert N.lib().vhx_abi_version() == 6
     assert ctypes.sizeof(N.TreeDesc) == 8 * 4 + 7 * 8
     assert ctypes.sizeof(N.Camera) == 4 * 4 + 4 * 12 + 8 + 64
-    assert ctypes.sizeof(N.Hits) == 8 * 8
+    assert ctypes.sizeof(N.Hits) == 9 * 8
 
 
 def test_gpu_entry_points_fail_cleanly_without_a_device():

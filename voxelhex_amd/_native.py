@@ -80,6 +80,7 @@ class Hits(ctypes.Structure):
     _fields_ = [
         ("value", c_void_p), ("cell", c_void_p), ("voxel", c_void_p), ("impact", c_void_p),
         ("normal", c_void_p), ("depth", c_void_p), ("rgba", c_void_p), ("bytes", c_void_p),
+        ("shadowed", c_void_p),  # ABI 6
     ]
 
 
@@ -110,6 +111,7 @@ SIGNATURES = [
     ("vhx_update_range", c_int, [c_void_p, c_int, c_u64, c_u64, c_void_p]),
     ("vhx_update_ranges", c_int, [c_void_p, c_void_p, c_u32]),
     ("vhx_set_depth_prepass", c_int, [c_void_p, c_int, ctypes.c_float]),
+    ("vhx_set_shadow_light", c_int, [c_void_p, c_void_p]),
     ("vhx_read_derived", c_int, [c_void_p, c_int, c_u64, c_u64, c_void_p]),
     ("vhx_tree_device_bytes", c_int, [c_void_p, P(c_u64)]),
     ("vhx_trace_primary", c_int, [c_void_p, P(Camera), c_u32, c_u32, c_u32, c_u32, P(Hits), c_int]),

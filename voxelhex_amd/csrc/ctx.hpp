@@ -120,6 +120,10 @@ struct vhx_ctx {
     hipStream_t upd_stream = nullptr;  // the stream of the last scatter (reads upd)
     // depth-prepass mode (vhx_set_depth_prepass; opt-in, not the reference path)
     bool prepass = false, in_prepass = false;
+    // fused hard shadows (vhx_set_shadow_light): each hit's shadow ray traced in the lane that finished its primary ray
+    bool shadow_on = false;
+    float shadow_light[3] = {0.f, 0.f, 0.f};
+    bool keep_ev0 = false;  // the shadow rays of a frame traced after it: its time runs from the primary trace's ev0
     float prepass_margin = 0.0f;
     DevBuf prepass_depth;  // the half-resolution depth frame
     // Ray schedule of a trace: step budgets of the passes before the final (unbounded) one, the sparse-wave thresholds

@@ -151,6 +151,7 @@ struct CamD {
 struct OutD {
     uint32_t *value, *cell, *voxel, *rgba, *bytes;
     float *impact, *normal, *depth;
+    uint32_t *shadowed;  // fused hard shadows (vhx_set_shadow_light)
 };
 
 // examples/gpu_render.rs:199, 236-251
@@ -271,6 +272,7 @@ struct PassQ {
     uint32_t qxcd;       // queue passes: runs of this many chunks dealt over the 8 XCDs, one counter each (0 = off)
     uint32_t sparse;     // budgeted passes with saved state: abandon a wave's rays once fewer lanes trace (0 = off)
     uint32_t *zero;      // pass 0 with block lists: the queue passes' work counters, zeroed by workgroup 0
+    float lx, ly, lz;    // fused hard shadows (the FUSE kernels): the light
 };
 
 // Rays per wave of a queue pass over n rays: fixed, or (rpw == 0) as many as spread the pass over about `tw` waves.
@@ -779,7 +781,45 @@ __device__ __forceinline__ void zero_ctl(uint32_t *zero) {
         for (uint32_t w = threadIdx.x; w < QCTL_WORDS - 16u; w += blockDim.x) zero[w] = 0u;
 }
 
-template <bool COUNT, int BD, bool FAST = false, bool MIP = false>
+// Fused hard shadows (vhx_set_shadow_light; the FUSE instantiations, BASELINE config 5): a lane whose primary ray
+// finished goes on, in the same pass, with the hit's shadow ray -- the shadow semantics of vhx_trace_shadows (from
+// impact + normal * 1e-3 toward the light) -- while the nodes of the hit's descent are still in this
+// CU's caches. A shadow ray abandoned at the pass budget saves its state at its pixel's index (the primary ray's is
+// done by then) and is listed with VHX_QSHADOW; a queue pass recomputes its ray from the stored hit record.
+#define VHX_QSHADOW 0x80000000u
+__device__ __forceinline__ void hit_shadow_ray(const PassQ &q, float ix, float iy, float iz, float nx, float ny,
+                                               float nz, F3d &o, F3d &d) {
+    o = mk(ix + nx * 1e-3f, iy + ny * 1e-3f, iz + nz * 1e-3f);  // shadow_ray's op order
+    d = vnorm(mk(q.lx - o.x, q.ly - o.y, q.lz - o.z));
+}
+__device__ __forceinline__ void store_fused_shadow(const OutD &o, uint64_t i, bool shadowed) {
+    o.shadowed[i] = shadowed ? 1u : 0u;  // store_shadow's darkening
+    if (shadowed && o.rgba) o.rgba[i] = ((o.rgba[i] >> 1) & 0x007F7F7Fu) | (o.rgba[i] & 0xFF000000u);
+}
+// the steps a pass's budget leaves a shadow ray started after a primary ray that used `used` of them (at least 1;
+// any split is bit-identical, the traversal being deterministic)
+__device__ __forceinline__ uint32_t rest_budget(uint32_t budget, uint32_t used) {
+    return budget >= VHX_MAX_ITERS ? budget : (budget > used + 1u ? budget - used : 1u);
+}
+// the shadow continuation of a finished primary ray h (output entry li of o, state index sidx); false: abandoned
+template <int BD>
+__device__ __forceinline__ bool fused_shadow(const DevTree &t, const uint64_t *occ_tab, const PassQ &q, const OutD &o,
+                                             uint64_t li, const HitOut &h, uint32_t sidx) {
+    if (!h.hit) {
+        o.shadowed[li] = 0u;
+        return true;
+    }
+    F3d so, sd;
+    hit_shadow_ray(q, h.ix, h.iy, h.iz, h.nx, h.ny, h.nz, so, sd);
+    HitOut hs;
+    hs.bytes = 0;
+    const bool fin =
+        get_by_ray<false, BD>(t, occ_tab, so, sd, hs, rest_budget(q.budget, h.iters), q.state, sidx, false, 0.0f, q.sparse);
+    if (fin) store_fused_shadow(o, li, hs.hit);
+    return fin;
+}
+
+template <bool COUNT, int BD, bool FAST = false, bool MIP = false, bool FUSE = false>
 __global__ void __launch_bounds__(256) k_trace_primary(DevTree t, CamD cam, OutD out, uint32_t T, uint32_t tiles_x,
                                                        uint32_t tile_start, uint32_t tile_stride, uint32_t layout,
                                                        uint32_t blocks_per_tile_x, uint32_t blocks_per_tile,
@@ -813,6 +853,7 @@ __global__ void __launch_bounds__(256) k_trace_primary(DevTree t, CamD cam, OutD
     const uint64_t idx = layout == VHX_LAYOUT_FRAMEBUFFER ? (uint64_t)py * cam.width + px
                                                           : (uint64_t)j * T * T + (uint64_t)ly * T + lx;
     bool done = true;
+    uint32_t tag = 0u;  // FUSE: VHX_QSHADOW when the ray left over is the hit's shadow ray
     if (valid) {
         F3d o, d;
         HitOut h;
@@ -829,17 +870,22 @@ __global__ void __launch_bounds__(256) k_trace_primary(DevTree t, CamD cam, OutD
                                                     q.qmode ? (bid * 4u + wave) * 64u : (uint32_t)idx, false, start,
                                                     q.sparse, nullptr, 0, q.qmode != 0);
         }
-        if (done)
+        if (done) {
             store(t, out, idx, o, h);
-        else if (COUNT && q.state)
+            if (FUSE && !fused_shadow<BD>(t, occ_tab, q, out, idx, h, (uint32_t)idx)) {
+                done = false;
+                tag = VHX_QSHADOW;
+            }
+        } else if (COUNT && q.state) {
             out.bytes[idx] = h.bytes;  // the running count, continued by the pass that resumes the ray
+        }
     }
     // every entry of the output gets its flag, so the flags need no clearing between frames: in the tile layout
     // every in-tile entry (frame padding included, done = true there); in the framebuffer layout only pixels of the
     // frame (a lane past the frame edge has no entry of its own: its idx aliases the next row or runs past the end)
     if (q.flags && (layout == VHX_LAYOUT_FRAMEBUFFER ? valid : (lx < T && ly < T)))
         q.flags[idx] = done ? 0 : 1;
-    if ((lo.tx || lo.tl) && q.tmp) wave_append(!done, (uint32_t)idx, q.tmp, q.counts, bid * 4u + wave);
+    if ((lo.tx || lo.tl) && q.tmp) wave_append(!done, (uint32_t)idx | tag, q.tmp, q.counts, bid * 4u + wave);
 }
 
 // Pass 0 of a batch of frames (vhx_trace_primary_batch): frame f's 16x16 pixel blocks are blocks [f * nblocks_frame,
@@ -852,7 +898,7 @@ struct TileB {
     uint32_t T, tiles_x, ntiles, stride, bpx, bpt;
     const uint32_t *starts;
 };
-template <int BD>
+template <int BD, bool FUSE = false>
 __global__ void __launch_bounds__(256) k_trace_primary_batch(DevTree t, const CamD *__restrict__ cams,
                                                              const OutD *__restrict__ outs, uint32_t nblocks_frame,
                                                              uint32_t blocks_x, uint32_t npix, PassQ q,
@@ -892,6 +938,7 @@ __global__ void __launch_bounds__(256) k_trace_primary_batch(DevTree t, const Ca
     }
     const uint64_t idx = (uint64_t)f * npix + local;
     bool done = true;
+    uint32_t tag = 0u;  // FUSE: VHX_QSHADOW when the ray left over is the hit's shadow ray
     if (valid) {
         F3d o, d;
         HitOut h;
@@ -906,11 +953,17 @@ __global__ void __launch_bounds__(256) k_trace_primary_batch(DevTree t, const Ca
                                          q.qmode ? (bid * 4u + wave) * 64u : (uint32_t)idx, false, 0.0f, q.sparse,
                                          nullptr, 0, q.qmode != 0);
         }
-        if (done) store(t, outs[f], local, o, h);
+        if (done) {
+            store(t, outs[f], local, o, h);
+            if (FUSE && !fused_shadow<BD>(t, occ_tab, q, outs[f], local, h, (uint32_t)idx)) {
+                done = false;
+                tag = VHX_QSHADOW;
+            }
+        }
     }
     // every entry gets its flag (a tile set's entries past the frame edge or past a smaller set's tiles: 0)
     if (q.flags && entry) q.flags[idx] = done ? 0 : 1;
-    if ((lo.tx || lo.tl) && q.tmp) wave_append(!done, (uint32_t)idx, q.tmp, q.counts, bid * 4u + wave);
+    if ((lo.tx || lo.tl) && q.tmp) wave_append(!done, (uint32_t)idx | tag, q.tmp, q.counts, bid * 4u + wave);
 }
 
 template <bool COUNT, int BD, bool MIP = false>
@@ -987,7 +1040,7 @@ __global__ void k_put_queue_args(QueueArgs a, QueueArgs *dst) {
     if (threadIdx.x == 0) *dst = a;
 }
 
-template <bool COUNT, int BD, bool MIP = false>
+template <bool COUNT, int BD, bool MIP = false, bool FUSE = false>
 __global__ void __launch_bounds__(256) VHX_QUEUE_ATTR k_trace_queue(DevTree t, const QueueArgs *qa, const uint32_t *__restrict__ in,
                                                      const uint32_t *in_n, uint32_t *grab, PassQ q) {
     __shared__ uint64_t occ_tab[OCC_TAB_WORDS];
@@ -1034,13 +1087,33 @@ __global__ void __launch_bounds__(256) VHX_QUEUE_ATTR k_trace_queue(DevTree t, c
         }
         const uint32_t i = base + lane;
         bool push = false;
-        uint32_t idx = 0;
+        uint32_t idx = 0, tag = 0;
         if (lane < rpw && i < n) {
             idx = in[i];
             F3d o, d;
             const QueueArgs *a = qa;
             asm volatile("" : "+s"(a));  // loads through `a` stay here (not hoisted into live registers)
-            ray_of(a->cam, a->src, idx, o, d);
+            // FUSE: the entry's frame outputs (a batch's frame, or the frame's); a shadow entry's ray from its hit record
+            bool sh = false;
+            OutD fo{};
+            uint64_t li = 0;
+            if (FUSE) {
+                sh = (idx & VHX_QSHADOW) != 0u;
+                idx &= ~VHX_QSHADOW;
+                if (a->src.kind == 4u) {
+                    const uint32_t f = idx / a->src.npix;
+                    fo = a->src.outs[f];
+                    li = idx - f * a->src.npix;
+                } else {
+                    fo = a->out;
+                    li = idx;
+                }
+            }
+            if (FUSE && sh)
+                hit_shadow_ray(q, fo.impact[3 * li], fo.impact[3 * li + 1], fo.impact[3 * li + 2], fo.normal[3 * li],
+                               fo.normal[3 * li + 1], fo.normal[3 * li + 2], o, d);
+            else
+                ray_of(a->cam, a->src, idx, o, d);
             HitOut h;
             h.bytes = COUNT && q.resume ? a->out.bytes[idx] : 0u;
             // queue-state mode: resumed from queue position i, abandoned into this chunk's list slots (base = chunk *
@@ -1052,7 +1125,18 @@ __global__ void __launch_bounds__(256) VHX_QUEUE_ATTR k_trace_queue(DevTree t, c
             asm volatile("" : "+s"(b));
             if (!fin) {
                 push = true;
+                tag = FUSE && sh ? VHX_QSHADOW : 0u;
                 if (COUNT && q.state) b->out.bytes[idx] = h.bytes;
+            } else if (FUSE) {
+                if (sh) {
+                    store_fused_shadow(fo, li, h.hit);
+                } else {  // a primary ray finished here: its shadow ray goes on in this lane
+                    store(t, fo, li, o, h);
+                    if (!fused_shadow<BD>(t, occ_tab, q, fo, li, h, idx)) {
+                        push = true;
+                        tag = VHX_QSHADOW;
+                    }
+                }
             } else if (b->src.kind == 3u) {
                 store_shadow(b->out, idx, h);
             } else if (b->src.kind == 5u) {
@@ -1071,7 +1155,7 @@ __global__ void __launch_bounds__(256) VHX_QUEUE_ATTR k_trace_queue(DevTree t, c
         if (q.tmp) {  // this chunk's abandoned rays, in lane order
             const uint32_t chunk = base / rpw;
             const uint64_t m = __ballot(push);
-            if (push) q.tmp[(uint64_t)chunk * rpw + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = idx;
+            if (push) q.tmp[(uint64_t)chunk * rpw + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = idx | tag;
             if (lane == 0) q.counts[chunk] = (uint32_t)__popcll(m);
         }
     }
@@ -1364,7 +1448,8 @@ static int map_out(vhx_ctx *c, const vhx_hits *h, uint64_t n, int on_device, Hos
     } fields[] = {{h->value, 4, (void **)&ho.dev.value},   {h->cell, 4, (void **)&ho.dev.cell},
                   {h->voxel, 12, (void **)&ho.dev.voxel},  {h->impact, 12, (void **)&ho.dev.impact},
                   {h->normal, 12, (void **)&ho.dev.normal}, {h->depth, 4, (void **)&ho.dev.depth},
-                  {h->rgba, 4, (void **)&ho.dev.rgba},     {h->bytes, 4, (void **)&ho.dev.bytes}};
+                  {h->rgba, 4, (void **)&ho.dev.rgba},     {h->bytes, 4, (void **)&ho.dev.bytes},
+                  {h->shadowed, 4, (void **)&ho.dev.shadowed}};
     if (on_device) {
         for (auto &f : fields) *f.dst = f.user;
         return VHX_OK;
@@ -1481,6 +1566,9 @@ static PassQ pass_q(const vhx_ctx *c, uint32_t p, uint32_t npass, bool qm = fals
     q.sparse = last || !q.state ? 0u : c->sparse[p];
     q.qmode = qm && q.state ? 1u : 0u;
     q.sin = q.qmode ? (const uint4 *)c->stateq.ptr : nullptr;
+    q.lx = c->shadow_light[0];
+    q.ly = c->shadow_light[1];
+    q.lz = c->shadow_light[2];
     return q;
 }
 
@@ -1488,7 +1576,9 @@ static PassQ pass_q(const vhx_ctx *c, uint32_t p, uint32_t npass, bool qm = fals
 // (listed: the ordered primary pass 0; first_queue: pass 0 is itself a queue pass, the shadow path), every pass saves
 // (save_from 0, resume on), and no queue is node-sorted (the sort reorders a queue by the states at output indices)
 static bool queue_state_mode(const vhx_ctx *c, bool listed, bool first_queue, uint32_t npass) {
-    if (!c->qstate || !c->resume || c->save_from != 0 || npass < 2 || !(listed || first_queue)) return false;
+    // (fused shadows keep states at output indices: a pixel's primary and shadow ray are never pending together)
+    if (!c->qstate || !c->resume || c->save_from != 0 || npass < 2 || !(listed || first_queue) || c->shadow_on)
+        return false;
     if (!c->stateq.ptr) return false;
     for (uint32_t p = 1; p < npass && p < 32u; ++p)
         if (c->qsort && ((c->qsort_passes >> p) & 1u)) return false;
@@ -1635,7 +1725,7 @@ static int put_qargs(vhx_ctx *c, const CamD &cam, const RaySrc &src, const OutD 
 // its per-workgroup lists (P0_LISTS, in workgroup order; P0_ORDERED, already in the queue order, ListOrder), or its
 // per-ray flags in the queue order (P0_FLAGS).
 enum { P0_LISTS = 0, P0_FLAGS = 1, P0_ORDERED = 2 };
-template <bool COUNT, int BD, bool MIP = false>
+template <bool COUNT, int BD, bool MIP = false, bool FUSE = false>
 static int launch_queue_passes(vhx_ctx *c, const DevTree &t, const CamD &cam, const RaySrc &src, const OutD &o,
                                uint32_t first, uint32_t npass, uint64_t nout, uint64_t nblocks0,
                                int pass0 = P0_LISTS, uint32_t order_w = 0, uint32_t order_h = 0,
@@ -1678,7 +1768,7 @@ static int launch_queue_passes(vhx_ctx *c, const DevTree &t, const CamD &cam, co
         // the waves in flight
         if (frames > 1 && p > 0) qwaves = (uint32_t)std::min<uint64_t>((uint64_t)qwaves * frames, 20ull * c->cus);
         const unsigned qgrid = (qwaves * 64u + c->qblock - 1) / c->qblock;
-        k_trace_queue<COUNT, BD, MIP><<<qgrid, c->qblock, 0, c->stream>>>(t, qa, in, in_n,
+        k_trace_queue<COUNT, BD, MIP, FUSE><<<qgrid, c->qblock, 0, c->stream>>>(t, qa, in, in_n,
                                                                          ctl + 16u + QCTL_PASS_WORDS * p, q);
         debug_passes(c, "queue pass");
         if (p + 1 < npass) {
@@ -2148,6 +2238,8 @@ void vhx::copy_sched(vhx_ctx *c, const vhx_ctx *owner) {
     std::memcpy(c->sparse, owner->sparse, sizeof(c->sparse));
     c->prepass = owner->prepass;
     c->prepass_margin = owner->prepass_margin;
+    c->shadow_on = owner->shadow_on;
+    std::memcpy(c->shadow_light, owner->shadow_light, sizeof(c->shadow_light));
 }
 
 extern "C" {
@@ -2394,6 +2486,11 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
     if (t.mips && (out->bytes || (c->prepass && !c->in_prepass)))
         return fail(c, VHX_E_INVALID_ARG, "vhx_trace_primary: byte counting and the depth prepass are not available "
                                           "with node MIPs (vhx_set_node_mips)");
+    // fused hard shadows (vhx_set_shadow_light): the shadow rays start from the stored hit records
+    const bool shadows = c->shadow_on && !c->in_prepass;
+    if (shadows && (!out->value || !out->impact || !out->normal || !out->shadowed || out->bytes || t.mips || c->prepass))
+        return fail(c, VHX_E_INVALID_ARG, "vhx_trace_primary with a shadow light: value, impact, normal and shadowed "
+                                          "outputs needed; no byte counting, node MIPs or depth prepass");
     const CamD cd = cam_of(cam);
     uint32_t npass = 1;
     rc = prepare_passes(c, nout, nblocks, npass);
@@ -2472,6 +2569,9 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
     if ((listed ? nb0 * 4 : nb0) > 0x7FFFFFFFull) return fail(c, VHX_E_INVALID_ARG, "frame too large");
     const int p0 = listed ? P0_ORDERED : P0_FLAGS;
     const bool qm = queue_state_mode(c, listed, false, npass);
+    // shadows fuse into the ladder where pass 0 lists its rays (the list entries carry the shadow tag); a single pass
+    // or the lone frame's flag compaction traces them after the primary rays instead (below)
+    const bool fuse = shadows && listed && npass > 1;
     auto launch = [&](auto bd_tag) {
         constexpr int BD = decltype(bd_tag)::value;
         PassQ q0 = pass_q(c, 0, npass, qm);
@@ -2488,10 +2588,15 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
             k_trace_primary<true, BD><<<g0, 256, 0, c->stream>>>(
                 t, cd, ho.dev, T, tiles_x, tile_start, tile_stride, layout, bpx, bpt, q0, FastD{}, lo);
             qrc = launch_queue_passes<true, BD>(c, t, cd, src, ho.dev, 1, npass, nout, nb0, p0, ow, oh, 1, qm);
+        } else if (fuse) {  // listed pass 0 and queue passes with the shadow continuations
+            k_trace_primary<false, BD, false, false, true><<<g0, 256, 0, c->stream>>>(
+                t, cd, ho.dev, T, tiles_x, tile_start, tile_stride, layout, bpx, bpt, q0, FastD{}, lo);
+            qrc = launch_queue_passes<false, BD, false, true>(c, t, cd, src, ho.dev, 1, npass, nout, nb0, p0, ow, oh, 1,
+                                                              qm);
         } else {
             if (fast)
                 k_trace_primary<false, BD, true><<<g0, 256, 0, c->stream>>>(
-                    t, cd, ho.dev, T, tiles_x, tile_start, tile_stride, layout, bpx, bpt, q0, fd, lo);
+                    t, cd, ho.dev, T, tiles_x, tile_start, tile_stride, layout, bpx, bpt, q0, FastD{}, lo);
             else
                 k_trace_primary<false, BD><<<g0, 256, 0, c->stream>>>(
                     t, cd, ho.dev, T, tiles_x, tile_start, tile_stride, layout, bpx, bpt, q0, FastD{}, lo);
@@ -2509,6 +2614,15 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
     VHX_HIP(c, hipEventRecord(c->ev1, c->stream));
     c->timed = true;
     if ((rc = tscope.end())) return rc;  // a later write of the tree waits for this frame
+    if (shadows && !fuse) {
+        // the frame's shadow rays after its primary rays (vhx_trace_shadows on the same stream); the frame's time then
+        // spans both (ev0 of the primary trace, ev1 re-recorded by the shadow trace)
+        c->keep_ev0 = true;
+        rc = vhx_trace_shadows(c, c->shadow_light, nout, ho.dev.value, ho.dev.impact, ho.dev.normal, ho.dev.shadowed,
+                               ho.dev.rgba, nullptr);
+        c->keep_ev0 = false;
+        if (rc) return rc;
+    }
     return finish_out(c, ho);
 }
 
@@ -2543,6 +2657,9 @@ static int trace_batch(vhx_ctx *c, const vhx_camera *cams, uint32_t n, const vhx
                                               "same non-empty width x height");
         if (outs[k].bytes)
             return fail(c, VHX_E_INVALID_ARG, std::string(fn) + ": byte counting is a vhx_trace_primary option");
+        if (c->shadow_on && (!outs[k].value || !outs[k].impact || !outs[k].normal || !outs[k].shadowed))
+            return fail(c, VHX_E_INVALID_ARG, std::string(fn) + " with a shadow light: value, impact, normal and "
+                                              "shadowed outputs needed");
     }
     // per frame: its output entries (a tile set: its tiles' entries), the index stride between frames (npix) and the
     // pass-0 workgroups (nbf)
@@ -2606,7 +2723,7 @@ static int trace_batch(vhx_ctx *c, const vhx_camera *cams, uint32_t n, const vhx
     for (uint32_t k = 0; k < n; ++k) {
         hc[k] = cam_of(&cams[k]);
         ho[k] = OutD{outs[k].value, outs[k].cell,   outs[k].voxel, outs[k].rgba,
-                     nullptr,       outs[k].impact, outs[k].normal, outs[k].depth};
+                     nullptr,       outs[k].impact, outs[k].normal, outs[k].depth, outs[k].shadowed};
     }
     if (T) std::memcpy((uint8_t *)P.ptr + cam_bytes + out_bytes, starts, (size_t)n * 4);
     uint32_t npass = 1;
@@ -2642,6 +2759,7 @@ static int trace_batch(vhx_ctx *c, const vhx_camera *cams, uint32_t n, const vhx
     }
     if (listed && (rc = ensure_lists(c, nbf0 * n))) return rc;
     const bool qm = queue_state_mode(c, listed, false, npass);
+    const bool fuse = c->shadow_on && listed && npass > 1;  // vhx_trace_primary's rule
     auto launch = [&](auto bd_tag) {
         constexpr int BD = decltype(bd_tag)::value;
         PassQ q0 = pass_q(c, 0, npass, qm);
@@ -2649,10 +2767,17 @@ static int trace_batch(vhx_ctx *c, const vhx_camera *cams, uint32_t n, const vhx
             q0.zero = (uint32_t *)c->qctl.ptr + 16;
         else if (npass > 1)
             q0.flags = (uint8_t *)c->flags.ptr;
-        k_trace_primary_batch<BD><<<(unsigned)(nbf0 * n), 256, 0, c->stream>>>(t, dcams, douts, (uint32_t)nbf0, bx,
-                                                                               (uint32_t)npix, q0, lo, tb);
-        qrc = launch_queue_passes<false, BD>(c, t, cd, src, OutD{}, 1, npass, nout, nbf0 * n,
-                                             listed ? P0_ORDERED : P0_FLAGS, T ? 0u : W, H, n, qm);
+        if (fuse) {
+            k_trace_primary_batch<BD, true><<<(unsigned)(nbf0 * n), 256, 0, c->stream>>>(
+                t, dcams, douts, (uint32_t)nbf0, bx, (uint32_t)npix, q0, lo, tb);
+            qrc = launch_queue_passes<false, BD, false, true>(c, t, cd, src, OutD{}, 1, npass, nout, nbf0 * n,
+                                                              P0_ORDERED, T ? 0u : W, H, n, qm);
+        } else {
+            k_trace_primary_batch<BD><<<(unsigned)(nbf0 * n), 256, 0, c->stream>>>(t, dcams, douts, (uint32_t)nbf0, bx,
+                                                                                   (uint32_t)npix, q0, lo, tb);
+            qrc = launch_queue_passes<false, BD>(c, t, cd, src, OutD{}, 1, npass, nout, nbf0 * n,
+                                                 listed ? P0_ORDERED : P0_FLAGS, T ? 0u : W, H, n, qm);
+        }
     };
     if (!dispatch_bd(c->tree->desc.brick_dim, launch)) return fail(c, VHX_E_INVALID_ARG, "unsupported brick_dim");
     if (qrc) return qrc;
@@ -2662,7 +2787,18 @@ static int trace_batch(vhx_ctx *c, const vhx_camera *cams, uint32_t n, const vhx
     c->last_fb_h = T ? 0u : H;
     VHX_HIP(c, hipEventRecord(c->ev1, c->stream));
     c->timed = true;
-    return tscope.end();
+    if ((rc = tscope.end())) return rc;
+    if (c->shadow_on && !fuse) {  // the frames' shadow rays after their primary rays (vhx_trace_primary's fallback)
+        c->keep_ev0 = true;
+        for (uint32_t k = 0; k < n && !rc; ++k) {
+            const uint64_t ent = T ? set_tiles(k) * T * T : npix;
+            if (ent)
+                rc = vhx_trace_shadows(c, c->shadow_light, ent, outs[k].value, outs[k].impact, outs[k].normal,
+                                       outs[k].shadowed, outs[k].rgba, nullptr);
+        }
+        c->keep_ev0 = false;
+    }
+    return rc;
 }
 
 int vhx_trace_primary_batch(vhx_ctx *c, const vhx_camera *cams, uint32_t n, const vhx_hits *outs) {
@@ -2727,6 +2863,15 @@ int vhx_profile_counters(vhx_ctx *c, uint64_t *out, uint32_t n, int reset) {
     (void)reset;
     return fail(c, VHX_E_STATE, "vhx_profile_counters: libvhx was built without VHX_PROF");
 #endif
+}
+
+int vhx_set_shadow_light(vhx_ctx *c, const float *light) {
+    if (!c) return VHX_E_INVALID_ARG;
+    if (light && !(std::isfinite(light[0]) && std::isfinite(light[1]) && std::isfinite(light[2])))
+        return fail(c, VHX_E_INVALID_ARG, "vhx_set_shadow_light: a finite light position");
+    c->shadow_on = light != nullptr;
+    for (int k = 0; k < 3; ++k) c->shadow_light[k] = light ? light[k] : 0.0f;
+    return VHX_OK;
 }
 
 int vhx_set_depth_prepass(vhx_ctx *c, int enable, float margin) {
@@ -2886,7 +3031,7 @@ int vhx_trace_shadows(vhx_ctx *c, const float light[3], uint64_t n, const uint32
     so.rgba = rgba;
     so.bytes = bytes;
     CamD cd{};
-    VHX_HIP(c, hipEventRecord(c->ev0, c->stream));
+    if (!c->keep_ev0) VHX_HIP(c, hipEventRecord(c->ev0, c->stream));  // (a fused-shadow fallback keeps the primary's)
     // no reset_passes: the hit compaction (k_count_flags) zeroes the queue passes' counters
     if (bytes) VHX_HIP(c, hipMemsetAsync(bytes, 0, n * 4, c->stream));
     // wave-dense secondary rays: the hit pixels, in frame order, are pass 0's queue

@@ -155,7 +155,8 @@ class Viewport:
 
 
 HIT_FIELDS = (("value", np.uint32, 1), ("cell", np.uint32, 1), ("voxel", np.uint32, 3), ("impact", np.float32, 3),
-              ("normal", np.float32, 3), ("depth", np.float32, 1), ("rgba", np.uint32, 1), ("bytes", np.uint32, 1))
+              ("normal", np.float32, 3), ("depth", np.float32, 1), ("rgba", np.uint32, 1), ("bytes", np.uint32, 1),
+              ("shadowed", np.uint32, 1))
 
 
 def _hits_struct(arrays):
@@ -283,6 +284,12 @@ class Raytracer:
     def set_depth_prepass(self, enable=True, margin=0.0):
         """vhx_set_depth_prepass: the opt-in half-resolution depth-prepass fast mode (not the reference's semantics)."""
         self._check(N.lib().vhx_set_depth_prepass(self._h, 1 if enable else 0, float(margin)))
+
+    def set_shadow_light(self, light=None):
+        """vhx_set_shadow_light: fused hard shadows (config 5) in trace_primary / trace_primary_batch /
+        trace_tiles_batch, whose outputs then need value, impact, normal and shadowed; None turns them off."""
+        lt = None if light is None else (ctypes.c_float * 3)(*[float(v) for v in light])
+        self._check(N.lib().vhx_set_shadow_light(self._h, lt))
 
     def set_pass_budgets(self, budgets):
         """Step budgets of the multi-pass ray scheduler (vhx_set_pass_budgets); () = one unbounded pass."""
