@@ -72,10 +72,10 @@ def parse():
     p.add_argument("--tile", type=int, default=64)
     p.add_argument("--shadows", action="store_true",
                    help="config 5: each step = primary frame + one hard-shadow ray per hit toward (S,S,S)")
-    p.add_argument("--shadow-mode", choices=("fused", "separate"), default="fused",
-                   help="--shadows: 'fused' = the shadow rays run in the primary trace (vhx_set_shadow_light: a lane "
-                        "goes on with its hit's shadow ray), 'separate' = vhx_trace_primary then vhx_trace_shadows "
-                        "(_batch) on the same stream (DESIGN.md §8.1)")
+    p.add_argument("--shadow-mode", choices=("fused", "separate"), default="separate",
+                   help="--shadows: 'separate' = vhx_trace_primary then vhx_trace_shadows (_batch) on the same stream; "
+                        "'fused' = the shadow rays run in the primary trace (vhx_set_shadow_light: a lane goes on with "
+                        "its hit's shadow ray), bit-identical and measured 4-5 %% slower (DESIGN.md §8.1)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-roofline", action="store_true")
     p.add_argument("--no-frame-check", action="store_true",
@@ -545,7 +545,8 @@ def main():
         # batches wherever they are the faster line: one GPU, primary rays on the exact path, and no explicit
         # --inflight (which asks for that many per-frame contexts). Config 5 (--shadows) keeps twenty per-frame
         # contexts: its batches (vhx_trace_shadows_batch, --batch K) measured 1.31 against 1.17-1.23 ms per frame
-        # (docs/DESIGN_LOG.md §16.3)
+        # (docs/DESIGN_LOG.md §16.3), 1.08 against 0.99-1.00 ms in round 6 (profiles/r06/shadows/); fused shadows
+        # batch (7 x 3)
         # The multi-GPU ranks (vhx_mgpu) batch too: each rank's tile sets of K frames as one vhx_trace_tiles_batch
         # (vhx_mgpu_render_batch) -- a rank's share of a config-4 frame is half a headline frame, and traced one frame
         # at a time it ran at 55 % of the whole frame's rate (scripts/probes/probe_tiles.py)

@@ -53,7 +53,8 @@ def _assert_same(a, b, what):
 
 
 @pytest.mark.parametrize("size,bd", [(64, 4), (256, 4), (128, 8), (32, 2), (16, 1)])
-@pytest.mark.parametrize("tune", ["adaptive=0", "adaptive=0;budgets=1,3,7,15", "adaptive=0;sparse=60,60,60", None])
+@pytest.mark.parametrize("tune", ["adaptive=0", "adaptive=0;budgets=1,3,7,15", "adaptive=0;sparse=60,60,60",
+                                  "adaptive=0;sbudget=40", "adaptive=0;sbudget=1", None])
 def test_fused_frame_equals_primary_then_shadows(size, bd, tune):
     """adaptive=0 keeps the frames-in-flight schedule for a lone frame, so pass 0 lists its rays and the shadows fuse;
     tune None is the lone frame's schedule, where they are traced after the primary rays."""

@@ -124,6 +124,7 @@ struct vhx_ctx {
     bool shadow_on = false;
     float shadow_light[3] = {0.f, 0.f, 0.f};
     bool keep_ev0 = false;  // the shadow rays of a frame traced after it: its time runs from the primary trace's ev0
+    uint32_t shadow_budget = 0;  // fused shadows: a shadow ray's steps in its primary ray's budgeted pass (tune "sbudget")
     float prepass_margin = 0.0f;
     DevBuf prepass_depth;  // the half-resolution depth frame
     // Ray schedule of a trace: step budgets of the passes before the final (unbounded) one, the sparse-wave thresholds
@@ -136,6 +137,7 @@ struct vhx_ctx {
         uint32_t queue_waves_per_cu;         // waves of a queue pass per CU
         uint32_t qorder;                     // order of a primary frame's pass-0 queue (vhx_ctx::qorder below)
         uint32_t qsort;                      // queue passes: segments of this many queue entries sorted by saved node
+        uint32_t queue_waves0_per_cu;        // waves of a first queue pass over fresh rays (the shadow rays) per CU
     };
     // Adaptive scheduling (default; vhx_set_pass_budgets or a tuning key fixes the schedule instead): at each
     // trace the context looks at the other contexts of its tree (vhx_create_shared) and picks
@@ -153,8 +155,11 @@ struct vhx_ctx {
     //    three-budget ladders 1.31-1.51 ms, fewer rays per wave in a last pass no better): every extra pass lengthens a
     //    lone frame's critical path.
     bool adaptive = true;
-    Sched sched_busy = {{24u, 72u, 216u, 648u}, 5u, {12u}, 3u, VHX_QORDER_BUSY, VHX_QSORT_BUSY};
-    Sched sched_idle = {{64u}, 2u, {0u}, 8u, VHX_QORDER_IDLE, VHX_QSORT_IDLE};
+    // first queue pass (shadow pass 0, 82 % memory waits): 4 waves per CU with frames in flight -- config 5 at twenty
+    // contexts 0.993-1.000 ms per frame against 1.110-1.128 at 32 per CU, 1.029-1.034 at 8 and 0.995-1.000 at 3
+    // (profiles/r06/shadows/) -- and 32 alone (the lone shadow frame 2.83 against 3.09-3.27 ms at 4)
+    Sched sched_busy = {{24u, 72u, 216u, 648u}, 5u, {12u}, 3u, VHX_QORDER_BUSY, VHX_QSORT_BUSY, 4u};
+    Sched sched_idle = {{64u}, 2u, {0u}, 8u, VHX_QORDER_IDLE, VHX_QSORT_IDLE, 32u};
     int last_sched = -1;  // the schedule of the last trace: 1 busy, 0 idle, -1 fixed (vhx_get_pass_budgets)
     // the schedule in force (the selected one, or the fixed one)
     uint32_t budgets[VHX_MAX_BUDGETS] = {24u, 72u, 216u, 648u};
@@ -186,7 +191,8 @@ struct vhx_ctx {
     // frames in flight 4 per CU (equal within noise there; profiles/r03/qwaves_r03.log)
     uint32_t queue_waves = 1024;
     uint32_t cus = 256;            // compute units of the device (the adaptive schedules' queue waves are per CU)
-    uint32_t queue_waves0 = 8192;  // waves of a first queue pass over fresh rays (tune "qwaves0")
+    uint32_t queue_waves0 = 8192;  // waves of a first queue pass over fresh rays (the schedule's per-CU figure x CUs)
+    uint32_t queue_waves0_force = 0;  // tune "qwaves0": a fixed figure in every schedule (0 = the schedule's)
     uint32_t queue_waves_mid = 0;  // waves of a budgeted queue pass after the first (tune "qwavesm"; 0 = queue_waves)
     uint32_t qxcd = 16;            // queue passes: XCD-dealt chunk runs (tune "qxcd" = run length, 0 = one counter)
     bool qxcd_all = false;         // deal every queue pass, not only the last (tune "qxcd_all=1", diagnostics)

@@ -273,6 +273,7 @@ struct PassQ {
     uint32_t sparse;     // budgeted passes with saved state: abandon a wave's rays once fewer lanes trace (0 = off)
     uint32_t *zero;      // pass 0 with block lists: the queue passes' work counters, zeroed by workgroup 0
     float lx, ly, lz;    // fused hard shadows (the FUSE kernels): the light
+    uint32_t sbud;       // fused: a shadow ray's steps in the budgeted pass its primary ray finished (0 = the rest)
 };
 
 // Rays per wave of a queue pass over n rays: fixed, or (rpw == 0) as many as spread the pass over about `tw` waves.
@@ -814,7 +815,9 @@ __device__ __forceinline__ bool fused_shadow(const DevTree &t, const uint64_t *o
     HitOut hs;
     hs.bytes = 0;
     const bool fin =
-        get_by_ray<false, BD>(t, occ_tab, so, sd, hs, rest_budget(q.budget, h.iters), q.state, sidx, false, 0.0f, q.sparse);
+        get_by_ray<false, BD>(t, occ_tab, so, sd, hs,
+                              q.sbud && q.budget < VHX_MAX_ITERS ? q.sbud : rest_budget(q.budget, h.iters), q.state,
+                              sidx, false, 0.0f, q.sparse);
     if (fin) store_fused_shadow(o, li, hs.hit);
     return fin;
 }
@@ -1505,6 +1508,7 @@ static void select_schedule(vhx_ctx *c, bool batch = false) {
     std::memcpy(c->sparse, s.sparse, sizeof(c->sparse));
     c->npass = s.npass;
     c->queue_waves = s.queue_waves_per_cu * c->cus;
+    c->queue_waves0 = c->queue_waves0_force ? c->queue_waves0_force : s.queue_waves0_per_cu * c->cus;
     c->qorder = s.qorder;
     c->qsort = c->qsort_force >= 0 ? (uint32_t)c->qsort_force : s.qsort;
     c->last_sched = busy ? 1 : 0;
@@ -1569,6 +1573,7 @@ static PassQ pass_q(const vhx_ctx *c, uint32_t p, uint32_t npass, bool qm = fals
     q.lx = c->shadow_light[0];
     q.ly = c->shadow_light[1];
     q.lz = c->shadow_light[2];
+    q.sbud = c->shadow_budget;
     return q;
 }
 
@@ -1893,6 +1898,7 @@ int vhx_set_pass_budgets(vhx_ctx *c, const uint32_t *budgets, uint32_t n) {
     if (c->adaptive) {  // leaving the adaptive choice: the rest of the schedule is the busy one's
         std::memcpy(c->sparse, c->sched_busy.sparse, sizeof(c->sparse));
         c->queue_waves = c->sched_busy.queue_waves_per_cu * c->cus;
+        c->queue_waves0 = c->queue_waves0_force ? c->queue_waves0_force : c->sched_busy.queue_waves0_per_cu * c->cus;
         c->qorder = c->sched_busy.qorder;
         c->adaptive = false;
     }
@@ -1972,9 +1978,12 @@ static int apply_tuning(vhx_ctx *c, const std::string &key, const std::string &v
     } else if (key == "scan_multi") {  // 0 = every scan on one workgroup
         if (!parse_u32(val, x)) return bad();
         c->scan_multi = x;
+    } else if (key == "sbudget") {  // fused shadows: steps of a shadow ray in its primary ray's pass (0 = the rest)
+        if (!parse_u32(val, x)) return bad();
+        c->shadow_budget = x;
     } else if (key == "qwaves0") {
         if (!parse_u32(val, x) || x == 0) return bad();
-        c->queue_waves0 = x;
+        c->queue_waves0 = c->queue_waves0_force = x;
     } else if (key == "qxcd") {
         if (!parse_u32(val, x)) return bad();
         c->qxcd = x;
@@ -2058,6 +2067,7 @@ int vhx_set_adaptive_schedule(vhx_ctx *c, int on) {
         std::memcpy(c->sparse, s.sparse, sizeof(c->sparse));
         c->npass = s.npass;
         c->queue_waves = s.queue_waves_per_cu * c->cus;
+        c->queue_waves0 = c->queue_waves0_force ? c->queue_waves0_force : s.queue_waves0_per_cu * c->cus;
         c->qorder = s.qorder;
         c->last_sched = -1;
     }
@@ -2229,6 +2239,8 @@ void vhx::copy_sched(vhx_ctx *c, const vhx_ctx *owner) {
     c->queue_blocks = owner->queue_blocks;
     c->queue_waves = owner->queue_waves;
     c->queue_waves0 = owner->queue_waves0;
+    c->queue_waves0_force = owner->queue_waves0_force;
+    c->shadow_budget = owner->shadow_budget;
     c->queue_waves_mid = owner->queue_waves_mid;
     c->qxcd = owner->qxcd;
     c->qxcd_all = owner->qxcd_all;
@@ -2596,7 +2608,7 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
         } else {
             if (fast)
                 k_trace_primary<false, BD, true><<<g0, 256, 0, c->stream>>>(
-                    t, cd, ho.dev, T, tiles_x, tile_start, tile_stride, layout, bpx, bpt, q0, FastD{}, lo);
+                    t, cd, ho.dev, T, tiles_x, tile_start, tile_stride, layout, bpx, bpt, q0, fd, lo);
             else
                 k_trace_primary<false, BD><<<g0, 256, 0, c->stream>>>(
                     t, cd, ho.dev, T, tiles_x, tile_start, tile_stride, layout, bpx, bpt, q0, FastD{}, lo);
