@@ -132,7 +132,8 @@ int main(int argc, char **argv) {
     printf("frame0 %ux%u hits %llu trace_ms %.3f\n", cam.width, cam.height, (unsigned long long)hits, ms);
 
     /* ---- batches (vhx_trace_primary_batch), device outputs: two batches back to back on ONE context (3 + 2 frames
-     * of the same camera; the staging ring lets the second call queue behind the first without a host wait), an
+     * of the same camera; with the staging ring on, "stage_slots=4", the second call queues behind the first without a
+     * host wait), an
      * aliasing batch that must be refused, then the hard shadows of two frames as one vhx_trace_shadows_batch ---- */
     {
         enum { NB = 5 };
@@ -153,6 +154,7 @@ int main(int argc, char **argv) {
                           (float *)dd[k], (uint32_t *)dr[k], NULL, NULL};
             bh[k] = z;
         }
+        CHECK(vhx_set_tuning(ctx, "stage_slots=4"));
         CHECK(vhx_trace_primary_batch(ctx, bc, 3, bh));
         CHECK(vhx_trace_primary_batch(ctx, bc + 3, 2, bh + 3));
         vhx_hits alias[2] = {bh[0], bh[0]};

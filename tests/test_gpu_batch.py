@@ -120,20 +120,24 @@ def test_batch_headline_frames_match_golden():
         rt.close()
 
 
-def test_batches_in_flight_on_shared_contexts(gpu):
+@pytest.mark.parametrize("slots", [1, 4])
+def test_batches_in_flight_on_shared_contexts(gpu, slots):
     """Two shared contexts, each submitting batches on its own stream without waiting: every frame equals a lone
-    trace (the batch's queues, state and argument copies are per context)."""
+    trace (the batch's queues, state and argument copies are per context). Five batches per context: with the
+    staging ring on ("stage_slots=4") the ring wraps onto slots whose copies may not have run yet."""
     import torch
     flat = vhx.FlatTree.build_scene(N.VHX_SCENE_LATTICE_CUBE, 256, 4)
     owner = vhx.Raytracer(0)
     try:
         owner.upload(flat)
         other = owner.shared()
+        for ctx in (owner, other):
+            ctx.set_tuning(f"stage_slots={slots}")
         W, H = 480, 270
-        cams = _orbit(256, W, H, 12, step=0.1)
+        cams = _orbit(256, W, H, 30, step=0.1)
         outs = [_outs(W * H, ("rgba", "depth")) for _ in cams]
         torch.cuda.synchronize()
-        for b in range(4):  # batches 0, 2 on the owner, 1, 3 on the other context, in flight together
+        for b in range(10):  # even batches on the owner, odd ones on the other context, in flight together
             ctx = owner if b % 2 == 0 else other
             ctx.trace_primary_batch(cams[3 * b:3 * b + 3], outs[3 * b:3 * b + 3])
         owner.sync()

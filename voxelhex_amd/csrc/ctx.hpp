@@ -106,11 +106,16 @@ struct vhx_ctx {
     } pinned[2];
     uint32_t pinned_next = 0;
     // vhx_trace_primary_batch: the batch's cameras and outputs (a ring of pinned staging slots, and their device
-    // copy). A slot is rewritten only once the copy that read it has run; with VHX_STAGE_SLOTS slots a caller can queue
-    // that many batches on one context before the host waits (the device copy itself is stream-ordered)
+    // copy). A slot is rewritten only once the copy that read it has run; with N slots in use a caller can queue N
+    // batches on one context before the host waits (the device copy itself is stream-ordered)
     static constexpr uint32_t VHX_STAGE_SLOTS = 4;
     Pinned batch_pinned[VHX_STAGE_SLOTS];
     uint32_t batch_next = 0;
+    // slots in use (tune "stage_slots"). 1: a batch waits on the host until the context's previous batch started on
+    // the GPU. Measured (profiles/r06/stage_slots/): the bench default (batches of 7 on 3 contexts) 0.483-0.487 ms
+    // per frame at 1 slot against 0.500-0.507 at 4 and 0.501-0.502 at 2; 2 contexts 0.517-0.518 against 0.525-0.531;
+    // one context equal (0.654-0.662). Letting the host run further ahead only slows the contexts' interleaving
+    uint32_t stage_slots = 1;
     DevBuf batch_args;
     // vhx_trace_shadows_batch: the frames' ShD records and hit-value pointers (pinned staging ring, device copy)
     Pinned shadow_pinned[VHX_STAGE_SLOTS];

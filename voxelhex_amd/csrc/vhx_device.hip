@@ -1978,6 +1978,9 @@ static int apply_tuning(vhx_ctx *c, const std::string &key, const std::string &v
     } else if (key == "scan_multi") {  // 0 = every scan on one workgroup
         if (!parse_u32(val, x)) return bad();
         c->scan_multi = x;
+    } else if (key == "stage_slots") {  // batch staging ring slots in use (1 = wait for the previous batch's copy)
+        if (!parse_u32(val, x) || x == 0 || x > vhx_ctx::VHX_STAGE_SLOTS) return bad();
+        c->stage_slots = x;
     } else if (key == "sbudget") {  // fused shadows: steps of a shadow ray in its primary ray's pass (0 = the rest)
         if (!parse_u32(val, x)) return bad();
         c->shadow_budget = x;
@@ -2241,6 +2244,7 @@ void vhx::copy_sched(vhx_ctx *c, const vhx_ctx *owner) {
     c->queue_waves0 = owner->queue_waves0;
     c->queue_waves0_force = owner->queue_waves0_force;
     c->shadow_budget = owner->shadow_budget;
+    c->stage_slots = owner->stage_slots;
     c->queue_waves_mid = owner->queue_waves_mid;
     c->qxcd = owner->qxcd;
     c->qxcd_all = owner->qxcd_all;
@@ -2642,7 +2646,7 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
 // (VHX_STAGE_SLOTS batches ago on this context) has not run yet
 static int stage_slot(vhx_ctx *c, vhx_ctx::Pinned *ring, uint32_t &next, uint64_t bytes, vhx_ctx::Pinned *&out) {
     vhx_ctx::Pinned &P = ring[next];
-    next = (next + 1) % vhx_ctx::VHX_STAGE_SLOTS;
+    next = (next + 1) % std::max<uint32_t>(1u, std::min(c->stage_slots, vhx_ctx::VHX_STAGE_SLOTS));
     if (P.used) VHX_HIP(c, hipEventSynchronize(P.done));
     if (P.bytes < bytes) {
         if (P.ptr) VHX_HIP(c, hipHostFree(P.ptr));
