@@ -65,7 +65,7 @@ def test_frames_in_flight_match_golden(F):
             # frame takes > 1 ms; the frames-in-flight schedule) -- and the frames are the same either way
             sched = [r.pass_budgets() for r in ctxs]
             assert sched[0] == ((64,), "idle"), sched[0]
-            assert all(sc == ((24, 72, 216, 648), "busy") for sc in sched[1:]), sched
+            assert all(sc == ((32, 128, 768), "busy") for sc in sched[1:]), sched
             for s in streams:
                 s.synchronize()
             for f, (c, o) in enumerate(zip(cams, outs)):

@@ -260,11 +260,11 @@ def test_full_size_shadows_vs_oracle(gpu, oracle):
     assert sh.sum() > 100000
 
 
-DEFAULT_BUDGETS = (24, 72, 216, 648)  # the library default (ctx.hpp)
+DEFAULT_BUDGETS = (32, 128, 768)  # the library default (ctx.hpp)
 
 
 @pytest.mark.parametrize("budgets", [(), (1,), (1, 2, 3), (1, 2, 3, 4), (4, 40), (8, 64, 512), (64,),
-                                     (16, 64, 256, 1024), (1, 2, 4, 8, 16, 32), DEFAULT_BUDGETS])
+                                     (16, 64, 256, 1024), (1, 2, 4, 8, 16, 32), (24, 72, 216, 648), DEFAULT_BUDGETS])
 def test_multipass_schedule_is_bit_identical(gpu, oracle, budgets):
     """The multi-pass scheduler (vhx_set_pass_budgets) abandons and re-traces rays; every schedule, down to a
     1-step first budget that requeues nearly every ray, must give the oracle's results (incl. byte counts)."""

@@ -143,11 +143,16 @@ struct vhx_ctx {
         uint32_t qorder;                     // order of a primary frame's pass-0 queue (vhx_ctx::qorder below)
         uint32_t qsort;                      // queue passes: segments of this many queue entries sorted by saved node
         uint32_t queue_waves0_per_cu;        // waves of a first queue pass over fresh rays (the shadow rays) per CU
+        uint32_t shadow_budgets[VHX_MAX_BUDGETS];  // the ladder of a shadow trace (vhx_trace_shadows / _batch)
+        uint32_t shadow_npass;
     };
     // Adaptive scheduling (default; vhx_set_pass_budgets or a tuning key fixes the schedule instead): at each
     // trace the context looks at the other contexts of its tree (vhx_create_shared) and picks
-    //  * `busy` when any of them still has a frame in flight on another stream: {24, 72, 216, 648} with 4 queue waves per
-    //    CU -- the bench frame at eight frames in flight 0.561-0.567 ms against 0.593-0.598 for round 2's {24, 96, 768}
+    //  * `busy` when any of them still has a frame in flight on another stream, or a batch: {32, 128, 768} since round 6
+    //    -- with batches of 7 on 3 contexts 0.4761-0.4770 ms per frame over 100 frames against 0.4867-0.4873 for
+    //    {24, 72, 216, 648}, and in the driver's 20-frame window 0.487-0.496 against 0.500-0.514 ms (four alternating
+    //    runs; {40, 160, 640} and {32, 128, 512} within noise of it, {24, 96, 768} between; profiles/r06/ladder/).
+    //    Rounds 3-5: {24, 72, 216, 648} with 4 queue waves per CU -- the bench frame at eight frames in flight 0.561-0.567 ms against 0.593-0.598 for round 2's {24, 96, 768}
     //    at 8 waves per CU (profiles/r03/sched_r03.log, ladder_r03b.log; 4 against 8 queue waves per CU is within noise
     //    at eight frames in flight, 0.562-0.566 against 0.563-0.565 ms, qwaves_r03.log): the queue passes are most of
     //    the frame period (pass_share_r03.log); a finer ladder re-packs the surviving rays into full waves more often,
@@ -163,12 +168,14 @@ struct vhx_ctx {
     // first queue pass (shadow pass 0, 82 % memory waits): 4 waves per CU with frames in flight -- config 5 at twenty
     // contexts 0.993-1.000 ms per frame against 1.110-1.128 at 32 per CU, 1.029-1.034 at 8 and 0.995-1.000 at 3
     // (profiles/r06/shadows/) -- and 32 alone (the lone shadow frame 2.83 against 3.09-3.27 ms at 4)
-    Sched sched_busy = {{24u, 72u, 216u, 648u}, 5u, {12u}, 3u, VHX_QORDER_BUSY, VHX_QSORT_BUSY, 4u};
-    Sched sched_idle = {{64u}, 2u, {0u}, 8u, VHX_QORDER_IDLE, VHX_QSORT_IDLE, 32u};
+    // shadow traces keep {24, 72, 216, 648} with frames in flight: config 5 at twenty contexts 1.007-1.016 ms per frame
+    // in the driver's window against 1.029-1.033 with {32, 128, 768} (profiles/r06/ladder/)
+    Sched sched_busy = {{32u, 128u, 768u}, 4u, {12u}, 3u, VHX_QORDER_BUSY, VHX_QSORT_BUSY, 4u, {24u, 72u, 216u, 648u}, 5u};
+    Sched sched_idle = {{64u}, 2u, {0u}, 8u, VHX_QORDER_IDLE, VHX_QSORT_IDLE, 32u, {64u}, 2u};
     int last_sched = -1;  // the schedule of the last trace: 1 busy, 0 idle, -1 fixed (vhx_get_pass_budgets)
     // the schedule in force (the selected one, or the fixed one)
-    uint32_t budgets[VHX_MAX_BUDGETS] = {24u, 72u, 216u, 648u};
-    uint32_t npass = 5;
+    uint32_t budgets[VHX_MAX_BUDGETS] = {32u, 128u, 768u};
+    uint32_t npass = 4;
     uint32_t rpw[VHX_MAX_BUDGETS + 1] = {64u, 64u, 64u, 64u, 64u, 64u, 64u};  // rays per wave of each pass (tune "rpw=64,16" style override; 0 = adaptive)
     uint32_t tw = 1024;            // adaptive rays per wave: target waves per queue pass (tune "tw")
     uint32_t scan_multi = 8;       // chunk scans of more segments (SCAN_SEG counts) run on one workgroup per segment

@@ -50,9 +50,9 @@ __device__ unsigned long long g_prof[5 * 16 * 2];
     do {                         \
     } while (0)
 #endif
-// pass slots of the default schedule {24, 72, 216, 648} (round 2's {24, 96, 768} uses slots 0, 1, 3, 4)
+// pass slots of the profile counters: {24, 72, 216, 648} uses slots 0-3, the default {32, 128, 768} slots 0, 2, 3
 __device__ __forceinline__ uint32_t pass_of_budget(uint32_t b) {
-    return b >= VHX_MAX_ITERS ? 4u : (b <= 24u ? 0u : (b <= 96u ? 1u : (b <= 256u ? 2u : 3u)));
+    return b >= VHX_MAX_ITERS ? 4u : (b <= 32u ? 0u : (b <= 96u ? 1u : (b <= 256u ? 2u : 3u)));
 }
 
 struct DevTree {

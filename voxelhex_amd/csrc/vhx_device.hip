@@ -901,8 +901,18 @@ struct TileB {
     uint32_t T, tiles_x, ntiles, stride, bpx, bpt;
     const uint32_t *starts;
 };
+// VHX_BATCH_WAVES (a variant build): waves per SIMD the batch pass 0 must allow (0: the compiler's choice, 72 VGPRs
+// for brick_dim 4 = 7 waves)
+#ifndef VHX_BATCH_WAVES
+#define VHX_BATCH_WAVES 0
+#endif
+#if VHX_BATCH_WAVES
+#define VHX_BATCH_ATTR __attribute__((amdgpu_waves_per_eu(VHX_BATCH_WAVES)))
+#else
+#define VHX_BATCH_ATTR
+#endif
 template <int BD, bool FUSE = false>
-__global__ void __launch_bounds__(256) k_trace_primary_batch(DevTree t, const CamD *__restrict__ cams,
+__global__ void __launch_bounds__(256) VHX_BATCH_ATTR k_trace_primary_batch(DevTree t, const CamD *__restrict__ cams,
                                                              const OutD *__restrict__ outs, uint32_t nblocks_frame,
                                                              uint32_t blocks_x, uint32_t npix, PassQ q,
                                                              ListOrder lo = ListOrder{}, TileB tb = TileB{}) {
@@ -1043,7 +1053,9 @@ __global__ void k_put_queue_args(QueueArgs a, QueueArgs *dst) {
     if (threadIdx.x == 0) *dst = a;
 }
 
-template <bool COUNT, int BD, bool MIP = false, bool FUSE = false>
+// QM: the queue-state mode (PassQ::qmode) as a separate instantiation: carried as a run-time flag, its state pointers
+// and slot indices cost the default kernel 2 VGPRs and 4 spilled ones
+template <bool COUNT, int BD, bool MIP = false, bool FUSE = false, bool QM = false>
 __global__ void __launch_bounds__(256) VHX_QUEUE_ATTR k_trace_queue(DevTree t, const QueueArgs *qa, const uint32_t *__restrict__ in,
                                                      const uint32_t *in_n, uint32_t *grab, PassQ q) {
     __shared__ uint64_t occ_tab[OCC_TAB_WORDS];
@@ -1122,8 +1134,8 @@ __global__ void __launch_bounds__(256) VHX_QUEUE_ATTR k_trace_queue(DevTree t, c
             // queue-state mode: resumed from queue position i, abandoned into this chunk's list slots (base = chunk *
             // rays per wave, the chunk's list position)
             const bool fin = get_by_ray<COUNT, BD, false, MIP>(
-                t, occ_tab, o, d, h, q.budget, q.state, q.qmode ? base : idx, q.resume != 0, 0.0f, q.sparse,
-                q.qmode ? q.sin : nullptr, i, q.qmode && q.tmp);
+                t, occ_tab, o, d, h, q.budget, q.state, QM ? base : idx, q.resume != 0, 0.0f, q.sparse,
+                QM ? q.sin : nullptr, QM ? i : 0u, QM && q.tmp);
             const QueueArgs *b = qa;
             asm volatile("" : "+s"(b));
             if (!fin) {
@@ -1486,7 +1498,7 @@ static int finish_out(vhx_ctx *c, HostOut &ho) {
 // Adaptive scheduling (ctx.hpp, Sched): the busy schedule while another context of the tree has a frame in flight on
 // another stream (its last trace's use event not yet reached), else the idle one. A host-side query per other context;
 // no waits.
-static void select_schedule(vhx_ctx *c, bool batch = false) {
+static void select_schedule(vhx_ctx *c, bool batch = false, bool shadow = false) {
     if (!c->adaptive) {
         c->last_sched = -1;
         c->qsort = c->qsort_force >= 0 ? (uint32_t)c->qsort_force : c->sched_busy.qsort;  // a fixed schedule: the busy one's
@@ -1504,9 +1516,9 @@ static void select_schedule(vhx_ctx *c, bool batch = false) {
             }
     }
     const vhx_ctx::Sched &s = busy ? c->sched_busy : c->sched_idle;
-    std::memcpy(c->budgets, s.budgets, sizeof(c->budgets));
+    std::memcpy(c->budgets, shadow ? s.shadow_budgets : s.budgets, sizeof(c->budgets));
     std::memcpy(c->sparse, s.sparse, sizeof(c->sparse));
-    c->npass = s.npass;
+    c->npass = shadow ? s.shadow_npass : s.npass;
     c->queue_waves = s.queue_waves_per_cu * c->cus;
     c->queue_waves0 = c->queue_waves0_force ? c->queue_waves0_force : s.queue_waves0_per_cu * c->cus;
     c->qorder = s.qorder;
@@ -1516,7 +1528,7 @@ static void select_schedule(vhx_ctx *c, bool batch = false) {
 
 static int prepare_passes(vhx_ctx *c, uint64_t nout, uint64_t nblocks0, uint32_t &npass, bool shadow = false,
                           bool batch = false) {
-    select_schedule(c, batch);
+    select_schedule(c, batch, shadow);
     npass = nout < 0x7FFFFFFFull ? c->npass : 1u;
     if (npass < 2 && !shadow) return VHX_OK;
     uint64_t chunks = std::max(nblocks0, (nout + 1023) / 1024), list = nblocks0 * 256;
@@ -1582,7 +1594,9 @@ static PassQ pass_q(const vhx_ctx *c, uint32_t p, uint32_t npass, bool qm = fals
 // (save_from 0, resume on), and no queue is node-sorted (the sort reorders a queue by the states at output indices)
 static bool queue_state_mode(const vhx_ctx *c, bool listed, bool first_queue, uint32_t npass) {
     // (fused shadows keep states at output indices: a pixel's primary and shadow ray are never pending together)
-    if (!c->qstate || !c->resume || c->save_from != 0 || npass < 2 || !(listed || first_queue) || c->shadow_on)
+    // (and MIP frames: the queue kernel's queue-state instantiation is built for the exact path only)
+    if (!c->qstate || !c->resume || c->save_from != 0 || npass < 2 || !(listed || first_queue) || c->shadow_on ||
+        c->tree->mips_on)
         return false;
     if (!c->stateq.ptr) return false;
     for (uint32_t p = 1; p < npass && p < 32u; ++p)
@@ -1773,8 +1787,15 @@ static int launch_queue_passes(vhx_ctx *c, const DevTree &t, const CamD &cam, co
         // the waves in flight
         if (frames > 1 && p > 0) qwaves = (uint32_t)std::min<uint64_t>((uint64_t)qwaves * frames, 20ull * c->cus);
         const unsigned qgrid = (qwaves * 64u + c->qblock - 1) / c->qblock;
-        k_trace_queue<COUNT, BD, MIP, FUSE><<<qgrid, c->qblock, 0, c->stream>>>(t, qa, in, in_n,
-                                                                         ctl + 16u + QCTL_PASS_WORDS * p, q);
+        uint32_t *grab = ctl + 16u + QCTL_PASS_WORDS * p;
+        if constexpr (!FUSE && !MIP) {  // (the queue-state mode excludes fused shadows; MIP frames never list pass 0)
+            if (q.qmode)
+                k_trace_queue<COUNT, BD, MIP, FUSE, true><<<qgrid, c->qblock, 0, c->stream>>>(t, qa, in, in_n, grab, q);
+            else
+                k_trace_queue<COUNT, BD, MIP, FUSE><<<qgrid, c->qblock, 0, c->stream>>>(t, qa, in, in_n, grab, q);
+        } else {
+            k_trace_queue<COUNT, BD, MIP, FUSE><<<qgrid, c->qblock, 0, c->stream>>>(t, qa, in, in_n, grab, q);
+        }
         debug_passes(c, "queue pass");
         if (p + 1 < npass) {
             rc = compact_chunks(c, 0, in_n, q.rpw, q.rpw, (uint32_t *)c->queue[p & 1u].ptr, ctl + p,
