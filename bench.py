@@ -104,7 +104,7 @@ def parse():
                    help="opt-in approximate mode (vhx_set_depth_prepass, not the reference semantics): a half-resolution "
                         "depth prepass, full-resolution rays start at the min of 4 texels minus MARGIN")
     p.add_argument("--budgets", default=None, metavar="B1,B2,...",
-                   help="step budgets of the pass schedule (vhx_set_pass_budgets; \"\" = one pass); default: the library's adaptive choice ({24, 72, 216, 648} with frames in flight, {64} for a lone frame), one pass with --mip-lod (its rays are short: 0.092 against 0.136 ms per depth-1 frame, profiles/r02/mips/headline/budgets)")
+                   help="step budgets of the pass schedule (vhx_set_pass_budgets; \"\" = one pass); default: the library's adaptive choice ({32, 128, 768} with frames in flight, {24, 72, 216, 648} for shadow traces, {64} for a lone frame), one pass with --mip-lod (its rays are short: 0.092 against 0.136 ms per depth-1 frame, profiles/r02/mips/headline/budgets)")
     p.add_argument("--mip-lod", type=int, default=None, metavar="DEPTH",
                    help="opt-in MIP stand-in mode (not the reference path): the scene inserted into a host BoxTree with "
                         "MIP maps on, flattened down to DEPTH (vhx_boxtree_flatten_lod) and traced with its node MIPs "
@@ -562,8 +562,9 @@ def main():
     if args.inflight is None:
         args.inflight = 2 if args.batch else 20
     if args.batch and int(os.environ.get("WORLD_SIZE", "1")) == 1 and os.environ.get("VHX_BENCH_MGPU1") != "1":
-        # one stream per batch in flight: the box's default hardware queues (GPU_MAX_HW_QUEUES unset: 4) suffice
-        queues = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
+        # one stream per batch in flight: the box's default hardware queues (GPU_MAX_HW_QUEUES unset: 4) suffice for
+        # three contexts (the default stream holds one queue); more contexts get a queue each
+        queues = hw_queues(args.inflight) if args.inflight > 3 else int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
     else:
         # per-frame contexts, or a multi-GPU rank's batch contexts plus its communication stream: a queue each
         queues = hw_queues(max(1, args.inflight))

@@ -166,7 +166,7 @@ int vhx_sync(vhx_ctx *ctx, float *last_trace_ms);
  * such rays per wave; the last pass is unbounded. n = 0 is a single pass. Budgets strictly increasing,
  * 0 < b < 2^22, n <= VHX_MAX_BUDGETS.
  * By default the schedule is adaptive: a trace submitted while another context of the same tree (vhx_create_shared)
- * has a frame in flight on another stream runs the frames-in-flight schedule {24, 72, 216, 648}; otherwise (one frame
+ * has a frame in flight on another stream runs the frames-in-flight schedule {32, 128, 768} (shadow traces {24, 72, 216, 648}); otherwise (one frame
  * at a time, or frames serialised on one stream) the lone-frame schedule {64}. vhx_set_pass_budgets fixes the
  * budgets (and ends the adaptive choice; vhx_set_adaptive_schedule(ctx, 1) restores it). vhx_set_adaptive_schedule(ctx,
  * 0) fixes the frames-in-flight schedule whatever the last trace ran. */
