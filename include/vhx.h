@@ -301,6 +301,13 @@ int vhx_profile_counters(vhx_ctx *ctx, uint64_t *out, uint32_t n, int reset);
  * iterations, [7] probes, [8] ADVANCE walks, [9] steps, [10] hit value, [16..63] node-load wait histogram in 64-cycle
  * buckets (the last one open). Shader cycles (s_memtime). */
 int vhx_chain_profile(vhx_ctx *ctx, const vhx_camera *cam, const uint32_t *pixels, uint32_t n, uint64_t *out);
+/* Early tail of lone frames (scheduling only; off by default: vhx_set_tuning "tail=1" turns it on, "tail_min",
+ * "tail_rpw", "tail_cap", "tail_prio" tune it): a lone vhx_trace_primary of a whole framebuffer records the pixels whose rays took >= tail_min steps, and
+ * the context's next lone frame of the same size traces them from its start on a second stream while the rest of the
+ * frame takes the pass ladder -- the longest rays' chains no longer start last. Results are bit-identical either way.
+ * Diagnostics: *listed = the pixels the next lone frame would trace early (0: none recorded, or tail off), *width /
+ * *height = the frame size they were recorded for (either may be null); synchronises the context's stream. */
+int vhx_tail_info(vhx_ctx *ctx, uint32_t *listed, uint32_t *width, uint32_t *height);
 /* Traces n explicit rays; rays = 6 f32 per ray (origin xyz, direction xyz), host or device per on_device. */
 int vhx_trace_rays(vhx_ctx *ctx, const float *rays, uint64_t n, const vhx_hits *out, int on_device);
 /* Hard shadows (BASELINE config 5; the reference has no shadow rays — semantics defined in docs/DESIGN_LOG.md §9): for

@@ -119,6 +119,7 @@ SIGNATURES = [
     ("vhx_trace_tiles_batch", c_int, [c_void_p, c_void_p, c_u32, c_u32, c_void_p, c_u32, c_void_p]),
     ("vhx_profile_counters", c_int, [c_void_p, P(c_u64), c_u32, c_int]),
     ("vhx_chain_profile", c_int, [c_void_p, c_void_p, P(c_u32), c_u32, P(c_u64)]),
+    ("vhx_tail_info", c_int, [c_void_p, P(c_u32), P(c_u32), P(c_u32)]),
     ("vhx_trace_rays", c_int, [c_void_p, c_void_p, c_u64, P(Hits), c_int]),
     ("vhx_trace_shadows", c_int, [c_void_p, P(c_f32), c_u64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                   c_void_p]),

@@ -130,6 +130,21 @@ struct vhx_ctx {
     float shadow_light[3] = {0.f, 0.f, 0.f};
     bool keep_ev0 = false;  // the shadow rays of a frame traced after it: its time runs from the primary trace's ev0
     uint32_t shadow_budget = 0;  // fused shadows: a shadow ray's steps in its primary ray's budgeted pass (tune "sbudget")
+    // Early tail (lone frames; tune "tail=1" turns it on, off by default until it pays): a lone frame's time is its
+    // longest rays' serial chains, which the pass ladder starts last. Each lone frame records the pixels whose rays
+    // took >= tail_min steps (tail_list, at most tail_cap; word 0 the count, entries from word 64); the next lone
+    // frame of the same size traces those pixels from its start, tail_rpw to a wave, on a second stream of high
+    // priority (k_trace_tail) while its other pixels go through the usual passes (pass 0 skips the listed ones,
+    // tail_mask). Scheduling only: every pixel is traced once, completely, by the same get_by_ray, so the frame is
+    // bit-identical whatever the list holds.
+    bool tail_on = false;
+    uint32_t tail_min = 512, tail_cap = 4096, tail_rpw = 4, tail_prio = 0;
+    DevBuf tail_list[2], tail_mask;
+    uint32_t tail_cur = 0, tail_w = 0, tail_h = 0;  // tail_list[tail_cur]: the last recorded list, of a tail_w x tail_h frame
+    bool tail_valid = false;
+    uint32_t *tail_rec = nullptr;  // during a recording trace: the list its final pass appends to
+    hipStream_t tail_stream = nullptr;
+    hipEvent_t tail_fork = nullptr, tail_join = nullptr;
     float prepass_margin = 0.0f;
     DevBuf prepass_depth;  // the half-resolution depth frame
     // Ray schedule of a trace: step budgets of the passes before the final (unbounded) one, the sparse-wave thresholds

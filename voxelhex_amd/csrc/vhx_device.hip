@@ -274,7 +274,18 @@ struct PassQ {
     uint32_t *zero;      // pass 0 with block lists: the queue passes' work counters, zeroed by workgroup 0
     float lx, ly, lz;    // fused hard shadows (the FUSE kernels): the light
     uint32_t sbud;       // fused: a shadow ray's steps in the budgeted pass its primary ray finished (0 = the rest)
+    // early tail (vhx_ctx::tail_*): pass 0 skips the pixels set in `skip` (the early tail traces them); the final pass
+    // appends the pixels of rays that took >= tail_min steps to tail_out (count at word 0, entries from word 64)
+    const uint32_t *skip;
+    uint32_t *tail_out;
+    uint32_t tail_min, tail_cap;
 };
+
+// one more pixel of the early-tail list (at most cap; the count keeps growing past it, the entries stop)
+__device__ __forceinline__ void tail_record(uint32_t *list, uint32_t cap, uint32_t idx) {
+    const uint32_t k = atomicAdd(list, 1u);
+    if (k < cap) list[64u + k] = idx;
+}
 
 // Rays per wave of a queue pass over n rays: fixed, or (rpw == 0) as many as spread the pass over about `tw` waves.
 // Long rays traced 64 per wave pay for their divergence (the bench frame's 256 longest: 1.05 ms at 64 per wave,
@@ -857,7 +868,9 @@ __global__ void __launch_bounds__(256) k_trace_primary(DevTree t, CamD cam, OutD
                                                           : (uint64_t)j * T * T + (uint64_t)ly * T + lx;
     bool done = true;
     uint32_t tag = 0u;  // FUSE: VHX_QSHADOW when the ray left over is the hit's shadow ray
-    if (valid) {
+    // the early tail traces the pixels in q.skip (its kernel stores them): done here, no store, no flag
+    const bool skipped = valid && q.skip && ((q.skip[idx >> 5] >> (idx & 31u)) & 1u) != 0u;
+    if (valid && !skipped) {
         F3d o, d;
         HitOut h;
         h.bytes = 0;
@@ -1165,6 +1178,7 @@ __global__ void __launch_bounds__(256) VHX_QUEUE_ATTR k_trace_queue(DevTree t, c
                 store(t, b->src.outs[f], idx - f * b->src.npix, o, h);
             } else {
                 store(t, b->out, idx, o, h);
+                if (q.tail_out && h.iters >= q.tail_min) tail_record(q.tail_out, q.tail_cap, idx);
             }
         }
         if (q.tmp) {  // this chunk's abandoned rays, in lane order
@@ -1174,6 +1188,51 @@ __global__ void __launch_bounds__(256) VHX_QUEUE_ATTR k_trace_queue(DevTree t, c
             if (lane == 0) q.counts[chunk] = (uint32_t)__popcll(m);
         }
     }
+}
+
+// Early tail (vhx_ctx::tail_*): the pixels of a recorded list as bits of the frame's skip mask (cleared before)
+__global__ void k_tail_mask(const uint32_t *__restrict__ list, uint32_t cap, uint32_t npix, uint32_t *mask) {
+    const uint32_t n = min(list[0], cap);
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const uint32_t idx = list[64u + i];
+        if (idx < npix) atomicOr(mask + (idx >> 5), 1u << (idx & 31u));
+    }
+}
+
+// Early tail: the listed pixels of a framebuffer frame traced to the end from the start of the frame, rpw to a wave
+// (entry i of the list in wave i / rpw), on the context's second stream while pass 0 skips them; each still-long ray
+// is listed again for the next lone frame. Same ray, traversal and store as k_trace_primary + the queue passes.
+template <int BD>
+__global__ void __launch_bounds__(256) k_trace_tail(DevTree t, CamD cam, OutD out, const uint32_t *__restrict__ list,
+                                                    uint32_t *next, uint32_t cap, uint32_t tail_min, uint32_t rpw,
+                                                    uint32_t prio) {
+    __shared__ uint64_t occ_tab[OCC_TAB_WORDS];
+    fill_occ_tab(occ_tab);
+    __syncthreads();
+    // issue priority of these waves over the frame's other waves on their SIMD (a serial chain is what they carry)
+    if (prio == 3u) __builtin_amdgcn_s_setprio(3);
+    else if (prio == 2u) __builtin_amdgcn_s_setprio(2);
+    else if (prio == 1u) __builtin_amdgcn_s_setprio(1);
+    const uint32_t n = min(list[0], cap);
+    const uint32_t lane = threadIdx.x & 63u, wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const uint32_t i = wave * rpw + lane;
+    if (lane >= rpw || i >= n) return;
+    const uint32_t idx = list[64u + i];
+    if (idx >= cam.width * cam.height) return;
+    const uint32_t px = idx % cam.width, py = idx / cam.width;
+    F3d o, d;
+    HitOut h;
+    h.bytes = 0;
+    if (glass_clear_miss(cam, px, py, (float)t.size)) {
+        o = mk(cam.ox, cam.oy, cam.oz);
+        h.hit = false;
+        h.iters = 0;
+    } else {
+        primary_ray(cam, px, py, o, d);
+        get_by_ray<false, BD>(t, occ_tab, o, d, h, VHX_MAX_ITERS, nullptr, 0u, false, 0.0f, 0u);
+    }
+    store(t, out, idx, o, h);
+    if (h.iters >= tail_min) tail_record(next, cap, idx);
 }
 
 // Scatters rank-gathered tile buffers into framebuffers. Rank r's part of `gathered` holds `planes` planes of
@@ -1586,6 +1645,10 @@ static PassQ pass_q(const vhx_ctx *c, uint32_t p, uint32_t npass, bool qm = fals
     q.ly = c->shadow_light[1];
     q.lz = c->shadow_light[2];
     q.sbud = c->shadow_budget;
+    q.skip = nullptr;
+    q.tail_out = last ? c->tail_rec : nullptr;
+    q.tail_min = c->tail_min;
+    q.tail_cap = c->tail_cap;
     return q;
 }
 
@@ -1894,8 +1957,14 @@ void vhx_destroy(vhx_ctx *c) {
     if (c->use_ev) (void)hipEventDestroy(c->use_ev);
     for (DevBuf *b : {&c->scratch, &c->rays, &c->queue[0], &c->queue[1], &c->qctl, &c->tmp, &c->counts, &c->offsets,
                       &c->flags, &c->qargs, &c->state, &c->stateq, &c->upd, &c->prepass_depth, &c->batch_args, &c->scan_part,
-                      &c->shadow_args})
+                      &c->shadow_args, &c->tail_list[0], &c->tail_list[1], &c->tail_mask})
         if (b->ptr) (void)hipFree(b->ptr);
+    if (c->tail_stream) {
+        (void)hipStreamSynchronize(c->tail_stream);
+        (void)hipStreamDestroy(c->tail_stream);
+    }
+    if (c->tail_fork) (void)hipEventDestroy(c->tail_fork);
+    if (c->tail_join) (void)hipEventDestroy(c->tail_join);
     std::vector<vhx_ctx::Pinned *> pins = {&c->pinned[0], &c->pinned[1]};
     for (auto &P : c->batch_pinned) pins.push_back(&P);
     for (auto &P : c->shadow_pinned) pins.push_back(&P);
@@ -1999,6 +2068,22 @@ static int apply_tuning(vhx_ctx *c, const std::string &key, const std::string &v
     } else if (key == "scan_multi") {  // 0 = every scan on one workgroup
         if (!parse_u32(val, x)) return bad();
         c->scan_multi = x;
+    } else if (key == "tail") {  // early tail of lone frames (vhx_ctx::tail_*): 1 on, 0 off
+        if (!parse_u32(val, x) || x > 1) return bad();
+        c->tail_on = x != 0;
+    } else if (key == "tail_min") {  // steps from which a ray joins the next lone frame's early tail
+        if (!parse_u32(val, x) || x == 0) return bad();
+        c->tail_min = x;
+    } else if (key == "tail_rpw") {  // early-tail rays per wave
+        if (!parse_u32(val, x) || x == 0 || x > 64) return bad();
+        c->tail_rpw = x;
+    } else if (key == "tail_prio") {  // s_setprio of the early-tail waves (0-3)
+        if (!parse_u32(val, x) || x > 3) return bad();
+        c->tail_prio = x;
+    } else if (key == "tail_cap") {  // longest list recorded
+        if (!parse_u32(val, x) || x > (1u << 20)) return bad();
+        c->tail_cap = x;
+        c->tail_valid = false;  // (a list recorded under another cap may hold more entries)
     } else if (key == "stage_slots") {  // batch staging ring slots in use (1 = wait for the previous batch's copy)
         if (!parse_u32(val, x) || x == 0 || x > vhx_ctx::VHX_STAGE_SLOTS) return bad();
         c->stage_slots = x;
@@ -2266,6 +2351,12 @@ void vhx::copy_sched(vhx_ctx *c, const vhx_ctx *owner) {
     c->queue_waves0_force = owner->queue_waves0_force;
     c->shadow_budget = owner->shadow_budget;
     c->stage_slots = owner->stage_slots;
+    c->tail_on = owner->tail_on;
+    c->tail_min = owner->tail_min;
+    c->tail_rpw = owner->tail_rpw;
+    c->tail_prio = owner->tail_prio;
+    if (c->tail_cap != owner->tail_cap) c->tail_valid = false;
+    c->tail_cap = owner->tail_cap;
     c->queue_waves_mid = owner->queue_waves_mid;
     c->qxcd = owner->qxcd;
     c->qxcd_all = owner->qxcd_all;
@@ -2609,6 +2700,37 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
     // shadows fuse into the ladder where pass 0 lists its rays (the list entries carry the shadow tag); a single pass
     // or the lone frame's flag compaction traces them after the primary rays instead (below)
     const bool fuse = shadows && listed && npass > 1;
+    // early tail (vhx_ctx::tail_*): a lone frame (the idle schedule) of a whole framebuffer on the exact path records
+    // its longest rays; with a list recorded by this context's last such frame of the same size, they start now
+    const bool tail = c->tail_on && !fast && !ho.dev.bytes && !t.mips && !shadows && !listed && npass > 1 &&
+                      c->last_sched == 0 && layout == VHX_LAYOUT_FRAMEBUFFER && T == 16 && tile_start == 0 &&
+                      tile_stride == 1 && c->tail_cap > 0;
+    bool tail_use = false;
+    const uint32_t tail_blocks = (c->tail_cap + c->tail_rpw * 4u - 1u) / (c->tail_rpw * 4u);
+    if (tail) {
+        const uint64_t lbytes = (64ull + c->tail_cap) * 4ull, mbytes = ((nout + 31) / 32) * 4;
+        if ((rc = ensure(c, c->tail_list[0], lbytes)) || (rc = ensure(c, c->tail_list[1], lbytes)) ||
+            (rc = ensure(c, c->tail_mask, mbytes)))
+            return rc;
+        if (!c->tail_stream) {
+            int least = 0, greatest = 0;
+            VHX_HIP(c, hipDeviceGetStreamPriorityRange(&least, &greatest));
+            VHX_HIP(c, hipStreamCreateWithPriority(&c->tail_stream, hipStreamNonBlocking, greatest));
+            VHX_HIP(c, hipEventCreateWithFlags(&c->tail_fork, hipEventDisableTiming));
+            VHX_HIP(c, hipEventCreateWithFlags(&c->tail_join, hipEventDisableTiming));
+        }
+        uint32_t *next = (uint32_t *)c->tail_list[c->tail_cur ^ 1u].ptr;
+        VHX_HIP(c, hipMemsetAsync(next, 0, 4, c->stream));
+        tail_use = c->tail_valid && c->tail_w == cam->width && c->tail_h == cam->height;
+        if (tail_use) {
+            VHX_HIP(c, hipMemsetAsync(c->tail_mask.ptr, 0, mbytes, c->stream));
+            k_tail_mask<<<16, 256, 0, c->stream>>>((const uint32_t *)c->tail_list[c->tail_cur].ptr, c->tail_cap,
+                                                   (uint32_t)nout, (uint32_t *)c->tail_mask.ptr);
+            VHX_HIP(c, hipEventRecord(c->tail_fork, c->stream));
+            VHX_HIP(c, hipStreamWaitEvent(c->tail_stream, c->tail_fork, 0));
+        }
+        c->tail_rec = next;
+    }
     auto launch = [&](auto bd_tag) {
         constexpr int BD = decltype(bd_tag)::value;
         PassQ q0 = pass_q(c, 0, npass, qm);
@@ -2631,6 +2753,12 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
             qrc = launch_queue_passes<false, BD, false, true>(c, t, cd, src, ho.dev, 1, npass, nout, nb0, p0, ow, oh, 1,
                                                               qm);
         } else {
+            if (tail_use) {  // the listed long rays first, on the second stream; pass 0 skips them
+                k_trace_tail<BD><<<tail_blocks, 256, 0, c->tail_stream>>>(
+                    t, cd, ho.dev, (const uint32_t *)c->tail_list[c->tail_cur].ptr, c->tail_rec, c->tail_cap,
+                    c->tail_min, c->tail_rpw, c->tail_prio);
+                q0.skip = (const uint32_t *)c->tail_mask.ptr;
+            }
             if (fast)
                 k_trace_primary<false, BD, true><<<g0, 256, 0, c->stream>>>(
                     t, cd, ho.dev, T, tiles_x, tile_start, tile_stride, layout, bpx, bpt, q0, fd, lo);
@@ -2641,6 +2769,19 @@ int vhx_trace_primary(vhx_ctx *c, const vhx_camera *cam, uint32_t T, uint32_t ti
         }
     };
     const bool bd_ok = dispatch_bd(c->tree->desc.brick_dim, launch);
+    c->tail_rec = nullptr;
+    if (tail) {
+        // the frame ends with its early tail (joined before ev1 and the trace's use event); its record is next frame's
+        // list (the list it traced stays valid: an error below still leaves two well-formed lists)
+        if (tail_use) {
+            VHX_HIP(c, hipEventRecord(c->tail_join, c->tail_stream));
+            VHX_HIP(c, hipStreamWaitEvent(c->stream, c->tail_join, 0));
+        }
+        c->tail_cur ^= 1u;
+        c->tail_valid = true;
+        c->tail_w = cam->width;
+        c->tail_h = cam->height;
+    }
     if (!bd_ok) return fail(c, VHX_E_INVALID_ARG, "unsupported brick_dim");
     if (qrc) return qrc;
     VHX_HIP(c, hipGetLastError());
@@ -2846,6 +2987,22 @@ int vhx_trace_tiles_batch(vhx_ctx *c, const vhx_camera *cams, uint32_t n, uint32
                           uint32_t tile_stride, const vhx_hits *outs) {
     if (tile_size == 0) return c ? fail(c, VHX_E_INVALID_ARG, "vhx_trace_tiles_batch: tile_size 0") : VHX_E_INVALID_ARG;
     return trace_batch(c, cams, n, outs, tile_size, tile_starts, tile_stride, "vhx_trace_tiles_batch");
+}
+
+int vhx_tail_info(vhx_ctx *c, uint32_t *listed, uint32_t *width, uint32_t *height) {
+    if (!c) return VHX_E_INVALID_ARG;
+    uint32_t n = 0;
+    if (c->tail_on && c->tail_valid && c->tail_list[c->tail_cur].ptr) {
+        VHX_HIP(c, hipSetDevice(c->device));
+        VHX_STREAM(c);
+        VHX_HIP(c, hipMemcpyAsync(&n, c->tail_list[c->tail_cur].ptr, 4, hipMemcpyDeviceToHost, c->stream));
+        VHX_HIP(c, hipStreamSynchronize(c->stream));
+        n = std::min(n, c->tail_cap);
+    }
+    if (listed) *listed = n;
+    if (width) *width = c->tail_valid ? c->tail_w : 0u;
+    if (height) *height = c->tail_valid ? c->tail_h : 0u;
+    return VHX_OK;
 }
 
 int vhx_chain_profile(vhx_ctx *c, const vhx_camera *cam, const uint32_t *pixels, uint32_t n, uint64_t *out) {

@@ -300,6 +300,12 @@ class Raytracer:
         """Restores (or ends) the adaptive choice between the frames-in-flight and the lone-frame schedule."""
         self._check(N.lib().vhx_set_adaptive_schedule(self._h, 1 if on else 0))
 
+    def tail_info(self):
+        """vhx_tail_info: (pixels the next lone frame traces early, (width, height) they were recorded for)."""
+        n, w, h = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+        self._check(N.lib().vhx_tail_info(self._h, ctypes.byref(n), ctypes.byref(w), ctypes.byref(h)))
+        return n.value, (w.value, h.value)
+
     def pass_budgets(self):
         """(budgets of the last trace, schedule): schedule "busy" (frames in flight), "idle" (lone frame) or "fixed"."""
         b = (ctypes.c_uint32 * N.VHX_MAX_BUDGETS)()
