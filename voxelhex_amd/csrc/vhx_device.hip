@@ -2059,6 +2059,9 @@ static int apply_tuning(vhx_ctx *c, const std::string &key, const std::string &v
         if (!parse_u32(val, x) || x == 0) return bad();
         if (c->adaptive) vhx_set_adaptive_schedule(c, 0);
         c->queue_waves = x;
+    } else if (key == "qwpc_idle" || key == "qwpc_busy") {  // queue waves per CU of one schedule (stays adaptive)
+        if (!parse_u32(val, x) || x == 0 || x > 64) return bad();
+        (key == "qwpc_idle" ? c->sched_idle : c->sched_busy).queue_waves_per_cu = x;
     } else if (key == "qwavesm") {
         if (!parse_u32(val, x)) return bad();
         c->queue_waves_mid = x;
