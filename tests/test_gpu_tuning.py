@@ -58,11 +58,17 @@ def test_set_tuning_validates_and_applies():
         rt.set_tuning("budgets=16,128;qorder=32r")
         assert rt.pass_budgets() == ((16, 128), "fixed")
         for bad in ("nokey=1", "budgets=3,2", "qblock=100", "qorder=12", "rpw=65", "split_tune=3,2,1,1", "adaptive",
-                    "budgets=1;bogus=2", "sparse=1,x", "qsort=100", "qsort=4096", "qsort=768"):
+                    "budgets=1;bogus=2", "sparse=1,x", "qsort=100", "qsort=4096", "qsort=768", "stage_slots=0",
+                    "stage_slots=5", "tail=2", "tail_min=0", "tail_rpw=0", "tail_rpw=65", "tail_prio=4",
+                    "tail_cap=2000000", "qwpc_idle=0", "qwpc_busy=65", "sbudget=x", "qwaves0=0"):
             with pytest.raises(Exception):
                 rt.set_tuning(bad)
             assert rt.pass_budgets() == ((16, 128), "fixed"), bad  # a refused spec changes nothing
+        # the round-6 keys that leave the schedule alone
+        rt.set_tuning("stage_slots=4;tail=1;tail_min=300;tail_rpw=8;tail_prio=2;tail_cap=512;sbudget=48;qwaves0=2048")
+        assert rt.pass_budgets() == ((16, 128), "fixed")
         rt.set_tuning({"adaptive": 1})
+        rt.set_tuning("qwpc_idle=8;qwpc_busy=3")  # per-schedule figures: the choice stays adaptive
         rt.set_tuning("budgets=")
         assert rt.pass_budgets()[0] == ()
     finally:
