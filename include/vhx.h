@@ -183,7 +183,8 @@ int vhx_get_pass_budgets(const vhx_ctx *ctx, uint32_t *budgets, uint32_t *n, int
  * qwavesm, qwaves0, qxcd, qxcd_all (0/1), sparse (list, fixes the schedule), qorder ("[m]N[z|r]" or 0), qsort (0 or
  * 256..2048: segment node sort of the queue passes, docs/DESIGN_LOG.md §15.3), qsortp (pass mask), qsortb (workgroups),
  * qwpc_idle / qwpc_busy (queue waves per CU of one schedule, which stays adaptive), stage_slots (1..4: batch staging
- * ring), sbudget (fused shadows: a shadow ray's steps in its primary ray's pass), tail / tail_min / tail_rpw /
+ * ring), finter (0/1: batch pass 0 frame-major / frames interleaved block by block), sbudget (fused shadows: a shadow
+ * ray's steps in its primary ray's pass), tail / tail_min / tail_rpw /
  * tail_cap / tail_prio (the early tail of lone frames, vhx_tail_info). The
  * library reads no environment variable for any of them (docs/DESIGN_LOG.md §15). Unknown keys or malformed values:
  * VHX_E_INVALID_ARG and nothing is changed. */

@@ -72,7 +72,7 @@ def test_batch_vs_oracle(gpu, oracle):
 @pytest.mark.parametrize("tune", ["budgets=1,2,3,5,8,13", "budgets=4", "budgets=", "qorder=0", "qorder=8r",
                                   "qorder=m16", "qorder=32z", "rpw=0,16,8,4", "resume=0", "qsort=256",
                                   "qwaves=64;qxcd=0", "sparse=60,60,60", "p0lists=0", "qorder=16z", "qorder=128z",
-                                  "scan_multi=1"])
+                                  "scan_multi=1", "finter=0", "finter=0;qstate=1", "finter=0;p0lists=0"])
 def test_batch_schedules_are_bit_identical(gpu, tune):
     flat = vhx.FlatTree.build_scene(N.VHX_SCENE_LATTICE_CUBE, 256, 4)
     rt = vhx.Raytracer(0, tune=tune)
@@ -250,7 +250,7 @@ def test_shadow_batch_argument_errors(gpu):
 @pytest.mark.parametrize("W,H,T,stride,starts", [(200, 136, 64, 3, (0, 1, 2)), (200, 136, 16, 5, (0, 4, 4, 9)),
                                                  (97, 33, 32, 2, (0, 1, 5)), (256, 256, 64, 1, (0, 0)),
                                                  (130, 70, 20, 2, (1, 0, 3))])
-@pytest.mark.parametrize("tune", [None, "tlists=0", "budgets=4", "qstate=1", "resume=0"])
+@pytest.mark.parametrize("tune", [None, "tlists=0", "budgets=4", "qstate=1", "resume=0", "finter=0"])
 def test_tiles_batch_equals_single_tile_traces(W, H, T, stride, starts, tune):
     """vhx_trace_tiles_batch (a rank's tile sets of several frames, the multi-GPU split's batch): every frame equals
     the single TILES-layout trace of its camera and tile set bit for bit, padding entries included (both untouched),

@@ -279,6 +279,7 @@ struct PassQ {
     const uint32_t *skip;
     uint32_t *tail_out;
     uint32_t tail_min, tail_cap;
+    uint32_t finter;  // batch pass 0: frames interleaved block by block (vhx_ctx::frame_interleave)
 };
 
 // one more pixel of the early-tail list (at most cap; the count keeps growing past it, the entries stop)
@@ -934,7 +935,11 @@ __global__ void __launch_bounds__(256) VHX_BATCH_ATTR k_trace_primary_batch(DevT
     zero_ctl(q.zero);
     __syncthreads();
     const uint32_t bid = xcd_block(blockIdx.x, gridDim.x, q.xcd_group);
-    const uint32_t f = bid / nblocks_frame, sb = bid - f * nblocks_frame;
+    // frame-major (all of frame 0's blocks, then frame 1's, ...) or interleaved (block sb of every frame in turn: the
+    // frames' rays through one screen region run together and share the caches)
+    const uint32_t nfr = gridDim.x / nblocks_frame;
+    const uint32_t f = q.finter ? bid % nfr : bid / nblocks_frame;
+    const uint32_t sb = q.finter ? bid / nfr : bid - f * nblocks_frame;
     const CamD cam = cams[f];
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
     uint32_t px, py, local;
@@ -1649,6 +1654,7 @@ static PassQ pass_q(const vhx_ctx *c, uint32_t p, uint32_t npass, bool qm = fals
     q.tail_out = last ? c->tail_rec : nullptr;
     q.tail_min = c->tail_min;
     q.tail_cap = c->tail_cap;
+    q.finter = c->frame_interleave ? 1u : 0u;
     return q;
 }
 
@@ -2087,6 +2093,9 @@ static int apply_tuning(vhx_ctx *c, const std::string &key, const std::string &v
         if (!parse_u32(val, x) || x > (1u << 20)) return bad();
         c->tail_cap = x;
         c->tail_valid = false;  // (a list recorded under another cap may hold more entries)
+    } else if (key == "finter") {  // batches: pass-0 blocks of the frames interleaved (1) or frame-major (0)
+        if (!parse_u32(val, x) || x > 1) return bad();
+        c->frame_interleave = x != 0;
     } else if (key == "stage_slots") {  // batch staging ring slots in use (1 = wait for the previous batch's copy)
         if (!parse_u32(val, x) || x == 0 || x > vhx_ctx::VHX_STAGE_SLOTS) return bad();
         c->stage_slots = x;
@@ -2354,6 +2363,7 @@ void vhx::copy_sched(vhx_ctx *c, const vhx_ctx *owner) {
     c->queue_waves0_force = owner->queue_waves0_force;
     c->shadow_budget = owner->shadow_budget;
     c->stage_slots = owner->stage_slots;
+    c->frame_interleave = owner->frame_interleave;
     c->tail_on = owner->tail_on;
     c->tail_min = owner->tail_min;
     c->tail_rpw = owner->tail_rpw;
