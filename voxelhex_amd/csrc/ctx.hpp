@@ -207,8 +207,8 @@ struct vhx_ctx {
     // "tlists=0" falls back to flags compacted in output-index order)
     bool tile_lists = true;
     // batch pass 0: the frames' blocks interleaved (block b of frame 0, of frame 1, ...) instead of frame-major (tune
-    // "finter"): the frames' rays through one screen region run together, on one XCD (xcd_block runs), and share its
-    // L2 -- the headline in the driver's window 0.5115-0.5147 against 0.5200-0.5366 ms per frame (four alternating
+    // "finter"): the frames' rays through one screen region run together and share the caches (the XCD placement of
+    // those workgroups measured indifferent) -- the headline in the driver's window 0.5115-0.5147 against 0.5200-0.5366 ms per frame (four alternating
     // runs), 100 frames 0.4914 against 0.5041-0.5085, config 4 1.786-1.794 against 1.863-1.879, the moving camera
     // 0.721-0.723 against 0.737-0.740 (profiles/r06/finter/)
     bool frame_interleave = true;
